@@ -1,0 +1,378 @@
+#!/usr/bin/env python3
+"""Physics-free full-step traces from the reference task classes.
+
+Run in the build container only (needs /root/reference):
+
+    python tests/golden/make_traces.py
+
+The reference ``Ant`` / ``Humanoid`` / ``Cartpole`` classes are constructed on
+top of a fake ``gym`` object (SURVEY.md §8(c) "Full-step oracle", Appendix D):
+``simulate`` overwrites the sim state with a seeded "physics output" that the
+trace records, ``set_*_indexed`` copy rows into the sim buffers immediately and
+``refresh_*`` are no-ops.  ``VecTask.step`` (vec_task.py:362-410) then runs the
+reference's own ordering: action clamp -> pre_physics_step -> simulate ->
+post_physics_step (progress += 1, reset_idx on the previous step's reset_buf,
+compute_observations, compute_reward) -> timeout_buf -> obs clamp.
+
+Every reset-noise draw the reference makes with the global torch RNG is
+recorded as raw U(0,1) samples scattered to per-env rows, so the build's task
+layer can replay the exact same resets from injected noise.
+
+Output: tests/golden/trace_{ant,humanoid,cartpole}.npz
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+import yaml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _refshim  # noqa: E402
+
+_refshim.install()
+from isaacgym import gymapi  # noqa: E402
+from isaacgymenvs.utils import torch_jit_utils as tju  # noqa: E402
+
+REF = _refshim.REF
+
+
+class _Prop:
+    def __init__(self, **k):
+        self.__dict__.update(k)
+
+
+class FakeGym:
+    """Physics-free stand-in for isaacgym.gymapi.Gym (Appendix D surface)."""
+
+    def __init__(self, spec, num_envs):
+        self.spec = spec
+        self.N = num_envs
+        nd = spec["num_dof"]
+        self.root = torch.zeros(num_envs * spec.get("actors", 1), 13)
+        self.root[:, 2] = spec.get("start_z", 0.0)
+        self.root[:, 6] = 1.0
+        self.dof = torch.zeros(num_envs * nd, 2)
+        self.sensors = torch.zeros(num_envs * spec.get("sensors", 0), 6)
+        self.dof_force = torch.zeros(num_envs * nd)
+        self.calls = []
+        self.inject = None
+
+    # --- setup --------------------------------------------------------------------------
+    def create_sim(self, *a):
+        return "sim"
+
+    def add_ground(self, *a):
+        pass
+
+    def load_asset(self, *a):
+        return "asset"
+
+    def get_asset_dof_count(self, a):
+        return self.spec["num_dof"]
+
+    def get_asset_rigid_body_count(self, a):
+        return len(self.spec["bodies"])
+
+    def get_asset_joint_count(self, a):
+        return self.spec["num_dof"]
+
+    def get_asset_rigid_body_name(self, a, i):
+        return self.spec["bodies"][i]
+
+    def find_asset_rigid_body_index(self, a, name):
+        return self.spec["bodies"].index(name)
+
+    def get_asset_actuator_properties(self, a):
+        return [_Prop(motor_effort=g) for g in self.spec["gears"]]
+
+    def create_asset_force_sensor(self, *a):
+        return 0
+
+    def create_env(self, *a):
+        return "env"
+
+    def create_actor(self, *a):
+        return 0
+
+    def set_rigid_body_color(self, *a):
+        pass
+
+    def enable_actor_dof_force_sensors(self, *a):
+        pass
+
+    def get_actor_dof_properties(self, env, h):
+        nd = self.spec["num_dof"]
+        return {"lower": np.array(self.spec.get("lower", [0.0] * nd), dtype=np.float32),
+                "upper": np.array(self.spec.get("upper", [0.0] * nd), dtype=np.float32),
+                "driveMode": np.zeros(nd, dtype=np.int32),
+                "stiffness": np.zeros(nd, dtype=np.float32),
+                "damping": np.zeros(nd, dtype=np.float32)}
+
+    def set_actor_dof_properties(self, *a):
+        pass
+
+    def find_actor_rigid_body_handle(self, env, h, name):
+        return self.spec["bodies"].index(name)
+
+    def prepare_sim(self, sim):
+        pass
+
+    # --- tensors ------------------------------------------------------------------------
+    def acquire_actor_root_state_tensor(self, sim):
+        return self.root
+
+    def acquire_dof_state_tensor(self, sim):
+        return self.dof
+
+    def acquire_force_sensor_tensor(self, sim):
+        return self.sensors
+
+    def acquire_dof_force_tensor(self, sim):
+        return self.dof_force
+
+    def refresh_dof_state_tensor(self, sim):
+        pass
+
+    refresh_actor_root_state_tensor = refresh_force_sensor_tensor = refresh_dof_force_tensor = refresh_dof_state_tensor
+
+    def set_dof_actuation_force_tensor(self, sim, t):
+        self.calls.append(("actuation", t.clone()))
+
+    def set_actor_root_state_tensor_indexed(self, sim, data, idx, n):
+        idx = idx.long()
+        self.root[idx] = data[idx]
+        self.calls.append(("root_indexed", idx.clone()))
+
+    def set_dof_state_tensor_indexed(self, sim, data, idx, n):
+        nd = self.spec["num_dof"]
+        idx = idx.long()
+        d = data.view(self.N, nd, 2)
+        self.dof.view(self.N, nd, 2)[idx] = d[idx]
+        self.calls.append(("dof_indexed", idx.clone()))
+
+    def simulate(self, sim):
+        if self.inject is not None:
+            root, dof, sens, dforce = self.inject
+            self.root.copy_(root)
+            self.dof.copy_(dof)
+            if sens is not None:
+                self.sensors.copy_(sens)
+            if dforce is not None:
+                self.dof_force.copy_(dforce)
+
+    def fetch_results(self, *a):
+        pass
+
+
+def install_fake(fake):
+    from isaacgym import gymtorch
+    gymapi.acquire_gym = lambda: fake
+    gymtorch.wrap_tensor = lambda t: t
+    gymtorch.unwrap_tensor = lambda t: t
+
+
+def load_task_cfg(name, num_envs, episode_length=None):
+    with open(os.path.join(REF, "isaacgymenvs/cfg/task", name + ".yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg["physics_engine"] = "physx"
+    cfg["env"]["numEnvs"] = num_envs
+    if episode_length is not None:
+        cfg["env"]["episodeLength"] = episode_length
+    cfg["sim"]["use_gpu_pipeline"] = False
+    cfg["sim"]["physx"] = {}
+    return cfg
+
+
+class RandRecorder:
+    """Wraps the task module's ``torch_rand_float`` so each draw's raw U(0,1) is kept."""
+
+    def __init__(self):
+        self.draws = []
+
+    def __call__(self, lower, upper, shape, device):
+        u = torch.rand(*shape, device=device)
+        self.draws.append(u.clone())
+        return (upper - lower) * u + lower
+
+
+def physics_output(g, N, nd, lo, hi, z_range, nsens):
+    root = torch.zeros(N, 13)
+    root[:, 0:2] = torch.randn(N, 2, generator=g)
+    root[:, 2] = z_range[0] + (z_range[1] - z_range[0]) * torch.rand(N, generator=g)
+    yaw = (torch.rand(N, generator=g) * 2 - 1) * math.pi
+    rp = (torch.rand(N, 2, generator=g) * 2 - 1) * 0.5
+    root[:, 3:7] = tju.quat_from_euler_xyz(rp[:, 0], rp[:, 1], yaw)
+    root[:, 7:13] = torch.randn(N, 6, generator=g)
+    pos = lo + (hi - lo) * (torch.rand(N, nd, generator=g) * 1.1 - 0.05)
+    vel = torch.randn(N, nd, generator=g) * 3
+    dof = torch.stack([pos, vel], dim=-1).reshape(N * nd, 2)
+    sens = torch.randn(N * nsens, 6, generator=g) * 10 if nsens else None
+    return root, dof, sens
+
+
+def run_locomotion(task, N=64, T=8, ep_len=5):
+    import importlib
+    mod = importlib.import_module("isaacgymenvs.tasks." + task.lower())
+    if task == "Ant":
+        d = math.pi / 180
+        spec = dict(num_dof=8, sensors=4, start_z=0.44, gears=[15.0] * 8,
+                    bodies=["torso", "front_left_leg", "front_left_foot", "front_right_leg", "front_right_foot",
+                            "left_back_leg", "left_back_foot", "right_back_leg", "right_back_foot"],
+                    lower=[x * d for x in [-40, 30, -40, -100, -40, -100, -40, 30]],
+                    upper=[x * d for x in [40, 100, 40, -30, 40, -30, 40, 100]])
+        z_range, nsens, cls = (0.25, 0.7), 4, mod.Ant
+    else:
+        d = math.pi / 180
+        deg = [(-45, 45), (-75, 30), (-35, 35), (-45, 15), (-60, 35), (-120, 45), (-160, 2), (-50, 50), (-50, 50),
+               (-45, 15), (-60, 35), (-120, 45), (-160, 2), (-50, 50), (-50, 50), (-90, 70), (-90, 70), (-90, 50),
+               (-90, 70), (-90, 70), (-90, 50)]
+        spec = dict(num_dof=21, sensors=2, start_z=1.34,
+                    gears=[67.5, 67.5, 67.5, 45, 45, 135, 90, 22.5, 22.5, 45, 45, 135, 90, 22.5, 22.5,
+                           67.5, 67.5, 45, 67.5, 67.5, 45],
+                    bodies=["torso", "head", "lower_waist", "pelvis", "right_thigh", "right_shin", "right_foot",
+                            "left_thigh", "left_shin", "left_foot", "right_upper_arm", "right_lower_arm",
+                            "right_hand", "left_upper_arm", "left_lower_arm", "left_hand"],
+                    lower=[a * d for a, _ in deg], upper=[b * d for _, b in deg])
+        z_range, nsens, cls = (0.7, 1.4), 2, mod.Humanoid
+    fake = FakeGym(spec, N)
+    install_fake(fake)
+    rec = RandRecorder()
+    mod.torch_rand_float = rec
+    cfg = load_task_cfg(task, N, ep_len)
+    torch.manual_seed(0)
+    env = cls(cfg, "cpu", "cpu", -1, True, False, False)
+    nd = spec["num_dof"]
+    lo = torch.tensor(spec["lower"])
+    hi = torch.tensor(spec["upper"])
+    lo, hi = torch.minimum(lo, hi), torch.maximum(lo, hi)
+    g = torch.Generator().manual_seed(1)
+    out = {k: [] for k in ("actions", "phys_root", "phys_dof", "phys_sensors", "phys_dof_force", "noise",
+                           "reset_mask", "obs", "rew", "reset", "progress", "timeouts", "potentials",
+                           "prev_potentials", "root_after", "dof_after", "reset_in", "progress_in")}
+    out["init_obs"] = env.reset()["obs"].clone()
+    for t in range(T):
+        actions = torch.rand(N, env.num_actions, generator=g) * 2.4 - 1.2  # exercises the ±1 clip
+        root, dof, sens = physics_output(g, N, nd, lo, hi, z_range, nsens)
+        dforce = torch.randn(N * nd, generator=g) * 20 if task == "Humanoid" else None
+        fake.inject = (root, dof, sens, dforce)
+        reset_in = env.reset_buf.clone()
+        progress_in = env.progress_buf.clone()
+        rec.draws.clear()
+        obs_dict, rew, reset, extras = env.step(actions)
+        ids = reset_in.nonzero(as_tuple=False).flatten()
+        noise = torch.zeros(N, 2 * nd)
+        if len(ids) > 0:
+            noise[ids, :nd] = rec.draws[0]
+            noise[ids, nd:] = rec.draws[1]
+        mask = torch.zeros(N, dtype=torch.int64)
+        mask[ids] = 1
+        out["actions"].append(actions)
+        out["phys_root"].append(root)
+        out["phys_dof"].append(dof.view(N, nd, 2))
+        out["phys_sensors"].append(sens.view(N, nsens * 6))
+        out["phys_dof_force"].append(dforce.view(N, nd) if dforce is not None else torch.zeros(N, nd))
+        out["noise"].append(noise)
+        out["reset_mask"].append(mask)
+        out["obs"].append(obs_dict["obs"].clone())
+        out["rew"].append(rew.clone())
+        out["reset"].append(reset.clone())
+        out["progress"].append(env.progress_buf.clone())
+        out["timeouts"].append(extras["time_outs"].clone().long())
+        out["potentials"].append(env.potentials.clone())
+        out["prev_potentials"].append(env.prev_potentials.clone())
+        out["root_after"].append(env.root_states.clone())
+        out["dof_after"].append(env.dof_state.view(N, nd, 2).clone())
+        out["reset_in"].append(reset_in)
+        out["progress_in"].append(progress_in)
+    res = {k: (torch.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
+    res["lower"], res["upper"] = lo, hi
+    res["episode_length"] = torch.tensor(ep_len)
+    return res
+
+
+def run_cartpole(N=64, T=12):
+    import importlib
+    mod = importlib.import_module("isaacgymenvs.tasks.cartpole")
+    spec = dict(num_dof=2, sensors=0, gears=[], bodies=["slider", "cart", "pole"])
+    fake = FakeGym(spec, N)
+    install_fake(fake)
+    draws = []
+
+    class _TorchProxy:
+        def __getattr__(self, k):
+            return getattr(torch, k)
+
+        def rand(self, *shape, **kw):
+            u = torch.rand(*shape, **kw)
+            draws.append(u.clone())
+            return u
+
+    mod.torch = _TorchProxy()
+    cfg = load_task_cfg("Cartpole", N)
+    torch.manual_seed(0)
+    env = mod.Cartpole(cfg, "cpu", "cpu", -1, True, False, False)
+    g = torch.Generator().manual_seed(2)
+    keys = ("actions", "phys_dof", "noise", "reset_mask", "obs", "rew", "reset", "progress", "timeouts",
+            "dof_after", "reset_in", "progress_in", "actuation")
+    out = {k: [] for k in keys}
+    for t in range(T):
+        actions = torch.rand(N, 1, generator=g) * 2.4 - 1.2
+        dof = torch.randn(N, 2, 2, generator=g) * torch.tensor([[[2.0, 1.0], [1.0, 2.0]]])
+        fake.inject = (fake.root, dof.reshape(N * 2, 2), None, None)
+        reset_in = env.reset_buf.clone()
+        progress_in = env.progress_buf.clone()
+        draws.clear()
+        fake.calls.clear()
+        obs_dict, rew, reset, extras = env.step(actions)
+        ids = reset_in.nonzero(as_tuple=False).flatten()
+        noise = torch.zeros(N, 4)
+        if len(ids) > 0:
+            noise[ids, :2] = draws[0]
+            noise[ids, 2:] = draws[1]
+        mask = torch.zeros(N, dtype=torch.int64)
+        mask[ids] = 1
+        act = [c[1] for c in fake.calls if c[0] == "actuation"][0]
+        out["actions"].append(actions)
+        out["phys_dof"].append(dof)
+        out["noise"].append(noise)
+        out["reset_mask"].append(mask)
+        out["obs"].append(obs_dict["obs"].clone())
+        out["rew"].append(rew.clone())
+        out["reset"].append(reset.clone())
+        out["progress"].append(env.progress_buf.clone())
+        out["timeouts"].append(extras["time_outs"].clone().long())
+        out["dof_after"].append(env.dof_state.view(N, 2, 2).clone())
+        out["reset_in"].append(reset_in)
+        out["progress_in"].append(progress_in)
+        out["actuation"].append(act.view(N, 2).clone())
+    return {k: torch.stack(v) for k, v in out.items()}
+
+
+def save(name, d):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **{k: (v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
+                                 for k, v in d.items()})
+    print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    # one task per process: vec_task keeps a process-global sim (vec_task.py:55-64)
+    if which == "all":
+        import subprocess
+        for t in ("ant", "humanoid", "cartpole"):
+            subprocess.check_call([sys.executable, __file__, t])
+        return
+    if which == "ant":
+        save("trace_ant.npz", run_locomotion("Ant"))
+    elif which == "humanoid":
+        save("trace_humanoid.npz", run_locomotion("Humanoid"))
+    elif which == "cartpole":
+        save("trace_cartpole.npz", run_cartpole())
+
+
+if __name__ == "__main__":
+    main()
