@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""env-steps/s of the fused VecTask.step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--task Ant] [--num-envs 65536]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+One "step" = one VecTask.step of every env on every rank (controlFrequencyInv=1,
+2 physics substeps), random U(-1,1) actions generated on device before the timed
+region, inputs resident in HBM.  Envs are independent, so ranks shard them
+(weak scaling: --num-envs per GPU, no data-path collective).  Rank 0 prints ONE
+JSON line.  See DESIGN.md §Measurement for the roofline accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "isaacgymenvs-ma_amd"))
+
+# algorithmic (compulsory) HBM bytes per env-step: every gym/VecTask-visible tensor
+# read and written once per control step; model tables amortised to 0.
+ALGO_BYTES = {"Ant": 673, "Humanoid": 1161, "Cartpole": 89, "MAAnt": 2800}
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md (spec)
+
+
+def cpu_baseline(task, seconds=12.0, n=4096):
+    """CPU oracle (fp32 task layer + fp64 physics restatement), OpenMP over envs, bounded sample."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    from migym import configs, model as M, taskdefs
+    cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+    cfg = configs.task_config(task, n)
+    spec = M.load_builtin(taskdefs.TASK_INFO[task][1])
+    sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[task][5])
+    tp = taskdefs.task_params(task, cfg, spec)
+    mnp = M.pack_model(spec)
+    h = O.HostEnv(tp, spec, n)
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (8, n, tp.num_actions)).astype(np.float32)
+    h.actions[:] = acts[0]
+    h.env_step(mnp, sp, tp, 0, 0, cores)  # warm-up (first step resets every env)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds and steps < 500:
+        h.actions[:] = acts[steps % 8]
+        h.env_step(mnp, sp, tp, 0, steps + 1, cores)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{task} {n} envs x {steps} steps ({dt:.1f} s), oracle/ CPU restatement "
+                      f"(fp64 physics, fp32 task layer), not PhysX"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--task", default="Ant")
+    ap.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = f"cuda:{local}"
+    torch.cuda.set_device(dev)
+
+    import migym
+    n = args.num_envs
+    env = migym.make(seed=rank, task=args.task, num_envs=n, sim_device=dev, rl_device=dev, headless=True,
+                     multi_gpu=world > 1)
+    na = env.num_actions
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
+    for i in range(args.warmup):
+        env.step(pool[i % 8])
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        env.step(pool[i % 8])
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    total_envs = n * env.num_agents * world if args.task == "MAAnt" else n * world
+    value = n * world * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+    if rank == 0:
+        per_launch = ALGO_BYTES[args.task] * n
+        achieved = per_launch / (kern_ms * 1e-3)
+        out = {
+            "metric": "env-steps/sec (whole node) at num_envs=65536; 1/2/4/8 MI355X scaling",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (U(-1,1) actions, device-resident)",
+            "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, 2 substeps, PGS x4",
+                       "task": args.task, "num_envs_per_gpu": n, "num_envs_total": total_envs,
+                       "parallelism": f"env-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK, "traffic": None,
+                         "kernel": "k_env_step", "kernel_ms": kern_ms,
+                         "algo_bytes_per_env_step": ALGO_BYTES[args.task]},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds)
+            except Exception as ex:  # noqa: BLE001
+                out["cpu_baseline"] = {"error": repr(ex)}
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

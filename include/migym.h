@@ -1,0 +1,221 @@
+/*
+ * migym.h — C ABI of the MI355X-native physics-step + observation/reward path.
+ *
+ * This is the drop-in boundary that sits where the reference calls the closed
+ * isaacgym tensor API.  Every entry point replaces one call
+ * the reference's task layer makes on its hot path; the replaced call is cited
+ * (paths relative to the reference checkout):
+ *
+ *   mg_sim_create        gym.create_sim + load_asset + create_env/create_actor loop
+ *                        + prepare_sim              (tasks/base/vec_task.py:255-263,
+ *                                                    tasks/ant.py:135-197)
+ *   mg_sim_bind          gym.acquire_*_tensor + gymtorch.wrap_tensor
+ *                                                   (tasks/ant.py:78-95, humanoid.py:75-95)
+ *   mg_sim_simulate      gym.simulate(sim)          (tasks/base/vec_task.py:381-384)
+ *   mg_set_indexed       gym.set_actor_root_state_tensor_indexed /
+ *                        gym.set_dof_state_tensor_indexed
+ *                                                   (tasks/ant.py:265-271, cartpole.py:153-155)
+ *   mg_compute_observations   compute_{ant,humanoid}_observations / cartpole obs
+ *                                                   (tasks/ant.py:374-408, humanoid.py:378-413,
+ *                                                    cartpole.py:131-142)
+ *   mg_compute_reward    compute_{ant,humanoid,cartpole}_reward
+ *                                                   (tasks/ant.py:325-371, humanoid.py:323-375,
+ *                                                    cartpole.py:180-196)
+ *   mg_env_step          one whole VecTask.step after the action tensor is on device:
+ *                        clamp -> pre_physics_step -> simulate x controlFrequencyInv ->
+ *                        post_physics_step (progress, masked reset_idx, obs, reward)
+ *                        -> timeout_buf -> obs clamp  (tasks/base/vec_task.py:362-410,
+ *                        tasks/ant.py:252-297) — no host synchronisation.
+ *
+ * Conventions
+ *   - All tensors are device memory owned by the caller (PyTorch); pointers must
+ *     stay valid for the call; layouts are the gym-visible ones:
+ *       root_states (N*A, 13) f32 [px py pz qx qy qz qw vx vy vz wx wy wz]
+ *       dof_state   (N*A*nD, 2) f32 [q, qdot];  sensors (N*A*S, 6) f32;
+ *       dof_force   (N*A*nD) f32;  actions (N*A, nA) f32
+ *       reset/progress/timeout buffers int64 (torch.long), as the reference.
+ *   - Kernels are asynchronous on the caller's HIP stream (hipStream_t passed as
+ *     void*; NULL = default stream).  No entry point synchronises the device.
+ *   - Return 0 on success, a negative MG_E* code otherwise; mg_last_error()
+ *     returns a thread-local message.  No C++ exception crosses the ABI.
+ *   - One mg_sim per (process, device); calls on one handle are not thread-safe.
+ */
+#ifndef MIGYM_H
+#define MIGYM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MG_VERSION 1
+
+#define MG_MAX_NODES 40
+#define MG_MAX_BODIES 40
+#define MG_MAX_GEOMS 48
+#define MG_MAX_PAIRS 192
+#define MG_MAX_SENSORS 8
+
+enum { MG_JT_FREE = 0, MG_JT_FIXED = 1, MG_JT_HINGE = 2, MG_JT_SLIDE = 3 };
+enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4 };
+enum { MG_OK = 0, MG_EINVAL = -1, MG_EDEVICE = -2, MG_ENOMEM = -3, MG_ECAPACITY = -4 };
+enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2 };
+enum { MG_SET_ROOT_STATE = 0, MG_SET_DOF_STATE = 1 };
+
+/* One articulation ("actor asset") as a dynamics tree of 1-DOF nodes.
+ * Produced by migym/model.py (pack_model); field order == MODEL_DTYPE. */
+typedef struct mg_model {
+  int32_t num_nodes, num_dofs, fixed_base, num_bodies;
+  int32_t num_geoms, num_pairs, num_sensors, nv;
+  int32_t parent[MG_MAX_NODES];
+  int32_t jtype[MG_MAX_NODES];
+  int32_t limited[MG_MAX_NODES];
+  int32_t node_body[MG_MAX_NODES];
+  float t[MG_MAX_NODES][3];        /* joint anchor in parent node frame */
+  float r0[MG_MAX_NODES][4];       /* rest rotation parent node -> node (xyzw) */
+  float axis[MG_MAX_NODES][3];     /* joint axis, node frame (unit) */
+  float mass[MG_MAX_NODES];
+  float com[MG_MAX_NODES][3];      /* node frame */
+  float inertia[MG_MAX_NODES][6];  /* about COM, node frame: xx yy zz xy xz yz */
+  float armature[MG_MAX_NODES];
+  float damping[MG_MAX_NODES];
+  float stiffness[MG_MAX_NODES];
+  float lower[MG_MAX_NODES];
+  float upper[MG_MAX_NODES];
+  int32_t body_node[MG_MAX_BODIES];
+  int32_t body_parent[MG_MAX_BODIES];
+  float body_pos[MG_MAX_BODIES][3];  /* body origin in its node frame */
+  float body_quat[MG_MAX_BODIES][4];
+  float body_com[MG_MAX_BODIES][3];  /* body COM in body frame */
+  int32_t geom_type[MG_MAX_GEOMS];
+  int32_t geom_node[MG_MAX_GEOMS];
+  int32_t geom_body[MG_MAX_GEOMS];
+  int32_t geom_pad[MG_MAX_GEOMS];
+  float geom_size[MG_MAX_GEOMS][3];
+  float geom_pos[MG_MAX_GEOMS][3];   /* node frame */
+  float geom_quat[MG_MAX_GEOMS][4];  /* node frame; capsule axis = local z */
+  int32_t pair[MG_MAX_PAIRS][2];     /* self-collision geom pairs */
+  int32_t sensor_body[MG_MAX_SENSORS];
+} mg_model;
+
+/* Simulation parameters (cfg['sim'] of the task YAML: Ant.yaml:42-61). */
+typedef struct mg_sim_params {
+  float dt;                 /* control dt (sim.dt) */
+  int32_t substeps;         /* sim.substeps */
+  float gravity[3];
+  int32_t pos_iters;        /* physx.num_position_iterations: PGS sweeps per substep */
+  float contact_offset;     /* physx.contact_offset: contacts generated below this gap */
+  float rest_offset;        /* physx.rest_offset */
+  float max_depen_vel;      /* physx.max_depenetration_velocity */
+  float friction;           /* ground-plane friction coefficient */
+  float baumgarte;          /* penetration recovery factor (build-defined) */
+  float limit_margin;       /* joint-limit rows are built when within this distance */
+  int32_t max_contacts;     /* per-actor contact capacity (<= MG_MAX_CONTACTS) */
+  int32_t agents;           /* articulations per env (MA layouts; 1 otherwise) */
+} mg_sim_params;
+
+/* Gym-visible state buffers the sim reads/writes (zero-copy, caller owned). */
+typedef struct mg_state_views {
+  float* root_states;       /* (N*A, 13) */
+  float* dof_state;         /* (N*A*nD, 2) */
+  const float* dof_actuation; /* (N*A*nD) effort, may be NULL (= zero) */
+  float* sensors;           /* (N*A*S, 6), may be NULL */
+  float* dof_force;         /* (N*A*nD), may be NULL */
+  float* rigid_body_states; /* (N*A*nB, 13), may be NULL */
+} mg_state_views;
+
+/* Task constants (cfg['env'] of the task YAML). */
+typedef struct mg_task_params {
+  int32_t task_id;          /* MG_TASK_* */
+  int32_t num_obs;
+  int32_t num_actions;
+  int32_t max_episode_length;
+  float dt;
+  float clip_actions;       /* env.clipActions (inf if absent) */
+  float clip_obs;           /* env.clipObservations (inf if absent) */
+  float power_scale;        /* env.powerScale; Cartpole: maxEffort */
+  float dof_vel_scale;
+  float angular_velocity_scale;
+  float contact_force_scale;
+  float heading_weight;
+  float up_weight;
+  float actions_cost_scale;
+  float energy_cost_scale;
+  float joints_at_limit_cost_scale;
+  float death_cost;
+  float termination_height;
+  float max_motor_effort;
+  float reset_dist;         /* Cartpole resetDist */
+  float target[3];          /* walk target (ant.py:105) */
+  float start_pos[3];       /* actor start pose (ant.py:163-166) */
+  float start_rot[4];
+  float motor_effort[64];   /* per-DOF gear (actuator order, applied by DOF position) */
+  float dof_lower[64];      /* task-side dof limits (swapped if lower>upper, ant.py:199-206) */
+  float dof_upper[64];
+  float initial_dof_pos[64];
+} mg_task_params;
+
+/* Task-layer buffers (VecTask.allocate_buffers, vec_task.py:302-325). */
+typedef struct mg_task_buffers {
+  const float* actions;     /* (N*A, nA) raw policy actions (clamped inside) */
+  float* actions_out;       /* (N*A, nA) clamped actions kept for obs (self.actions), may == NULL */
+  float* obs;               /* (N*A, nO) obs_buf (unclamped, like the reference) */
+  float* obs_clamped;       /* (N*A, nO) obs_dict['obs'] = clamp(obs_buf), may be NULL */
+  float* rew;               /* (N*A) */
+  int64_t* reset;           /* (N*A) */
+  int64_t* progress;        /* (N*A) */
+  uint8_t* timeout;         /* (N*A) torch.bool, like VecTask.timeout_buf after step */
+  float* potentials;        /* (N*A) */
+  float* prev_potentials;   /* (N*A) */
+  float* up_vec;            /* (N*A, 3) */
+  float* heading_vec;       /* (N*A, 3) */
+  const float* noise;       /* (N*A, 2*nD) injected U(0,1) reset noise, or NULL = device RNG */
+  uint64_t seed;            /* device RNG seed (counter-based, keyed by global env id) */
+  uint64_t step_counter;    /* VecTask.control_steps: RNG counter */
+  int64_t env_offset;       /* global id of this shard's first env (multi-GPU) */
+} mg_task_buffers;
+
+const char* mg_last_error(void);
+int mg_version(void);
+size_t mg_model_sizeof(void);
+size_t mg_task_params_sizeof(void);
+size_t mg_task_buffers_sizeof(void);
+size_t mg_sim_params_sizeof(void);
+
+typedef struct mg_sim mg_sim;
+
+int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
+                  mg_sim** out);
+int mg_sim_bind(mg_sim* sim, const mg_state_views* views);
+int mg_sim_simulate(mg_sim* sim, void* stream);
+int mg_sim_destroy(mg_sim* sim);
+
+/* Scatter rows of `src` (same layout as the bound buffer) into the bound
+ * buffer for the actor indices idx[0..n) (int32, global actor ids). */
+int mg_set_indexed(mg_sim* sim, int32_t which, const float* src, const int32_t* idx, int32_t n, void* stream);
+
+/* Reference jit functions, one thread per env. Inputs/outputs as in the
+ * reference signatures; `root_states` etc. may alias the sim buffers. */
+int mg_compute_observations(const mg_task_params* tp, int32_t n, const float* root_states, const float* dof_state,
+                            const float* dof_force, const float* sensors, const float* actions,
+                            float* potentials, float* prev_potentials, float* up_vec, float* heading_vec,
+                            float* obs, void* stream);
+int mg_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, const float* actions,
+                      const float* potentials, const float* prev_potentials, const int64_t* progress,
+                      int64_t* reset, float* rew, void* stream);
+
+/* Task-layer half of VecTask.step after the physics (post_physics_step +
+ * timeout + obs clamp).  With `sim`==NULL the state views in `views` are used
+ * as the post-physics state (physics-free replay, parity tests). */
+int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views,
+                    const mg_task_buffers* tb, int32_t n, void* stream);
+
+/* Whole VecTask.step: actions -> actuation -> simulate -> post_physics. */
+int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIGYM_H */

@@ -1,0 +1,339 @@
+// migym.hip — C-ABI (include/migym.h) and kernels of the MI355X physics-step +
+// observation/reward path.  One lane per actor/env; every kernel is
+// asynchronous on the caller's stream; no entry point synchronises.
+#include <hip/hip_runtime.h>
+
+#include <new>
+#include <string>
+
+#include "../../include/migym.h"
+#include "physics.hpp"
+#include "task.hpp"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MG_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+  return MG_OK;
+}
+constexpr int kBlock = 64;
+inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
+}  // namespace
+
+struct mg_sim {
+  mg_model host_model;
+  mg_model* d_model;
+  mg_sim_params params;
+  int32_t n;        // actors
+  int32_t device;
+  mg_state_views views;
+  bool bound;
+};
+
+// ------------------------------------------------------------------------------------------------ kernels
+template <int MN, int MC>
+__global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p, int n,
+                                                     float* __restrict__ root, float* __restrict__ dof,
+                                                     const float* __restrict__ act, float* __restrict__ sensors,
+                                                     float* __restrict__ dof_force) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int nd = m->num_dofs, ns = m->num_sensors;
+  float tau[MN];
+  for (int i = 0; i < nd; i++) tau[i] = act ? act[(size_t)nd * e + i] : 0.0f;
+  mg::simulate_actor<MN, MC>(m, &p, root + (size_t)13 * e, dof + (size_t)2 * nd * e, tau,
+                             sensors ? sensors + (size_t)6 * ns * e : nullptr,
+                             dof_force ? dof_force + (size_t)nd * e : nullptr);
+}
+
+__global__ __launch_bounds__(kBlock) void k_observations(mg_task_params tp, int n, const float* __restrict__ root,
+                                                         const float* __restrict__ dof, const float* __restrict__ dforce,
+                                                         const float* __restrict__ sensors,
+                                                         const float* __restrict__ actions, float* pot, float* prev_pot,
+                                                         float* up, float* heading, float* obs) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int nd = mg::t_dofs(&tp), ns = mg::t_sensors(&tp);
+  mg::obs_env(&tp, root + (size_t)13 * e, dof + (size_t)2 * nd * e, dforce ? dforce + (size_t)nd * e : nullptr,
+              sensors ? sensors + (size_t)6 * ns * e : nullptr, actions + (size_t)tp.num_actions * e, pot + e,
+              prev_pot + e, up + 3 * (size_t)e, heading + 3 * (size_t)e, obs + (size_t)tp.num_obs * e);
+}
+
+__global__ __launch_bounds__(kBlock) void k_reward(mg_task_params tp, int n, const float* __restrict__ obs,
+                                                   const float* __restrict__ actions, const float* __restrict__ pot,
+                                                   const float* __restrict__ prev_pot,
+                                                   const int64_t* __restrict__ progress, int64_t* reset, float* rew) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  mg::reward_env(&tp, obs + (size_t)tp.num_obs * e, actions + (size_t)tp.num_actions * e, pot[e], prev_pot[e],
+                 progress[e], reset + e, rew + e);
+}
+
+// post_physics_step + VecTask.step tail for env e (state already advanced)
+__device__ __forceinline__ void post_physics_env(const mg_task_params& tp, const mg_state_views& v,
+                                                 const mg_task_buffers& tb, int e, const float* act) {
+  const int nd = mg::t_dofs(&tp), ns = mg::t_sensors(&tp), no = tp.num_obs;
+  float* root = v.root_states + (size_t)13 * e;
+  float* dof = v.dof_state + (size_t)2 * nd * e;
+  int64_t progress = tb.progress[e] + 1;
+  int64_t reset = tb.reset[e];
+  float pot = tb.potentials ? tb.potentials[e] : 0.0f;
+  float prev = tb.prev_potentials ? tb.prev_potentials[e] : 0.0f;
+  if (reset != 0) {
+    mg::reset_env(&tp, tb.noise ? tb.noise + (size_t)2 * nd * e : nullptr, tb.seed,
+                  (uint64_t)(tb.env_offset + e), tb.step_counter, root, dof, &pot, &prev);
+    progress = 0;
+    reset = 0;
+  }
+  float* o = tb.obs + (size_t)no * e;
+  float up[3], hd[3];
+  mg::obs_env(&tp, root, dof, v.dof_force ? v.dof_force + (size_t)nd * e : nullptr,
+              v.sensors ? v.sensors + (size_t)6 * ns * e : nullptr, act, &pot, &prev, up, hd, o);
+  float rew;
+  mg::reward_env(&tp, o, act, pot, prev, progress, &reset, &rew);
+  const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
+  tb.rew[e] = rew;
+  tb.reset[e] = reset;
+  tb.progress[e] = progress;
+  tb.timeout[e] = (uint8_t)(((float)progress >= max_ep_m1) && (reset != 0));
+  if (tp.task_id != MG_TASK_CARTPOLE) {
+    tb.potentials[e] = pot;
+    tb.prev_potentials[e] = prev;
+    for (int k = 0; k < 3; k++) {
+      tb.up_vec[3 * (size_t)e + k] = up[k];
+      tb.heading_vec[3 * (size_t)e + k] = hd[k];
+    }
+  }
+  if (tb.obs_clamped)
+    for (int i = 0; i < no; i++) tb.obs_clamped[(size_t)no * e + i] = mg::clampf(o[i], tp.clip_obs);
+}
+
+__global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                         int n) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int na = tp.num_actions;
+  float act[64];
+  for (int i = 0; i < na; i++) {
+    act[i] = mg::clampf(tb.actions[(size_t)na * e + i], tp.clip_actions);
+    if (tb.actions_out) tb.actions_out[(size_t)na * e + i] = act[i];
+  }
+  post_physics_env(tp, v, tb, e, act);
+}
+
+// The whole VecTask.step for one env, fused: clamp -> actuation -> simulate -> post_physics.
+template <int MN, int MC>
+__global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
+                                                     mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
+  float act[MN];
+  for (int i = 0; i < na; i++) {
+    act[i] = mg::clampf(tb.actions[(size_t)na * e + i], tp.clip_actions);
+    if (tb.actions_out) tb.actions_out[(size_t)na * e + i] = act[i];
+  }
+  float tau[MN];
+  for (int i = 0; i < nd; i++) {
+    float t;
+    if (tp.task_id == MG_TASK_CARTPOLE) t = i == 0 ? act[0] * tp.power_scale : 0.0f;  // cartpole.py:159-163
+    else t = act[i] * tp.motor_effort[i] * tp.power_scale;                           // ant.py:283-285
+    tau[i] = t;
+    if (v.dof_actuation) const_cast<float*>(v.dof_actuation)[(size_t)nd * e + i] = t;
+  }
+  mg::simulate_actor<MN, MC>(m, &p, v.root_states + (size_t)13 * e, v.dof_state + (size_t)2 * nd * e, tau,
+                             v.sensors ? v.sensors + (size_t)6 * ns * e : nullptr,
+                             v.dof_force ? v.dof_force + (size_t)nd * e : nullptr);
+  post_physics_env(tp, v, tb, e, act);
+}
+
+__global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
+                              int nidx, int row) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nidx * row) return;
+  const int r = t / row, c = t % row;
+  const size_t a = (size_t)idx[r] * row + c;
+  dst[a] = src[a];
+}
+
+// ------------------------------------------------------------------------------------------------ dispatch
+// Kernel instances by capacity: nodes MN, contacts MC (chosen as the smallest that fits the model).
+#define MG_INSTANCES(X) X(4, 8) X(9, 16) X(16, 24) X(24, 32) X(40, 48)
+
+template <template <int, int> class F, typename... A>
+static int dispatch(const mg_model& m, int max_contacts, A... args) {
+#define MG_TRY(MN, MC)                                          \
+  if (m.num_nodes <= MN && max_contacts <= MC) {                \
+    F<MN, MC>::run(args...);                                    \
+    return MG_OK;                                               \
+  }
+  MG_INSTANCES(MG_TRY)
+#undef MG_TRY
+  return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
+}
+
+template <int MN, int MC>
+struct RunSimulate {
+  static void run(hipStream_t s, const mg_sim* sim) {
+    const mg_state_views& v = sim->views;
+    hipLaunchKernelGGL((k_simulate<MN, MC>), dim3(grid_for(sim->n)), dim3(kBlock), 0, s, sim->d_model, sim->params,
+                       sim->n, v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force);
+  }
+};
+template <int MN, int MC>
+struct RunEnvStep {
+  static void run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
+    hipLaunchKernelGGL((k_env_step<MN, MC>), dim3(grid_for(sim->n)), dim3(kBlock), 0, s, sim->d_model, sim->params,
+                       *tp, sim->views, *tb, sim->n);
+  }
+};
+
+// ------------------------------------------------------------------------------------------------ C ABI
+extern "C" {
+
+const char* mg_last_error(void) { return g_err.c_str(); }
+int mg_version(void) { return MG_VERSION; }
+size_t mg_model_sizeof(void) { return sizeof(mg_model); }
+size_t mg_task_params_sizeof(void) { return sizeof(mg_task_params); }
+size_t mg_task_buffers_sizeof(void) { return sizeof(mg_task_buffers); }
+size_t mg_sim_params_sizeof(void) { return sizeof(mg_sim_params); }
+
+int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
+                  mg_sim** out) {
+  if (!model || !params || !out || num_envs <= 0) return fail(MG_EINVAL, "mg_sim_create: bad arguments");
+  if (model->num_nodes < 1 || model->num_nodes > MG_MAX_NODES || model->num_geoms > MG_MAX_GEOMS ||
+      model->num_pairs > MG_MAX_PAIRS || model->num_sensors > MG_MAX_SENSORS || model->num_bodies > MG_MAX_BODIES)
+    return fail(MG_EINVAL, "mg_sim_create: model tables out of range");
+  for (int i = 1; i < model->num_nodes; i++)
+    if (model->parent[i] < 0 || model->parent[i] >= i)
+      return fail(MG_EINVAL, "mg_sim_create: nodes must be topologically ordered (parent < child)");
+  if (params->substeps < 1 || params->dt <= 0.0f || params->max_contacts < 0)
+    return fail(MG_EINVAL, "mg_sim_create: bad sim params");
+  if (hipSetDevice(device) != hipSuccess) return fail(MG_EDEVICE, "mg_sim_create: hipSetDevice failed");
+  mg_sim* s = new (std::nothrow) mg_sim();
+  if (!s) return fail(MG_ENOMEM, "mg_sim_create: out of host memory");
+  s->host_model = *model;
+  s->params = *params;
+  s->n = num_envs;
+  s->device = device;
+  s->bound = false;
+  if (hipMalloc(&s->d_model, sizeof(mg_model)) != hipSuccess) {
+    delete s;
+    return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(model) failed");
+  }
+  if (hipMemcpy(s->d_model, model, sizeof(mg_model), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(s->d_model);
+    delete s;
+    return fail(MG_EDEVICE, "mg_sim_create: model upload failed");
+  }
+  *out = s;
+  return MG_OK;
+}
+
+int mg_sim_bind(mg_sim* sim, const mg_state_views* views) {
+  if (!sim || !views || !views->root_states || !views->dof_state) return fail(MG_EINVAL, "mg_sim_bind: bad views");
+  if (sim->host_model.num_sensors > 0 && !views->sensors)
+    return fail(MG_EINVAL, "mg_sim_bind: model has force sensors but no sensor buffer");
+  sim->views = *views;
+  sim->bound = true;
+  return MG_OK;
+}
+
+int mg_sim_simulate(mg_sim* sim, void* stream) {
+  if (!sim || !sim->bound) return fail(MG_EINVAL, "mg_sim_simulate: sim not bound");
+  int rc = dispatch<RunSimulate>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
+                                 (const mg_sim*)sim);
+  if (rc) return rc;
+  return check_launch("mg_sim_simulate");
+}
+
+int mg_sim_destroy(mg_sim* sim) {
+  if (!sim) return MG_OK;
+  (void)hipFree(sim->d_model);
+  delete sim;
+  return MG_OK;
+}
+
+int mg_set_indexed(mg_sim* sim, int32_t which, const float* src, const int32_t* idx, int32_t n, void* stream) {
+  if (!sim || !sim->bound || !src || (n > 0 && !idx)) return fail(MG_EINVAL, "mg_set_indexed: bad arguments");
+  if (n == 0) return MG_OK;
+  float* dst;
+  int row;
+  if (which == MG_SET_ROOT_STATE) {
+    dst = sim->views.root_states;
+    row = 13;
+  } else if (which == MG_SET_DOF_STATE) {
+    dst = sim->views.dof_state;
+    row = 2 * sim->host_model.num_dofs;
+  } else {
+    return fail(MG_EINVAL, "mg_set_indexed: unknown target");
+  }
+  if (dst == src) return MG_OK;  // caller wrote into the bound buffer itself (gym views alias sim memory)
+  const int total = n * row;
+  hipLaunchKernelGGL(k_set_indexed, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, dst, src, idx, n,
+                     row);
+  return check_launch("mg_set_indexed");
+}
+
+int mg_compute_observations(const mg_task_params* tp, int32_t n, const float* root_states, const float* dof_state,
+                            const float* dof_force, const float* sensors, const float* actions, float* potentials,
+                            float* prev_potentials, float* up_vec, float* heading_vec, float* obs, void* stream) {
+  if (!tp || n < 0 || !dof_state || !obs || !actions) return fail(MG_EINVAL, "mg_compute_observations: bad args");
+  if (tp->task_id != MG_TASK_CARTPOLE && (!root_states || !potentials || !prev_potentials || !up_vec || !heading_vec))
+    return fail(MG_EINVAL, "mg_compute_observations: locomotion task needs root/potential buffers");
+  if (n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_observations, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, n, root_states,
+                     dof_state, dof_force, sensors, actions, potentials, prev_potentials, up_vec, heading_vec, obs);
+  return check_launch("mg_compute_observations");
+}
+
+int mg_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, const float* actions,
+                      const float* potentials, const float* prev_potentials, const int64_t* progress, int64_t* reset,
+                      float* rew, void* stream) {
+  if (!tp || n < 0 || !obs || !actions || !progress || !reset || !rew) return fail(MG_EINVAL, "mg_compute_reward");
+  if (tp->task_id != MG_TASK_CARTPOLE && (!potentials || !prev_potentials))
+    return fail(MG_EINVAL, "mg_compute_reward: locomotion task needs potentials");
+  if (n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_reward, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, n, obs, actions,
+                     potentials, prev_potentials, progress, reset, rew);
+  return check_launch("mg_compute_reward");
+}
+
+int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views, const mg_task_buffers* tb,
+                    int32_t n, void* stream) {
+  if (!tp || !tb) return fail(MG_EINVAL, "mg_post_physics: bad args");
+  mg_state_views v;
+  if (sim) {
+    if (!sim->bound) return fail(MG_EINVAL, "mg_post_physics: sim not bound");
+    v = sim->views;
+    n = sim->n;
+  } else {
+    if (!views) return fail(MG_EINVAL, "mg_post_physics: need views without a sim");
+    v = *views;
+  }
+  if (n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_post_physics, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n);
+  return check_launch("mg_post_physics");
+}
+
+int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {
+  if (!sim || !sim->bound || !tp || !tb || !tb->actions || !tb->obs || !tb->rew || !tb->reset || !tb->progress ||
+      !tb->timeout)
+    return fail(MG_EINVAL, "mg_env_step: bad arguments");
+  if (tp->task_id != MG_TASK_CARTPOLE && (!tb->potentials || !tb->prev_potentials || !tb->up_vec || !tb->heading_vec))
+    return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
+  if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
+    return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
+  int rc = dispatch<RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream, (const mg_sim*)sim,
+                                tp, tb);
+  if (rc) return rc;
+  return check_launch("mg_env_step");
+}
+
+}  // extern "C"

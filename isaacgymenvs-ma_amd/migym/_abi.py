@@ -1,0 +1,135 @@
+"""ctypes mirror of ``include/migym.h`` and the loader for ``libmigym.so``.
+
+The product path calls ONLY the HIP library built from ``csrc/`` (see
+``build.py``).  If the library is missing, :func:`lib` raises: there is no CPU
+fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import model as _model
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "_lib", "libmigym.so")
+
+MG_TASK_CARTPOLE, MG_TASK_ANT, MG_TASK_HUMANOID = 0, 1, 2
+MG_SET_ROOT_STATE, MG_SET_DOF_STATE = 0, 1
+
+
+class SimParams(C.Structure):
+    _fields_ = [("dt", C.c_float), ("substeps", C.c_int32), ("gravity", C.c_float * 3),
+                ("pos_iters", C.c_int32), ("contact_offset", C.c_float), ("rest_offset", C.c_float),
+                ("max_depen_vel", C.c_float), ("friction", C.c_float), ("baumgarte", C.c_float),
+                ("limit_margin", C.c_float), ("max_contacts", C.c_int32), ("agents", C.c_int32)]
+
+
+class StateViews(C.Structure):
+    _fields_ = [("root_states", C.c_void_p), ("dof_state", C.c_void_p), ("dof_actuation", C.c_void_p),
+                ("sensors", C.c_void_p), ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p)]
+
+
+class TaskParams(C.Structure):
+    _fields_ = [("task_id", C.c_int32), ("num_obs", C.c_int32), ("num_actions", C.c_int32),
+                ("max_episode_length", C.c_int32), ("dt", C.c_float), ("clip_actions", C.c_float),
+                ("clip_obs", C.c_float), ("power_scale", C.c_float), ("dof_vel_scale", C.c_float),
+                ("angular_velocity_scale", C.c_float), ("contact_force_scale", C.c_float),
+                ("heading_weight", C.c_float), ("up_weight", C.c_float), ("actions_cost_scale", C.c_float),
+                ("energy_cost_scale", C.c_float), ("joints_at_limit_cost_scale", C.c_float),
+                ("death_cost", C.c_float), ("termination_height", C.c_float), ("max_motor_effort", C.c_float),
+                ("reset_dist", C.c_float), ("target", C.c_float * 3), ("start_pos", C.c_float * 3),
+                ("start_rot", C.c_float * 4), ("motor_effort", C.c_float * 64), ("dof_lower", C.c_float * 64),
+                ("dof_upper", C.c_float * 64), ("initial_dof_pos", C.c_float * 64)]
+
+
+class TaskBuffers(C.Structure):
+    _fields_ = [("actions", C.c_void_p), ("actions_out", C.c_void_p), ("obs", C.c_void_p),
+                ("obs_clamped", C.c_void_p), ("rew", C.c_void_p), ("reset", C.c_void_p),
+                ("progress", C.c_void_p), ("timeout", C.c_void_p), ("potentials", C.c_void_p),
+                ("prev_potentials", C.c_void_p), ("up_vec", C.c_void_p), ("heading_vec", C.c_void_p),
+                ("noise", C.c_void_p), ("seed", C.c_uint64), ("step_counter", C.c_uint64),
+                ("env_offset", C.c_int64)]
+
+
+def model_bytes(spec) -> np.ndarray:
+    """mg_model POD for a ModelSpec (numpy structured scalar; pass .ctypes.data)."""
+    return np.ascontiguousarray(_model.pack_model(spec))
+
+
+def ptr(t):
+    """data_ptr of a torch tensor / numpy array, or None."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+# ---------------------------------------------------------------------------------------------
+EXPORTS = {
+    "mg_last_error": (C.c_char_p, []),
+    "mg_version": (C.c_int, []),
+    "mg_model_sizeof": (C.c_size_t, []),
+    "mg_task_params_sizeof": (C.c_size_t, []),
+    "mg_task_buffers_sizeof": (C.c_size_t, []),
+    "mg_sim_params_sizeof": (C.c_size_t, []),
+    "mg_sim_create": (C.c_int, [C.c_void_p, C.POINTER(SimParams), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "mg_sim_bind": (C.c_int, [C.c_void_p, C.POINTER(StateViews)]),
+    "mg_sim_simulate": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mg_sim_destroy": (C.c_int, [C.c_void_p]),
+    "mg_set_indexed": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]),
+    "mg_compute_observations": (C.c_int, [C.POINTER(TaskParams), C.c_int32] + [C.c_void_p] * 10 + [C.c_void_p]),
+    "mg_compute_reward": (C.c_int, [C.POINTER(TaskParams), C.c_int32] + [C.c_void_p] * 7 + [C.c_void_p]),
+    "mg_post_physics": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(StateViews),
+                                  C.POINTER(TaskBuffers), C.c_int32, C.c_void_p]),
+    "mg_env_step": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p]),
+}
+
+_LIB = None
+
+
+class MigymError(RuntimeError):
+    pass
+
+
+def _bind(lib):
+    for name, (res, args) in EXPORTS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def check_layout(lib):
+    sizes = {"mg_model_sizeof": _model.MODEL_DTYPE.itemsize, "mg_task_params_sizeof": C.sizeof(TaskParams),
+             "mg_task_buffers_sizeof": C.sizeof(TaskBuffers), "mg_sim_params_sizeof": C.sizeof(SimParams)}
+    for fn, py in sizes.items():
+        c = getattr(lib, fn)()
+        if c != py:
+            raise MigymError(f"ABI layout mismatch: {fn}() = {c}, Python mirror = {py}")
+
+
+def lib(path: str | None = None):
+    """Load the HIP library (raises if it was not built)."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or os.environ.get("MIGYM_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise MigymError(f"libmigym.so not found at {p}: run `python __graft_entry__.py build` "
+                         "(the product path has no CPU fallback)")
+    handle = _bind(C.CDLL(p))
+    check_layout(handle)
+    if path is None:
+        _LIB = handle
+    return handle
+
+
+def check(rc, l=None):
+    if rc != 0:
+        l = l or lib()
+        msg = l.mg_last_error()
+        raise MigymError(f"migym call failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,752 @@
+"""Robot-model loader: MJCF / URDF  ->  flat articulation tables.
+
+Counterpart of the closed ``gym.load_asset`` importer the reference calls in
+``tasks/ant.py:154``, ``tasks/humanoid.py:158`` and ``tasks/cartpole.py:89``.
+The importer semantics are the build's own (physics parity
+unpinned) and follow MuJoCo's MJCF conventions:
+
+* bodies are visited depth first in file order; that order is the gym rigid-body
+  order and the order of their joints is the DOF order (what the reference's
+  ``dof_limits_lower``/``find_asset_rigid_body_index`` index into);
+* every 1-DOF joint becomes one *node* of the dynamics tree.  A body with k
+  joints becomes a chain of k nodes; the first k-1 are massless and all k share
+  the body's orientation after their own rotation (MuJoCo ``mj_kinematics``
+  anchor rule).  A body with no joint is welded into its parent's node
+  (masses, geoms and the body frame are composed in);
+* node frames sit at the joint anchor; the joint axis is constant in the node
+  frame.  A node stores its anchor ``t`` and rest rotation ``r0`` relative to
+  its parent node;
+* ``inertiafromgeom``: geom volume x density (MJCF default 1000), capsule =
+  cylinder + two hemispheres; URDF links without ``<inertia>`` get the
+  inertia of their collision box at the given mass (cartpole.urdf has none).
+
+The result is a :class:`ModelSpec`; :func:`pack_model` turns it into the
+``mg_model`` POD struct declared in ``include/migym.h`` that both the HIP kernels
+and the C oracle consume.  Model tables for the shipped tasks are generated in
+the build container by ``tools/build_models.py`` into ``migym/assets/*.json``
+so the GPU box never needs the reference checkout.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass, field, asdict
+from typing import Dict, List, Optional
+
+import numpy as np
+
+# ---------------------------------------------------------------------------------------------
+# constants shared with include/migym.h (checked at load time against mg_model_sizeof())
+MAX_NODES = 40
+MAX_BODIES = 40
+MAX_GEOMS = 48
+MAX_PAIRS = 192
+MAX_SENSORS = 8
+
+JT_FREE, JT_FIXED, JT_HINGE, JT_SLIDE = 0, 1, 2, 3
+GT_PLANE, GT_SPHERE, GT_CAPSULE, GT_BOX, GT_CYLINDER = 0, 1, 2, 3, 4
+_GEOM_TYPES = {"plane": GT_PLANE, "sphere": GT_SPHERE, "capsule": GT_CAPSULE, "box": GT_BOX,
+               "cylinder": GT_CYLINDER}
+
+
+# ---------------------------------------------------------------------------------------------
+# small rigid-transform helpers (quaternions are xyzw, like the gym root state)
+def qmul(a, b):
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw,
+                     aw * bw - ax * bx - ay * by - az * bz])
+
+
+def qrot(q, v):
+    x, y, z, w = q
+    u = np.array([x, y, z])
+    v = np.asarray(v, dtype=np.float64)
+    t = 2.0 * np.cross(u, v)
+    return v + w * t + np.cross(u, t)
+
+
+def qmat(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def qnorm(q):
+    q = np.asarray(q, dtype=np.float64)
+    return q / np.linalg.norm(q)
+
+
+def quat_from_wxyz(w, x, y, z):
+    return qnorm([x, y, z, w])
+
+
+def quat_from_axis_angle(axis, ang):
+    axis = np.asarray(axis, dtype=np.float64)
+    axis = axis / np.linalg.norm(axis)
+    s = math.sin(ang / 2)
+    return np.array([axis[0] * s, axis[1] * s, axis[2] * s, math.cos(ang / 2)])
+
+
+def quat_from_euler(e, seq="xyz"):
+    """MJCF default eulerseq 'xyz' = rotations about the moving x, then y, then z axes."""
+    q = np.array([0, 0, 0, 1.0])
+    for ang, ax in zip(e, seq):
+        axis = {"x": [1, 0, 0], "y": [0, 1, 0], "z": [0, 0, 1]}[ax.lower()]
+        q = qmul(q, quat_from_axis_angle(axis, ang))
+    return q
+
+
+def quat_from_rpy(r, p, y):
+    """URDF rpy = fixed-axis X-Y-Z, i.e. R = Rz(y) Ry(p) Rx(r)."""
+    return qmul(quat_from_axis_angle([0, 0, 1], y),
+                qmul(quat_from_axis_angle([0, 1, 0], p), quat_from_axis_angle([1, 0, 0], r)))
+
+
+def quat_from_zaxis(z):
+    """Minimal rotation taking +z onto ``z`` (MuJoCo fromto/zaxis convention)."""
+    z = np.asarray(z, dtype=np.float64)
+    z = z / np.linalg.norm(z)
+    c = z[2]
+    if c > 1 - 1e-12:
+        return np.array([0, 0, 0, 1.0])
+    if c < -1 + 1e-12:
+        return np.array([1.0, 0, 0, 0])
+    axis = np.cross([0, 0, 1.0], z)
+    return quat_from_axis_angle(axis, math.acos(max(-1.0, min(1.0, c))))
+
+
+@dataclass
+class Xform:
+    pos: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    rot: np.ndarray = field(default_factory=lambda: np.array([0, 0, 0, 1.0]))
+
+    def compose(self, other: "Xform") -> "Xform":
+        return Xform(self.pos + qrot(self.rot, other.pos), qnorm(qmul(self.rot, other.rot)))
+
+    def apply(self, p):
+        return self.pos + qrot(self.rot, p)
+
+
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class Node:
+    name: str
+    parent: int
+    jtype: int
+    t: List[float]
+    r0: List[float]
+    axis: List[float]
+    body: int                      # gym body index whose joint this is (-1 root handled separately)
+    mass: float = 0.0
+    com: List[float] = field(default_factory=lambda: [0.0, 0.0, 0.0])
+    inertia: List[float] = field(default_factory=lambda: [0.0] * 6)   # about COM, node frame: xx yy zz xy xz yz
+    armature: float = 0.0
+    damping: float = 0.0
+    stiffness: float = 0.0
+    lower: float = 0.0
+    upper: float = 0.0
+    limited: int = 0
+
+
+@dataclass
+class Body:
+    name: str
+    node: int
+    pos: List[float]               # body origin in node frame
+    quat: List[float]              # body orientation in node frame
+    parent_body: int
+    mass: float = 0.0
+    com: List[float] = field(default_factory=lambda: [0.0, 0.0, 0.0])   # body COM in body frame
+
+
+@dataclass
+class Geom:
+    name: str
+    gtype: int
+    node: int
+    body: int
+    size: List[float]              # sphere r | capsule r,half | box half-extents | cylinder r,half
+    pos: List[float]               # center in node frame
+    quat: List[float]              # orientation in node frame (capsule/cylinder axis = local z)
+    contype: int = 1
+    conaffinity: int = 1
+
+
+@dataclass
+class ModelSpec:
+    name: str
+    fixed_base: int
+    nodes: List[Node]
+    bodies: List[Body]
+    geoms: List[Geom]
+    pairs: List[List[int]]         # self-collision geom pairs (i, j)
+    actuators: List[Dict]          # MJCF actuator order: {joint, gear, kind, kp, forcerange}
+    dof_names: List[str]
+    sensors: List[int] = field(default_factory=list)
+    self_collision: int = 0
+
+    @property
+    def num_dofs(self):
+        return len(self.nodes) - 1
+
+    def dof_index(self, joint_name):
+        return self.dof_names.index(joint_name)
+
+    def body_index(self, name):
+        return [b.name for b in self.bodies].index(name)
+
+    # -------------------------------------------------------------------------------------
+    def to_json(self, path):
+        d = asdict(self)
+        with open(path, "w") as f:
+            json.dump(d, f, indent=1)
+
+    @staticmethod
+    def from_json(path) -> "ModelSpec":
+        with open(path) as f:
+            d = json.load(f)
+        d["nodes"] = [Node(**n) for n in d["nodes"]]
+        d["bodies"] = [Body(**b) for b in d["bodies"]]
+        d["geoms"] = [Geom(**g) for g in d["geoms"]]
+        return ModelSpec(**d)
+
+    def total_mass(self):
+        return sum(n.mass for n in self.nodes)
+
+
+# ---------------------------------------------------------------------------------------------
+# mass properties of primitive geoms (inertia about the geom center, geom frame)
+def geom_mass_inertia(gtype, size, density):
+    if gtype == GT_SPHERE:
+        r = size[0]
+        m = density * 4.0 / 3.0 * math.pi * r ** 3
+        i = 0.4 * m * r * r
+        return m, np.diag([i, i, i])
+    if gtype == GT_CAPSULE:
+        r, hl = size[0], size[1]
+        h = 2 * hl
+        mc = density * math.pi * r * r * h
+        ms = density * 4.0 / 3.0 * math.pi * r ** 3
+        ixx = mc * (3 * r * r + h * h) / 12.0 + ms * (0.4 * r * r + 0.375 * r * h + 0.25 * h * h)
+        izz = mc * r * r / 2.0 + ms * 0.4 * r * r
+        return mc + ms, np.diag([ixx, ixx, izz])
+    if gtype == GT_BOX:
+        x, y, z = size
+        m = density * 8 * x * y * z
+        return m, np.diag([m * (y * y + z * z) / 3, m * (x * x + z * z) / 3, m * (x * x + y * y) / 3])
+    if gtype == GT_CYLINDER:
+        r, hl = size[0], size[1]
+        h = 2 * hl
+        m = density * math.pi * r * r * h
+        return m, np.diag([m * (3 * r * r + h * h) / 12, m * (3 * r * r + h * h) / 12, m * r * r / 2])
+    return 0.0, np.zeros((3, 3))
+
+
+class _MassAccum:
+    """Accumulates point masses with inertia in a common frame (parallel-axis)."""
+
+    def __init__(self):
+        self.m = 0.0
+        self.mc = np.zeros(3)
+        self.I0 = np.zeros((3, 3))   # inertia about the frame origin
+
+    def add(self, m, c, Ic_frame):
+        c = np.asarray(c, dtype=np.float64)
+        self.m += m
+        self.mc += m * c
+        self.I0 += Ic_frame + m * (np.dot(c, c) * np.eye(3) - np.outer(c, c))
+
+    def result(self):
+        if self.m <= 0:
+            return 0.0, np.zeros(3), np.zeros((3, 3))
+        c = self.mc / self.m
+        Ic = self.I0 - self.m * (np.dot(c, c) * np.eye(3) - np.outer(c, c))
+        return self.m, c, Ic
+
+
+def _inertia6(I):
+    return [float(I[0, 0]), float(I[1, 1]), float(I[2, 2]), float(I[0, 1]), float(I[0, 2]), float(I[1, 2])]
+
+
+# ---------------------------------------------------------------------------------------------
+def _floats(s, n=None):
+    v = [float(x) for x in s.split()]
+    return v if n is None else v[:n]
+
+
+class _Defaults:
+    def __init__(self):
+        self.classes: Dict[str, Dict[str, Dict[str, str]]] = {"main": {}}
+        self.parent: Dict[str, Optional[str]] = {"main": None}
+
+    def parse(self, elem, cls="main", parent=None):
+        if cls not in self.classes:
+            self.classes[cls] = {}
+        self.parent[cls] = parent
+        for child in elem:
+            if child.tag == "default":
+                self.parse(child, child.get("class", "main"), cls)
+            else:
+                self.classes[cls].setdefault(child.tag, {}).update(child.attrib)
+
+    def attrs(self, tag, cls):
+        chain = []
+        c = cls
+        while c is not None:
+            chain.append(c)
+            c = self.parent.get(c)
+        out = {}
+        for c in reversed(chain):
+            out.update(self.classes.get(c, {}).get(tag, {}))
+        return out
+
+
+def _geom_size_and_frame(a, angle_scale):
+    gtype = _GEOM_TYPES.get(a.get("type", "sphere"), None)
+    size = _floats(a.get("size", "0 0 0"))
+    if "fromto" in a:
+        ft = _floats(a["fromto"])
+        p0, p1 = np.array(ft[:3]), np.array(ft[3:])
+        center = 0.5 * (p0 + p1)
+        half = 0.5 * np.linalg.norm(p1 - p0)
+        rot = quat_from_zaxis(p1 - p0)
+        return gtype, [size[0], half, 0.0], Xform(center, rot)
+    pos = np.array(_floats(a.get("pos", "0 0 0")))
+    rot = _orientation(a, angle_scale)
+    sz = (size + [0, 0, 0])[:3]
+    return gtype, sz, Xform(pos, rot)
+
+
+def _orientation(a, angle_scale):
+    if "quat" in a:
+        w, x, y, z = _floats(a["quat"])
+        return quat_from_wxyz(w, x, y, z)
+    if "euler" in a:
+        return quat_from_euler([v * angle_scale for v in _floats(a["euler"])])
+    if "axisangle" in a:
+        v = _floats(a["axisangle"])
+        return quat_from_axis_angle(v[:3], v[3] * angle_scale)
+    if "zaxis" in a:
+        return quat_from_zaxis(_floats(a["zaxis"]))
+    return np.array([0, 0, 0, 1.0])
+
+
+def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True) -> ModelSpec:
+    """Parse an MJCF file (with <include>) into a :class:`ModelSpec`."""
+    root = _read_mjcf_tree(path)
+    compiler = root.find("compiler")
+    angle_scale = math.pi / 180.0
+    if compiler is not None and compiler.get("angle", "degree") == "radian":
+        angle_scale = 1.0
+    defaults = _Defaults()
+    for d in root.findall("default"):
+        defaults.parse(d)
+    world = root.find("worldbody")
+    bodies_xml = [b for b in world.findall("body")]
+    if len(bodies_xml) != 1:
+        raise ValueError("expected exactly one top-level body")
+    top = bodies_xml[0]
+
+    nodes: List[Node] = []
+    bodies: List[Body] = []
+    geoms: List[Geom] = []
+    dof_names: List[str] = []
+    mass_acc: Dict[int, _MassAccum] = {}
+    body_mass: Dict[int, _MassAccum] = {}
+
+    def joint_list(b, cls):
+        out = []
+        for j in b:
+            if j.tag == "freejoint":
+                out.append(("free", j.attrib, cls))
+            elif j.tag == "joint":
+                a = defaults.attrs("joint", j.get("class", cls))
+                a.update(j.attrib)
+                out.append((a.get("type", "hinge"), a, cls))
+        return out
+
+    def add_body_content(b, cls, node_idx, body_idx, T_node_body: Xform):
+        # geoms and mass, expressed in node frame
+        explicit = b.find("inertial")
+        acc = mass_acc.setdefault(node_idx, _MassAccum())
+        bacc = body_mass.setdefault(body_idx, _MassAccum())
+        for g in b.findall("geom"):
+            a = defaults.attrs("geom", g.get("class", cls))
+            a.update(g.attrib)
+            if a.get("type", "sphere") == "plane":
+                continue
+            gtype, size, Xg = _geom_size_and_frame(a, angle_scale)
+            if gtype is None:
+                continue   # meshes: not supported by this loader revision (ShadowHand forearm)
+            Xn = T_node_body.compose(Xg)
+            contype = int(a.get("contype", "1"))
+            conaff = int(a.get("conaffinity", "1"))
+            if explicit is None:
+                density = float(a.get("density", "1000"))
+                if "mass" in a:
+                    m0, _ = geom_mass_inertia(gtype, size, 1.0)
+                    density = float(a["mass"]) / m0 if m0 > 0 else 0.0
+                m, Ig = geom_mass_inertia(gtype, size, density)
+                R = qmat(Xn.rot)
+                acc.add(m, Xn.pos, R @ Ig @ R.T)
+                Rb = qmat(Xg.rot)
+                bacc.add(m, Xg.pos, Rb @ Ig @ Rb.T)
+            if contype == 0 and conaff == 0:
+                continue
+            geoms.append(Geom(name=a.get("name", f"g{len(geoms)}"), gtype=gtype, node=node_idx, body=body_idx,
+                              size=[float(s) for s in size], pos=[float(v) for v in Xn.pos],
+                              quat=[float(v) for v in Xn.rot], contype=contype, conaffinity=conaff))
+        if explicit is not None:
+            m = float(explicit.get("mass"))
+            ipos = np.array(_floats(explicit.get("pos", "0 0 0")))
+            irot = _orientation(explicit.attrib, angle_scale)
+            if "diaginertia" in explicit.attrib:
+                Id = np.diag(_floats(explicit.get("diaginertia")))
+            else:
+                f = _floats(explicit.get("fullinertia"))
+                Id = np.array([[f[0], f[3], f[4]], [f[3], f[1], f[5]], [f[4], f[5], f[2]]])
+            Xi = T_node_body.compose(Xform(ipos, irot))
+            R = qmat(Xi.rot)
+            acc.add(m, Xi.pos, R @ Id @ R.T)
+            Rb = qmat(irot)
+            bacc.add(m, ipos, Rb @ Id @ Rb.T)
+
+    def visit(b, cls, parent_node, T_parent: Xform, parent_body):
+        """T_parent: parent body frame expressed in parent_node frame."""
+        cls = b.get("childclass", cls)
+        body_idx = len(bodies)
+        bpos = np.array(_floats(b.get("pos", "0 0 0")))
+        brot = _orientation(b.attrib, angle_scale)
+        joints = joint_list(b, cls)
+        if parent_node < 0:
+            # root body: its frame is the actor frame (start pose supplied by the task)
+            jt = JT_FREE if (joints and joints[0][0] == "free") else JT_FIXED
+            nodes.append(Node(name=b.get("name", "root"), parent=-1, jtype=jt, t=[0, 0, 0], r0=[0, 0, 0, 1],
+                              axis=[0, 0, 1], body=body_idx))
+            node_idx = 0
+            T_body = Xform()
+        elif not joints:
+            node_idx = parent_node
+            T_body = T_parent.compose(Xform(bpos, brot))
+        else:
+            prev_anchor = None
+            node_idx = parent_node
+            for k, (jt, a, _) in enumerate(joints):
+                if jt not in ("hinge", "slide"):
+                    raise ValueError(f"joint type {jt} unsupported inside the tree")
+                p = np.array(_floats(a.get("pos", "0 0 0")))
+                axis = np.array(_floats(a.get("axis", "0 0 1")))
+                axis = axis / np.linalg.norm(axis)
+                if k == 0:
+                    Xa = T_parent.compose(Xform(bpos, brot))
+                    t = Xa.apply(p)
+                    r0 = Xa.rot
+                else:
+                    t = p - prev_anchor
+                    r0 = np.array([0, 0, 0, 1.0])
+                limited = a.get("limited", "false") == "true"
+                rng = _floats(a.get("range", "0 0"))
+                scale = angle_scale if jt == "hinge" else 1.0
+                lo, hi = rng[0] * scale, rng[1] * scale
+                nodes.append(Node(name=a.get("name", f"j{len(nodes)}"), parent=node_idx,
+                                  jtype=JT_HINGE if jt == "hinge" else JT_SLIDE,
+                                  t=[float(v) for v in t], r0=[float(v) for v in r0],
+                                  axis=[float(v) for v in axis], body=body_idx,
+                                  armature=float(a.get("armature", "0")), damping=float(a.get("damping", "0")),
+                                  stiffness=float(a.get("stiffness", "0")), lower=lo, upper=hi,
+                                  limited=int(limited)))
+                dof_names.append(nodes[-1].name)
+                node_idx = len(nodes) - 1
+                prev_anchor = p
+            T_body = Xform(-prev_anchor, np.array([0, 0, 0, 1.0]))
+        bodies.append(Body(name=b.get("name", f"b{body_idx}"), node=node_idx, pos=[float(v) for v in T_body.pos],
+                           quat=[float(v) for v in T_body.rot], parent_body=parent_body))
+        add_body_content(b, cls, node_idx, body_idx, T_body)
+        for c in b.findall("body"):
+            visit(c, cls, node_idx, T_body, body_idx)
+
+    visit(top, "main", -1, Xform(), -1)
+
+    for i, n in enumerate(nodes):
+        if i in mass_acc:
+            m, c, Ic = mass_acc[i].result()
+            n.mass, n.com, n.inertia = float(m), [float(v) for v in c], _inertia6(Ic)
+    for i, b in enumerate(bodies):
+        if i in body_mass:
+            m, c, _ = body_mass[i].result()
+            b.mass, b.com = float(m), [float(v) for v in c]
+
+    actuators = []
+    act = root.find("actuator")
+    if act is not None:
+        for a0 in act:
+            a = defaults.attrs(a0.tag, a0.get("class", "main"))
+            a.update(a0.attrib)
+            actuators.append(dict(kind=a0.tag, joint=a.get("joint"), gear=float(_floats(a.get("gear", "1"))[0]),
+                                  kp=float(a.get("kp", "0")),
+                                  forcerange=_floats(a.get("forcerange", "0 0"))))
+
+    spec = ModelSpec(name=name or os.path.splitext(os.path.basename(path))[0],
+                     fixed_base=int(nodes[0].jtype == JT_FIXED), nodes=nodes, bodies=bodies, geoms=geoms,
+                     pairs=[], actuators=actuators, dof_names=dof_names, self_collision=int(self_collision))
+    if self_collision:
+        spec.pairs = self_collision_pairs(spec)
+    return spec
+
+
+def _read_mjcf_tree(path):
+    tree = ET.parse(path)
+    root = tree.getroot()
+    base = os.path.dirname(path)
+
+    def expand(elem):
+        out = []
+        for child in list(elem):
+            if child.tag == "include":
+                inc = ET.parse(os.path.join(base, child.get("file"))).getroot()
+                out.extend(expand(inc))
+            else:
+                child[:] = expand(child)
+                out.append(child)
+        return out
+
+    root[:] = expand(root)
+    # merge repeated top-level sections (several <default>/<worldbody> after includes)
+    return root
+
+
+def self_collision_pairs(spec: ModelSpec):
+    """Geom pairs that may collide inside one articulation.
+
+    PhysX never collides two links joined by a joint; the build additionally
+    skips geoms of the same body.  (Humanoid: humanoid.py:194 filter 0.)"""
+    pairs = []
+    for i, gi in enumerate(spec.geoms):
+        for j in range(i + 1, len(spec.geoms)):
+            gj = spec.geoms[j]
+            bi, bj = gi.body, gj.body
+            if bi == bj:
+                continue
+            if spec.bodies[bi].parent_body == bj or spec.bodies[bj].parent_body == bi:
+                continue
+            if spec.bodies[bi].node == spec.bodies[bj].node:
+                continue
+            pairs.append([i, j])
+    return pairs
+
+
+# ---------------------------------------------------------------------------------------------
+def load_urdf(path, name=None, fix_base=True) -> ModelSpec:
+    """URDF loader (prismatic / revolute / continuous / fixed joints)."""
+    root = ET.parse(path).getroot()
+    links = {l.get("name"): l for l in root.findall("link")}
+    joints = root.findall("joint")
+    child_of = {j.find("child").get("link"): j for j in joints}
+    children: Dict[str, List] = {}
+    for j in joints:
+        children.setdefault(j.find("parent").get("link"), []).append(j)
+    root_link = [n for n in links if n not in child_of][0]
+
+    nodes: List[Node] = []
+    bodies: List[Body] = []
+    geoms: List[Geom] = []
+    dof_names: List[str] = []
+    accs: Dict[int, _MassAccum] = {}
+    baccs: Dict[int, _MassAccum] = {}
+
+    def origin(e):
+        o = e.find("origin") if e is not None else None
+        if o is None:
+            return Xform()
+        xyz = np.array(_floats(o.get("xyz", "0 0 0")))
+        rpy = _floats(o.get("rpy", "0 0 0"))
+        return Xform(xyz, quat_from_rpy(*rpy))
+
+    def link_content(link, node_idx, body_idx, T: Xform):
+        col_boxes = []
+        for c in link.findall("collision"):
+            Xc = origin(c)
+            geo = c.find("geometry")
+            box = geo.find("box")
+            sph = geo.find("sphere")
+            cyl = geo.find("cylinder")
+            if box is not None:
+                half = [0.5 * v for v in _floats(box.get("size"))]
+                g = (GT_BOX, half)
+                col_boxes.append((Xc, half))
+            elif sph is not None:
+                g = (GT_SPHERE, [float(sph.get("radius")), 0, 0])
+            elif cyl is not None:
+                g = (GT_CYLINDER, [float(cyl.get("radius")), 0.5 * float(cyl.get("length")), 0])
+            else:
+                continue
+            Xn = T.compose(Xc)
+            geoms.append(Geom(name=f"{link.get('name')}_col{len(geoms)}", gtype=g[0], node=node_idx, body=body_idx,
+                              size=[float(v) for v in g[1]], pos=[float(v) for v in Xn.pos],
+                              quat=[float(v) for v in Xn.rot]))
+        inert = link.find("inertial")
+        if inert is None:
+            return
+        Xi = origin(inert)
+        mass_e = inert.find("mass")
+        ie = inert.find("inertia")
+        dens = inert.find("density")
+        if mass_e is not None:
+            m = float(mass_e.get("value"))
+            if ie is not None:
+                f = {k: float(ie.get(k, "0")) for k in ("ixx", "iyy", "izz", "ixy", "ixz", "iyz")}
+                I = np.array([[f["ixx"], f["ixy"], f["ixz"]], [f["ixy"], f["iyy"], f["iyz"]],
+                              [f["ixz"], f["iyz"], f["izz"]]])
+            elif col_boxes:
+                _, half = col_boxes[0]
+                x, y, z = half
+                I = np.diag([m * (y * y + z * z) / 3, m * (x * x + z * z) / 3, m * (x * x + y * y) / 3])
+            else:
+                I = np.eye(3) * 1e-4 * m
+        elif dens is not None and col_boxes:
+            Xc, half = col_boxes[0]
+            m, I = geom_mass_inertia(GT_BOX, half, float(dens.get("value")))
+            Xi = Xc
+        else:
+            return
+        Xn = T.compose(Xi)
+        R = qmat(Xn.rot)
+        accs.setdefault(node_idx, _MassAccum()).add(m, Xn.pos, R @ I @ R.T)
+        Rb = qmat(Xi.rot)
+        baccs.setdefault(body_idx, _MassAccum()).add(m, Xi.pos, Rb @ I @ Rb.T)
+
+    def visit(link_name, parent_node, T_parent: Xform, parent_body):
+        body_idx = len(bodies)
+        link = links[link_name]
+        if parent_node < 0:
+            nodes.append(Node(name=link_name, parent=-1, jtype=JT_FIXED if fix_base else JT_FREE, t=[0, 0, 0],
+                              r0=[0, 0, 0, 1], axis=[0, 0, 1], body=body_idx))
+            node_idx, T = 0, Xform()
+        else:
+            j = child_of[link_name]
+            jt = j.get("type")
+            Xj = T_parent.compose(origin(j))
+            if jt == "fixed":
+                node_idx, T = parent_node, Xj
+            else:
+                ax = j.find("axis")
+                axis = np.array(_floats(ax.get("xyz"))) if ax is not None else np.array([1.0, 0, 0])
+                axis = axis / np.linalg.norm(axis)
+                lim = j.find("limit")
+                lo = float(lim.get("lower", "0")) if lim is not None else 0.0
+                hi = float(lim.get("upper", "0")) if lim is not None else 0.0
+                dyn = j.find("dynamics")
+                nodes.append(Node(name=j.get("name"), parent=parent_node,
+                                  jtype=JT_SLIDE if jt == "prismatic" else JT_HINGE,
+                                  t=[float(v) for v in Xj.pos], r0=[float(v) for v in Xj.rot],
+                                  axis=[float(v) for v in axis], body=body_idx,
+                                  damping=float(dyn.get("damping", "0")) if dyn is not None else 0.0,
+                                  lower=lo, upper=hi, limited=int(jt in ("prismatic", "revolute"))))
+                dof_names.append(j.get("name"))
+                node_idx, T = len(nodes) - 1, Xform()
+        bodies.append(Body(name=link_name, node=node_idx, pos=[float(v) for v in T.pos],
+                           quat=[float(v) for v in T.rot], parent_body=parent_body))
+        link_content(link, node_idx, body_idx, T)
+        for j in children.get(link_name, []):
+            visit(j.find("child").get("link"), node_idx, T, body_idx)
+
+    visit(root_link, -1, Xform(), -1)
+    for i, n in enumerate(nodes):
+        if i in accs:
+            m, c, Ic = accs[i].result()
+            n.mass, n.com, n.inertia = float(m), [float(v) for v in c], _inertia6(Ic)
+    for i, b in enumerate(bodies):
+        if i in baccs:
+            m, c, _ = baccs[i].result()
+            b.mass, b.com = float(m), [float(v) for v in c]
+    return ModelSpec(name=name or root.get("name"), fixed_base=int(fix_base), nodes=nodes, bodies=bodies,
+                     geoms=geoms, pairs=[], actuators=[], dof_names=dof_names)
+
+
+# ---------------------------------------------------------------------------------------------
+# packing into the mg_model POD struct (layout mirrors include/migym.h)
+def _model_dtype():
+    f4, i4 = np.float32, np.int32
+    N, B, G, P, S = MAX_NODES, MAX_BODIES, MAX_GEOMS, MAX_PAIRS, MAX_SENSORS
+    return np.dtype([
+        ("num_nodes", i4), ("num_dofs", i4), ("fixed_base", i4), ("num_bodies", i4),
+        ("num_geoms", i4), ("num_pairs", i4), ("num_sensors", i4), ("nv", i4),
+        ("parent", i4, N), ("jtype", i4, N), ("limited", i4, N), ("node_body", i4, N),
+        ("t", f4, (N, 3)), ("r0", f4, (N, 4)), ("axis", f4, (N, 3)),
+        ("mass", f4, N), ("com", f4, (N, 3)), ("inertia", f4, (N, 6)),
+        ("armature", f4, N), ("damping", f4, N), ("stiffness", f4, N), ("lower", f4, N), ("upper", f4, N),
+        ("body_node", i4, B), ("body_parent", i4, B),
+        ("body_pos", f4, (B, 3)), ("body_quat", f4, (B, 4)), ("body_com", f4, (B, 3)),
+        ("geom_type", i4, G), ("geom_node", i4, G), ("geom_body", i4, G), ("geom_pad", i4, G),
+        ("geom_size", f4, (G, 3)), ("geom_pos", f4, (G, 3)), ("geom_quat", f4, (G, 4)),
+        ("pair", i4, (P, 2)),
+        ("sensor_body", i4, S),
+    ])
+
+
+MODEL_DTYPE = _model_dtype()
+
+
+def pack_model(spec: ModelSpec) -> np.ndarray:
+    if len(spec.nodes) > MAX_NODES or len(spec.bodies) > MAX_BODIES or len(spec.geoms) > MAX_GEOMS:
+        raise ValueError("model exceeds mg_model capacity")
+    if len(spec.pairs) > MAX_PAIRS or len(spec.sensors) > MAX_SENSORS:
+        raise ValueError("model exceeds mg_model pair/sensor capacity")
+    m = np.zeros((), dtype=MODEL_DTYPE)
+    m["num_nodes"] = len(spec.nodes)
+    m["num_dofs"] = len(spec.nodes) - 1
+    m["fixed_base"] = spec.fixed_base
+    m["num_bodies"] = len(spec.bodies)
+    m["num_geoms"] = len(spec.geoms)
+    m["num_pairs"] = len(spec.pairs)
+    m["num_sensors"] = len(spec.sensors)
+    m["nv"] = (0 if spec.fixed_base else 6) + len(spec.nodes) - 1
+    m["parent"][:] = -1
+    for i, n in enumerate(spec.nodes):
+        m["parent"][i] = n.parent
+        m["jtype"][i] = n.jtype
+        m["limited"][i] = n.limited
+        m["node_body"][i] = n.body
+        m["t"][i] = n.t
+        m["r0"][i] = n.r0
+        m["axis"][i] = n.axis
+        m["mass"][i] = n.mass
+        m["com"][i] = n.com
+        m["inertia"][i] = n.inertia
+        m["armature"][i] = n.armature
+        m["damping"][i] = n.damping
+        m["stiffness"][i] = n.stiffness
+        m["lower"][i] = n.lower
+        m["upper"][i] = n.upper
+    for i, b in enumerate(spec.bodies):
+        m["body_node"][i] = b.node
+        m["body_parent"][i] = b.parent_body
+        m["body_pos"][i] = b.pos
+        m["body_quat"][i] = b.quat
+        m["body_com"][i] = b.com
+    for i, g in enumerate(spec.geoms):
+        m["geom_type"][i] = g.gtype
+        m["geom_node"][i] = g.node
+        m["geom_body"][i] = g.body
+        m["geom_size"][i] = g.size
+        m["geom_pos"][i] = g.pos
+        m["geom_quat"][i] = g.quat
+    for i, p in enumerate(spec.pairs):
+        m["pair"][i] = p
+    for i, s in enumerate(spec.sensors):
+        m["sensor_body"][i] = s
+    return m
+
+
+ASSET_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
+
+
+def load_builtin(name) -> ModelSpec:
+    """Load one of the shipped model tables (generated by tools/build_models.py)."""
+    return ModelSpec.from_json(os.path.join(ASSET_DIR, name + ".json"))

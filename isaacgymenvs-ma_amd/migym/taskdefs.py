@@ -1,0 +1,101 @@
+"""Per-task constants -> ``mg_task_params`` / ``mg_sim_params``.
+
+What the reference task constructors compute once at setup
+(tasks/ant.py:43-114 + 135-212, tasks/humanoid.py:43-117 + 138-217,
+tasks/cartpole.py:36-113) and then pass to their jit functions every step.
+"""
+from __future__ import annotations
+
+import math
+
+from . import _abi
+from . import model as M
+
+TASK_INFO = {
+    # name: (task_id, model table, num_obs, num_actions, start z, max_contacts)
+    "Cartpole": (_abi.MG_TASK_CARTPOLE, "cartpole", 4, 1, 2.0, 4),
+    "Ant": (_abi.MG_TASK_ANT, "ant", 60, 8, 0.44, 16),
+    "Humanoid": (_abi.MG_TASK_HUMANOID, "humanoid", 108, 21, 1.34, 32),
+}
+
+# build-defined solver constants
+BAUMGARTE = 0.2
+LIMIT_MARGIN = 0.1
+
+
+def sim_params(cfg: dict, max_contacts: int, agents: int = 1) -> _abi.SimParams:
+    s = cfg["sim"]
+    px = s.get("physx", {})
+    p = _abi.SimParams()
+    p.dt = float(s["dt"])
+    p.substeps = int(s.get("substeps", 2))
+    for i, g in enumerate(s.get("gravity", [0.0, 0.0, -9.81])):
+        p.gravity[i] = float(g)
+    p.pos_iters = int(px.get("num_position_iterations", 4))
+    p.contact_offset = float(px.get("contact_offset", 0.02))
+    p.rest_offset = float(px.get("rest_offset", 0.0))
+    p.max_depen_vel = float(px.get("max_depenetration_velocity", 10.0))
+    plane = cfg["env"].get("plane", {})
+    p.friction = float(plane.get("staticFriction", 1.0))
+    p.baumgarte = BAUMGARTE
+    p.limit_margin = LIMIT_MARGIN
+    p.max_contacts = int(max_contacts)
+    p.agents = int(agents)
+    return p
+
+
+def dof_limits(spec: M.ModelSpec):
+    """lower/upper as the reference reads them (swapped when lower > upper: ant.py:199-206)."""
+    lo, hi = [], []
+    for n in spec.nodes[1:]:
+        a, b = n.lower, n.upper
+        if a > b:
+            a, b = b, a
+        lo.append(a)
+        hi.append(b)
+    return lo, hi
+
+
+def task_params(task: str, cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
+    base = "Ant" if task == "MAAnt" else task
+    task_id, _, nobs, nact, z0, _ = TASK_INFO[base]
+    env = cfg["env"]
+    tp = _abi.TaskParams()
+    tp.task_id = task_id
+    tp.num_obs = nobs
+    tp.num_actions = nact
+    tp.dt = float(cfg["sim"]["dt"])
+    tp.clip_actions = float(env.get("clipActions", math.inf))
+    tp.clip_obs = float(env.get("clipObservations", math.inf))
+    tp.target[:] = (1000.0, 0.0, 0.0)
+    tp.start_pos[:] = (0.0, 0.0, z0)
+    tp.start_rot[:] = (0.0, 0.0, 0.0, 1.0)
+    if base == "Cartpole":
+        tp.max_episode_length = 500                       # cartpole.py:44 (hard-coded)
+        tp.power_scale = float(env["maxEffort"])
+        tp.reset_dist = float(env["resetDist"])
+        return tp
+    tp.max_episode_length = int(env["episodeLength"])
+    tp.power_scale = float(env["powerScale"])
+    tp.dof_vel_scale = float(env["dofVelocityScale"])
+    tp.angular_velocity_scale = float(env.get("angularVelocityScale", 0.1))
+    tp.contact_force_scale = float(env["contactForceScale"])
+    tp.heading_weight = float(env["headingWeight"])
+    tp.up_weight = float(env["upWeight"])
+    tp.actions_cost_scale = float(env["actionsCost"])
+    tp.energy_cost_scale = float(env["energyCost"])
+    tp.joints_at_limit_cost_scale = float(env["jointsAtLimitCost"])
+    tp.death_cost = float(env["deathCost"])
+    tp.termination_height = float(env["terminationHeight"])
+    # actuator gears in MJCF actuator order, applied by DOF position (ant.py:159-161, humanoid.py:160-161)
+    gears = [a["gear"] for a in spec.actuators]
+    for i, g in enumerate(gears):
+        tp.motor_effort[i] = float(g)
+    tp.max_motor_effort = float(max(gears)) if gears else 1.0
+    lo, hi = dof_limits(spec)
+    for i, (a, b) in enumerate(zip(lo, hi)):
+        tp.dof_lower[i] = a
+        tp.dof_upper[i] = b
+        # initial_dof_pos: 0 clamped into the limits (ant.py:96-99)
+        tp.initial_dof_pos[i] = a if a > 0 else (b if b < 0 else 0.0)
+    return tp

@@ -1,0 +1,276 @@
+"""VecTask on the MI355X path — same contract as the reference's
+``isaacgymenvs/tasks/base/vec_task.py`` (Env 67-206, VecTask 208-457).
+
+The reference drives PhysX through ``gym.simulate`` plus a dozen ATen kernels
+per step and synchronises with the host every step (``reset_buf.nonzero()``,
+ant.py:291-293).  Here one ``mg_env_step`` launch runs the whole
+``VecTask.step`` for every env (clamp -> pre_physics_step -> simulate ->
+post_physics_step -> timeout -> obs clamp), with no host synchronisation.
+
+Kept reference semantics:
+  * ``reset_buf`` starts at ones, so the first ``step`` resets every env;
+    ``reset()`` returns the current (unclamped-then-clamped) obs without computing
+    observations (vec_task.py:428-440).
+  * resets requested by a step's reward are applied at the start of the next
+    step's post-physics phase, before observations (ant.py:287-297).
+  * ``extras['time_outs']`` is a bool tensor (vec_task.py:396, 402).
+  * observations are clamped to ``clipObservations`` and moved to ``rl_device``.
+Differences (documented in DESIGN.md / INTEGRATION.md): reset noise comes from a
+counter-based device RNG keyed by (seed, global env id, control step) instead
+of the global torch generator; returned obs/rew/reset tensors are persistent
+buffers overwritten by the next step (rl_games copies them immediately).
+"""
+from __future__ import annotations
+
+import abc
+import math
+from typing import Any, Dict, Tuple
+
+import numpy as np
+import torch
+
+from ... import _abi
+from ... import model as M
+from ... import spaces
+from ... import taskdefs
+
+
+class Env(abc.ABC):
+    def __init__(self, config: Dict[str, Any], rl_device: str, sim_device: str, graphics_device_id: int,
+                 headless: bool):
+        split = sim_device.split(":")
+        self.device_type = split[0]
+        self.device_id = int(split[1]) if len(split) > 1 else 0
+        self.device = "cpu"
+        if config["sim"]["use_gpu_pipeline"]:
+            if self.device_type.lower() in ("cuda", "gpu"):
+                self.device = "cuda:" + str(self.device_id)
+            else:
+                config["sim"]["use_gpu_pipeline"] = False
+        self.rl_device = rl_device
+        self.headless = headless
+        self.graphics_device_id = graphics_device_id
+        env = config["env"]
+        self.num_environments = env["numEnvs"]
+        self.num_agents = env.get("numAgents", 1)
+        self.num_observations = env.get("numObservations", 0)
+        self.num_states = env.get("numStates", 0)
+        self.obs_space = spaces.Box(np.ones(self.num_obs) * -np.inf, np.ones(self.num_obs) * np.inf)
+        self.state_space = spaces.Box(np.ones(self.num_states) * -np.inf, np.ones(self.num_states) * np.inf)
+        self.num_actions = env["numActions"]
+        self.control_freq_inv = env.get("controlFrequencyInv", 1)
+        self.act_space = spaces.Box(np.ones(self.num_actions) * -1.0, np.ones(self.num_actions) * 1.0)
+        self.clip_obs = env.get("clipObservations", math.inf)
+        self.clip_actions = env.get("clipActions", math.inf)
+        self.total_train_env_frames = 0
+        self.control_steps = 0
+
+    @property
+    def observation_space(self):
+        return self.obs_space
+
+    @property
+    def action_space(self):
+        return self.act_space
+
+    @property
+    def num_envs(self) -> int:
+        return self.num_environments
+
+    @property
+    def num_acts(self) -> int:
+        return self.num_actions
+
+    @property
+    def num_obs(self) -> int:
+        return self.num_observations
+
+    def set_train_info(self, env_frames, *args, **kwargs):
+        self.total_train_env_frames = env_frames
+
+    def get_env_state(self):
+        return None
+
+    def set_env_state(self, env_state):
+        pass
+
+
+class VecTask(Env):
+    """Base class of the MI355X tasks.  Subclasses set ``task_name`` and fill
+    ``cfg['env']['numObservations'/'numActions']`` before calling ``__init__``."""
+
+    metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 24}
+    task_name = None
+
+    def __init__(self, config, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
+                 force_render=False):
+        self.cfg = config
+        super().__init__(config, rl_device, sim_device, graphics_device_id, headless)
+        if self.device == "cpu":
+            raise RuntimeError("migym simulates on the MI355X only: use pipeline='gpu' and sim_device='cuda:N' "
+                               "(the reference's CPU PhysX pipeline has no counterpart on this path)")
+        if not torch.cuda.is_available():
+            raise RuntimeError("migym needs a HIP device (torch.cuda.is_available() is False)")
+        self.virtual_screen_capture = virtual_screen_capture
+        self.force_render = force_render
+        self.dt = float(config["sim"]["dt"])
+        self.control_freq_inv = int(config["env"].get("controlFrequencyInv", 1))
+        self.viewer = None
+        self.seed = int(config.get("seed", 0) or 0)
+        self.env_offset = int(config.get("env_offset", 0))
+        self._lib = _abi.lib()
+        self.create_sim()
+        self.allocate_buffers()
+        self.obs_dict = {}
+        self.extras = {}
+
+    # ---------------------------------------------------------------------------------- setup
+    def create_sim(self):
+        base = "Ant" if self.task_name == "MAAnt" else self.task_name
+        _, table, _, _, _, max_contacts = taskdefs.TASK_INFO[base]
+        self.model_spec = M.load_builtin(table)
+        self.num_dof = self.model_spec.num_dofs
+        self.num_bodies = len(self.model_spec.bodies)
+        self.num_actors = self.num_envs * self.num_agents
+        self.sim_params = taskdefs.sim_params(self.cfg, max_contacts, self.num_agents)
+        self.task_params = taskdefs.task_params(self.task_name, self.cfg, self.model_spec)
+        self._model_np = _abi.model_bytes(self.model_spec)
+        torch.cuda.set_device(self.device_id)
+        h = _abi.C.c_void_p()
+        _abi.check(self._lib.mg_sim_create(self._model_np.ctypes.data, _abi.C.byref(self.sim_params),
+                                           self.num_actors, self.device_id, _abi.C.byref(h)), self._lib)
+        self.sim = h
+        dev, f = self.device, torch.float32
+        A, nd, ns = self.num_actors, self.num_dof, len(self.model_spec.sensors)
+        # gym-visible state tensors (acquire_*_tensor + wrap_tensor): zero-copy, owned by torch
+        self.root_states = torch.zeros((A, 13), device=dev, dtype=f)
+        self.root_states[:, 0:3] = torch.tensor(list(self.task_params.start_pos), device=dev)
+        self.root_states[:, 3:7] = torch.tensor(list(self.task_params.start_rot), device=dev)
+        self.initial_root_states = self.root_states.clone()
+        self.initial_root_states[:, 7:13] = 0
+        self.dof_state = torch.zeros((A * nd, 2), device=dev, dtype=f)
+        self.dof_pos = self.dof_state.view(A, nd, 2)[..., 0]
+        self.dof_vel = self.dof_state.view(A, nd, 2)[..., 1]
+        self.dof_actuation = torch.zeros((A * nd,), device=dev, dtype=f)
+        self.sensor_tensor = torch.zeros((A * max(ns, 1), 6), device=dev, dtype=f)
+        self.vec_sensor_tensor = self.sensor_tensor.view(A, max(ns, 1) * 6)
+        self.dof_force_tensor = torch.zeros((A, nd), device=dev, dtype=f)
+        lo, hi = taskdefs.dof_limits(self.model_spec)
+        self.dof_limits_lower = torch.tensor(lo, device=dev, dtype=f)
+        self.dof_limits_upper = torch.tensor(hi, device=dev, dtype=f)
+        self.initial_dof_pos = torch.tensor(list(self.task_params.initial_dof_pos)[:nd], device=dev,
+                                            dtype=f).repeat(A, 1)
+        v = _abi.StateViews()
+        v.root_states, v.dof_state = _abi.ptr(self.root_states), _abi.ptr(self.dof_state)
+        v.dof_actuation, v.sensors = _abi.ptr(self.dof_actuation), _abi.ptr(self.sensor_tensor)
+        v.dof_force, v.rigid_body_states = _abi.ptr(self.dof_force_tensor), None
+        self._views = v
+        _abi.check(self._lib.mg_sim_bind(self.sim, _abi.C.byref(v)), self._lib)
+
+    def allocate_buffers(self):
+        dev, A = self.device, self.num_actors
+        self.obs_buf = torch.zeros((A, self.num_obs), device=dev, dtype=torch.float)
+        self.states_buf = torch.zeros((self.num_envs, self.num_states), device=dev, dtype=torch.float)
+        self.rew_buf = torch.zeros(A, device=dev, dtype=torch.float)
+        self.reset_buf = torch.ones(A, device=dev, dtype=torch.long)
+        self.timeout_buf = torch.zeros(A, device=dev, dtype=torch.bool)
+        self.progress_buf = torch.zeros(A, device=dev, dtype=torch.long)
+        self.randomize_buf = torch.zeros(self.num_envs, device=dev, dtype=torch.long)
+        self.actions = torch.zeros((A, self.num_actions), device=dev, dtype=torch.float)
+        self._clamp_obs = math.isfinite(float(self.clip_obs))
+        self.obs_clamped = torch.zeros_like(self.obs_buf) if self._clamp_obs else self.obs_buf
+        pot = -1000.0 / self.dt
+        self.potentials = torch.full((A,), pot, device=dev, dtype=torch.float)
+        self.prev_potentials = self.potentials.clone()
+        self.up_vec = torch.zeros((A, 3), device=dev, dtype=torch.float)
+        self.up_vec[:, 2] = 1.0
+        self.heading_vec = torch.zeros((A, 3), device=dev, dtype=torch.float)
+        self.heading_vec[:, 0] = 1.0
+        self.targets = torch.tensor([[1000.0, 0.0, 0.0]], device=dev).repeat(A, 1)
+        self._noise = None
+        tb = _abi.TaskBuffers()
+        tb.actions_out, tb.obs = _abi.ptr(self.actions), _abi.ptr(self.obs_buf)
+        tb.obs_clamped = _abi.ptr(self.obs_clamped) if self._clamp_obs else None
+        tb.rew, tb.reset, tb.progress = _abi.ptr(self.rew_buf), _abi.ptr(self.reset_buf), _abi.ptr(self.progress_buf)
+        tb.timeout = _abi.ptr(self.timeout_buf)
+        tb.potentials, tb.prev_potentials = _abi.ptr(self.potentials), _abi.ptr(self.prev_potentials)
+        tb.up_vec, tb.heading_vec = _abi.ptr(self.up_vec), _abi.ptr(self.heading_vec)
+        tb.seed, tb.env_offset = self.seed, self.env_offset
+        self._tb = tb
+
+    # ---------------------------------------------------------------------------------- hot path
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def step(self, actions: torch.Tensor) -> Tuple[Dict[str, torch.Tensor], torch.Tensor, torch.Tensor,
+                                                   Dict[str, Any]]:
+        """VecTask.step (vec_task.py:362-410) as one fused device launch per control step."""
+        a = actions
+        if a.device != torch.device(self.device) or a.dtype != torch.float32 or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.float32).contiguous()
+        if a.shape != (self.num_actors, self.num_actions):
+            raise ValueError(f"actions must be {(self.num_actors, self.num_actions)}, got {tuple(a.shape)}")
+        self._actions_in = a   # keep alive until the launch has consumed it
+        tb = self._tb
+        tb.actions = a.data_ptr()
+        tb.noise = _abi.ptr(self._noise)
+        stream = self._stream()
+        for k in range(self.control_freq_inv):
+            tb.step_counter = self.control_steps
+            _abi.check(self._lib.mg_env_step(self.sim, _abi.C.byref(self.task_params), _abi.C.byref(tb), stream),
+                       self._lib)
+        self.control_steps += 1
+        self.extras["time_outs"] = self.timeout_buf.to(self.rl_device)
+        self.post_step_extras()
+        self.obs_dict["obs"] = self.obs_clamped.to(self.rl_device)
+        if self.num_states > 0:
+            self.obs_dict["states"] = self.get_state()
+        return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    def post_step_extras(self):
+        """Task-specific extras (e.g. Ant's true_objective); cheap device views only."""
+
+    # ---------------------------------------------------------------------------------- API
+    def get_state(self):
+        return torch.clamp(self.states_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+
+    def zero_actions(self) -> torch.Tensor:
+        return torch.zeros([self.num_actors, self.num_actions], dtype=torch.float32, device=self.rl_device)
+
+    def reset(self):
+        """Returns the current observations without computing them (vec_task.py:428-440)."""
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        if self.num_states > 0:
+            self.obs_dict["states"] = self.get_state()
+        return self.obs_dict
+
+    def reset_idx(self, env_ids):
+        """Marks ``env_ids`` for reset; the fused step applies it before its observations
+        (same point in the step as the reference's reset_idx, ant.py:291-293)."""
+        self.reset_buf[env_ids] = 1
+
+    def reset_done(self):
+        done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
+        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        if self.num_states > 0:
+            self.obs_dict["states"] = self.get_state()
+        return self.obs_dict, done_env_ids
+
+    def set_reset_noise(self, noise: torch.Tensor | None):
+        """Inject per-env U(0,1) reset noise rows (N*A, 2*nD) instead of the device RNG
+        (parity tests replay the reference's torch draws through this)."""
+        self._noise = None if noise is None else noise.to(self.device, torch.float32).contiguous()
+
+    def render(self, mode="rgb_array"):
+        return None
+
+    def close(self):
+        if getattr(self, "sim", None) is not None:
+            self._lib.mg_sim_destroy(self.sim)
+            self.sim = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

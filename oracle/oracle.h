@@ -1,0 +1,67 @@
+/*
+ * oracle.h — CPU restatement used ONLY as the parity checker and the CPU
+ * baseline (tests/, __graft_entry__.smoke(), bench.py cpu_baseline leg).
+ * Nothing in the product links or calls this library.
+ *
+ * PARITY STATUS
+ *   obs / reward / reset bookkeeping: PINNED.  The restatement follows the
+ *     reference's @torch.jit.script functions (tasks/ant.py:325-408,
+ *     tasks/humanoid.py:323-413, tasks/cartpole.py:119-196,
+ *     utils/torch_jit_utils.py:41-276) and VecTask.step ordering
+ *     (tasks/base/vec_task.py:362-410); tests/test_oracle_golden.py checks it
+ *     against tests/golden/jit_*.npz and trace_*.npz, produced by running the
+ *     reference code itself (tests/golden/make_golden.py, make_traces.py).
+ *   physics (gym.simulate): PARITY UNPINNED.  The reference physics is the
+ *     closed isaacgym/PhysX binary (not in the reference tree, not installable
+ *     offline).  This file restates the build's own documented algorithm
+ *     (DESIGN.md §Physics): composite-rigid-body mass matrix + Cholesky in
+ *     fp64 — deliberately NOT the O(n) articulated-body recursion the HIP
+ *     kernels use — with the same contact set, PGS row order and integrator,
+ *     and is pinned by analytic known-answer tests (free fall, energy,
+ *     pendulum, joint limits, resting contact) in tests/test_oracle_physics.py.
+ */
+#ifndef MIGYM_ORACLE_H
+#define MIGYM_ORACLE_H
+#include "../include/migym.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* counter-based uniform in [0,1): identical integer recipe on the GPU */
+float orc_uniform(uint64_t seed, uint64_t env, uint64_t counter, uint32_t k);
+
+/* gym.simulate on host buffers (gym layouts), fp64 internally, one actor per
+ * row; `threads` OpenMP threads (0 = library default). */
+int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* root_states, float* dof_state,
+                 const float* dof_actuation, float* sensors, float* dof_force, int32_t threads);
+
+/* Debug/KAT hooks for one actor: mass matrix (nv*nv row-major, includes the
+ * armature + implicit damping/stiffness diagonal for substep h) and the
+ * unconstrained generalized acceleration. */
+int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
+                    double* M_out);
+int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
+                          const float* tau, double* qacc_out);
+/* contacts detected for one actor at the given state: returns count; writes
+ * (node, px,py,pz, nx,ny,nz, depth, nodeB) records of 9 doubles */
+int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, double* out,
+                 int32_t cap);
+/* world poses of the gym rigid bodies (n_bodies x 13, velocity at body COM) */
+int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out);
+
+int orc_compute_observations(const mg_task_params* tp, int32_t n, const float* root_states, const float* dof_state,
+                             const float* dof_force, const float* sensors, const float* actions,
+                             float* potentials, float* prev_potentials, float* up_vec, float* heading_vec,
+                             float* obs);
+int orc_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, const float* actions,
+                       const float* potentials, const float* prev_potentials, const int64_t* progress,
+                       int64_t* reset, float* rew);
+int orc_post_physics(const mg_task_params* tp, const mg_state_views* v, const mg_task_buffers* tb, int32_t n);
+int orc_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp, const mg_state_views* v,
+                 const mg_task_buffers* tb, int32_t n, int32_t threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

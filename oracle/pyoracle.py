@@ -1,0 +1,162 @@
+"""ctypes binding of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg —
+never by the product package.  Parity status: see oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle.so")
+sys.path.insert(0, os.path.join(HERE, "..", "isaacgymenvs-ma_amd"))
+from migym import _abi  # noqa: E402  (struct mirrors only)
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        l = C.CDLL(LIB)
+        P = C.c_void_p
+        l.orc_uniform.restype = C.c_float
+        l.orc_uniform.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]
+        l.orc_simulate.argtypes = [P, C.POINTER(_abi.SimParams), C.c_int32, P, P, P, P, P, C.c_int32]
+        l.orc_mass_matrix.argtypes = [P, C.POINTER(_abi.SimParams), P, P, P]
+        l.orc_free_acceleration.argtypes = [P, C.POINTER(_abi.SimParams), P, P, P, P]
+        l.orc_contacts.argtypes = [P, C.POINTER(_abi.SimParams), P, P, P, C.c_int32]
+        l.orc_rigid_body_states.argtypes = [P, P, P, P]
+        l.orc_compute_observations.argtypes = [C.POINTER(_abi.TaskParams), C.c_int32] + [P] * 10
+        l.orc_compute_reward.argtypes = [C.POINTER(_abi.TaskParams), C.c_int32] + [P] * 7
+        l.orc_post_physics.argtypes = [C.POINTER(_abi.TaskParams), C.POINTER(_abi.StateViews),
+                                       C.POINTER(_abi.TaskBuffers), C.c_int32]
+        l.orc_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
+                                   C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32, C.c_int32]
+        _lib = l
+    return _lib
+
+
+def f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
+
+
+def p(a):
+    return None if a is None else a.ctypes.data
+
+
+def simulate(model_np, sp, root, dof, act=None, sensors=None, dof_force=None, threads=0):
+    n = root.shape[0]
+    lib().orc_simulate(model_np.ctypes.data, C.byref(sp), n, p(root), p(dof), p(act), p(sensors), p(dof_force),
+                       threads)
+
+
+def mass_matrix(model_np, sp, root13, dof2):
+    out = np.zeros(46 * 46)
+    nv = lib().orc_mass_matrix(model_np.ctypes.data, C.byref(sp), p(f32(root13)), p(f32(dof2)), p(out))
+    return out[: nv * nv].reshape(nv, nv)
+
+
+def free_acceleration(model_np, sp, root13, dof2, tau=None):
+    out = np.zeros(46)
+    nv = lib().orc_free_acceleration(model_np.ctypes.data, C.byref(sp), p(f32(root13)), p(f32(dof2)),
+                                     p(None if tau is None else f32(tau)), p(out))
+    return out[:nv]
+
+
+def contacts(model_np, sp, root13, dof2, cap=64):
+    out = np.zeros(9 * cap)
+    n = lib().orc_contacts(model_np.ctypes.data, C.byref(sp), p(f32(root13)), p(f32(dof2)), p(out), cap)
+    return out[: 9 * n].reshape(n, 9)
+
+
+def rigid_body_states(model_np, root13, dof2, nbodies):
+    out = np.zeros((nbodies, 13), dtype=np.float32)
+    lib().orc_rigid_body_states(model_np.ctypes.data, p(f32(root13)), p(f32(dof2)), p(out))
+    return out
+
+
+def compute_observations(tp, root, dof, dof_force, sensors, actions, potentials, prev_potentials, up, heading,
+                         obs):
+    lib().orc_compute_observations(C.byref(tp), root.shape[0], p(root), p(dof), p(dof_force), p(sensors),
+                                   p(actions), p(potentials), p(prev_potentials), p(up), p(heading), p(obs))
+
+
+def compute_reward(tp, obs, actions, potentials, prev_potentials, progress, reset, rew):
+    lib().orc_compute_reward(C.byref(tp), obs.shape[0], p(obs), p(actions), p(potentials), p(prev_potentials),
+                             p(progress), p(reset), p(rew))
+
+
+def uniform(seed, env, counter, k):
+    return lib().orc_uniform(seed, env, counter, k)
+
+
+class HostEnv:
+    """Host buffers for the oracle's full step (same layout the GPU path binds)."""
+
+    def __init__(self, tp, spec, n, agents=1):
+        nd = spec.num_dofs
+        na, no = tp.num_actions, tp.num_obs
+        ns = len(spec.sensors)
+        self.n = n
+        self.root = np.zeros((n, 13), np.float32)
+        self.root[:, 0:3] = np.array(tp.start_pos[:3], np.float32)
+        self.root[:, 3:7] = np.array(tp.start_rot[:4], np.float32)
+        self.dof = np.zeros((n, nd, 2), np.float32)
+        self.act_eff = np.zeros((n, nd), np.float32)
+        self.sensors = np.zeros((n, max(ns, 1) * 6), np.float32)
+        self.dof_force = np.zeros((n, nd), np.float32)
+        self.actions = np.zeros((n, na), np.float32)
+        self.actions_out = np.zeros((n, na), np.float32)
+        self.obs = np.zeros((n, no), np.float32)
+        self.obs_clamped = np.zeros((n, no), np.float32)
+        self.rew = np.zeros(n, np.float32)
+        self.reset = np.ones(n, np.int64)
+        self.progress = np.zeros(n, np.int64)
+        self.timeout = np.zeros(n, np.uint8)
+        pot = -1000.0 / tp.dt
+        self.potentials = np.full(n, pot, np.float32)
+        self.prev_potentials = np.full(n, pot, np.float32)
+        self.up = np.zeros((n, 3), np.float32)
+        self.heading = np.zeros((n, 3), np.float32)
+        self.noise = None
+
+    def views(self):
+        v = _abi.StateViews()
+        v.root_states, v.dof_state, v.dof_actuation = p(self.root), p(self.dof), p(self.act_eff)
+        v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), None
+        return v
+
+    def buffers(self, seed=0, step=0):
+        b = _abi.TaskBuffers()
+        b.actions, b.actions_out, b.obs, b.obs_clamped = p(self.actions), p(self.actions_out), p(self.obs), \
+            p(self.obs_clamped)
+        b.rew, b.reset, b.progress, b.timeout = p(self.rew), p(self.reset), p(self.progress), p(self.timeout)
+        b.potentials, b.prev_potentials = p(self.potentials), p(self.prev_potentials)
+        b.up_vec, b.heading_vec = p(self.up), p(self.heading)
+        b.noise = p(self.noise)
+        b.seed, b.step_counter, b.env_offset = seed, step, 0
+        return b
+
+    def post_physics(self, tp, seed=0, step=0):
+        v, b = self.views(), self.buffers(seed, step)
+        lib().orc_post_physics(C.byref(tp), C.byref(v), C.byref(b), self.n)
+
+    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0):
+        v, b = self.views(), self.buffers(seed, step)
+        lib().orc_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v), C.byref(b), self.n, threads)

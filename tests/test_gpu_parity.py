@@ -1,0 +1,331 @@
+"""GPU parity: the HIP path (through the C ABI) vs the golden fixtures and vs the
+CPU oracle.  Needs an MI355X: run with ``pytest -m gpu``.
+
+Tolerances (stated per north_star, obs/reward parity <= 1e-4 relative):
+  * jit obs/reward kernels vs the reference's own outputs: rtol 1e-4, atol 1e-4
+    (fp32 with the reference's op order; transcendentals differ by ulps);
+    potentials bit-exact (same fp32 sequence); resets exact.
+  * physics (one control step from identical states, fp32 GPU vs fp64 oracle):
+    positions/angles atol 2e-4, velocities atol 2e-3 + 2e-3 |v| (see
+    DESIGN.md §Parity for the derivation), sensors atol 1e-2 |F|max.
+  * RNG: the device counter RNG equals the oracle's bit for bit.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import pyoracle as O
+from migym import _abi, configs, model as M, taskdefs
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda:0"
+
+
+def load(name):
+    return dict(np.load(os.path.join(G, name)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return _abi.lib()
+
+
+def T(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(DEV, dtype).contiguous()
+
+
+def P(t):
+    return None if t is None else t.data_ptr()
+
+
+def setup(task, n_contacts=None):
+    cfg = configs.task_config(task, 16)
+    spec = M.load_builtin(taskdefs.TASK_INFO[task][1])
+    sp = taskdefs.sim_params(cfg, n_contacts or taskdefs.TASK_INFO[task][5])
+    tp = taskdefs.task_params(task, cfg, spec)
+    return spec, sp, tp
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# -------------------------------------------------------------------------------------- jit kernels
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_observation_kernel_matches_reference(lib, task):
+    d = load(f"jit_{task.lower()}.npz")
+    spec, sp, tp = setup(task)
+    n = d["root"].shape[0]
+    nd = tp.num_actions
+    root = T(d["root"])
+    dof = T(np.stack([d["dof_pos"], d["dof_vel"]], -1))
+    dforce = T(d.get("dof_force", np.zeros((n, nd))))
+    sens = T(d["sensors"])
+    act = T(d["actions"])
+    pot = T(d["potentials_in"])
+    prev = torch.zeros(n, device=DEV)
+    up = torch.zeros((n, 3), device=DEV)
+    hd = torch.zeros((n, 3), device=DEV)
+    obs = torch.zeros((n, tp.num_obs), device=DEV)
+    _abi.check(lib.mg_compute_observations(C.byref(tp), n, P(root), P(dof), P(dforce), P(sens), P(act), P(pot),
+                                           P(prev), P(up), P(hd), P(obs), stream()), lib)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(obs.cpu().numpy(), d["obs"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_array_equal(pot.cpu().numpy(), d["potentials"])
+    np.testing.assert_array_equal(prev.cpu().numpy(), d["prev_potentials"])
+    np.testing.assert_allclose(up.cpu().numpy(), d["up_vec"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(hd.cpu().numpy(), d["heading_vec"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("task", ["Ant", "Humanoid", "Cartpole"])
+def test_reward_kernel_matches_reference(lib, task):
+    d = load(f"jit_{task.lower()}.npz")
+    spec, sp, tp = setup(task)
+    obs = T(d["obs"])
+    n = obs.shape[0]
+    act = T(d["actions"]) if "actions" in d else torch.zeros((n, 1), device=DEV)
+    pot = T(d["potentials"]) if "potentials" in d else torch.zeros(n, device=DEV)
+    prev = T(d["prev_potentials"]) if "prev_potentials" in d else torch.zeros(n, device=DEV)
+    prog = T(d["progress"], torch.int64)
+    reset = T(d["reset_buf"], torch.int64)
+    rew = torch.zeros(n, device=DEV)
+    _abi.check(lib.mg_compute_reward(C.byref(tp), n, P(obs), P(act), P(pot), P(prev), P(prog), P(reset), P(rew),
+                                     stream()), lib)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(rew.cpu().numpy(), d["rew"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_array_equal(reset.cpu().numpy(), d["reset"])
+
+
+class DevEnv:
+    """Device buffers mirroring pyoracle.HostEnv (so both paths see identical inputs)."""
+
+    def __init__(self, h: O.HostEnv):
+        self.h = h
+        self.root = T(h.root)
+        self.dof = T(h.dof)
+        self.act_eff = T(h.act_eff)
+        self.sensors = T(h.sensors)
+        self.dof_force = T(h.dof_force)
+        self.actions = T(h.actions)
+        self.actions_out = T(h.actions_out)
+        self.obs = T(h.obs)
+        self.obs_clamped = T(h.obs_clamped)
+        self.rew = T(h.rew)
+        self.reset = T(h.reset, torch.int64)
+        self.progress = T(h.progress, torch.int64)
+        self.timeout = torch.zeros(h.n, dtype=torch.bool, device=DEV)
+        self.potentials = T(h.potentials)
+        self.prev_potentials = T(h.prev_potentials)
+        self.up = T(h.up)
+        self.heading = T(h.heading)
+        self.noise = None
+
+    def views(self):
+        v = _abi.StateViews()
+        v.root_states, v.dof_state, v.dof_actuation = P(self.root), P(self.dof), P(self.act_eff)
+        v.sensors, v.dof_force, v.rigid_body_states = P(self.sensors), P(self.dof_force), None
+        return v
+
+    def buffers(self, seed=0, step=0):
+        b = _abi.TaskBuffers()
+        b.actions, b.actions_out, b.obs, b.obs_clamped = P(self.actions), P(self.actions_out), P(self.obs), \
+            P(self.obs_clamped)
+        b.rew, b.reset, b.progress, b.timeout = P(self.rew), P(self.reset), P(self.progress), P(self.timeout)
+        b.potentials, b.prev_potentials = P(self.potentials), P(self.prev_potentials)
+        b.up_vec, b.heading_vec = P(self.up), P(self.heading)
+        b.noise = P(self.noise)
+        b.seed, b.step_counter, b.env_offset = seed, step, 0
+        return b
+
+
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_post_physics_replays_reference_trace(lib, task):
+    d = load(f"trace_{task.lower()}.npz")
+    spec, sp, tp = setup(task)
+    tp.max_episode_length = int(d["episode_length"])
+    Tn, N = d["actions"].shape[:2]
+    h = O.HostEnv(tp, spec, N)
+    e = DevEnv(h)
+    for t in range(Tn):
+        e.actions.copy_(T(d["actions"][t]))
+        e.root.copy_(T(d["phys_root"][t]))
+        e.dof.copy_(T(d["phys_dof"][t]))
+        e.sensors.copy_(T(d["phys_sensors"][t]))
+        e.dof_force.copy_(T(d["phys_dof_force"][t]))
+        e.noise = T(d["noise"][t])
+        v, b = e.views(), e.buffers()
+        _abi.check(lib.mg_post_physics(None, C.byref(tp), C.byref(v), C.byref(b), N, stream()), lib)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(e.root.cpu().numpy(), d["root_after"][t])
+        np.testing.assert_allclose(e.dof.cpu().numpy(), d["dof_after"][t], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(e.obs_clamped.cpu().numpy(), d["obs"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(e.rew.cpu().numpy(), d["rew"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_array_equal(e.reset.cpu().numpy(), d["reset"][t])
+        np.testing.assert_array_equal(e.progress.cpu().numpy(), d["progress"][t])
+        np.testing.assert_array_equal(e.timeout.cpu().numpy().astype(np.int64), d["timeouts"][t])
+        np.testing.assert_array_equal(e.potentials.cpu().numpy(), d["potentials"][t])
+
+
+def test_cartpole_post_physics_replays_reference_trace(lib):
+    d = load("trace_cartpole.npz")
+    spec, sp, tp = setup("Cartpole")
+    Tn, N = d["actions"].shape[:2]
+    h = O.HostEnv(tp, spec, N)
+    e = DevEnv(h)
+    for t in range(Tn):
+        e.actions.copy_(T(d["actions"][t]))
+        e.dof.copy_(T(d["phys_dof"][t]))
+        e.noise = T(d["noise"][t])
+        v, b = e.views(), e.buffers()
+        _abi.check(lib.mg_post_physics(None, C.byref(tp), C.byref(v), C.byref(b), N, stream()), lib)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(e.dof.cpu().numpy(), d["dof_after"][t], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(e.obs_clamped.cpu().numpy(), d["obs"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(e.rew.cpu().numpy(), d["rew"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_array_equal(e.reset.cpu().numpy(), d["reset"][t])
+        np.testing.assert_array_equal(e.progress.cpu().numpy(), d["progress"][t])
+
+
+def test_device_rng_equals_oracle_rng(lib):
+    spec, sp, tp = setup("Ant")
+    n = 1000
+    h = O.HostEnv(tp, spec, n)
+    h.reset[:] = 1
+    e = DevEnv(h)
+    v, b = e.views(), e.buffers(seed=1234, step=77)
+    _abi.check(lib.mg_post_physics(None, C.byref(tp), C.byref(v), C.byref(b), n, stream()), lib)
+    h.post_physics(tp, seed=1234, step=77)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(e.dof.cpu().numpy(), h.dof)
+
+
+# -------------------------------------------------------------------------------------- physics
+def random_states(spec, tp, n, rng, z_range, contact_frac=0.5):
+    nd = spec.num_dofs
+    root = np.zeros((n, 13), np.float32)
+    root[:, 0:2] = rng.uniform(-2, 2, (n, 2))
+    root[:, 2] = rng.uniform(*z_range, n)
+    yaw = rng.uniform(-np.pi, np.pi, n)
+    tilt = rng.normal(0, 0.3, (n, 2))
+    q = np.stack([tilt[:, 0] * 0.5, tilt[:, 1] * 0.5, np.sin(yaw / 2), np.cos(yaw / 2)], -1)
+    root[:, 3:7] = q / np.linalg.norm(q, axis=-1, keepdims=True)
+    root[:, 7:13] = rng.normal(0, 0.5, (n, 6))
+    lo, hi = np.array(tp.dof_lower[:nd]), np.array(tp.dof_upper[:nd])
+    dof = np.zeros((n, nd, 2), np.float32)
+    dof[:, :, 0] = lo + (hi - lo) * rng.uniform(-0.05, 1.05, (n, nd))
+    dof[:, :, 1] = rng.normal(0, 1.0, (n, nd))
+    return root, dof
+
+
+@pytest.mark.parametrize("task,n,z", [("Ant", 512, (0.25, 0.7)), ("Humanoid", 256, (0.6, 1.4)),
+                                      ("Cartpole", 256, (2.0, 2.0))])
+def test_physics_step_matches_oracle(lib, task, n, z):
+    spec, sp, tp = setup(task)
+    rng = np.random.default_rng(7)
+    root, dof = random_states(spec, tp, n, rng, z)
+    if task == "Cartpole":
+        root[:, :] = 0
+        root[:, 2] = 2.0
+        root[:, 6] = 1.0
+    act = (rng.uniform(-1, 1, (n, spec.num_dofs)) * (15.0 if task == "Ant" else 50.0)).astype(np.float32)
+    ns = max(len(spec.sensors), 1)
+    sens_h = np.zeros((n, ns * 6), np.float32)
+    dfor_h = np.zeros((n, spec.num_dofs), np.float32)
+    mnp = M.pack_model(spec)
+    r_h, d_h = root.copy(), dof.copy()
+    O.simulate(mnp, sp, r_h, d_h, act, sens_h, dfor_h, threads=8)
+    # device
+    r_d, d_d, a_d = T(root), T(dof), T(act)
+    s_d, f_d = torch.zeros((n, ns * 6), device=DEV), torch.zeros((n, spec.num_dofs), device=DEV)
+    h = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(h)), lib)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force = P(r_d), P(d_d), P(a_d), P(s_d), P(f_d)
+    _abi.check(lib.mg_sim_bind(h, C.byref(v)), lib)
+    _abi.check(lib.mg_sim_simulate(h, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(h)
+    rg, dg = r_d.cpu().numpy(), d_d.cpu().numpy()
+    np.testing.assert_allclose(rg[:, 0:7], r_h[:, 0:7], atol=2e-4)
+    np.testing.assert_allclose(dg[..., 0], d_h[..., 0], atol=2e-4)
+    np.testing.assert_allclose(rg[:, 7:13], r_h[:, 7:13], atol=2e-3, rtol=2e-3)
+    np.testing.assert_allclose(dg[..., 1], d_h[..., 1], atol=2e-3, rtol=2e-3)
+    sg = s_d.cpu().numpy()
+    if len(spec.sensors):
+        scale = max(1.0, np.abs(sens_h).max())
+        np.testing.assert_allclose(sg, sens_h, atol=1e-2 * scale)
+    fg = f_d.cpu().numpy()
+    np.testing.assert_allclose(fg, dfor_h, atol=1e-2 * max(1.0, np.abs(dfor_h).max()))
+
+
+@pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128), ("Cartpole", 256)])
+def test_fused_env_step_matches_oracle(lib, task, n):
+    """mg_env_step (the bench path) vs orc_env_step over 3 control steps, device RNG resets."""
+    spec, sp, tp = setup(task)
+    h = O.HostEnv(tp, spec, n)
+    e = DevEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    rng = np.random.default_rng(3)
+    for t in range(3):
+        a = rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32)
+        h.actions[:] = a
+        e.actions.copy_(T(a))
+        h.env_step(mnp, sp, tp, seed=5, step=t, threads=8)
+        _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=5, step=t)), stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    np.testing.assert_array_equal(e.reset.cpu().numpy(), h.reset)
+    np.testing.assert_array_equal(e.progress.cpu().numpy(), h.progress)
+    og = e.obs.cpu().numpy()
+    bad = np.abs(og - h.obs) > (2e-2 + 2e-2 * np.abs(h.obs))
+    assert bad.mean() < 1e-3, (bad.sum(), np.argwhere(bad)[:10])
+    np.testing.assert_allclose(e.rew.cpu().numpy(), h.rew, atol=5e-2, rtol=5e-2)
+
+
+def test_set_indexed_scatters_rows(lib):
+    spec, sp, tp = setup("Ant")
+    n = 100
+    mnp = M.pack_model(spec)
+    root = torch.zeros((n, 13), device=DEV)
+    dof = torch.zeros((n * 8, 2), device=DEV)
+    src = torch.randn((n, 13), device=DEV)
+    idx = torch.tensor([3, 7, 50, 99], dtype=torch.int32, device=DEV)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state, v.sensors = P(root), P(dof), P(torch.zeros((n * 4, 6), device=DEV))
+    _abi.check(lib.mg_sim_bind(sim, C.byref(v)), lib)
+    _abi.check(lib.mg_set_indexed(sim, _abi.MG_SET_ROOT_STATE, P(src), P(idx), 4, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    exp = torch.zeros_like(root)
+    exp[idx.long()] = src[idx.long()]
+    assert torch.equal(root, exp)
+
+
+# -------------------------------------------------------------------------------------- full size
+@pytest.mark.parametrize("task,n", [("Ant", 65536), ("Humanoid", 32768)])
+def test_full_size_rollout_is_sane(task, n):
+    import migym
+    env = migym.make(seed=0, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    resets = 0
+    for _ in range(20):
+        a = torch.rand((n, env.num_actions), device=DEV, generator=g) * 2 - 1
+        obs, rew, reset, extras = env.step(a)
+        resets += int(reset.sum())
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+    assert torch.isfinite(env.root_states).all()
+    # every env left the initial all-reset state; torsos are above ground
+    assert int(env.progress_buf.min()) >= 0 and float(env.root_states[:, 2].min()) > 0.0
+    assert extras["time_outs"].dtype == torch.bool
+    env.close()

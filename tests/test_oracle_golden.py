@@ -1,0 +1,140 @@
+"""The oracle's task layer vs the reference's own outputs (golden fixtures).
+
+Pins oracle/oracle_task.c to tasks/ant.py:325-408, tasks/humanoid.py:323-413,
+tasks/cartpole.py:131-196 and the VecTask.step ordering
+(tasks/base/vec_task.py:362-410) via tests/golden/*.npz, which
+tests/golden/make_golden.py / make_traces.py produced by running the reference
+code.  Tolerance: the oracle computes in fp32 like the reference, so 2e-5
+relative + 2e-5 absolute (transcendental ulp differences), exact for ints.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+from migym import model as M, taskdefs, configs
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+RTOL, ATOL = 2e-5, 2e-5
+
+
+def load(name):
+    return dict(np.load(os.path.join(G, name)))
+
+
+def tparams(task):
+    cfg = configs.task_config(task, 16)
+    spec = M.load_builtin(taskdefs.TASK_INFO[task][1])
+    return taskdefs.task_params(task, cfg, spec), spec
+
+
+def _obs_case(task, d, nsens):
+    tp, spec = tparams(task)
+    n = d["root"].shape[0]
+    nd = tp.num_actions
+    # golden limits are the reference's dof limits; they must equal the model's
+    np.testing.assert_allclose(np.array(tp.dof_lower[:nd]), d["lo"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(np.array(tp.dof_upper[:nd]), d["hi"], rtol=0, atol=1e-6)
+    root = O.f32(d["root"])
+    dof = O.f32(np.stack([d["dof_pos"], d["dof_vel"]], -1))
+    dforce = O.f32(d.get("dof_force", np.zeros((n, nd))))
+    sens = O.f32(d["sensors"])
+    act = O.f32(d["actions"])
+    pot = O.f32(d["potentials_in"]).copy()
+    prev = np.zeros(n, np.float32)
+    up = np.zeros((n, 3), np.float32)
+    hd = np.zeros((n, 3), np.float32)
+    obs = np.zeros((n, tp.num_obs), np.float32)
+    O.compute_observations(tp, root, dof, dforce, sens, act, pot, prev, up, hd, obs)
+    return tp, obs, pot, prev, up, hd
+
+
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_locomotion_observations_match_reference(task):
+    d = load(f"jit_{task.lower()}.npz")
+    tp, obs, pot, prev, up, hd = _obs_case(task, d, 4 if task == "Ant" else 2)
+    np.testing.assert_allclose(obs, d["obs"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_array_equal(pot, d["potentials"])            # fp32 order reproduced exactly
+    np.testing.assert_array_equal(prev, d["prev_potentials"])
+    np.testing.assert_allclose(up, d["up_vec"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(hd, d["heading_vec"], rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_locomotion_reward_match_reference(task):
+    d = load(f"jit_{task.lower()}.npz")
+    tp, _ = tparams(task)
+    obs = O.f32(d["obs"])
+    n = obs.shape[0]
+    reset = O.i64(d["reset_buf"]).copy()
+    rew = np.zeros(n, np.float32)
+    O.compute_reward(tp, obs, O.f32(d["actions"]), O.f32(d["potentials"]), O.f32(d["prev_potentials"]),
+                     O.i64(d["progress"]), reset, rew)
+    np.testing.assert_allclose(rew, d["rew"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_array_equal(reset, d["reset"])
+
+
+def test_cartpole_reward_match_reference():
+    d = load("jit_cartpole.npz")
+    tp, _ = tparams("Cartpole")
+    obs = O.f32(d["obs"])
+    n = obs.shape[0]
+    reset = O.i64(d["reset_buf"]).copy()
+    rew = np.zeros(n, np.float32)
+    O.compute_reward(tp, obs, np.zeros((n, 1), np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32),
+                     O.i64(d["progress"]), reset, rew)
+    np.testing.assert_allclose(rew, d["rew"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_array_equal(reset, d["reset"])
+
+
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_full_step_trace_matches_reference(task):
+    """Replays the reference's physics-free VecTask.step trace through the oracle's
+    post-physics path with the reference's own reset-noise draws injected."""
+    d = load(f"trace_{task.lower()}.npz")
+    tp, spec = tparams(task)
+    tp.max_episode_length = int(d["episode_length"])
+    T, N = d["actions"].shape[:2]
+    h = O.HostEnv(tp, spec, N)
+    for t in range(T):
+        h.actions[:] = d["actions"][t]
+        h.root[:] = d["phys_root"][t]
+        h.dof[:] = d["phys_dof"][t]
+        h.sensors[:] = d["phys_sensors"][t]
+        h.dof_force[:] = d["phys_dof_force"][t]
+        h.noise = O.f32(d["noise"][t])
+        np.testing.assert_array_equal(h.reset, d["reset_in"][t])
+        np.testing.assert_array_equal(h.progress, d["progress_in"][t])
+        h.post_physics(tp)
+        np.testing.assert_allclose(h.root, d["root_after"][t], rtol=0, atol=0)
+        np.testing.assert_allclose(h.dof, d["dof_after"][t], rtol=1e-7, atol=1e-7)
+        np.testing.assert_allclose(h.obs_clamped, d["obs"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(h.rew, d["rew"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_array_equal(h.reset, d["reset"][t])
+        np.testing.assert_array_equal(h.progress, d["progress"][t])
+        np.testing.assert_array_equal(h.timeout, d["timeouts"][t])
+        np.testing.assert_array_equal(h.potentials, d["potentials"][t])
+        np.testing.assert_array_equal(h.prev_potentials, d["prev_potentials"][t])
+
+
+def test_cartpole_trace_matches_reference():
+    d = load("trace_cartpole.npz")
+    tp, spec = tparams("Cartpole")
+    T, N = d["actions"].shape[:2]
+    h = O.HostEnv(tp, spec, N)
+    for t in range(T):
+        h.actions[:] = d["actions"][t]
+        h.dof[:] = d["phys_dof"][t]
+        h.noise = O.f32(d["noise"][t])
+        h.post_physics(tp)
+        np.testing.assert_allclose(h.dof, d["dof_after"][t], rtol=1e-7, atol=1e-7)
+        np.testing.assert_allclose(h.obs_clamped, d["obs"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(h.rew, d["rew"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_array_equal(h.reset, d["reset"][t])
+        np.testing.assert_array_equal(h.progress, d["progress"][t])
+        np.testing.assert_array_equal(h.timeout, d["timeouts"][t])
+        # actuation written by pre_physics_step: 400 * clamp(a) on DOF 0 only (cartpole.py:159-163)
+        a = np.clip(d["actions"][t][:, 0], -1, 1) * 400.0
+        np.testing.assert_allclose(d["actuation"][t][:, 0], a, rtol=1e-6)
+        assert np.all(d["actuation"][t][:, 1] == 0)
