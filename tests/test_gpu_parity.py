@@ -320,7 +320,8 @@ def test_full_size_rollout_is_sane(task, n):
     resets = 0
     for _ in range(20):
         a = torch.rand((n, env.num_actions), device=DEV, generator=g) * 2 - 1
-        obs, rew, reset, extras = env.step(a)
+        obs_dict, rew, reset, extras = env.step(a)
+        obs = obs_dict["obs"]
         resets += int(reset.sum())
     torch.cuda.synchronize()
     assert torch.isfinite(obs).all() and torch.isfinite(rew).all()

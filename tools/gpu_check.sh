@@ -22,3 +22,7 @@ fi
 if [ "$STAGE" = all ] || [ "$STAGE" = bench ]; then
   run bench 600 python bench.py --steps 100 --warmup 10 || exit $?
 fi
+if [ "$STAGE" = all ] || [ "$STAGE" = prof ]; then
+  export TMPDIR=/tmp
+  run rocprof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o trace --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline || exit $?
+fi
