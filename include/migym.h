@@ -62,6 +62,7 @@ enum { MG_JT_FREE = 0, MG_JT_FIXED = 1, MG_JT_HINGE = 2, MG_JT_SLIDE = 3 };
 enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4 };
 enum { MG_OK = 0, MG_EINVAL = -1, MG_EDEVICE = -2, MG_ENOMEM = -3, MG_ECAPACITY = -4 };
 enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2 };
+#define MG_MAX_AGENTS 8
 enum { MG_SET_ROOT_STATE = 0, MG_SET_DOF_STATE = 1 };
 
 /* One articulation ("actor asset") as a dynamics tree of 1-DOF nodes.
@@ -155,6 +156,13 @@ typedef struct mg_task_params {
   float dof_lower[64];      /* task-side dof limits (swapped if lower>upper, ant.py:199-206) */
   float dof_upper[64];
   float initial_dof_pos[64];
+  /* multi-agent layout (SURVEY.md §8(a) A-MA; franka_reach_MA.py:22-38, 598-612, 875-889):
+   * actors are env-major (actor = env * num_agents + agent); an env resets only when all
+   * of its agents are done (AND filter); obs rows append the other agents' torso positions
+   * relative to self in cyclic-shift order.  num_agents = 1 for single-agent tasks. */
+  int32_t num_agents;
+  int32_t pad_ma;
+  float agent_offset[8][3]; /* start-pose / target offset of each agent within its env */
 } mg_task_params;
 
 /* Task-layer buffers (VecTask.allocate_buffers, vec_task.py:302-325). */

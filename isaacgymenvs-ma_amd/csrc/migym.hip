@@ -60,7 +60,8 @@ __global__ __launch_bounds__(kBlock) void k_observations(mg_task_params tp, int 
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int nd = mg::t_dofs(&tp), ns = mg::t_sensors(&tp);
-  mg::obs_env(&tp, root + (size_t)13 * e, dof + (size_t)2 * nd * e, dforce ? dforce + (size_t)nd * e : nullptr,
+  const float zero3[3] = {0.0f, 0.0f, 0.0f};
+  mg::obs_env(&tp, zero3, root + (size_t)13 * e, dof + (size_t)2 * nd * e, dforce ? dforce + (size_t)nd * e : nullptr,
               sensors ? sensors + (size_t)6 * ns * e : nullptr, actions + (size_t)tp.num_actions * e, pot + e,
               prev_pot + e, up + 3 * (size_t)e, heading + 3 * (size_t)e, obs + (size_t)tp.num_obs * e);
 }
@@ -75,43 +76,68 @@ __global__ __launch_bounds__(kBlock) void k_reward(mg_task_params tp, int n, con
                  progress[e], reset + e, rew + e);
 }
 
-// post_physics_step + VecTask.step tail for env e (state already advanced)
+// post_physics_step + VecTask.step tail for actor a (state already advanced).  Multi-agent:
+// actors of one env are adjacent lanes of one wave (64 % num_agents == 0), so the env-level
+// AND of the agents' reset flags is a ballot and the other agents' torso positions are shuffles.
 __device__ __forceinline__ void post_physics_env(const mg_task_params& tp, const mg_state_views& v,
-                                                 const mg_task_buffers& tb, int e, const float* act) {
+                                                 const mg_task_buffers& tb, int a, const float* act,
+                                                 int64_t reset_in) {
   const int nd = mg::t_dofs(&tp), ns = mg::t_sensors(&tp), no = tp.num_obs;
-  float* root = v.root_states + (size_t)13 * e;
-  float* dof = v.dof_state + (size_t)2 * nd * e;
-  int64_t progress = tb.progress[e] + 1;
-  int64_t reset = tb.reset[e];
-  float pot = tb.potentials ? tb.potentials[e] : 0.0f;
-  float prev = tb.prev_potentials ? tb.prev_potentials[e] : 0.0f;
-  if (reset != 0) {
-    mg::reset_env(&tp, tb.noise ? tb.noise + (size_t)2 * nd * e : nullptr, tb.seed,
-                  (uint64_t)(tb.env_offset + e), tb.step_counter, root, dof, &pot, &prev);
+  const int A = tp.num_agents > 1 ? tp.num_agents : 1;
+  const int k = a % A;
+  const float* off = tp.agent_offset[k];
+  float* root = v.root_states + (size_t)13 * a;
+  float* dof = v.dof_state + (size_t)2 * nd * a;
+  int64_t progress = tb.progress[a] + 1;
+  int64_t reset = reset_in;
+  bool do_reset = reset != 0;
+  if (A > 1) {  // AND filter (franka_reach_MA.py:875-885)
+    const int lane = threadIdx.x & 63;
+    const unsigned long long m = __ballot(reset != 0);
+    const unsigned long long full = (A >= 64) ? ~0ull : ((1ull << A) - 1ull);
+    do_reset = ((m >> (lane - k)) & full) == full;
+  }
+  float pot = tb.potentials ? tb.potentials[a] : 0.0f;
+  float prev = tb.prev_potentials ? tb.prev_potentials[a] : 0.0f;
+  if (do_reset) {
+    mg::reset_env(&tp, off, tb.noise ? tb.noise + (size_t)2 * nd * a : nullptr, tb.seed,
+                  (uint64_t)(tb.env_offset + a), tb.step_counter, root, dof, &pot, &prev);
     progress = 0;
     reset = 0;
   }
-  float* o = tb.obs + (size_t)no * e;
+  float* o = tb.obs + (size_t)no * a;
   float up[3], hd[3];
-  mg::obs_env(&tp, root, dof, v.dof_force ? v.dof_force + (size_t)nd * e : nullptr,
-              v.sensors ? v.sensors + (size_t)6 * ns * e : nullptr, act, &pot, &prev, up, hd, o);
+  mg::obs_env(&tp, off, root, dof, v.dof_force ? v.dof_force + (size_t)nd * a : nullptr,
+              v.sensors ? v.sensors + (size_t)6 * ns * a : nullptr, act, &pot, &prev, up, hd, o);
+  if (A > 1) {  // "others" block: cyclic shift starting after self (franka_reach_MA.py:604-608)
+    const int lane = threadIdx.x & 63;
+    const float px = root[0], py = root[1], pz = root[2];
+    const int base = no - 3 * (A - 1);
+    for (int j = 1; j < A; j++) {
+      const int src = lane - k + (k + j) % A;
+      const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
+      o[base + 3 * (j - 1) + 0] = qx - px;
+      o[base + 3 * (j - 1) + 1] = qy - py;
+      o[base + 3 * (j - 1) + 2] = qz - pz;
+    }
+  }
   float rew;
   mg::reward_env(&tp, o, act, pot, prev, progress, &reset, &rew);
   const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
-  tb.rew[e] = rew;
-  tb.reset[e] = reset;
-  tb.progress[e] = progress;
-  tb.timeout[e] = (uint8_t)(((float)progress >= max_ep_m1) && (reset != 0));
+  tb.rew[a] = rew;
+  tb.reset[a] = reset;
+  tb.progress[a] = progress;
+  tb.timeout[a] = (uint8_t)(((float)progress >= max_ep_m1) && (reset != 0));
   if (tp.task_id != MG_TASK_CARTPOLE) {
-    tb.potentials[e] = pot;
-    tb.prev_potentials[e] = prev;
-    for (int k = 0; k < 3; k++) {
-      tb.up_vec[3 * (size_t)e + k] = up[k];
-      tb.heading_vec[3 * (size_t)e + k] = hd[k];
+    tb.potentials[a] = pot;
+    tb.prev_potentials[a] = prev;
+    for (int c = 0; c < 3; c++) {
+      tb.up_vec[3 * (size_t)a + c] = up[c];
+      tb.heading_vec[3 * (size_t)a + c] = hd[c];
     }
   }
   if (tb.obs_clamped)
-    for (int i = 0; i < no; i++) tb.obs_clamped[(size_t)no * e + i] = mg::clampf(o[i], tp.clip_obs);
+    for (int i = 0; i < no; i++) tb.obs_clamped[(size_t)no * a + i] = mg::clampf(o[i], tp.clip_obs);
 }
 
 __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
@@ -124,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_s
     act[i] = mg::clampf(tb.actions[(size_t)na * e + i], tp.clip_actions);
     if (tb.actions_out) tb.actions_out[(size_t)na * e + i] = act[i];
   }
-  post_physics_env(tp, v, tb, e, act);
+  post_physics_env(tp, v, tb, e, act, tb.reset[e]);
 }
 
 // The whole VecTask.step for one env, fused: clamp -> actuation -> simulate -> post_physics.
@@ -134,6 +160,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict_
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
+  const int64_t reset_in = tb.reset[e];
   float act[MN];
   for (int i = 0; i < na; i++) {
     act[i] = mg::clampf(tb.actions[(size_t)na * e + i], tp.clip_actions);
@@ -150,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict_
   mg::simulate_actor<MN, MC>(m, &p, v.root_states + (size_t)13 * e, v.dof_state + (size_t)2 * nd * e, tau,
                              v.sensors ? v.sensors + (size_t)6 * ns * e : nullptr,
                              v.dof_force ? v.dof_force + (size_t)nd * e : nullptr);
-  post_physics_env(tp, v, tb, e, act);
+  post_physics_env(tp, v, tb, e, act, reset_in);
 }
 
 __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
@@ -308,6 +335,9 @@ int mg_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, con
 int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views, const mg_task_buffers* tb,
                     int32_t n, void* stream) {
   if (!tp || !tb) return fail(MG_EINVAL, "mg_post_physics: bad args");
+  if (tp->num_agents > 1 && (64 % tp->num_agents != 0 || tp->num_agents > MG_MAX_AGENTS ||
+                             (sim ? sim->n : n) % tp->num_agents != 0))
+    return fail(MG_EINVAL, "mg_post_physics: num_agents must divide 64 and the actor count");
   mg_state_views v;
   if (sim) {
     if (!sim->bound) return fail(MG_EINVAL, "mg_post_physics: sim not bound");
@@ -330,6 +360,9 @@ int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb
     return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
   if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
     return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
+  if (tp->num_agents > 1 && (64 % tp->num_agents != 0 || sim->n % tp->num_agents != 0 ||
+                             tp->num_agents > MG_MAX_AGENTS))
+    return fail(MG_EINVAL, "mg_env_step: num_agents must divide 64 and the actor count");
   int rc = dispatch<RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream, (const mg_sim*)sim,
                                 tp, tb);
   if (rc) return rc;

@@ -62,9 +62,11 @@ struct LocoFeat {
       potential;
 };
 
-__device__ __forceinline__ void loco_features(const mg_task_params* tp, const float* root, LocoFeat& f) {
+__device__ __forceinline__ void loco_features(const mg_task_params* tp, const float* root, const float* off,
+                                              LocoFeat& f) {
   const float* pos = root;
-  float tt0 = tp->target[0] - pos[0], tt1 = tp->target[1] - pos[1], tt2 = 0.0f;
+  const float tg0 = tp->target[0] + off[0], tg1 = tp->target[1] + off[1], tg2 = tp->target[2] + off[2];
+  float tt0 = tg0 - pos[0], tt1 = tg1 - pos[1], tt2 = 0.0f;
   float nrm = sqrtf(tt0 * tt0 + tt1 * tt1 + tt2 * tt2);
   f.potential = -nrm / tp->dt;
   float nc = nrm < 1e-9f ? 1e-9f : nrm;
@@ -86,7 +88,7 @@ __device__ __forceinline__ void loco_features(const mg_task_params* tp, const fl
   float siny = 2.0f * (qw * qz + qx * qy);
   float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
   f.yaw = t_mod2pi(atan2f(siny, cosy));
-  float wta = atan2f(tp->target[2] - pos[2], tp->target[0] - pos[0]);
+  float wta = atan2f(tg2 - pos[2], tg0 - pos[0]);
   f.angle_to_target = wta - f.yaw;
 }
 
@@ -98,16 +100,16 @@ __device__ __forceinline__ int t_dofs(const mg_task_params* tp) {
 }
 
 // obs row e (writes potentials/prev_potentials/up/heading like compute_*_observations)
-__device__ void obs_env(const mg_task_params* tp, const float* root, const float* dof, const float* dof_force,
-                        const float* sen, const float* act, float* pot, float* prev_pot, float* up, float* heading,
-                        float* o) {
+__device__ void obs_env(const mg_task_params* tp, const float* off, const float* root, const float* dof,
+                        const float* dof_force, const float* sen, const float* act, float* pot, float* prev_pot,
+                        float* up, float* heading, float* o) {
   const int nd = t_dofs(tp), na = tp->num_actions;
   if (tp->task_id == MG_TASK_CARTPOLE) {
     o[0] = dof[0]; o[1] = dof[1]; o[2] = dof[2]; o[3] = dof[3];
     return;
   }
   LocoFeat f;
-  loco_features(tp, root, f);
+  loco_features(tp, root, off, f);
   *prev_pot = *pot;
   *pot = f.potential;
   for (int i = 0; i < 3; i++) { up[i] = f.up_vec[i]; heading[i] = f.heading_vec[i]; }
@@ -182,8 +184,8 @@ __device__ void reward_env(const mg_task_params* tp, const float* o, const float
 }
 
 // reset_idx for one env.  noise: row of 2*nD U(0,1) (or NULL: device counter RNG)
-__device__ void reset_env(const mg_task_params* tp, const float* noise, uint64_t seed, uint64_t env_gid,
-                          uint64_t counter, float* root, float* dof, float* pot, float* prev_pot) {
+__device__ void reset_env(const mg_task_params* tp, const float* off, const float* noise, uint64_t seed,
+                          uint64_t env_gid, uint64_t counter, float* root, float* dof, float* pot, float* prev_pot) {
   const int nd = t_dofs(tp);
   for (int i = 0; i < nd; i++) {
     float up = noise ? noise[i] : uniform01(seed, env_gid, counter, (uint32_t)i);
@@ -202,10 +204,10 @@ __device__ void reset_env(const mg_task_params* tp, const float* noise, uint64_t
     }
   }
   if (tp->task_id != MG_TASK_CARTPOLE) {
-    for (int k = 0; k < 3; k++) root[k] = tp->start_pos[k];
+    for (int k = 0; k < 3; k++) root[k] = tp->start_pos[k] + off[k];
     for (int k = 0; k < 4; k++) root[3 + k] = tp->start_rot[k];
     for (int k = 7; k < 13; k++) root[k] = 0.0f;
-    float t0 = tp->target[0] - tp->start_pos[0], t1 = tp->target[1] - tp->start_pos[1], t2 = 0.0f;
+    float t0 = (tp->target[0] + off[0]) - root[0], t1 = (tp->target[1] + off[1]) - root[1], t2 = 0.0f;
     float nrm = sqrtf(t0 * t0 + t1 * t1 + t2 * t2);
     *prev_pot = -nrm / tp->dt;
     *pot = *prev_pot;

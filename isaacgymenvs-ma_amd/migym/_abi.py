@@ -42,7 +42,8 @@ class TaskParams(C.Structure):
                 ("death_cost", C.c_float), ("termination_height", C.c_float), ("max_motor_effort", C.c_float),
                 ("reset_dist", C.c_float), ("target", C.c_float * 3), ("start_pos", C.c_float * 3),
                 ("start_rot", C.c_float * 4), ("motor_effort", C.c_float * 64), ("dof_lower", C.c_float * 64),
-                ("dof_upper", C.c_float * 64), ("initial_dof_pos", C.c_float * 64)]
+                ("dof_upper", C.c_float * 64), ("initial_dof_pos", C.c_float * 64),
+                ("num_agents", C.c_int32), ("pad_ma", C.c_int32), ("agent_offset", (C.c_float * 3) * 8)]
 
 
 class TaskBuffers(C.Structure):

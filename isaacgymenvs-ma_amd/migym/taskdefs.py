@@ -56,12 +56,34 @@ def dof_limits(spec: M.ModelSpec):
     return lo, hi
 
 
+def agent_offsets(A: int, spacing: float):
+    """Agent k of an env starts at (col, row) of a ceil(sqrt(A))-wide grid, centred on the env origin."""
+    cols = int(math.ceil(math.sqrt(A)))
+    rows = int(math.ceil(A / cols))
+    out = []
+    for k in range(A):
+        c, r = k % cols, k // cols
+        out.append(((c - (cols - 1) / 2.0) * spacing, (r - (rows - 1) / 2.0) * spacing, 0.0))
+    return out
+
+
 def task_params(task: str, cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     base = "Ant" if task == "MAAnt" else task
     task_id, _, nobs, nact, z0, _ = TASK_INFO[base]
     env = cfg["env"]
     tp = _abi.TaskParams()
     tp.task_id = task_id
+    tp.num_agents = 1
+    if task == "MAAnt":
+        # build-defined multi-agent Ant (SURVEY.md §8(a) A-MA): A ants on a square grid,
+        # obs = Ant obs + the other agents' torso positions relative to self (3 (A-1))
+        A = int(env.get("numAgents", 4))
+        if A < 1 or A > 8 or 64 % A:
+            raise ValueError("numAgents must be 1, 2, 4 or 8")
+        tp.num_agents = A
+        nobs = nobs + 3 * (A - 1)
+        for k, off in enumerate(agent_offsets(A, float(env.get("agentSpacing", 2.0)))):
+            tp.agent_offset[k][:] = off
     tp.num_obs = nobs
     tp.num_actions = nact
     tp.dt = float(cfg["sim"]["dt"])

@@ -145,6 +145,10 @@ class VecTask(Env):
         # gym-visible state tensors (acquire_*_tensor + wrap_tensor): zero-copy, owned by torch
         self.root_states = torch.zeros((A, 13), device=dev, dtype=f)
         self.root_states[:, 0:3] = torch.tensor(list(self.task_params.start_pos), device=dev)
+        if self.num_agents > 1:
+            offs = torch.tensor([list(self.task_params.agent_offset[k]) for k in range(self.num_agents)],
+                                device=dev, dtype=f)
+            self.root_states[:, 0:3] += offs.repeat(self.num_envs, 1)
         self.root_states[:, 3:7] = torch.tensor(list(self.task_params.start_rot), device=dev)
         self.initial_root_states = self.root_states.clone()
         self.initial_root_states[:, 7:13] = 0
@@ -187,6 +191,10 @@ class VecTask(Env):
         self.heading_vec = torch.zeros((A, 3), device=dev, dtype=torch.float)
         self.heading_vec[:, 0] = 1.0
         self.targets = torch.tensor([[1000.0, 0.0, 0.0]], device=dev).repeat(A, 1)
+        if self.num_agents > 1:
+            self.targets += self.root_states[:, 0:3] - self.root_states[:, 0:3].new_tensor(
+                list(self.task_params.start_pos))
+            self.targets[:, 2] = 0.0
         self._noise = None
         tb = _abi.TaskBuffers()
         tb.actions_out, tb.obs = _abi.ptr(self.actions), _abi.ptr(self.obs_buf)

@@ -63,10 +63,24 @@ class Humanoid(_Locomotion):
 
 
 class MAAnt(_Locomotion):
-    """Multi-agent Ant (build-defined, SURVEY.md §8(a) row A-MA) — see tasks/ma_ant.py."""
+    """Multi-agent Ant (build-defined, SURVEY.md §8(a) row A-MA).
+
+    ``numAgents`` (default 4) ant actors per env on a square grid ``agentSpacing`` apart.
+    Buffers are ``(num_envs * num_agents, ...)`` env-major like the fork's MA tasks
+    (franka_reach_MA.py:22-38); obs per agent = the 60-d Ant obs + the other agents' torso
+    positions relative to self in cyclic-shift order (franka_reach_MA.py:604-608) = 69-d for
+    A = 4; reward per agent = compute_ant_reward; an env resets only when all of its agents
+    are done (AND filter, franka_reach_MA.py:875-885).  Agents do not collide with each other
+    (each is an independent articulation).
+    """
     task_name = "MAAnt"
     num_obs_default = 60
     num_act_default = 8
 
-    def __init__(self, *a, **k):
-        raise NotImplementedError("MAAnt lands with the multi-agent kernels")
+    def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
+                 force_render=False):
+        A = int(cfg["env"].get("numAgents", 4))
+        cfg["env"]["numAgents"] = A
+        self.num_obs_default = 60 + 3 * (A - 1)
+        super().__init__(cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture,
+                         force_render)

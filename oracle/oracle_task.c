@@ -102,10 +102,12 @@ typedef struct {
   float potential;
 } loco_feat;
 
-static void loco_features(const mg_task_params* tp, const float* root, const float* inv_start, loco_feat* f) {
+static void loco_features(const mg_task_params* tp, const float* root, const float* inv_start, const float* off,
+                          loco_feat* f) {
   const float* pos = root;
   const float* rot = root + 3;
-  float to_target[3] = {tp->target[0] - pos[0], tp->target[1] - pos[1], 0.0f};
+  const float tg[3] = {tp->target[0] + off[0], tp->target[1] + off[1], tp->target[2] + off[2]};
+  float to_target[3] = {tg[0] - pos[0], tg[1] - pos[1], 0.0f};
   float nrm = sqrtf(to_target[0] * to_target[0] + to_target[1] * to_target[1] + to_target[2] * to_target[2]);
   f->potential = -nrm / tp->dt;
   float nc = nrm < 1e-9f ? 1e-9f : nrm;
@@ -119,7 +121,7 @@ static void loco_features(const mg_task_params* tp, const float* root, const flo
   f_quat_rotate(f->torso_quat, root + 7, f->vel_loc, 1);
   f_quat_rotate(f->torso_quat, root + 10, f->angvel_loc, 1);
   f_euler_xyz(f->torso_quat, &f->roll, &f->pitch, &f->yaw);
-  float wta = atan2f(tp->target[2] - pos[2], tp->target[0] - pos[0]);
+  float wta = atan2f(tg[2] - pos[2], tg[0] - pos[0]);
   f->angle_to_target = wta - f->yaw;
 }
 
@@ -143,10 +145,12 @@ static void obs_one(const mg_task_params* tp, int e, const float* root_states, c
     return;
   }
   const float* root = root_states + 13 * e;
+  const int A = tp->num_agents > 1 ? tp->num_agents : 1;
+  const float* off = tp->agent_offset[e % A];
   float inv[4];
   inv_start_rot(tp, inv);
   loco_feat f;
-  loco_features(tp, root, inv, &f);
+  loco_features(tp, root, inv, off, &f);
   prev_potentials[e] = potentials[e];
   potentials[e] = f.potential;
   for (int i = 0; i < 3; i++) { up_vec[3 * e + i] = f.up_vec[i]; heading_vec[3 * e + i] = f.heading_vec[i]; }
@@ -175,6 +179,13 @@ static void obs_one(const mg_task_params* tp, int e, const float* root_states, c
     for (int i = 0; i < nd; i++) o[k++] = dof_force[(size_t)nd * e + i] * tp->contact_force_scale;
   for (int i = 0; i < 6 * ns; i++) o[k++] = sen[i] * tp->contact_force_scale;
   for (int i = 0; i < na; i++) o[k++] = act[i];
+  if (A > 1) {  /* others, cyclic shift after self (franka_reach_MA.py:604-608), relative to self */
+    const int ag = e % A, base = e - ag;
+    for (int j = 1; j < A; j++) {
+      const float* q = root_states + 13 * (base + (ag + j) % A);
+      for (int c = 0; c < 3; c++) o[k++] = q[c] - root[c];
+    }
+  }
 }
 
 int orc_compute_observations(const mg_task_params* tp, int32_t n, const float* root_states, const float* dof_state,
@@ -265,11 +276,13 @@ static void reset_one(const mg_task_params* tp, int e, const mg_state_views* v, 
       dof[2 * i] = q;
       dof[2 * i + 1] = vel;
     }
+    const int A = tp->num_agents > 1 ? tp->num_agents : 1;
+    const float* off = tp->agent_offset[e % A];
     float* root = v->root_states + 13 * e;
-    for (int k = 0; k < 3; k++) root[k] = tp->start_pos[k];
+    for (int k = 0; k < 3; k++) root[k] = tp->start_pos[k] + off[k];
     for (int k = 0; k < 4; k++) root[3 + k] = tp->start_rot[k];
     for (int k = 7; k < 13; k++) root[k] = 0.0f;
-    float tt[3] = {tp->target[0] - tp->start_pos[0], tp->target[1] - tp->start_pos[1], 0.0f};
+    float tt[3] = {(tp->target[0] + off[0]) - root[0], (tp->target[1] + off[1]) - root[1], 0.0f};
     float nrm = sqrtf(tt[0] * tt[0] + tt[1] * tt[1] + tt[2] * tt[2]);
     tb->prev_potentials[e] = -nrm / tp->dt;
     tb->potentials[e] = tb->prev_potentials[e];
@@ -280,28 +293,36 @@ static void reset_one(const mg_task_params* tp, int e, const mg_state_views* v, 
 
 int orc_post_physics(const mg_task_params* tp, const mg_state_views* v, const mg_task_buffers* tb, int32_t n) {
   int na = tp->num_actions, no = tp->num_obs;
+  const int A = tp->num_agents > 1 ? tp->num_agents : 1;
   float* act = tb->actions_out;
-  for (int e = 0; e < n; e++) {
-    for (int i = 0; i < na; i++) {
-      float a = tb->actions[(size_t)na * e + i];
-      a = a < tp->clip_actions ? a : tp->clip_actions;
-      a = a > -tp->clip_actions ? a : -tp->clip_actions;
-      act[(size_t)na * e + i] = a;
-    }
-    tb->progress[e] += 1;
-    if (tb->reset[e] != 0) reset_one(tp, e, v, tb);
-    obs_one(tp, e, v->root_states, v->dof_state, v->dof_force, v->sensors, act, tb->potentials,
-            tb->prev_potentials, tb->up_vec, tb->heading_vec, tb->obs);
-    reward_one(tp, e, tb->obs, act, tb->potentials, tb->prev_potentials, tb->progress, tb->reset, tb->rew);
-    float max_ep_m1 = (float)tp->max_episode_length - 1.0f;
-    tb->timeout[e] = (uint8_t)(((float)tb->progress[e] >= max_ep_m1) && (tb->reset[e] != 0));
-    if (tb->obs_clamped)
-      for (int i = 0; i < no; i++) {
-        float x = tb->obs[(size_t)no * e + i];
-        x = x < tp->clip_obs ? x : tp->clip_obs;
-        x = x > -tp->clip_obs ? x : -tp->clip_obs;
-        tb->obs_clamped[(size_t)no * e + i] = x;
+  for (int base = 0; base < n; base += A) {
+    /* env resets only when all its agents are done (AND filter, franka_reach_MA.py:875-885) */
+    int all_done = 1;
+    for (int k = 0; k < A; k++) all_done &= tb->reset[base + k] != 0;
+    for (int e = base; e < base + A; e++) {
+      for (int i = 0; i < na; i++) {
+        float a = tb->actions[(size_t)na * e + i];
+        a = a < tp->clip_actions ? a : tp->clip_actions;
+        a = a > -tp->clip_actions ? a : -tp->clip_actions;
+        act[(size_t)na * e + i] = a;
       }
+      tb->progress[e] += 1;
+      if (all_done) reset_one(tp, e, v, tb);
+    }
+    for (int e = base; e < base + A; e++) {
+      obs_one(tp, e, v->root_states, v->dof_state, v->dof_force, v->sensors, act, tb->potentials,
+              tb->prev_potentials, tb->up_vec, tb->heading_vec, tb->obs);
+      reward_one(tp, e, tb->obs, act, tb->potentials, tb->prev_potentials, tb->progress, tb->reset, tb->rew);
+      float max_ep_m1 = (float)tp->max_episode_length - 1.0f;
+      tb->timeout[e] = (uint8_t)(((float)tb->progress[e] >= max_ep_m1) && (tb->reset[e] != 0));
+      if (tb->obs_clamped)
+        for (int i = 0; i < no; i++) {
+          float x = tb->obs[(size_t)no * e + i];
+          x = x < tp->clip_obs ? x : tp->clip_obs;
+          x = x > -tp->clip_obs ? x : -tp->clip_obs;
+          tb->obs_clamped[(size_t)no * e + i] = x;
+        }
+    }
   }
   return 0;
 }

@@ -117,6 +117,10 @@ class HostEnv:
         self.root = np.zeros((n, 13), np.float32)
         self.root[:, 0:3] = np.array(tp.start_pos[:3], np.float32)
         self.root[:, 3:7] = np.array(tp.start_rot[:4], np.float32)
+        A = max(int(tp.num_agents), 1)
+        if A > 1:
+            offs = np.array([list(tp.agent_offset[k]) for k in range(A)], np.float32)
+            self.root[:, 0:3] += np.tile(offs, (n // A, 1))
         self.dof = np.zeros((n, nd, 2), np.float32)
         self.act_eff = np.zeros((n, nd), np.float32)
         self.sensors = np.zeros((n, max(ns, 1) * 6), np.float32)

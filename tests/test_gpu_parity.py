@@ -330,3 +330,59 @@ def test_full_size_rollout_is_sane(task, n):
     assert int(env.progress_buf.min()) >= 0 and float(env.root_states[:, 2].min()) > 0.0
     assert extras["time_outs"].dtype == torch.bool
     env.close()
+
+
+# -------------------------------------------------------------------------------------- multi-agent
+def ma_setup(A=4):
+    cfg = configs.task_config("MAAnt", 16)
+    cfg["env"]["numAgents"] = A
+    spec = M.load_builtin("ant")
+    return spec, taskdefs.sim_params(cfg, 16, A), taskdefs.task_params("MAAnt", cfg, spec)
+
+
+@pytest.mark.parametrize("A", [2, 4, 8])
+def test_multi_agent_env_step_matches_oracle(lib, A):
+    """MAAnt fused step (AND-filter resets via wave ballot, others-block via shuffles) vs the oracle."""
+    spec, sp, tp = ma_setup(A)
+    n = A * 96
+    h = O.HostEnv(tp, spec, n)
+    e = DevEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    rng = np.random.default_rng(11)
+    for t in range(4):
+        a = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+        h.actions[:] = a
+        e.actions.copy_(T(a))
+        if t == 2:  # force a mix of fully-done and partially-done envs
+            m = (rng.random(n) < 0.6).astype(np.int64)
+            h.reset[:] = m
+            e.reset.copy_(T(m, torch.int64))
+        h.env_step(mnp, sp, tp, seed=9, step=t, threads=8)
+        _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=9, step=t)), stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    np.testing.assert_array_equal(e.progress.cpu().numpy(), h.progress)
+    np.testing.assert_array_equal(e.reset.cpu().numpy(), h.reset)
+    og = e.obs.cpu().numpy()
+    assert og.shape[1] == 60 + 3 * (A - 1)
+    bad = np.abs(og - h.obs) > (2e-2 + 2e-2 * np.abs(h.obs))
+    assert bad.mean() < 1e-3, (bad.sum(), np.argwhere(bad)[:10])
+
+
+def test_multi_agent_make_full_size():
+    import migym
+    n = 4096
+    env = migym.make(seed=0, task="MAAnt", num_envs=n, sim_device=DEV, rl_device=DEV, headless=True)
+    assert env.num_agents == 4 and env.num_obs == 69
+    from migym.utils.rlgames_utils import RLGPUEnv
+    assert RLGPUEnv(env).get_env_info()["agents"] == 4
+    a = torch.rand((n * 4, 8), device=DEV) * 2 - 1
+    for _ in range(5):
+        obs, rew, reset, extras = env.step(a)
+    torch.cuda.synchronize()
+    assert obs["obs"].shape == (n * 4, 69) and rew.shape == (n * 4,)
+    assert torch.isfinite(obs["obs"]).all()
+    env.close()
