@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "isaacgymenvs-ma_amd"))
 
 # algorithmic (compulsory) HBM bytes per env-step: every gym/VecTask-visible tensor
 # read and written once per control step; model tables amortised to 0.
-ALGO_BYTES = {"Ant": 673, "Humanoid": 1161, "Cartpole": 89, "MAAnt": 2800}
+ALGO_BYTES = {"Ant": 673, "Humanoid": 1161, "Cartpole": 89, "MAAnt": 4 * 709}
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md (spec)
 
 
@@ -43,7 +43,7 @@ def cpu_baseline(task, seconds=12.0, n=4096):
     h.actions[:] = acts[0]
     h.env_step(mnp, sp, tp, 0, 0, cores)  # warm-up (first step resets every env)
     steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds and steps < 500:
+    while time.perf_counter() - t0 < seconds and steps < 5000:
         h.actions[:] = acts[steps % 8]
         h.env_step(mnp, sp, tp, 0, steps + 1, cores)
         steps += 1
@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--task", default="Ant")
     ap.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="all-gather obs/rew/reset of every rank each step (one RCCL collective)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -83,8 +85,18 @@ def main():
     na = env.num_actions
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
+    gather = None
+    if args.gather and world > 1:
+        from migym.dist import OutputGather
+        gather = OutputGather(env.num_actors, env.num_obs, dev)
+
+    def step(a):
+        obs, rew, reset, _ = env.step(a)
+        if gather is not None:
+            gather(obs["obs"], rew, reset)
+
     for i in range(args.warmup):
-        env.step(pool[i % 8])
+        step(pool[i % 8])
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -95,7 +107,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         starts[i].record(stream)
-        env.step(pool[i % 8])
+        step(pool[i % 8])
         ends[i].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -106,7 +118,6 @@ def main():
         t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-    total_envs = n * env.num_agents * world if args.task == "MAAnt" else n * world
     value = n * world * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     if rank == 0:
@@ -118,7 +129,9 @@ def main():
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (U(-1,1) actions, device-resident)",
             "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, 2 substeps, PGS x4",
-                       "task": args.task, "num_envs_per_gpu": n, "num_envs_total": total_envs,
+                       "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
+                       "agents_per_env": env.num_agents, "agent_steps_per_s": value * env.num_agents,
+                       "obs_allgather": bool(gather is not None),
                        "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": None,

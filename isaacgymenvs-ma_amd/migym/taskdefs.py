@@ -17,6 +17,7 @@ TASK_INFO = {
     "Ant": (_abi.MG_TASK_ANT, "ant", 60, 8, 0.44, 16),
     "Humanoid": (_abi.MG_TASK_HUMANOID, "humanoid", 108, 21, 1.34, 32),
 }
+TASK_INFO["MAAnt"] = TASK_INFO["Ant"]   # per-agent physics/obs of the multi-agent Ant are the Ant's
 
 # build-defined solver constants
 BAUMGARTE = 0.2

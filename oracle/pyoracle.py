@@ -146,7 +146,7 @@ class HostEnv:
         v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), None
         return v
 
-    def buffers(self, seed=0, step=0):
+    def buffers(self, seed=0, step=0, env_offset=0):
         b = _abi.TaskBuffers()
         b.actions, b.actions_out, b.obs, b.obs_clamped = p(self.actions), p(self.actions_out), p(self.obs), \
             p(self.obs_clamped)
@@ -154,13 +154,13 @@ class HostEnv:
         b.potentials, b.prev_potentials = p(self.potentials), p(self.prev_potentials)
         b.up_vec, b.heading_vec = p(self.up), p(self.heading)
         b.noise = p(self.noise)
-        b.seed, b.step_counter, b.env_offset = seed, step, 0
+        b.seed, b.step_counter, b.env_offset = seed, step, env_offset
         return b
 
-    def post_physics(self, tp, seed=0, step=0):
-        v, b = self.views(), self.buffers(seed, step)
+    def post_physics(self, tp, seed=0, step=0, env_offset=0):
+        v, b = self.views(), self.buffers(seed, step, env_offset)
         lib().orc_post_physics(C.byref(tp), C.byref(v), C.byref(b), self.n)
 
-    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0):
-        v, b = self.views(), self.buffers(seed, step)
+    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0):
+        v, b = self.views(), self.buffers(seed, step, env_offset)
         lib().orc_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v), C.byref(b), self.n, threads)
