@@ -7,7 +7,7 @@
 #include <string>
 
 #include "../../include/migym.h"
-#include "physics.hpp"
+#include "team_physics.hpp"
 #include "task.hpp"
 
 namespace {
@@ -37,19 +37,37 @@ struct mg_sim {
 };
 
 // ------------------------------------------------------------------------------------------------ kernels
-template <int MN, int MC>
+// gym.simulate: one team of T lanes per actor (team_physics.hpp)
+template <int T, int MN, int MC>
 __global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p, int n,
                                                      float* __restrict__ root, float* __restrict__ dof,
                                                      const float* __restrict__ act, float* __restrict__ sensors,
                                                      float* __restrict__ dof_force) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
+  constexpr int E = kBlock / T;
+  __shared__ mg::TeamLDS<T, MN, MC> lds[E];
+  const int team = threadIdx.x / T;
+  const int a = blockIdx.x * E + team;
+  const bool valid = a < n;
+  const int ac = valid ? a : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors;
-  float tau[MN];
-  for (int i = 0; i < nd; i++) tau[i] = act ? act[(size_t)nd * e + i] : 0.0f;
-  mg::simulate_actor<MN, MC>(m, &p, root + (size_t)13 * e, dof + (size_t)2 * nd * e, tau,
-                             sensors ? sensors + (size_t)6 * ns * e : nullptr,
-                             dof_force ? dof_force + (size_t)nd * e : nullptr);
+  mg::Team<T, MN, MC> t;
+  t.init(&lds[team], m, &p);
+  __syncthreads();
+  t.load(root + (size_t)13 * ac, dof + (size_t)2 * nd * ac, act ? act + (size_t)nd * ac : nullptr);
+  for (int st = 0; st < p.substeps; st++) t.substep();
+  t.outputs(lds[team].sens, lds[team].dforce);
+  t.stage_state();
+  __syncthreads();
+  if (valid) {
+    mg::TeamLDS<T, MN, MC>& L = lds[team];
+    if (!m->fixed_base)
+      for (int k = t.tl; k < 13; k += T) root[(size_t)13 * a + k] = L.root[k];
+    for (int k = t.tl; k < 2 * nd; k += T) dof[(size_t)2 * nd * a + k] = L.dof[k];
+    if (sensors)
+      for (int k = t.tl; k < 6 * ns; k += T) sensors[(size_t)6 * ns * a + k] = L.sens[k];
+    if (dof_force)
+      for (int k = t.tl; k < nd; k += T) dof_force[(size_t)nd * a + k] = L.dforce[k];
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_observations(mg_task_params tp, int n, const float* __restrict__ root,
@@ -153,31 +171,121 @@ __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_s
   post_physics_env(tp, v, tb, e, act, tb.reset[e]);
 }
 
-// The whole VecTask.step for one env, fused: clamp -> actuation -> simulate -> post_physics.
-template <int MN, int MC>
+// The whole VecTask.step for one actor, fused: clamp -> actuation -> simulate -> post_physics.
+// One team of T lanes per actor; the team leader (tl == 0) runs the task layer on the LDS-staged
+// state, the team writes it back to HBM.  Multi-agent: the agents of an env are consecutive
+// teams of one wave, so the AND-filter is a ballot over team leaders and the others-block a
+// shuffle from the other agents' leaders.
+template <int T, int MN, int MC>
 __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
+  constexpr int E = kBlock / T;
+  __shared__ mg::TeamLDS<T, MN, MC> lds[E];
+  const int team = threadIdx.x / T;
+  const int a = blockIdx.x * E + team;
+  const bool valid = a < n;
+  const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
-  const int64_t reset_in = tb.reset[e];
-  float act[MN];
-  for (int i = 0; i < na; i++) {
-    act[i] = mg::clampf(tb.actions[(size_t)na * e + i], tp.clip_actions);
-    if (tb.actions_out) tb.actions_out[(size_t)na * e + i] = act[i];
+  mg::TeamLDS<T, MN, MC>& L = lds[team];
+  mg::Team<T, MN, MC> t;
+  t.init(&L, m, &p);
+  __syncthreads();
+  const int64_t reset_in = tb.reset[ac];
+  // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
+  t.load(v.root_states + (size_t)13 * ac, v.dof_state + (size_t)2 * nd * ac, nullptr);
+  if (t.node > 0) {
+    const int d = t.node - 1;
+    float tau;
+    if (tp.task_id == MG_TASK_CARTPOLE) {
+      tau = d == 0 ? mg::clampf(tb.actions[(size_t)na * ac], tp.clip_actions) * tp.power_scale : 0.0f;
+    } else {
+      const float act = d < na ? mg::clampf(tb.actions[(size_t)na * ac + d], tp.clip_actions) : 0.0f;
+      tau = act * tp.motor_effort[d] * tp.power_scale;
+    }
+    t.tau = tau;
+    if (valid && v.dof_actuation) const_cast<float*>(v.dof_actuation)[(size_t)nd * a + d] = tau;
   }
-  float tau[MN];
-  for (int i = 0; i < nd; i++) {
-    float t;
-    if (tp.task_id == MG_TASK_CARTPOLE) t = i == 0 ? act[0] * tp.power_scale : 0.0f;  // cartpole.py:159-163
-    else t = act[i] * tp.motor_effort[i] * tp.power_scale;                           // ant.py:283-285
-    tau[i] = t;
-    if (v.dof_actuation) const_cast<float*>(v.dof_actuation)[(size_t)nd * e + i] = t;
+  for (int st = 0; st < p.substeps; st++) t.substep();
+  t.outputs(L.sens, L.dforce);
+  t.stage_state();
+  __syncthreads();
+
+  // ---------------- post_physics_step (ant.py:287-297) on the staged state
+  const int A = tp.num_agents > 1 ? tp.num_agents : 1;
+  const int k = a % A;
+  const float* off = tp.agent_offset[k];
+  const int lane = threadIdx.x & 63;
+  bool do_reset = reset_in != 0;
+  if (A > 1) {  // AND filter over the env's agents (franka_reach_MA.py:875-885)
+    const unsigned long long mk = __ballot(t.tl == 0 && valid && reset_in != 0);
+    bool all = true;
+    for (int j = 0; j < A; j++) all = all && ((mk >> ((team - k + j) * T)) & 1ull);
+    do_reset = all;
   }
-  mg::simulate_actor<MN, MC>(m, &p, v.root_states + (size_t)13 * e, v.dof_state + (size_t)2 * nd * e, tau,
-                             v.sensors ? v.sensors + (size_t)6 * ns * e : nullptr,
-                             v.dof_force ? v.dof_force + (size_t)nd * e : nullptr);
-  post_physics_env(tp, v, tb, e, act, reset_in);
+  float pot = 0.0f, prev = 0.0f, up[3] = {0, 0, 0}, hd[3] = {0, 0, 0};
+  int64_t progress = tb.progress[ac] + 1;
+  int64_t reset = reset_in;
+  float act[64];
+  if (t.tl == 0) {
+    for (int i = 0; i < na; i++) {
+      act[i] = mg::clampf(tb.actions[(size_t)na * ac + i], tp.clip_actions);
+      if (valid && tb.actions_out) tb.actions_out[(size_t)na * a + i] = act[i];
+    }
+    if (tb.potentials) { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
+    if (do_reset) {
+      mg::reset_env(&tp, off, tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr, tb.seed,
+                    (uint64_t)(tb.env_offset + a), tb.step_counter, L.root, L.dof, &pot, &prev);
+      progress = 0;
+      reset = 0;
+    }
+  }
+  __syncthreads();
+  const int no = tp.num_obs;
+  float* o = tb.obs + (size_t)no * ac;
+  if (t.tl == 0 && valid)
+    mg::obs_env(&tp, off, L.root, L.dof, L.dforce, L.sens, act, &pot, &prev, up, hd, o);
+  if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
+    const float px = L.root[0], py = L.root[1], pz = L.root[2];
+    const int base = no - 3 * (A - 1);
+    for (int j = 1; j < A; j++) {
+      const int src = (team - k + (k + j) % A) * T;
+      const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
+      if (t.tl == 0 && valid) {
+        o[base + 3 * (j - 1) + 0] = qx - px;
+        o[base + 3 * (j - 1) + 1] = qy - py;
+        o[base + 3 * (j - 1) + 2] = qz - pz;
+      }
+    }
+  }
+  if (t.tl == 0 && valid) {
+    float rew;
+    mg::reward_env(&tp, o, act, pot, prev, progress, &reset, &rew);
+    const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
+    tb.rew[a] = rew;
+    tb.reset[a] = reset;
+    tb.progress[a] = progress;
+    tb.timeout[a] = (uint8_t)(((float)progress >= max_ep_m1) && (reset != 0));
+    if (tp.task_id != MG_TASK_CARTPOLE) {
+      tb.potentials[a] = pot;
+      tb.prev_potentials[a] = prev;
+      for (int c = 0; c < 3; c++) {
+        tb.up_vec[3 * (size_t)a + c] = up[c];
+        tb.heading_vec[3 * (size_t)a + c] = hd[c];
+      }
+    }
+    if (tb.obs_clamped)
+      for (int i = 0; i < no; i++) tb.obs_clamped[(size_t)no * a + i] = mg::clampf(o[i], tp.clip_obs);
+  }
+  __syncthreads();
+  if (valid) {  // state write-back (gym layouts), team-cooperative
+    if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
+      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.root[q];
+    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.dof[q];
+    if (v.sensors)
+      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.sens[q];
+    if (v.dof_force)
+      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.dforce[q];
+  }
 }
 
 __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
@@ -190,34 +298,39 @@ __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------ dispatch
-// Kernel instances by capacity: nodes MN, contacts MC (chosen as the smallest that fits the model).
-#define MG_INSTANCES(X) X(4, 8) X(9, 16) X(16, 24) X(24, 32) X(40, 48)
+// Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
+// contacts MC.  The smallest instance that fits the model is launched.
+#define MG_INSTANCES(X) X(8, 4, 8) X(16, 9, 16) X(16, 16, 24) X(32, 24, 32) X(32, 32, 48) X(64, 40, 48)
 
-template <template <int, int> class F, typename... A>
+template <template <int, int, int> class F, typename... A>
 static int dispatch(const mg_model& m, int max_contacts, A... args) {
-#define MG_TRY(MN, MC)                                          \
-  if (m.num_nodes <= MN && max_contacts <= MC) {                \
-    F<MN, MC>::run(args...);                                    \
-    return MG_OK;                                               \
+  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
+  const int lanes = nv > m.num_sensors ? nv : m.num_sensors;
+#define MG_TRY(T, MN, MC)                                                       \
+  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6)) { \
+    F<T, MN, MC>::run(args...);                                                 \
+    return MG_OK;                                                               \
   }
   MG_INSTANCES(MG_TRY)
 #undef MG_TRY
   return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
 }
 
-template <int MN, int MC>
+template <int T, int MN, int MC>
 struct RunSimulate {
   static void run(hipStream_t s, const mg_sim* sim) {
     const mg_state_views& v = sim->views;
-    hipLaunchKernelGGL((k_simulate<MN, MC>), dim3(grid_for(sim->n)), dim3(kBlock), 0, s, sim->d_model, sim->params,
-                       sim->n, v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force);
+    const int E = kBlock / T;
+    hipLaunchKernelGGL((k_simulate<T, MN, MC>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
+                       sim->params, sim->n, v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force);
   }
 };
-template <int MN, int MC>
+template <int T, int MN, int MC>
 struct RunEnvStep {
   static void run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
-    hipLaunchKernelGGL((k_env_step<MN, MC>), dim3(grid_for(sim->n)), dim3(kBlock), 0, s, sim->d_model, sim->params,
-                       *tp, sim->views, *tb, sim->n);
+    const int E = kBlock / T;
+    hipLaunchKernelGGL((k_env_step<T, MN, MC>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
+                       sim->params, *tp, sim->views, *tb, sim->n);
   }
 };
 

@@ -1,0 +1,746 @@
+// team_physics.hpp — gym.simulate on gfx950 with one *team* of T lanes per actor
+// (SURVEY.md §8(a) rows A3-A9).  Same algorithm as physics.hpp/the oracle
+// (ABA + speculative contacts + PGS + semi-implicit Euler),
+// mapped onto a 64-wide wave so that nothing spills to scratch:
+//
+//   lane roles inside a team (tl = lane % T):
+//     * generalized-velocity column j = tl  (nu_j lives in lane j's registers;
+//       free base: j < 6 are the root twist [w; v_o], j >= 6 the joints)
+//     * tree node: node i >= 1 lives on lane col(i) = (free ? 5 : -1) + i, the
+//       root node on lane 0.  A node's kinematics (R, x, S, V), articulated
+//       inertia (21 floats) and ABA factors (U, 1/D) stay in its lane.
+//   tree recursions (FK, ABA backward/forward) are level-synchronous: nodes
+//   of one depth compute together and publish what children/parents need in
+//   the team's LDS tile; the per-child articulated-inertia contributions are
+//   summed by the parent lane from LDS (deterministic order, no atomics).
+//   contact generation: lane per geom / per self-pair, compaction by a team
+//   prefix scan (shuffles), preserving the oracle's contact order.
+//   constraint rows: the response column Y_r = M~^-1 J_r^T is produced by a
+//   test-force ABA solve whose output lands distributed — lane j keeps
+//   Y_r[j] in a register (Ycol[r]); PGS row updates are then a team dot
+//   product (butterfly shuffles) plus one FMA per lane.
+// All lanes of a wave run every phase (teams never diverge on barriers);
+// the block is one wave, so __syncthreads() is a cheap wave barrier.
+#pragma once
+#include "../../include/migym.h"
+#include "device_math.hpp"
+
+namespace mg {
+
+template <int T, int MN, int MC>
+struct TeamLDS {
+  static constexpr int MR = 3 * MC + 2 * (MN - 1);
+  float R[MN][9];
+  float x[MN][3];
+  float V[MN][6];
+  float S[MN][6];
+  float U[MN][6];
+  float Dinv[MN];
+  float slot[MN][27];
+  float acc[MN][6];
+  float ut[MN];
+  unsigned long long anc[MN];
+  float L0[21];
+  float proot[6];
+  int ncon, nrows;
+  float cp[MC][3], cn[MC][3], cd[MC];
+  int cA[MC], cB[MC], cgA[MC], cgB[MC];
+  float rw[MR][6];
+  float rb[MR], rW[MR], rlam[MR], rsg[MR];
+  int rkind[MR], rref[MR], rA[MR], rB[MR];
+  // task-layer staging (root / dof state of the actor after the physics)
+  float root[13];
+  float dof[2 * MN];
+  float sens[6 * MG_MAX_SENSORS];
+  float dforce[MN];
+};
+
+template <int T>
+__device__ __forceinline__ float team_sum(float v, int tb) {
+#pragma unroll
+  for (int m = T / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, T);
+  return __shfl(v, tb);  // identical bits in every lane of the team
+}
+template <int T>
+__device__ __forceinline__ int team_incl_scan(int v) {
+  const int tl = threadIdx.x % T;
+#pragma unroll
+  for (int d = 1; d < T; d <<= 1) {
+    int o = __shfl_up(v, d, T);
+    if (tl >= d) v += o;
+  }
+  return v;
+}
+template <int T>
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m));
+  return v;
+}
+
+__device__ __forceinline__ void tangent_basis_t(V3 n, V3* t1, V3* t2) {
+  V3 a = fabsf(n.x) < 0.57735f ? v3(1, 0, 0) : v3(0, 1, 0);
+  V3 t = cross(a, n);
+  t = t * (1.0f / sqrtf(dot(t, t)));
+  *t1 = t;
+  *t2 = cross(n, t);
+}
+
+// Per-lane context of one team.
+template <int T, int MN, int MC>
+struct Team {
+  using L = TeamLDS<T, MN, MC>;
+  static constexpr int MR = L::MR;
+  L* s;
+  const mg_model* m;
+  const mg_sim_params* p;
+  int tl, tb;          // team lane, first lane of the team (absolute)
+  bool freeb;
+  int nn, nv, ncol0;   // nodes, velocity columns, first joint column
+  int node;            // node owned by this lane (-1: none)
+  int depth, maxdepth;
+  int par;
+  // state
+  float nu;            // generalized velocity column tl (valid if tl < nv)
+  float qj, tau;       // joint position / actuation (node lanes)
+  V3 p0;               // root position (lane 0)
+  float q0[4];         // root orientation (lane 0)
+  // kinematics / dynamics of own node
+  M3 R;
+  V3 x;
+  SV S, V, c, U, pA;
+  Sym6 IA;
+  float Dinv, u;
+  float h;
+
+  __device__ int col_of(int i) const { return ncol0 - 1 + i; }
+
+  __device__ void init(L* lds, const mg_model* mm, const mg_sim_params* pp) {
+    s = lds;
+    m = mm;
+    p = pp;
+    tl = threadIdx.x % T;
+    tb = threadIdx.x - tl;
+    freeb = !m->fixed_base;
+    nn = m->num_nodes;
+    ncol0 = freeb ? 6 : 0;
+    nv = ncol0 + nn - 1;
+    node = -1;
+    if (freeb && tl == 0) node = 0;
+    if (tl >= ncol0 && tl - ncol0 + 1 < nn) node = tl - ncol0 + 1;
+    par = node > 0 ? m->parent[node] : -1;
+    depth = 0;
+    unsigned long long anc = 0ull;
+    if (node > 0) {
+      for (int k = node; k > 0; k = m->parent[k]) {
+        anc |= 1ull << k;
+        depth++;
+      }
+      anc |= 1ull;
+      s->anc[node] = anc;
+    }
+    if (tl == 0) s->anc[0] = 1ull;
+    maxdepth = wave_max<T>(depth);
+    h = p->dt / (float)p->substeps;
+    nu = 0.0f;
+    qj = 0.0f;
+    tau = 0.0f;
+  }
+  __device__ bool in_path(int target, int k) const { return target >= 0 && ((s->anc[target] >> k) & 1ull); }
+
+  // ---------------------------------------------------------------- FK (level-synchronous)
+  __device__ void fk() {
+    if (tl == 0) {
+      M3 R0 = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) s->R[0][3 * a + b] = R0.m[a][b];
+      s->x[0][0] = p0.x; s->x[0][1] = p0.y; s->x[0][2] = p0.z;
+      if (!freeb)
+        for (int k = 0; k < 6; k++) s->V[0][k] = 0.0f;
+    }
+    if (freeb && tl < 6) s->V[0][tl] = nu;
+    __syncthreads();
+    if (node == 0) {
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) R.m[a][b] = s->R[0][3 * a + b];
+      x = ld3(s->x[0]);
+      V = sv(ld3(s->V[0]), ld3(s->V[0] + 3));
+    }
+    for (int lev = 1; lev <= maxdepth; lev++) {
+      if (node > 0 && depth == lev) {
+        M3 Rp;
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) Rp.m[a][b] = s->R[par][3 * a + b];
+        V3 xp = ld3(s->x[par]);
+        SV Vp = sv(ld3(s->V[par]), ld3(s->V[par] + 3));
+        M3 Rp0 = mul(Rp, quat_to_mat(m->r0[node][0], m->r0[node][1], m->r0[node][2], m->r0[node][3]));
+        V3 tp = mul(Rp, ld3(m->t[node]));
+        V3 ax = ld3(m->axis[node]);
+        if (m->jtype[node] == MG_JT_HINGE) {
+          R = mul(Rp0, axis_angle(ax, qj));
+          x = xp + tp;
+          V3 sw = mul(R, ax);
+          S = sv(sw, cross(x - ld3(s->x[0]), sw));
+        } else {
+          R = Rp0;
+          V3 sw = mul(Rp0, ax);
+          x = xp + tp + sw * qj;
+          S = sv(v3(0, 0, 0), sw);
+        }
+        V = Vp + S * nu;
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) s->R[node][3 * a + b] = R.m[a][b];
+        s->x[node][0] = x.x; s->x[node][1] = x.y; s->x[node][2] = x.z;
+        s->V[node][0] = V.a.x; s->V[node][1] = V.a.y; s->V[node][2] = V.a.z;
+        s->V[node][3] = V.l.x; s->V[node][4] = V.l.y; s->V[node][5] = V.l.z;
+        s->S[node][0] = S.a.x; s->S[node][1] = S.a.y; s->S[node][2] = S.a.z;
+        s->S[node][3] = S.l.x; s->S[node][4] = S.l.y; s->S[node][5] = S.l.z;
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---------------------------------------------------------------- ABA (unconstrained step)
+  __device__ void aba() {
+    if (node >= 0) {
+      const V3 o = ld3(s->x[0]);
+      V3 cc = x + mul(R, ld3(m->com[node])) - o;
+      const float* in = m->inertia[node];
+      float Il[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
+      float Tm[3][3], Iw[6];
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Tm[a][b] = R.m[a][0] * Il[0][b] + R.m[a][1] * Il[1][b] + R.m[a][2] * Il[2][b];
+      const int idx[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+      for (int k = 0; k < 6; k++) {
+        int a = idx[k][0], b = idx[k][1];
+        Iw[k] = Tm[a][0] * R.m[b][0] + Tm[a][1] * R.m[b][1] + Tm[a][2] * R.m[b][2];
+      }
+      const float mass = m->mass[node];
+      IA = body_inertia(mass, cc, Iw);
+      SV IV = mul(IA, V);
+      V3 mg = ld3(p->gravity) * mass;
+      pA = crf(V, IV) - sv(cross(cc, mg), mg);
+      c = node == 0 ? szero() : crm(V, S * nu);
+    }
+    for (int lev = maxdepth; lev >= 1; lev--) {
+      if (node > 0 && depth == lev) {
+        U = mul(IA, S);
+        float D = dot(S, U) + m->armature[node] + h * m->damping[node] + h * h * m->stiffness[node];
+        Dinv = 1.0f / D;
+        float t = tau - m->damping[node] * nu - m->stiffness[node] * (qj + h * nu);
+        u = t - dot(S, pA);
+        Sym6 Ia = IA;
+        rank1_sub(Ia, U, Dinv);
+        SV pa = pA + mul(Ia, c) + U * (u * Dinv);
+        float* sl = s->slot[node];
+        for (int k = 0; k < 6; k++) { sl[k] = Ia.a[k]; sl[15 + k] = Ia.c[k]; }
+        for (int k = 0; k < 9; k++) sl[6 + k] = Ia.b[k];
+        sl[21] = pa.a.x; sl[22] = pa.a.y; sl[23] = pa.a.z;
+        sl[24] = pa.l.x; sl[25] = pa.l.y; sl[26] = pa.l.z;
+        s->U[node][0] = U.a.x; s->U[node][1] = U.a.y; s->U[node][2] = U.a.z;
+        s->U[node][3] = U.l.x; s->U[node][4] = U.l.y; s->U[node][5] = U.l.z;
+        s->Dinv[node] = Dinv;
+      }
+      __syncthreads();
+      if (node >= 0 && depth == lev - 1) {
+        for (int k = 1; k < nn; k++) {
+          if (m->parent[k] != node) continue;
+          const float* sl = s->slot[k];
+          for (int q = 0; q < 6; q++) { IA.a[q] += sl[q]; IA.c[q] += sl[15 + q]; }
+          for (int q = 0; q < 9; q++) IA.b[q] += sl[6 + q];
+          pA = pA + sv(v3(sl[21], sl[22], sl[23]), v3(sl[24], sl[25], sl[26]));
+        }
+      }
+    }
+    if (tl == 0) {
+      if (freeb) {
+        chol6(IA, s->L0);
+        SV a0 = chol6_solve(s->L0, pA * -1.0f);
+        s->acc[0][0] = a0.a.x; s->acc[0][1] = a0.a.y; s->acc[0][2] = a0.a.z;
+        s->acc[0][3] = a0.l.x; s->acc[0][4] = a0.l.y; s->acc[0][5] = a0.l.z;
+      } else {
+        for (int k = 0; k < 6; k++) s->acc[0][k] = 0.0f;
+      }
+    }
+    __syncthreads();
+    float qdd = 0.0f;
+    for (int lev = 1; lev <= maxdepth; lev++) {
+      if (node > 0 && depth == lev) {
+        SV ap = sv(ld3(s->acc[par]), ld3(s->acc[par] + 3)) + c;
+        qdd = (u - dot(U, ap)) * Dinv;
+        SV a = ap + S * qdd;
+        s->acc[node][0] = a.a.x; s->acc[node][1] = a.a.y; s->acc[node][2] = a.a.z;
+        s->acc[node][3] = a.l.x; s->acc[node][4] = a.l.y; s->acc[node][5] = a.l.z;
+      }
+      __syncthreads();
+    }
+    // nu* = nu + h * acc
+    if (tl < nv) {
+      float a = (freeb && tl < 6) ? s->acc[0][tl] : qdd;
+      nu += h * a;
+    }
+  }
+
+  // ---------------------------------------------------------------- test solve: Y = M~^-1 (J^T) column into lane regs
+  // generalized force: spatial force fw on nodeA (and -fw on nodeB), plus unit joint force sg on node jn.
+  __device__ float test_solve(int nodeA, int nodeB, SV fw, int jn, float sg) {
+    if (node > 0) s->ut[node] = 0.0f;
+    __syncthreads();
+    if (tl == 0) {
+      SV proot = szero();
+      for (int side = 0; side < 3; side++) {
+        int k;
+        SV pv;
+        float tq = 0.0f;
+        if (side == 0) { k = nodeA; pv = fw * -1.0f; }
+        else if (side == 1) { k = nodeB; pv = fw; }
+        else { k = jn; pv = szero(); tq = sg; }
+        if (k < 0 || (side == 2 && k == 0)) continue;
+        while (k > 0) {
+          SV Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3));
+          SV Uk = sv(ld3(s->U[k]), ld3(s->U[k] + 3));
+          float uk = tq - dot(Sk, pv);
+          s->ut[k] += uk;
+          pv = pv + Uk * (uk * s->Dinv[k]);
+          tq = 0.0f;
+          k = m->parent[k];
+        }
+        proot = proot + pv;
+      }
+      SV a0 = freeb ? chol6_solve(s->L0, proot * -1.0f) : szero();
+      s->acc[0][0] = a0.a.x; s->acc[0][1] = a0.a.y; s->acc[0][2] = a0.a.z;
+      s->acc[0][3] = a0.l.x; s->acc[0][4] = a0.l.y; s->acc[0][5] = a0.l.z;
+    }
+    __syncthreads();
+    float y = 0.0f;
+    for (int lev = 1; lev <= maxdepth; lev++) {
+      if (node > 0 && depth == lev) {
+        SV ap = sv(ld3(s->acc[par]), ld3(s->acc[par] + 3));
+        y = (s->ut[node] - dot(U, ap)) * Dinv;
+        SV a = ap + S * y;
+        s->acc[node][0] = a.a.x; s->acc[node][1] = a.a.y; s->acc[node][2] = a.a.z;
+        s->acc[node][3] = a.l.x; s->acc[node][4] = a.l.y; s->acc[node][5] = a.l.z;
+      }
+      __syncthreads();
+    }
+    if (freeb && tl < 6) y = s->acc[0][tl];
+    return tl < nv ? y : 0.0f;
+  }
+
+  // J_r[tl] for row r (contacts: root twist part / path projection; limits: unit on the dof column)
+  __device__ float jac_entry(int r) const {
+    const int kind = s->rkind[r];
+    if (tl >= nv) return 0.0f;
+    if (kind >= 2) return (node > 0 && node == s->rref[r]) ? s->rsg[r] : 0.0f;
+    const float* w = s->rw[r];
+    const int A = s->rA[r], B = s->rB[r];
+    if (freeb && tl < 6) {
+      float sgn = (A >= 0 ? 1.0f : 0.0f) - (B >= 0 ? 1.0f : 0.0f);
+      return sgn * w[tl];
+    }
+    if (node <= 0) return 0.0f;
+    float sgn = (in_path(A, node) ? 1.0f : 0.0f) - (in_path(B, node) ? 1.0f : 0.0f);
+    if (sgn == 0.0f) return 0.0f;
+    return sgn * (S.a.x * w[0] + S.a.y * w[1] + S.a.z * w[2] + S.l.x * w[3] + S.l.y * w[4] + S.l.z * w[5]);
+  }
+
+  // ---------------------------------------------------------------- collision -> LDS contact list
+  __device__ void geom_world(int g, V3* cw, M3* Rg) const {
+    const int nd = m->geom_node[g];
+    M3 Rn;
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) Rn.m[a][b] = s->R[nd][3 * a + b];
+    *cw = ld3(s->x[nd]) + mul(Rn, ld3(m->geom_pos[g]));
+    *Rg = mul(Rn, quat_to_mat(m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]));
+  }
+  __device__ bool geom_segment(int g, V3* a, V3* b, float* r) const {
+    V3 c;
+    M3 Rg;
+    geom_world(g, &c, &Rg);
+    int ty = m->geom_type[g];
+    if (ty == MG_GT_SPHERE) { *a = c; *b = c; *r = m->geom_size[g][0]; return true; }
+    if (ty == MG_GT_CAPSULE) {
+      V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * m->geom_size[g][1];
+      *a = c - ax; *b = c + ax; *r = m->geom_size[g][0];
+      return true;
+    }
+    return false;
+  }
+
+  __device__ void collide() {
+    const int cap = p->max_contacts < MC ? p->max_contacts : MC;
+    const float off = p->contact_offset;
+    int base = 0;
+    const int G = m->num_geoms;
+    // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
+    // pass 1 counts, a team scan places them, pass 2 recomputes and writes (no private arrays).
+    for (int g0 = 0; g0 < G; g0 += T) {
+      const int g = g0 + tl;
+      V3 c = v3(0, 0, 0);
+      M3 Rg;
+      int ty = -1;
+      if (g < G) {
+        geom_world(g, &c, &Rg);
+        ty = m->geom_type[g];
+      }
+      int cnt = 0;
+      for (int pass = 0; pass < 2; pass++) {
+        int k = 0, slot0 = 0;
+        if (pass == 1) {
+          const int incl = team_incl_scan<T>(cnt);
+          slot0 = base + incl - cnt;
+          base += __shfl(incl, tb + T - 1);
+        }
+        const int nc = ty == MG_GT_SPHERE ? 1 : (ty == MG_GT_CAPSULE ? 2 : (ty == MG_GT_BOX ? 8 : 0));
+        for (int q = 0; q < nc; q++) {
+          V3 e;
+          float r;
+          if (ty == MG_GT_SPHERE) {
+            e = c;
+            r = m->geom_size[g][0];
+          } else if (ty == MG_GT_CAPSULE) {
+            V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * m->geom_size[g][1];
+            e = q == 0 ? c - ax : c + ax;
+            r = m->geom_size[g][0];
+          } else {
+            V3 l = v3((q & 1 ? 1.f : -1.f) * m->geom_size[g][0], (q & 2 ? 1.f : -1.f) * m->geom_size[g][1],
+                      (q & 4 ? 1.f : -1.f) * m->geom_size[g][2]);
+            e = c + mul(Rg, l);
+            r = 0.0f;
+          }
+          const float d = e.z - r;
+          if (!(d < off)) continue;
+          if (pass == 0) {
+            cnt++;
+          } else {
+            const int slot = slot0 + k;
+            if (slot < cap) {
+              s->cp[slot][0] = e.x; s->cp[slot][1] = e.y; s->cp[slot][2] = e.z - r;
+              s->cn[slot][0] = 0.0f; s->cn[slot][1] = 0.0f; s->cn[slot][2] = 1.0f;
+              s->cd[slot] = d;
+              s->cA[slot] = m->geom_node[g]; s->cgA[slot] = g; s->cB[slot] = -1; s->cgB[slot] = -1;
+            }
+            k++;
+          }
+        }
+      }
+    }
+    // self-collision pairs: lane per pair, pair order preserved
+    const int P = m->num_pairs;
+    for (int p0 = 0; p0 < P; p0 += T) {
+      const int pi = p0 + tl;
+      int cnt = 0;
+      V3 pt, nrm;
+      float d = 0.0f;
+      int ga = 0, gb = 0;
+      if (pi < P) {
+        ga = m->pair[pi][0];
+        gb = m->pair[pi][1];
+        V3 a0, a1, b0, b1;
+        float ra, rb;
+        if (geom_segment(ga, &a0, &a1, &ra) && geom_segment(gb, &b0, &b1, &rb)) {
+          V3 ca = (a0 + a1) * 0.5f, cb = (b0 + b1) * 0.5f, dc = ca - cb;
+          float ha = sqrtf(dot(a1 - a0, a1 - a0)) * 0.5f, hb = sqrtf(dot(b1 - b0, b1 - b0)) * 0.5f;
+          float reach = ha + hb + ra + rb + off;
+          if (dot(dc, dc) <= reach * reach) {
+            float ss, tt;
+            closest_seg_seg_t(a0, a1, b0, b1, &ss, &tt);
+            V3 pa = a0 + (a1 - a0) * ss, pb = b0 + (b1 - b0) * tt, dv = pa - pb;
+            float dist = sqrtf(dot(dv, dv));
+            d = dist - ra - rb;
+            if (d < off && dist > 1e-9f) {
+              nrm = dv * (1.0f / dist);
+              pt = ((pa - nrm * ra) + (pb + nrm * rb)) * 0.5f;
+              cnt = 1;
+            }
+          }
+        }
+      }
+      const int incl = team_incl_scan<T>(cnt);
+      const int tot = __shfl(incl, tb + T - 1);
+      if (cnt) {
+        const int slot = base + incl - 1;
+        if (slot < cap) {
+          s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
+          s->cn[slot][0] = nrm.x; s->cn[slot][1] = nrm.y; s->cn[slot][2] = nrm.z;
+          s->cd[slot] = d;
+          s->cA[slot] = m->geom_node[ga]; s->cgA[slot] = ga; s->cB[slot] = m->geom_node[gb]; s->cgB[slot] = gb;
+        }
+      }
+      base += tot;
+    }
+    if (tl == 0) s->ncon = base < cap ? base : cap;
+    __syncthreads();
+  }
+
+  static __device__ void closest_seg_seg_t(V3 p1, V3 q1, V3 p2, V3 q2, float* s_out, float* t_out) {
+    V3 d1 = q1 - p1, d2 = q2 - p2, r = p1 - p2;
+    float a = dot(d1, d1), e = dot(d2, d2), f = dot(d2, r);
+    float sv_, tv;
+    const float eps = 1e-12f;
+    if (a <= eps && e <= eps) {
+      sv_ = tv = 0;
+    } else if (a <= eps) {
+      sv_ = 0;
+      tv = fminf(fmaxf(f / e, 0.0f), 1.0f);
+    } else {
+      float c = dot(d1, r);
+      if (e <= eps) {
+        tv = 0;
+        sv_ = fminf(fmaxf(-c / a, 0.0f), 1.0f);
+      } else {
+        float b = dot(d1, d2), den = a * e - b * b;
+        sv_ = den > eps ? (b * f - c * e) / den : 0.0f;
+        sv_ = fminf(fmaxf(sv_, 0.0f), 1.0f);
+        tv = (b * sv_ + f) / e;
+        if (tv < 0) {
+          tv = 0;
+          sv_ = fminf(fmaxf(-c / a, 0.0f), 1.0f);
+        } else if (tv > 1) {
+          tv = 1;
+          sv_ = fminf(fmaxf((b - c) / a, 0.0f), 1.0f);
+        }
+      }
+    }
+    *s_out = sv_;
+    *t_out = tv;
+  }
+
+  // ---------------------------------------------------------------- constraint rows
+  __device__ void build_rows() {
+    const int ncon = s->ncon;
+    const V3 o = ld3(s->x[0]);
+    for (int c = tl; c < ncon; c += T) {
+      V3 n = ld3(s->cn[c]), pt = ld3(s->cp[c]), t1, t2;
+      tangent_basis_t(n, &t1, &t2);
+      float deff = s->cd[c] - p->rest_offset;
+      float bn = deff >= 0.0f ? -deff / h : fminf(-p->baumgarte * deff / h, p->max_depen_vel);
+      V3 dirs[3] = {n, t1, t2};
+      for (int r = 0; r < 3; r++) {
+        const int row = 3 * c + r;
+        V3 w = cross(pt - o, dirs[r]);
+        s->rw[row][0] = w.x; s->rw[row][1] = w.y; s->rw[row][2] = w.z;
+        s->rw[row][3] = dirs[r].x; s->rw[row][4] = dirs[r].y; s->rw[row][5] = dirs[r].z;
+        s->rb[row] = r == 0 ? bn : 0.0f;
+        s->rkind[row] = r == 0 ? 0 : 1;
+        s->rref[row] = c;
+        s->rA[row] = s->cA[c];
+        s->rB[row] = s->cB[c];
+        s->rsg[row] = 0.0f;
+      }
+    }
+    // joint-limit rows in DOF order (lower, then upper)
+    int cnt = 0;
+    float dl = 0.0f, du = 0.0f;
+    bool lo = false, hi = false;
+    if (node > 0 && m->limited[node]) {
+      dl = qj - m->lower[node];
+      du = m->upper[node] - qj;
+      lo = dl < p->limit_margin;
+      hi = du < p->limit_margin;
+      cnt = (lo ? 1 : 0) + (hi ? 1 : 0);
+    }
+    const int incl = team_incl_scan<T>(cnt);
+    const int tot = __shfl(incl, tb + T - 1);
+    int row = 3 * ncon + incl - cnt;
+    for (int side = 0; side < 2; side++) {
+      bool on = side == 0 ? lo : hi;
+      if (!on) continue;
+      float d = side == 0 ? dl : du;
+      s->rb[row] = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
+      s->rkind[row] = 2 + side;
+      s->rref[row] = node;
+      s->rA[row] = -1;
+      s->rB[row] = -1;
+      s->rsg[row] = side == 0 ? 1.0f : -1.0f;
+      for (int k = 0; k < 6; k++) s->rw[row][k] = 0.0f;
+      row++;
+    }
+    if (tl == 0) s->nrows = 3 * ncon + tot;
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- one substep
+  __device__ void substep() {
+    fk();
+    aba();
+    collide();
+    build_rows();
+    const int nrows = s->nrows;
+    const int wave_rows = __builtin_amdgcn_readfirstlane(wave_max<T>(nrows));
+    float Ycol[MR];
+    for (int r = 0; r < wave_rows; r++) {
+      const bool active = r < nrows;
+      const int kind = active ? s->rkind[r] : 0;
+      int A = -1, B = -1, jn = -1;
+      float sg = 0.0f;
+      SV fw = szero();
+      if (active) {
+        if (kind >= 2) {
+          jn = s->rref[r];
+          sg = s->rsg[r];
+        } else {
+          A = s->rA[r];
+          B = s->rB[r];
+          const float* w = s->rw[r];
+          fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
+        }
+      }
+      const float y = test_solve(A, B, fw, jn, sg);
+      Ycol[r] = active ? y : 0.0f;
+      const float Wr = team_sum<T>(active ? jac_entry(r) * y : 0.0f, tb);
+      if (tl == 0 && active) {
+        s->rW[r] = Wr;
+        s->rlam[r] = 0.0f;
+      }
+    }
+    __syncthreads();
+    for (int it = 0; it < p->pos_iters; it++) {
+      for (int r = 0; r < wave_rows; r++) {
+        const bool active = r < nrows;
+        const float Jr = active ? jac_entry(r) : 0.0f;
+        const float v = team_sum<T>(Jr * nu, tb);
+        float dl = 0.0f;
+        if (active) {
+          const float W = s->rW[r];
+          if (W > 1e-12f) {
+            const float lam = s->rlam[r];
+            float lnew = lam + (s->rb[r] - v) / W;
+            if (s->rkind[r] == 1) {
+              const float lim = p->friction * s->rlam[3 * s->rref[r]];
+              lnew = fminf(fmaxf(lnew, -lim), lim);
+            } else {
+              lnew = fmaxf(lnew, 0.0f);
+            }
+            dl = lnew - lam;
+          }
+        }
+        if (tl == 0 && active) s->rlam[r] += dl;
+        nu += Ycol[r] * dl;
+      }
+    }
+    __syncthreads();
+    integrate();
+  }
+
+  __device__ void integrate() {
+    // root pose (lane 0 gathers the twist from lanes 0..5)
+    float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
+    float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
+    if (freeb) {
+      V3 om = v3(w0, w1, w2), vo = v3(v0, v1, v2);
+      V3 pn = p0 + vo * h;
+      float wn = sqrtf(dot(om, om));
+      float dq[4];
+      if (wn * h > 1e-12f) {
+        float ha = 0.5f * wn * h, sn = sinf(ha) / wn;
+        dq[0] = om.x * sn; dq[1] = om.y * sn; dq[2] = om.z * sn; dq[3] = cosf(ha);
+      } else {
+        dq[0] = 0.5f * h * om.x; dq[1] = 0.5f * h * om.y; dq[2] = 0.5f * h * om.z; dq[3] = 1.0f;
+      }
+      const float* a = dq;
+      const float* b = q0;
+      float qn[4] = {a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1],
+                     a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0],
+                     a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3],
+                     a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2]};
+      float l = 1.0f / sqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+      for (int k = 0; k < 4; k++) q0[k] = qn[k] * l;
+      V3 dp = pn - p0;
+      p0 = pn;
+      V3 vn = vo + cross(om, dp);
+      if (tl == 3) nu = vn.x;
+      if (tl == 4) nu = vn.y;
+      if (tl == 5) nu = vn.z;
+    }
+    if (node > 0) qj += h * nu;
+  }
+
+  // ---------------------------------------------------------------- sensors & DOF forces (last substep)
+  __device__ void outputs(float* sens_out, float* dforce_out) {
+    fk();  // post-step pose for the sensor body frames
+    const int NS = m->num_sensors;
+    if (sens_out && tl < NS) {
+      const int body = m->sensor_body[tl], nd = m->body_node[body];
+      M3 Rn;
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Rn.m[a][b] = s->R[nd][3 * a + b];
+      M3 Rb = mul(Rn, quat_to_mat(m->body_quat[body][0], m->body_quat[body][1], m->body_quat[body][2],
+                                  m->body_quat[body][3]));
+      V3 xb = ld3(s->x[nd]) + mul(Rn, ld3(m->body_pos[body]));
+      V3 F = v3(0, 0, 0), Tq = v3(0, 0, 0);
+      for (int c = 0; c < s->ncon; c++) {
+        float sg = 0.0f;
+        if (m->geom_body[s->cgA[c]] == body) sg = 1.0f;
+        else if (s->cgB[c] >= 0 && m->geom_body[s->cgB[c]] == body) sg = -1.0f;
+        if (sg == 0.0f) continue;
+        V3 n = ld3(s->cn[c]), t1, t2;
+        tangent_basis_t(n, &t1, &t2);
+        V3 f = (n * s->rlam[3 * c] + t1 * s->rlam[3 * c + 1] + t2 * s->rlam[3 * c + 2]) * (sg / h);
+        F = F + f;
+        Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
+      }
+      V3 Fl = mulT(Rb, F), Tl = mulT(Rb, Tq);
+      float* o = sens_out + 6 * tl;
+      o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
+    }
+    if (dforce_out && node > 0) {
+      float t = tau - m->damping[node] * nu - m->stiffness[node] * qj;
+      for (int r = 3 * s->ncon; r < s->nrows; r++) {
+        if (s->rref[r] != node) continue;
+        if (s->rkind[r] == 2) t += s->rlam[r] / h;
+        if (s->rkind[r] == 3) t -= s->rlam[r] / h;
+      }
+      dforce_out[node - 1] = t;
+    }
+  }
+
+  // ---------------------------------------------------------------- state I/O (gym layouts)
+  __device__ void load(const float* root, const float* dof, const float* act_tau) {
+    // root pose/twist: every lane reads the 13 floats (one cache line pair per actor)
+    if (tl == 0) {
+      p0 = ld3(root);
+      float n = sqrtf(root[3] * root[3] + root[4] * root[4] + root[5] * root[5] + root[6] * root[6]);
+      for (int k = 0; k < 4; k++) q0[k] = root[3 + k] / n;
+    }
+    q0[0] = __shfl(q0[0], tb); q0[1] = __shfl(q0[1], tb); q0[2] = __shfl(q0[2], tb); q0[3] = __shfl(q0[3], tb);
+    p0.x = __shfl(p0.x, tb); p0.y = __shfl(p0.y, tb); p0.z = __shfl(p0.z, tb);
+    if (freeb && tl < 6) {
+      M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
+      V3 cw = mul(Rr, ld3(m->body_com[0]));
+      V3 om = ld3(root + 10);
+      V3 vo = ld3(root + 7) - cross(om, cw);
+      float tw[6] = {om.x, om.y, om.z, vo.x, vo.y, vo.z};
+      nu = tw[tl];
+    }
+    if (node > 0) {
+      qj = dof[2 * (node - 1)];
+      nu = dof[2 * (node - 1) + 1];
+      tau = act_tau ? act_tau[node - 1] : 0.0f;
+    }
+  }
+
+  // writes the post-step state into the team's LDS staging (root[13], dof[2 nD])
+  __device__ void stage_state() {
+    float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
+    float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
+    if (tl == 0) {
+      s->root[0] = p0.x; s->root[1] = p0.y; s->root[2] = p0.z;
+      for (int k = 0; k < 4; k++) s->root[3 + k] = q0[k];
+      if (freeb) {
+        M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
+        V3 cw = mul(Rr, ld3(m->body_com[0]));
+        V3 om = v3(w0, w1, w2);
+        V3 vc = v3(v0, v1, v2) + cross(om, cw);
+        s->root[7] = vc.x; s->root[8] = vc.y; s->root[9] = vc.z;
+        s->root[10] = om.x; s->root[11] = om.y; s->root[12] = om.z;
+      }
+    }
+    if (node > 0) {
+      s->dof[2 * (node - 1)] = qj;
+      s->dof[2 * (node - 1) + 1] = nu;
+    }
+  }
+};
+
+}  // namespace mg
