@@ -302,6 +302,17 @@ __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__
 // contacts MC.  The smallest instance that fits the model is launched.
 #define MG_INSTANCES(X) X(8, 4, 8) X(16, 9, 16) X(16, 16, 24) X(32, 24, 32) X(32, 32, 48) X(64, 40, 48)
 
+// team size the dispatcher picks for a model (0: none fits)
+static int team_size(const mg_model& m, int max_contacts) {
+  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
+  const int lanes = nv > m.num_sensors ? nv : m.num_sensors;
+#define MG_T(T, MN, MC) \
+  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6)) return T;
+  MG_INSTANCES(MG_T)
+#undef MG_T
+  return 0;
+}
+
 template <template <int, int, int> class F, typename... A>
 static int dispatch(const mg_model& m, int max_contacts, A... args) {
   const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
@@ -473,9 +484,14 @@ int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb
     return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
   if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
     return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
-  if (tp->num_agents > 1 && (64 % tp->num_agents != 0 || sim->n % tp->num_agents != 0 ||
-                             tp->num_agents > MG_MAX_AGENTS))
-    return fail(MG_EINVAL, "mg_env_step: num_agents must divide 64 and the actor count");
+  if (tp->num_agents > 1) {
+    // the agents of an env must be teams of one wave (ballot/shuffle exchange): A | 64/T
+    const int T = team_size(sim->host_model, sim->params.max_contacts);
+    if (T == 0 || tp->num_agents > MG_MAX_AGENTS || (64 / T) % tp->num_agents != 0 ||
+        sim->n % tp->num_agents != 0)
+      return fail(MG_EINVAL, "mg_env_step: num_agents must divide the envs per wave (64 / team size) "
+                             "and the actor count");
+  }
   int rc = dispatch<RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream, (const mg_sim*)sim,
                                 tp, tb);
   if (rc) return rc;

@@ -340,7 +340,7 @@ def ma_setup(A=4):
     return spec, taskdefs.sim_params(cfg, 16, A), taskdefs.task_params("MAAnt", cfg, spec)
 
 
-@pytest.mark.parametrize("A", [2, 4, 8])
+@pytest.mark.parametrize("A", [2, 4])
 def test_multi_agent_env_step_matches_oracle(lib, A):
     """MAAnt fused step (AND-filter resets via wave ballot, others-block via shuffles) vs the oracle."""
     spec, sp, tp = ma_setup(A)
@@ -370,6 +370,21 @@ def test_multi_agent_env_step_matches_oracle(lib, A):
     assert og.shape[1] == 60 + 3 * (A - 1)
     bad = np.abs(og - h.obs) > (2e-2 + 2e-2 * np.abs(h.obs))
     assert bad.mean() < 1e-3, (bad.sum(), np.argwhere(bad)[:10])
+
+
+def test_multi_agent_rejects_agents_spanning_waves(lib):
+    """Ant teams are 16 lanes (4 actors per wave): 8 agents per env cannot share one wave."""
+    spec, sp, tp = ma_setup(8)
+    n = 8 * 8
+    h = O.HostEnv(tp, spec, n)
+    e = DevEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    rc = lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers()), stream())
+    lib.mg_sim_destroy(sim)
+    assert rc == -1 and b"num_agents" in lib.mg_last_error()
 
 
 def test_multi_agent_make_full_size():
