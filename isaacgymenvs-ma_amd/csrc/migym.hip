@@ -38,20 +38,23 @@ struct mg_sim {
 
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp)
-template <int T, int MN, int MC>
+template <int T, int MN, int MC, int MG, int MP>
 __global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p, int n,
                                                      float* __restrict__ root, float* __restrict__ dof,
                                                      const float* __restrict__ act, float* __restrict__ sensors,
                                                      float* __restrict__ dof_force) {
   constexpr int E = kBlock / T;
   __shared__ mg::TeamLDS<T, MN, MC> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  mg::load_tile(&tile, m);
+  __syncthreads();
   const int team = threadIdx.x / T;
   const int a = blockIdx.x * E + team;
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors;
-  mg::Team<T, MN, MC> t;
-  t.init(&lds[team], m, &p);
+  mg::Team<T, MN, MC, MG, MP> t;
+  t.init(&lds[team], &tile, m, &p);
   __syncthreads();
   t.load(root + (size_t)13 * ac, dof + (size_t)2 * nd * ac, act ? act + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
@@ -176,19 +179,22 @@ __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_s
 // state, the team writes it back to HBM.  Multi-agent: the agents of an env are consecutive
 // teams of one wave, so the AND-filter is a ballot over team leaders and the others-block a
 // shuffle from the other agents' leaders.
-template <int T, int MN, int MC>
+template <int T, int MN, int MC, int MG, int MP>
 __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
   constexpr int E = kBlock / T;
   __shared__ mg::TeamLDS<T, MN, MC> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  mg::load_tile(&tile, m);
+  __syncthreads();
   const int team = threadIdx.x / T;
   const int a = blockIdx.x * E + team;
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
   mg::TeamLDS<T, MN, MC>& L = lds[team];
-  mg::Team<T, MN, MC> t;
-  t.init(&L, m, &p);
+  mg::Team<T, MN, MC, MG, MP> t;
+  t.init(&L, &tile, m, &p);
   __syncthreads();
   const int64_t reset_in = tb.reset[ac];
   // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
@@ -300,47 +306,52 @@ __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__
 // ------------------------------------------------------------------------------------------------ dispatch
 // Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
 // contacts MC.  The smallest instance that fits the model is launched.
-#define MG_INSTANCES(X) X(8, 4, 8) X(16, 9, 16) X(16, 16, 24) X(32, 24, 32) X(32, 32, 48) X(64, 40, 48)
+#define MG_INSTANCES(X) \
+  X(8, 4, 8, 4, 0) X(16, 9, 16, 16, 0) X(16, 16, 24, 24, 32) X(32, 24, 32, 24, 160) X(32, 32, 48, 48, 192) \
+  X(64, 40, 48, 48, 192)
 
 // team size the dispatcher picks for a model (0: none fits)
 static int team_size(const mg_model& m, int max_contacts) {
   const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
   const int lanes = nv > m.num_sensors ? nv : m.num_sensors;
-#define MG_T(T, MN, MC) \
-  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6)) return T;
+#define MG_T(T, MN, MC, MG, MP)                                                                 \
+  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6) &&        \
+      m.num_geoms <= MG && m.num_pairs <= MP)                                                      \
+    return T;
   MG_INSTANCES(MG_T)
 #undef MG_T
   return 0;
 }
 
-template <template <int, int, int> class F, typename... A>
+template <template <int, int, int, int, int> class F, typename... A>
 static int dispatch(const mg_model& m, int max_contacts, A... args) {
   const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
   const int lanes = nv > m.num_sensors ? nv : m.num_sensors;
-#define MG_TRY(T, MN, MC)                                                       \
-  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6)) { \
-    F<T, MN, MC>::run(args...);                                                 \
-    return MG_OK;                                                               \
+#define MG_TRY(T, MN, MC, MG, MP)                                                              \
+  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6) &&       \
+      m.num_geoms <= MG && m.num_pairs <= MP) {                                                   \
+    F<T, MN, MC, MG, MP>::run(args...);                                                          \
+    return MG_OK;                                                                                 \
   }
   MG_INSTANCES(MG_TRY)
 #undef MG_TRY
   return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
 }
 
-template <int T, int MN, int MC>
+template <int T, int MN, int MC, int MG, int MP>
 struct RunSimulate {
   static void run(hipStream_t s, const mg_sim* sim) {
     const mg_state_views& v = sim->views;
     const int E = kBlock / T;
-    hipLaunchKernelGGL((k_simulate<T, MN, MC>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
+    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
                        sim->params, sim->n, v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force);
   }
 };
-template <int T, int MN, int MC>
+template <int T, int MN, int MC, int MG, int MP>
 struct RunEnvStep {
   static void run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
     const int E = kBlock / T;
-    hipLaunchKernelGGL((k_env_step<T, MN, MC>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
+    hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
                        sim->params, *tp, sim->views, *tb, sim->n);
   }
 };

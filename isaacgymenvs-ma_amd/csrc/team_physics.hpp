@@ -27,6 +27,60 @@
 
 namespace mg {
 
+// Block-shared LDS copy of the model tables the hot loops read ("model tile"):
+// loaded once per launch, so every per-node / per-geom constant is an LDS read
+// (~64 cycles) instead of a dependent global load.  Rows padded to odd strides.
+template <int MN, int MG, int MP>
+struct ModelTile {
+  int parent[MN], jtype[MN], limited[MN];
+  unsigned long long children[MN];
+  float nf[MN][31];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
+                      // 27 stiff, 28 lower, 29 upper
+  int gtype[MG], gnode[MG], gbody[MG];
+  float gf[MG][17];   // 0-2 pos, 3-11 R, 12-14 size
+  int pairs[MP > 0 ? MP : 1][2];
+  int nn, ng, np;
+};
+
+template <int MN, int MG, int MP>
+__device__ void load_tile(ModelTile<MN, MG, MP>* t, const mg_model* m) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int nn = m->num_nodes, ng = m->num_geoms < MG ? m->num_geoms : MG;
+  const int np = m->num_pairs < MP ? m->num_pairs : MP;
+  for (int i = tid; i < nn; i += nt) {
+    t->parent[i] = m->parent[i];
+    t->jtype[i] = m->jtype[i];
+    t->limited[i] = m->limited[i];
+    unsigned long long ch = 0ull;
+    for (int k = 1; k < nn; k++)
+      if (m->parent[k] == i) ch |= 1ull << k;
+    t->children[i] = ch;
+    float* f = t->nf[i];
+    M3 R0 = quat_to_mat(m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]);
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) f[3 * a + b] = R0.m[a][b];
+    for (int k = 0; k < 3; k++) { f[9 + k] = m->t[i][k]; f[12 + k] = m->axis[i][k]; f[15 + k] = m->com[i][k]; }
+    for (int k = 0; k < 6; k++) f[18 + k] = m->inertia[i][k];
+    f[24] = m->mass[i]; f[25] = m->armature[i]; f[26] = m->damping[i]; f[27] = m->stiffness[i];
+    f[28] = m->lower[i]; f[29] = m->upper[i];
+  }
+  for (int g = tid; g < ng; g += nt) {
+    t->gtype[g] = m->geom_type[g];
+    t->gnode[g] = m->geom_node[g];
+    t->gbody[g] = m->geom_body[g];
+    float* f = t->gf[g];
+    M3 Rg = quat_to_mat(m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]);
+    for (int k = 0; k < 3; k++) { f[k] = m->geom_pos[g][k]; f[12 + k] = m->geom_size[g][k]; }
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) f[3 + 3 * a + b] = Rg.m[a][b];
+  }
+  for (int q = tid; q < np; q += nt) {
+    t->pairs[q][0] = m->pair[q][0];
+    t->pairs[q][1] = m->pair[q][1];
+  }
+  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; }
+}
+
 template <int T, int MN, int MC>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
@@ -46,7 +100,8 @@ struct TeamLDS {
   float cp[MC][3], cn[MC][3], cd[MC];
   int cA[MC], cB[MC], cgA[MC], cgB[MC];
   float rw[MR][6];
-  float rb[MR], rW[MR], rlam[MR], rsg[MR];
+  float rb[MR], rW[MR], rlam[MR];
+  float Iinv[36];
   int rkind[MR], rref[MR], rA[MR], rB[MR];
   // task-layer staging (root / dof state of the actor after the physics)
   float root[13];
@@ -55,11 +110,18 @@ struct TeamLDS {
   float dforce[MN];
 };
 
+// Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + ds_swizzle xor 16 and
+// a bpermute xor 32.  Every step adds a lane to its partner symmetrically, so all lanes of the team
+// end with bit-identical sums (fp add is commutative) and no broadcast is needed.
 template <int T>
-__device__ __forceinline__ float team_sum(float v, int tb) {
-#pragma unroll
-  for (int m = T / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, T);
-  return __shfl(v, tb);  // identical bits in every lane of the team
+__device__ __forceinline__ float team_sum(float v, int) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad xor 1
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad xor 2
+  if (T >= 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  if (T >= 16) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  if (T >= 32) v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));      // xor 16
+  if (T >= 64) v += __shfl_xor(v, 32);
+  return v;
 }
 template <int T>
 __device__ __forceinline__ int team_incl_scan(int v) {
@@ -87,11 +149,13 @@ __device__ __forceinline__ void tangent_basis_t(V3 n, V3* t1, V3* t2) {
 }
 
 // Per-lane context of one team.
-template <int T, int MN, int MC>
+template <int T, int MN, int MC, int MG, int MP>
 struct Team {
   using L = TeamLDS<T, MN, MC>;
+  using MT = ModelTile<MN, MG, MP>;
   static constexpr int MR = L::MR;
   L* s;
+  const MT* mt;
   const mg_model* m;
   const mg_sim_params* p;
   int tl, tb;          // team lane, first lane of the team (absolute)
@@ -115,8 +179,9 @@ struct Team {
 
   __device__ int col_of(int i) const { return ncol0 - 1 + i; }
 
-  __device__ void init(L* lds, const mg_model* mm, const mg_sim_params* pp) {
+  __device__ void init(L* lds, const MT* tile, const mg_model* mm, const mg_sim_params* pp) {
     s = lds;
+    mt = tile;
     m = mm;
     p = pp;
     tl = threadIdx.x % T;
@@ -128,11 +193,11 @@ struct Team {
     node = -1;
     if (freeb && tl == 0) node = 0;
     if (tl >= ncol0 && tl - ncol0 + 1 < nn) node = tl - ncol0 + 1;
-    par = node > 0 ? m->parent[node] : -1;
+    par = node > 0 ? mt->parent[node] : -1;
     depth = 0;
     unsigned long long anc = 0ull;
     if (node > 0) {
-      for (int k = node; k > 0; k = m->parent[k]) {
+      for (int k = node; k > 0; k = mt->parent[k]) {
         anc |= 1ull << k;
         depth++;
       }
@@ -173,10 +238,14 @@ struct Team {
           for (int b = 0; b < 3; b++) Rp.m[a][b] = s->R[par][3 * a + b];
         V3 xp = ld3(s->x[par]);
         SV Vp = sv(ld3(s->V[par]), ld3(s->V[par] + 3));
-        M3 Rp0 = mul(Rp, quat_to_mat(m->r0[node][0], m->r0[node][1], m->r0[node][2], m->r0[node][3]));
-        V3 tp = mul(Rp, ld3(m->t[node]));
-        V3 ax = ld3(m->axis[node]);
-        if (m->jtype[node] == MG_JT_HINGE) {
+        const float* nf = mt->nf[node];
+        M3 R0;
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) R0.m[a][b] = nf[3 * a + b];
+        M3 Rp0 = mul(Rp, R0);
+        V3 tp = mul(Rp, ld3(nf + 9));
+        V3 ax = ld3(nf + 12);
+        if (mt->jtype[node] == MG_JT_HINGE) {
           R = mul(Rp0, axis_angle(ax, qj));
           x = xp + tp;
           V3 sw = mul(R, ax);
@@ -204,8 +273,9 @@ struct Team {
   __device__ void aba() {
     if (node >= 0) {
       const V3 o = ld3(s->x[0]);
-      V3 cc = x + mul(R, ld3(m->com[node])) - o;
-      const float* in = m->inertia[node];
+      const float* nf = mt->nf[node];
+      V3 cc = x + mul(R, ld3(nf + 15)) - o;
+      const float* in = nf + 18;
       float Il[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
       float Tm[3][3], Iw[6];
       for (int a = 0; a < 3; a++)
@@ -215,7 +285,7 @@ struct Team {
         int a = idx[k][0], b = idx[k][1];
         Iw[k] = Tm[a][0] * R.m[b][0] + Tm[a][1] * R.m[b][1] + Tm[a][2] * R.m[b][2];
       }
-      const float mass = m->mass[node];
+      const float mass = nf[24];
       IA = body_inertia(mass, cc, Iw);
       SV IV = mul(IA, V);
       V3 mg = ld3(p->gravity) * mass;
@@ -225,9 +295,10 @@ struct Team {
     for (int lev = maxdepth; lev >= 1; lev--) {
       if (node > 0 && depth == lev) {
         U = mul(IA, S);
-        float D = dot(S, U) + m->armature[node] + h * m->damping[node] + h * h * m->stiffness[node];
+        const float* nf = mt->nf[node];
+        float D = dot(S, U) + nf[25] + h * nf[26] + h * h * nf[27];
         Dinv = 1.0f / D;
-        float t = tau - m->damping[node] * nu - m->stiffness[node] * (qj + h * nu);
+        float t = tau - nf[26] * nu - nf[27] * (qj + h * nu);
         u = t - dot(S, pA);
         Sym6 Ia = IA;
         rank1_sub(Ia, U, Dinv);
@@ -243,8 +314,10 @@ struct Team {
       }
       __syncthreads();
       if (node >= 0 && depth == lev - 1) {
-        for (int k = 1; k < nn; k++) {
-          if (m->parent[k] != node) continue;
+        unsigned long long ch = mt->children[node];
+        while (ch) {
+          const int k = __builtin_ctzll(ch);
+          ch &= ch - 1;
           const float* sl = s->slot[k];
           for (int q = 0; q < 6; q++) { IA.a[q] += sl[q]; IA.c[q] += sl[15 + q]; }
           for (int q = 0; q < 9; q++) IA.b[q] += sl[6 + q];
@@ -255,12 +328,25 @@ struct Team {
     if (tl == 0) {
       if (freeb) {
         chol6(IA, s->L0);
-        SV a0 = chol6_solve(s->L0, pA * -1.0f);
-        s->acc[0][0] = a0.a.x; s->acc[0][1] = a0.a.y; s->acc[0][2] = a0.a.z;
-        s->acc[0][3] = a0.l.x; s->acc[0][4] = a0.l.y; s->acc[0][5] = a0.l.z;
+        s->proot[0] = pA.a.x; s->proot[1] = pA.a.y; s->proot[2] = pA.a.z;
+        s->proot[3] = pA.l.x; s->proot[4] = pA.l.y; s->proot[5] = pA.l.z;
       } else {
         for (int k = 0; k < 6; k++) s->acc[0][k] = 0.0f;
       }
+    }
+    __syncthreads();
+    if (freeb && tl < 6) {
+      // column tl of IA0^-1 from the Cholesky factor (6 lanes in parallel); a0 = -IA0^-1 pA0
+      const SV e = sv(v3(tl == 0 ? 1.f : 0.f, tl == 1 ? 1.f : 0.f, tl == 2 ? 1.f : 0.f),
+                      v3(tl == 3 ? 1.f : 0.f, tl == 4 ? 1.f : 0.f, tl == 5 ? 1.f : 0.f));
+      SV col = chol6_solve(s->L0, e);
+      float cv[6] = {col.a.x, col.a.y, col.a.z, col.l.x, col.l.y, col.l.z};
+      float a = 0.0f;
+      for (int k = 0; k < 6; k++) {
+        s->Iinv[6 * k + tl] = cv[k];
+        a -= cv[k] * s->proot[k];
+      }
+      s->acc[0][tl] = a;
     }
     __syncthreads();
     float qdd = 0.0f;
@@ -303,13 +389,20 @@ struct Team {
           s->ut[k] += uk;
           pv = pv + Uk * (uk * s->Dinv[k]);
           tq = 0.0f;
-          k = m->parent[k];
+          k = mt->parent[k];
         }
         proot = proot + pv;
       }
-      SV a0 = freeb ? chol6_solve(s->L0, proot * -1.0f) : szero();
-      s->acc[0][0] = a0.a.x; s->acc[0][1] = a0.a.y; s->acc[0][2] = a0.a.z;
-      s->acc[0][3] = a0.l.x; s->acc[0][4] = a0.l.y; s->acc[0][5] = a0.l.z;
+      s->proot[0] = proot.a.x; s->proot[1] = proot.a.y; s->proot[2] = proot.a.z;
+      s->proot[3] = proot.l.x; s->proot[4] = proot.l.y; s->proot[5] = proot.l.z;
+      if (!freeb)
+        for (int q = 0; q < 6; q++) s->acc[0][q] = 0.0f;
+    }
+    __syncthreads();
+    if (freeb && tl < 6) {
+      float a = 0.0f;
+      for (int q = 0; q < 6; q++) a -= s->Iinv[6 * tl + q] * s->proot[q];
+      s->acc[0][tl] = a;
     }
     __syncthreads();
     float y = 0.0f;
@@ -331,7 +424,7 @@ struct Team {
   __device__ float jac_entry(int r) const {
     const int kind = s->rkind[r];
     if (tl >= nv) return 0.0f;
-    if (kind >= 2) return (node > 0 && node == s->rref[r]) ? s->rsg[r] : 0.0f;
+    if (kind >= 2) return (node > 0 && node == s->rref[r]) ? (kind == 2 ? 1.0f : -1.0f) : 0.0f;
     const float* w = s->rw[r];
     const int A = s->rA[r], B = s->rB[r];
     if (freeb && tl < 6) {
@@ -346,22 +439,27 @@ struct Team {
 
   // ---------------------------------------------------------------- collision -> LDS contact list
   __device__ void geom_world(int g, V3* cw, M3* Rg) const {
-    const int nd = m->geom_node[g];
-    M3 Rn;
+    const int nd = mt->gnode[g];
+    const float* gf = mt->gf[g];
+    M3 Rn, Rl;
     for (int a = 0; a < 3; a++)
-      for (int b = 0; b < 3; b++) Rn.m[a][b] = s->R[nd][3 * a + b];
-    *cw = ld3(s->x[nd]) + mul(Rn, ld3(m->geom_pos[g]));
-    *Rg = mul(Rn, quat_to_mat(m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]));
+      for (int b = 0; b < 3; b++) {
+        Rn.m[a][b] = s->R[nd][3 * a + b];
+        Rl.m[a][b] = gf[3 + 3 * a + b];
+      }
+    *cw = ld3(s->x[nd]) + mul(Rn, ld3(gf));
+    *Rg = mul(Rn, Rl);
   }
   __device__ bool geom_segment(int g, V3* a, V3* b, float* r) const {
     V3 c;
     M3 Rg;
     geom_world(g, &c, &Rg);
-    int ty = m->geom_type[g];
-    if (ty == MG_GT_SPHERE) { *a = c; *b = c; *r = m->geom_size[g][0]; return true; }
+    int ty = mt->gtype[g];
+    const float* gs = mt->gf[g] + 12;
+    if (ty == MG_GT_SPHERE) { *a = c; *b = c; *r = gs[0]; return true; }
     if (ty == MG_GT_CAPSULE) {
-      V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * m->geom_size[g][1];
-      *a = c - ax; *b = c + ax; *r = m->geom_size[g][0];
+      V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * gs[1];
+      *a = c - ax; *b = c + ax; *r = gs[0];
       return true;
     }
     return false;
@@ -371,7 +469,7 @@ struct Team {
     const int cap = p->max_contacts < MC ? p->max_contacts : MC;
     const float off = p->contact_offset;
     int base = 0;
-    const int G = m->num_geoms;
+    const int G = mt->ng;
     // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
     // pass 1 counts, a team scan places them, pass 2 recomputes and writes (no private arrays).
     for (int g0 = 0; g0 < G; g0 += T) {
@@ -381,8 +479,9 @@ struct Team {
       int ty = -1;
       if (g < G) {
         geom_world(g, &c, &Rg);
-        ty = m->geom_type[g];
+        ty = mt->gtype[g];
       }
+      const float* gs = g < G ? mt->gf[g] + 12 : mt->gf[0] + 12;
       int cnt = 0;
       for (int pass = 0; pass < 2; pass++) {
         int k = 0, slot0 = 0;
@@ -397,14 +496,13 @@ struct Team {
           float r;
           if (ty == MG_GT_SPHERE) {
             e = c;
-            r = m->geom_size[g][0];
+            r = gs[0];
           } else if (ty == MG_GT_CAPSULE) {
-            V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * m->geom_size[g][1];
+            V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * gs[1];
             e = q == 0 ? c - ax : c + ax;
-            r = m->geom_size[g][0];
+            r = gs[0];
           } else {
-            V3 l = v3((q & 1 ? 1.f : -1.f) * m->geom_size[g][0], (q & 2 ? 1.f : -1.f) * m->geom_size[g][1],
-                      (q & 4 ? 1.f : -1.f) * m->geom_size[g][2]);
+            V3 l = v3((q & 1 ? 1.f : -1.f) * gs[0], (q & 2 ? 1.f : -1.f) * gs[1], (q & 4 ? 1.f : -1.f) * gs[2]);
             e = c + mul(Rg, l);
             r = 0.0f;
           }
@@ -418,7 +516,7 @@ struct Team {
               s->cp[slot][0] = e.x; s->cp[slot][1] = e.y; s->cp[slot][2] = e.z - r;
               s->cn[slot][0] = 0.0f; s->cn[slot][1] = 0.0f; s->cn[slot][2] = 1.0f;
               s->cd[slot] = d;
-              s->cA[slot] = m->geom_node[g]; s->cgA[slot] = g; s->cB[slot] = -1; s->cgB[slot] = -1;
+              s->cA[slot] = mt->gnode[g]; s->cgA[slot] = g; s->cB[slot] = -1; s->cgB[slot] = -1;
             }
             k++;
           }
@@ -426,7 +524,7 @@ struct Team {
       }
     }
     // self-collision pairs: lane per pair, pair order preserved
-    const int P = m->num_pairs;
+    const int P = mt->np;
     for (int p0 = 0; p0 < P; p0 += T) {
       const int pi = p0 + tl;
       int cnt = 0;
@@ -434,8 +532,8 @@ struct Team {
       float d = 0.0f;
       int ga = 0, gb = 0;
       if (pi < P) {
-        ga = m->pair[pi][0];
-        gb = m->pair[pi][1];
+        ga = mt->pairs[pi][0];
+        gb = mt->pairs[pi][1];
         V3 a0, a1, b0, b1;
         float ra, rb;
         if (geom_segment(ga, &a0, &a1, &ra) && geom_segment(gb, &b0, &b1, &rb)) {
@@ -464,7 +562,7 @@ struct Team {
           s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
           s->cn[slot][0] = nrm.x; s->cn[slot][1] = nrm.y; s->cn[slot][2] = nrm.z;
           s->cd[slot] = d;
-          s->cA[slot] = m->geom_node[ga]; s->cgA[slot] = ga; s->cB[slot] = m->geom_node[gb]; s->cgB[slot] = gb;
+          s->cA[slot] = mt->gnode[ga]; s->cgA[slot] = ga; s->cB[slot] = mt->gnode[gb]; s->cgB[slot] = gb;
         }
       }
       base += tot;
@@ -526,16 +624,15 @@ struct Team {
         s->rref[row] = c;
         s->rA[row] = s->cA[c];
         s->rB[row] = s->cB[c];
-        s->rsg[row] = 0.0f;
       }
     }
     // joint-limit rows in DOF order (lower, then upper)
     int cnt = 0;
     float dl = 0.0f, du = 0.0f;
     bool lo = false, hi = false;
-    if (node > 0 && m->limited[node]) {
-      dl = qj - m->lower[node];
-      du = m->upper[node] - qj;
+    if (node > 0 && mt->limited[node]) {
+      dl = qj - mt->nf[node][28];
+      du = mt->nf[node][29] - qj;
       lo = dl < p->limit_margin;
       hi = du < p->limit_margin;
       cnt = (lo ? 1 : 0) + (hi ? 1 : 0);
@@ -552,7 +649,6 @@ struct Team {
       s->rref[row] = node;
       s->rA[row] = -1;
       s->rB[row] = -1;
-      s->rsg[row] = side == 0 ? 1.0f : -1.0f;
       for (int k = 0; k < 6; k++) s->rw[row][k] = 0.0f;
       row++;
     }
@@ -578,7 +674,7 @@ struct Team {
       if (active) {
         if (kind >= 2) {
           jn = s->rref[r];
-          sg = s->rsg[r];
+          sg = kind == 2 ? 1.0f : -1.0f;
         } else {
           A = s->rA[r];
           B = s->rB[r];
@@ -671,8 +767,8 @@ struct Team {
       V3 F = v3(0, 0, 0), Tq = v3(0, 0, 0);
       for (int c = 0; c < s->ncon; c++) {
         float sg = 0.0f;
-        if (m->geom_body[s->cgA[c]] == body) sg = 1.0f;
-        else if (s->cgB[c] >= 0 && m->geom_body[s->cgB[c]] == body) sg = -1.0f;
+        if (mt->gbody[s->cgA[c]] == body) sg = 1.0f;
+        else if (s->cgB[c] >= 0 && mt->gbody[s->cgB[c]] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
         V3 n = ld3(s->cn[c]), t1, t2;
         tangent_basis_t(n, &t1, &t2);
@@ -685,7 +781,7 @@ struct Team {
       o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
     }
     if (dforce_out && node > 0) {
-      float t = tau - m->damping[node] * nu - m->stiffness[node] * qj;
+      float t = tau - mt->nf[node][26] * nu - mt->nf[node][27] * qj;
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
         if (s->rref[r] != node) continue;
         if (s->rkind[r] == 2) t += s->rlam[r] / h;
