@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="all-gather obs/rew/reset of every rank each step (one RCCL collective)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     args = ap.parse_args()
 
     import torch
@@ -71,12 +72,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(torch.cuda.device_count(), 1)
+    dev = f"cuda:{local % ndev}"
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = f"cuda:{local}"
-    torch.cuda.set_device(dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(dev))
+        else:
+            dist.init_process_group(args.backend)
 
     import migym
     n = args.num_envs
@@ -86,7 +90,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
     gather = None
-    if args.gather and world > 1:
+    if args.gather and world > 1 and args.backend == "nccl":
         from migym.dist import OutputGather
         gather = OutputGather(env.num_actors, env.num_obs, dev)
 
@@ -115,7 +119,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     value = n * world * args.steps / elapsed

@@ -18,8 +18,10 @@ def get_rlgames_env_creator(seed, task_config, task_name, sim_device, rl_device,
             local_rank = int(os.getenv("LOCAL_RANK", "0"))
             global_rank = int(os.getenv("RANK", "0"))
             world = int(os.getenv("WORLD_SIZE", "1"))
-            sim_device = f"cuda:{local_rank}"
-            rl_device = f"cuda:{local_rank}"
+            import torch
+            ndev = max(torch.cuda.device_count(), 1)
+            sim_device = f"cuda:{local_rank % ndev}"
+            rl_device = f"cuda:{local_rank % ndev}"
             cfg["rank"] = global_rank
             cfg["world_size"] = world
             cfg["env_offset"] = global_rank * int(cfg["env"]["numEnvs"])
