@@ -21,6 +21,9 @@
  *   mg_compute_reward    compute_{ant,humanoid,cartpole}_reward
  *                                                   (tasks/ant.py:325-371, humanoid.py:323-375,
  *                                                    cartpole.py:180-196)
+ *   (ShadowHand) mg_env_step also covers pre_physics_step's masked goal/env resets and
+ *                        PD targets (shadow_hand.py:586-698) and compute_hand_reward's
+ *                        global running mean (746-800, one finishing kernel).
  *   mg_env_step          one whole VecTask.step after the action tensor is on device:
  *                        clamp -> pre_physics_step -> simulate x controlFrequencyInv ->
  *                        post_physics_step (progress, masked reset_idx, obs, reward)
@@ -50,20 +53,24 @@
 extern "C" {
 #endif
 
-#define MG_VERSION 1
+#define MG_VERSION 2
 
 #define MG_MAX_NODES 40
 #define MG_MAX_BODIES 40
 #define MG_MAX_GEOMS 48
 #define MG_MAX_PAIRS 192
 #define MG_MAX_SENSORS 8
+#define MG_MAX_TENDONS 8
+#define MG_MAX_HAND_DOFS 32
 
 enum { MG_JT_FREE = 0, MG_JT_FIXED = 1, MG_JT_HINGE = 2, MG_JT_SLIDE = 3 };
 enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4 };
 enum { MG_OK = 0, MG_EINVAL = -1, MG_EDEVICE = -2, MG_ENOMEM = -3, MG_ECAPACITY = -4 };
-enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2 };
+enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2, MG_TASK_SHADOW_HAND = 3 };
 #define MG_MAX_AGENTS 8
-enum { MG_SET_ROOT_STATE = 0, MG_SET_DOF_STATE = 1 };
+enum { MG_SET_ROOT_STATE = 0, MG_SET_DOF_STATE = 1, MG_SET_DOF_TARGET = 2 };
+/* geom collision filter bits (mg_model.geom_filter) */
+enum { MG_COLLIDE_GROUND = 1, MG_COLLIDE_OBJECT = 2 };
 
 /* One articulation ("actor asset") as a dynamics tree of 1-DOF nodes.
  * Produced by migym/model.py (pack_model); field order == MODEL_DTYPE. */
@@ -93,12 +100,34 @@ typedef struct mg_model {
   int32_t geom_type[MG_MAX_GEOMS];
   int32_t geom_node[MG_MAX_GEOMS];
   int32_t geom_body[MG_MAX_GEOMS];
-  int32_t geom_pad[MG_MAX_GEOMS];
+  int32_t geom_filter[MG_MAX_GEOMS]; /* MG_COLLIDE_* bits */
   float geom_size[MG_MAX_GEOMS][3];
   float geom_pos[MG_MAX_GEOMS][3];   /* node frame */
   float geom_quat[MG_MAX_GEOMS][4];  /* node frame; capsule axis = local z */
   int32_t pair[MG_MAX_PAIRS][2];     /* self-collision geom pairs */
   int32_t sensor_body[MG_MAX_SENSORS];
+  /* ---- position drives, fixed tendons and the free object of hand tasks
+   * (shadow_hand.py:234-266, 684-698; shared.xml:55-72, 249-270) */
+  float drive_kp[MG_MAX_NODES];      /* PD drive stiffness (MJCF <position kp>); > 0 = DOF_MODE_POS */
+  float effort_limit[MG_MAX_NODES];  /* |drive force| limit (actuator forcerange) */
+  int32_t num_tendons;
+  int32_t gravity_off;               /* AssetOptions.disable_gravity of the articulation */
+  int32_t tendon_dof[MG_MAX_TENDONS][2];
+  float tendon_coef[MG_MAX_TENDONS][2];
+  float tendon_range[MG_MAX_TENDONS][2];
+  float tendon_limit_stiffness[MG_MAX_TENDONS];
+  float tendon_damping[MG_MAX_TENDONS];
+  /* One free rigid body per env next to the articulation (the manipulated object), plus a
+   * kinematic goal actor.  Root-state rows per env are then [articulation, object, goal] and
+   * rigid-body rows [articulation bodies..., object, goal]. */
+  int32_t obj_type;                  /* 0 = none, MG_GT_BOX */
+  int32_t obj_pad;
+  float obj_mass;
+  float obj_inertia[3];              /* principal moments, object frame (COM at the origin) */
+  float obj_size[3];                 /* box half extents */
+  float obj_lin_damping;
+  float obj_ang_damping;
+  float obj_gravity;                 /* 1 = the object falls under sim gravity */
 } mg_model;
 
 /* Simulation parameters (cfg['sim'] of the task YAML: Ant.yaml:42-61). */
@@ -125,6 +154,7 @@ typedef struct mg_state_views {
   float* sensors;           /* (N*A*S, 6), may be NULL */
   float* dof_force;         /* (N*A*nD), may be NULL */
   float* rigid_body_states; /* (N*A*nB, 13), may be NULL */
+  const float* dof_targets; /* (N*A*nD) PD position targets (set_dof_position_target_tensor), may be NULL */
 } mg_state_views;
 
 /* Task constants (cfg['env'] of the task YAML). */
@@ -163,6 +193,33 @@ typedef struct mg_task_params {
   int32_t num_agents;
   int32_t pad_ma;
   float agent_offset[8][3]; /* start-pose / target offset of each agent within its env */
+  /* in-hand manipulation (MG_TASK_SHADOW_HAND; tasks/shadow_hand.py:40-118, ShadowHand.yaml) */
+  int32_t num_fingertips;
+  int32_t fingertip_body[8];          /* gym rigid-body index of each fingertip */
+  int32_t actuated_dof[MG_MAX_HAND_DOFS]; /* action column -> DOF (actuator order) */
+  int32_t max_consecutive_successes;
+  int32_t use_relative_control;
+  int32_t ignore_z_rot;               /* pen */
+  int32_t obs_type;                   /* 0 = full_state (211) */
+  float dof_speed_scale;
+  float act_moving_average;
+  float dist_reward_scale;
+  float rot_reward_scale;
+  float rot_eps;
+  float action_penalty_scale;
+  float success_tolerance;
+  float reach_goal_bonus;
+  float fall_dist;
+  float fall_penalty;
+  float av_factor;
+  float vel_obs_scale;
+  float force_torque_obs_scale;
+  float reset_position_noise;
+  float reset_dof_pos_noise;
+  float reset_dof_vel_noise;
+  float object_start[3];             /* object_init_state position */
+  float goal_displacement[3];        /* goal actor = goal_states + displacement */
+  float goal_dz;                     /* goal_init = object_init + (0, 0, goal_dz) */
 } mg_task_params;
 
 /* Task-layer buffers (VecTask.allocate_buffers, vec_task.py:302-325). */
@@ -179,10 +236,19 @@ typedef struct mg_task_buffers {
   float* prev_potentials;   /* (N*A) */
   float* up_vec;            /* (N*A, 3) */
   float* heading_vec;       /* (N*A, 3) */
-  const float* noise;       /* (N*A, 2*nD) injected U(0,1) reset noise, or NULL = device RNG */
+  const float* noise;       /* (N*A, 2*nD) injected U(0,1) reset noise, or NULL = device RNG;
+                             * ShadowHand: (N, 61) = [goal-only draw 4 | reset_idx draw 53 |
+                             * reset_target_pose draw 4] (shadow_hand.py:587, 610) */
   uint64_t seed;            /* device RNG seed (counter-based, keyed by global env id) */
   uint64_t step_counter;    /* VecTask.control_steps: RNG counter */
   int64_t env_offset;       /* global id of this shard's first env (multi-GPU) */
+  /* in-hand manipulation (tasks/shadow_hand.py:186-219); unused by the other tasks */
+  float* prev_targets;      /* (N, nD) */
+  float* goal_states;       /* (N, 13) */
+  int64_t* reset_goal;      /* (N) reset_goal_buf */
+  float* successes;         /* (N) */
+  float* consecutive_successes; /* (1) running mean (shadow_hand.py:795-798) */
+  uint64_t* reduce_scratch; /* (2) device scratch: sum(resets), sum(successes * resets) */
 } mg_task_buffers;
 
 const char* mg_last_error(void);
@@ -191,6 +257,7 @@ size_t mg_model_sizeof(void);
 size_t mg_task_params_sizeof(void);
 size_t mg_task_buffers_sizeof(void);
 size_t mg_sim_params_sizeof(void);
+size_t mg_state_views_sizeof(void);
 
 typedef struct mg_sim mg_sim;
 

@@ -365,6 +365,7 @@ size_t mg_model_sizeof(void) { return sizeof(mg_model); }
 size_t mg_task_params_sizeof(void) { return sizeof(mg_task_params); }
 size_t mg_task_buffers_sizeof(void) { return sizeof(mg_task_buffers); }
 size_t mg_sim_params_sizeof(void) { return sizeof(mg_sim_params); }
+size_t mg_state_views_sizeof(void) { return sizeof(mg_state_views); }
 
 int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
                   mg_sim** out) {

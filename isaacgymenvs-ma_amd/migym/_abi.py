@@ -16,8 +16,10 @@ from . import model as _model
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "_lib", "libmigym.so")
 
-MG_TASK_CARTPOLE, MG_TASK_ANT, MG_TASK_HUMANOID = 0, 1, 2
-MG_SET_ROOT_STATE, MG_SET_DOF_STATE = 0, 1
+MG_TASK_CARTPOLE, MG_TASK_ANT, MG_TASK_HUMANOID, MG_TASK_SHADOW_HAND = 0, 1, 2, 3
+MG_SET_ROOT_STATE, MG_SET_DOF_STATE, MG_SET_DOF_TARGET = 0, 1, 2
+MG_MAX_HAND_DOFS = 32
+HAND_NOISE_COLS = 61   # [goal-only 4 | reset_idx 53 | reset_target_pose 4] (shadow_hand.py:587, 610)
 
 
 class SimParams(C.Structure):
@@ -29,7 +31,8 @@ class SimParams(C.Structure):
 
 class StateViews(C.Structure):
     _fields_ = [("root_states", C.c_void_p), ("dof_state", C.c_void_p), ("dof_actuation", C.c_void_p),
-                ("sensors", C.c_void_p), ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p)]
+                ("sensors", C.c_void_p), ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p),
+                ("dof_targets", C.c_void_p)]
 
 
 class TaskParams(C.Structure):
@@ -43,7 +46,19 @@ class TaskParams(C.Structure):
                 ("reset_dist", C.c_float), ("target", C.c_float * 3), ("start_pos", C.c_float * 3),
                 ("start_rot", C.c_float * 4), ("motor_effort", C.c_float * 64), ("dof_lower", C.c_float * 64),
                 ("dof_upper", C.c_float * 64), ("initial_dof_pos", C.c_float * 64),
-                ("num_agents", C.c_int32), ("pad_ma", C.c_int32), ("agent_offset", (C.c_float * 3) * 8)]
+                ("num_agents", C.c_int32), ("pad_ma", C.c_int32), ("agent_offset", (C.c_float * 3) * 8),
+                # in-hand manipulation (MG_TASK_SHADOW_HAND)
+                ("num_fingertips", C.c_int32), ("fingertip_body", C.c_int32 * 8),
+                ("actuated_dof", C.c_int32 * MG_MAX_HAND_DOFS), ("max_consecutive_successes", C.c_int32),
+                ("use_relative_control", C.c_int32), ("ignore_z_rot", C.c_int32), ("obs_type", C.c_int32),
+                ("dof_speed_scale", C.c_float), ("act_moving_average", C.c_float),
+                ("dist_reward_scale", C.c_float), ("rot_reward_scale", C.c_float), ("rot_eps", C.c_float),
+                ("action_penalty_scale", C.c_float), ("success_tolerance", C.c_float),
+                ("reach_goal_bonus", C.c_float), ("fall_dist", C.c_float), ("fall_penalty", C.c_float),
+                ("av_factor", C.c_float), ("vel_obs_scale", C.c_float), ("force_torque_obs_scale", C.c_float),
+                ("reset_position_noise", C.c_float), ("reset_dof_pos_noise", C.c_float),
+                ("reset_dof_vel_noise", C.c_float), ("object_start", C.c_float * 3),
+                ("goal_displacement", C.c_float * 3), ("goal_dz", C.c_float)]
 
 
 class TaskBuffers(C.Structure):
@@ -52,7 +67,9 @@ class TaskBuffers(C.Structure):
                 ("progress", C.c_void_p), ("timeout", C.c_void_p), ("potentials", C.c_void_p),
                 ("prev_potentials", C.c_void_p), ("up_vec", C.c_void_p), ("heading_vec", C.c_void_p),
                 ("noise", C.c_void_p), ("seed", C.c_uint64), ("step_counter", C.c_uint64),
-                ("env_offset", C.c_int64)]
+                ("env_offset", C.c_int64),
+                ("prev_targets", C.c_void_p), ("goal_states", C.c_void_p), ("reset_goal", C.c_void_p),
+                ("successes", C.c_void_p), ("consecutive_successes", C.c_void_p), ("reduce_scratch", C.c_void_p)]
 
 
 def model_bytes(spec) -> np.ndarray:
@@ -77,6 +94,7 @@ EXPORTS = {
     "mg_task_params_sizeof": (C.c_size_t, []),
     "mg_task_buffers_sizeof": (C.c_size_t, []),
     "mg_sim_params_sizeof": (C.c_size_t, []),
+    "mg_state_views_sizeof": (C.c_size_t, []),
     "mg_sim_create": (C.c_int, [C.c_void_p, C.POINTER(SimParams), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "mg_sim_bind": (C.c_int, [C.c_void_p, C.POINTER(StateViews)]),
     "mg_sim_simulate": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -106,7 +124,8 @@ def _bind(lib):
 
 def check_layout(lib):
     sizes = {"mg_model_sizeof": _model.MODEL_DTYPE.itemsize, "mg_task_params_sizeof": C.sizeof(TaskParams),
-             "mg_task_buffers_sizeof": C.sizeof(TaskBuffers), "mg_sim_params_sizeof": C.sizeof(SimParams)}
+             "mg_task_buffers_sizeof": C.sizeof(TaskBuffers), "mg_sim_params_sizeof": C.sizeof(SimParams),
+             "mg_state_views_sizeof": C.sizeof(StateViews)}
     for fn, py in sizes.items():
         c = getattr(lib, fn)()
         if c != py:

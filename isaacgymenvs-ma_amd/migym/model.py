@@ -44,6 +44,8 @@ MAX_BODIES = 40
 MAX_GEOMS = 48
 MAX_PAIRS = 192
 MAX_SENSORS = 8
+MAX_TENDONS = 8
+COLLIDE_GROUND, COLLIDE_OBJECT = 1, 2
 
 JT_FREE, JT_FIXED, JT_HINGE, JT_SLIDE = 0, 1, 2, 3
 GT_PLANE, GT_SPHERE, GT_CAPSULE, GT_BOX, GT_CYLINDER = 0, 1, 2, 3, 4
@@ -152,6 +154,8 @@ class Node:
     lower: float = 0.0
     upper: float = 0.0
     limited: int = 0
+    drive_kp: float = 0.0          # MJCF <position kp>: PD position drive (DOF_MODE_POS)
+    effort_limit: float = 0.0      # actuator forcerange (|force| clamp of the drive)
 
 
 @dataclass
@@ -176,6 +180,7 @@ class Geom:
     quat: List[float]              # orientation in node frame (capsule/cylinder axis = local z)
     contype: int = 1
     conaffinity: int = 1
+    filter: int = 3                # MG_COLLIDE_GROUND | MG_COLLIDE_OBJECT
 
 
 @dataclass
@@ -190,6 +195,9 @@ class ModelSpec:
     dof_names: List[str]
     sensors: List[int] = field(default_factory=list)
     self_collision: int = 0
+    tendons: List[Dict] = field(default_factory=list)   # {name, dofs[2], coefs[2], range[2], limit_stiffness, damping}
+    gravity_off: int = 0
+    obj: Optional[Dict] = None     # free object sharing the env: {type, size, mass, inertia, lin_damping, ...}
 
     @property
     def num_dofs(self):
@@ -337,8 +345,17 @@ def _orientation(a, angle_scale):
     return np.array([0, 0, 0, 1.0])
 
 
-def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True) -> ModelSpec:
-    """Parse an MJCF file (with <include>) into a :class:`ModelSpec`."""
+def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, collapse_fixed=False,
+              mesh_boxes=None) -> ModelSpec:
+    """Parse an MJCF file (with <include>) into a :class:`ModelSpec`.
+
+    ``collapse_fixed``: a jointless body is merged into its parent *body* (gym
+    ``AssetOptions.collapse_fixed_joints``, shadow_hand.py:236) instead of becoming a
+    rigid body of its own.  ``mesh_boxes``: {mesh name: (center, half extents)} box
+    stand-ins for convex-mesh collision geoms (the build has no convex-mesh narrowphase).
+    A fixed-base root body keeps its MJCF orientation (its translation is replaced by the
+    actor start pose): the reference places the object on the palm with the hand mount's
+    rotation applied and its position ignored (shadow_hand.py:306-318, robot.xml:3)."""
     root = _read_mjcf_tree(path)
     compiler = root.find("compiler")
     angle_scale = math.pi / 180.0
@@ -371,8 +388,10 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True) ->
                 out.append((a.get("type", "hinge"), a, cls))
         return out
 
-    def add_body_content(b, cls, node_idx, body_idx, T_node_body: Xform):
-        # geoms and mass, expressed in node frame
+    def add_body_content(b, cls, node_idx, body_idx, T_node_body: Xform, T_acc: Xform = None):
+        # geoms and mass, expressed in node frame; T_acc: this MJCF body in the frame of the gym
+        # body it is accumulated into (identity unless collapsed into its parent)
+        T_acc = T_acc or Xform()
         explicit = b.find("inertial")
         acc = mass_acc.setdefault(node_idx, _MassAccum())
         bacc = body_mass.setdefault(body_idx, _MassAccum())
@@ -381,9 +400,16 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True) ->
             a.update(g.attrib)
             if a.get("type", "sphere") == "plane":
                 continue
-            gtype, size, Xg = _geom_size_and_frame(a, angle_scale)
+            if a.get("type") == "mesh" and mesh_boxes and a.get("mesh") in mesh_boxes and \
+                    not (a.get("contype", "1") == "0" and a.get("conaffinity", "1") == "0"):
+                ctr, half = mesh_boxes[a["mesh"]]
+                Xm = Xform(np.array(_floats(a.get("pos", "0 0 0"))), _orientation(a, angle_scale))
+                gtype, size, Xg = GT_BOX, [float(v) for v in half], Xm.compose(Xform(np.array(ctr)))
+            else:
+                gtype, size, Xg = _geom_size_and_frame(a, angle_scale)
             if gtype is None:
-                continue   # meshes: not supported by this loader revision (ShadowHand forearm)
+                continue   # visual meshes
+            Xg = T_acc.compose(Xg)
             Xn = T_node_body.compose(Xg)
             contype = int(a.get("contype", "1"))
             conaff = int(a.get("conaffinity", "1"))
@@ -411,26 +437,40 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True) ->
             else:
                 f = _floats(explicit.get("fullinertia"))
                 Id = np.array([[f[0], f[3], f[4]], [f[3], f[1], f[5]], [f[4], f[5], f[2]]])
-            Xi = T_node_body.compose(Xform(ipos, irot))
+            Xib = T_acc.compose(Xform(ipos, irot))
+            Xi = T_node_body.compose(Xib)
             R = qmat(Xi.rot)
             acc.add(m, Xi.pos, R @ Id @ R.T)
-            Rb = qmat(irot)
-            bacc.add(m, ipos, Rb @ Id @ Rb.T)
+            Rb = qmat(Xib.rot)
+            bacc.add(m, Xib.pos, Rb @ Id @ Rb.T)
 
-    def visit(b, cls, parent_node, T_parent: Xform, parent_body):
-        """T_parent: parent body frame expressed in parent_node frame."""
+    def visit(b, cls, parent_node, T_parent: Xform, parent_body, T_acc_parent: Xform = None):
+        """T_parent: parent gym-body frame expressed in parent_node frame; T_acc_parent: parent MJCF
+        body in its gym body's frame (non-identity only inside a collapsed chain)."""
         cls = b.get("childclass", cls)
-        body_idx = len(bodies)
         bpos = np.array(_floats(b.get("pos", "0 0 0")))
         brot = _orientation(b.attrib, angle_scale)
         joints = joint_list(b, cls)
+        if parent_node >= 0 and not joints and collapse_fixed:
+            # welded into the parent gym body (collapse_fixed_joints)
+            T_acc = (T_acc_parent or Xform()).compose(Xform(bpos, brot))
+            add_body_content(b, cls, parent_node, parent_body, T_parent, T_acc)
+            for c in b.findall("body"):
+                visit(c, cls, parent_node, T_parent, parent_body, T_acc)
+            return
+        if T_acc_parent is not None:
+            # child of a collapsed body: its pose is relative to the collapsed MJCF body
+            T_rel = T_acc_parent.compose(Xform(bpos, brot))
+            bpos, brot = T_rel.pos, T_rel.rot
+        body_idx = len(bodies)
         if parent_node < 0:
-            # root body: its frame is the actor frame (start pose supplied by the task)
+            # root body: its frame is the actor frame (start pose supplied by the task); a fixed
+            # base keeps the MJCF orientation of the root body
             jt = JT_FREE if (joints and joints[0][0] == "free") else JT_FIXED
             nodes.append(Node(name=b.get("name", "root"), parent=-1, jtype=jt, t=[0, 0, 0], r0=[0, 0, 0, 1],
                               axis=[0, 0, 1], body=body_idx))
             node_idx = 0
-            T_body = Xform()
+            T_body = Xform(np.zeros(3), brot) if jt == JT_FIXED else Xform()
         elif not joints:
             node_idx = parent_node
             T_body = T_parent.compose(Xform(bpos, brot))
@@ -491,10 +531,35 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True) ->
             actuators.append(dict(kind=a0.tag, joint=a.get("joint"), gear=float(_floats(a.get("gear", "1"))[0]),
                                   kp=float(a.get("kp", "0")),
                                   forcerange=_floats(a.get("forcerange", "0 0"))))
+            if a0.tag == "position" and a.get("joint") in dof_names:
+                # gym maps an MJCF position actuator to a DOF_MODE_POS drive: stiffness = kp, damping =
+                # the joint damping, effort = forcerange (shadow_hand.py:241-242, 268-280)
+                nd = nodes[1 + dof_names.index(a["joint"])]
+                nd.drive_kp = float(a.get("kp", "0"))
+                fr = _floats(a.get("forcerange", "0 0"))
+                nd.effort_limit = float(max(abs(fr[0]), abs(fr[1]))) if a.get("forcelimited", "true") != "false" \
+                    else float("inf")
+    tendons = []
+    ten = root.find("tendon")
+    if ten is not None:
+        for t0 in ten.findall("fixed"):
+            js = t0.findall("joint")
+            if len(js) > 2:
+                raise ValueError("fixed tendons with more than two joints are not supported")
+            dofs = [dof_names.index(j.get("joint")) for j in js]
+            coefs = [float(j.get("coef", "1")) for j in js]
+            while len(dofs) < 2:
+                dofs.append(dofs[0])
+                coefs.append(0.0)
+            rng = _floats(t0.get("range", "0 0"))
+            tendons.append(dict(name=t0.get("name", f"t{len(tendons)}"), dofs=dofs, coefs=coefs, range=rng,
+                                limited=int(t0.get("limited", "false") == "true"),
+                                limit_stiffness=float(t0.get("stiffness", "0")), damping=float(t0.get("damping", "0"))))
 
     spec = ModelSpec(name=name or os.path.splitext(os.path.basename(path))[0],
                      fixed_base=int(nodes[0].jtype == JT_FIXED), nodes=nodes, bodies=bodies, geoms=geoms,
-                     pairs=[], actuators=actuators, dof_names=dof_names, self_collision=int(self_collision))
+                     pairs=[], actuators=actuators, dof_names=dof_names, self_collision=int(self_collision),
+                     tendons=tendons)
     if self_collision:
         spec.pairs = self_collision_pairs(spec)
     return spec
@@ -673,7 +738,7 @@ def load_urdf(path, name=None, fix_base=True) -> ModelSpec:
 # packing into the mg_model POD struct (layout mirrors include/migym.h)
 def _model_dtype():
     f4, i4 = np.float32, np.int32
-    N, B, G, P, S = MAX_NODES, MAX_BODIES, MAX_GEOMS, MAX_PAIRS, MAX_SENSORS
+    N, B, G, P, S, TD = MAX_NODES, MAX_BODIES, MAX_GEOMS, MAX_PAIRS, MAX_SENSORS, MAX_TENDONS
     return np.dtype([
         ("num_nodes", i4), ("num_dofs", i4), ("fixed_base", i4), ("num_bodies", i4),
         ("num_geoms", i4), ("num_pairs", i4), ("num_sensors", i4), ("nv", i4),
@@ -683,10 +748,16 @@ def _model_dtype():
         ("armature", f4, N), ("damping", f4, N), ("stiffness", f4, N), ("lower", f4, N), ("upper", f4, N),
         ("body_node", i4, B), ("body_parent", i4, B),
         ("body_pos", f4, (B, 3)), ("body_quat", f4, (B, 4)), ("body_com", f4, (B, 3)),
-        ("geom_type", i4, G), ("geom_node", i4, G), ("geom_body", i4, G), ("geom_pad", i4, G),
+        ("geom_type", i4, G), ("geom_node", i4, G), ("geom_body", i4, G), ("geom_filter", i4, G),
         ("geom_size", f4, (G, 3)), ("geom_pos", f4, (G, 3)), ("geom_quat", f4, (G, 4)),
         ("pair", i4, (P, 2)),
         ("sensor_body", i4, S),
+        ("drive_kp", f4, N), ("effort_limit", f4, N),
+        ("num_tendons", i4), ("gravity_off", i4),
+        ("tendon_dof", i4, (TD, 2)), ("tendon_coef", f4, (TD, 2)), ("tendon_range", f4, (TD, 2)),
+        ("tendon_limit_stiffness", f4, TD), ("tendon_damping", f4, TD),
+        ("obj_type", i4), ("obj_pad", i4), ("obj_mass", f4), ("obj_inertia", f4, 3), ("obj_size", f4, 3),
+        ("obj_lin_damping", f4), ("obj_ang_damping", f4), ("obj_gravity", f4),
     ])
 
 
@@ -696,7 +767,7 @@ MODEL_DTYPE = _model_dtype()
 def pack_model(spec: ModelSpec) -> np.ndarray:
     if len(spec.nodes) > MAX_NODES or len(spec.bodies) > MAX_BODIES or len(spec.geoms) > MAX_GEOMS:
         raise ValueError("model exceeds mg_model capacity")
-    if len(spec.pairs) > MAX_PAIRS or len(spec.sensors) > MAX_SENSORS:
+    if len(spec.pairs) > MAX_PAIRS or len(spec.sensors) > MAX_SENSORS or len(spec.tendons) > MAX_TENDONS:
         raise ValueError("model exceeds mg_model pair/sensor capacity")
     m = np.zeros((), dtype=MODEL_DTYPE)
     m["num_nodes"] = len(spec.nodes)
@@ -724,6 +795,8 @@ def pack_model(spec: ModelSpec) -> np.ndarray:
         m["stiffness"][i] = n.stiffness
         m["lower"][i] = n.lower
         m["upper"][i] = n.upper
+        m["drive_kp"][i] = n.drive_kp
+        m["effort_limit"][i] = n.effort_limit
     for i, b in enumerate(spec.bodies):
         m["body_node"][i] = b.node
         m["body_parent"][i] = b.parent_body
@@ -737,10 +810,28 @@ def pack_model(spec: ModelSpec) -> np.ndarray:
         m["geom_size"][i] = g.size
         m["geom_pos"][i] = g.pos
         m["geom_quat"][i] = g.quat
+        m["geom_filter"][i] = g.filter
     for i, p in enumerate(spec.pairs):
         m["pair"][i] = p
     for i, s in enumerate(spec.sensors):
         m["sensor_body"][i] = s
+    m["num_tendons"] = len(spec.tendons)
+    m["gravity_off"] = int(spec.gravity_off)
+    for i, t in enumerate(spec.tendons):
+        m["tendon_dof"][i] = t["dofs"]
+        m["tendon_coef"][i] = t["coefs"]
+        m["tendon_range"][i] = t["range"] if t.get("limited", 1) else [-np.inf, np.inf]
+        m["tendon_limit_stiffness"][i] = t["limit_stiffness"]
+        m["tendon_damping"][i] = t["damping"]
+    if spec.obj:
+        o = spec.obj
+        m["obj_type"] = o["type"]
+        m["obj_mass"] = o["mass"]
+        m["obj_inertia"] = o["inertia"]
+        m["obj_size"] = o["size"]
+        m["obj_lin_damping"] = o.get("lin_damping", 0.0)
+        m["obj_ang_damping"] = o.get("ang_damping", 0.0)
+        m["obj_gravity"] = o.get("gravity", 1)
     return m
 
 

@@ -36,6 +36,11 @@ float orc_uniform(uint64_t seed, uint64_t env, uint64_t counter, uint32_t k);
 int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* root_states, float* dof_state,
                  const float* dof_actuation, float* sensors, float* dof_force, int32_t threads);
 
+/* gym.simulate on the full state views: object/goal root rows, PD targets and rigid-body states
+ * of hand tasks included (views->dof_targets may be NULL = zero targets). */
+int orc_simulate_views(const mg_model* m, const mg_sim_params* p, int32_t n, const mg_state_views* v,
+                       int32_t threads);
+
 /* Debug/KAT hooks for one actor: mass matrix (nv*nv row-major, includes the
  * armature + implicit damping/stiffness diagonal for substep h) and the
  * unconstrained generalized acceleration. */

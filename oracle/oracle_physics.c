@@ -17,6 +17,12 @@
  *     [contact: normal, t1, t2]* then joint limits [lower, upper] per DOF;
  *     pos_iters sweeps (physx.num_position_iterations, Ant.yaml:53)
  *   - semi-implicit Euler; root quaternion by the exact exponential map
+ *   - hand tasks (SURVEY.md §8(a) A4-A8 for ShadowHand): PD position drives
+ *     (implicit spring/damper toward the target; an explicit +-effort force
+ *     when the explicit estimate saturates), fixed tendons as explicit
+ *     soft-limit springs + dampers, and one free rigid box per env whose
+ *     6 velocity columns [w; v_com] join the articulation's in one
+ *     block-diagonal system (contacts couple them)
  */
 #include <math.h>
 #include <stdlib.h>
@@ -29,7 +35,8 @@
 #endif
 
 #define MAXN MG_MAX_NODES
-#define MAXV (MG_MAX_NODES + 6)
+#define MAXV (MG_MAX_NODES + 12)
+#define OBJ_NODE (-2) /* contact side on the free object */
 #define MAXC 64
 #define MAXR (3 * MAXC + 2 * MG_MAX_NODES)
 
@@ -128,6 +135,11 @@ typedef struct {
   double p[3], q[4];     /* root pose */
   double nu0[6];         /* root spatial velocity at root origin [w; v_o] */
   double qj[MAXN], qd[MAXN];
+  double op[3], oq[4];   /* free object pose (COM = origin) */
+  double ow[3], ov[3];   /* object angular / COM linear velocity (world) */
+  const float* tgt;      /* PD targets (nD) or NULL */
+  int sat[MAXN];         /* drive saturated in the last substep */
+  double ttend[MAXN];    /* tendon generalized force of the last substep */
 } astate;
 
 typedef struct {
@@ -136,6 +148,7 @@ typedef struct {
   double I[MAXN][6][6];
   double V[MAXN][6];
   double o[3];
+  double oR[3][3], op[3]; /* free object pose */
 } kin;
 
 typedef struct {
@@ -144,6 +157,7 @@ typedef struct {
 } contact;
 
 static int nv_of(const mg_model* m) { return (m->fixed_base ? 0 : 6) + m->num_dofs; }
+static int nvt_of(const mg_model* m) { return nv_of(m) + (m->obj_type ? 6 : 0); } /* + object columns */
 static int dof_col(const mg_model* m, int node) { return (m->fixed_base ? 0 : 6) + node - 1; }
 
 static void load_state(const mg_model* m, const float* root, const float* dof, astate* s) {
@@ -244,15 +258,60 @@ static void forward_kinematics(const mg_model* m, const astate* s, kin* k) {
         k->I[i][3 + a][3 + b] = (a == b) ? mass : 0.0;
       }
   }
+  if (m->obj_type) {
+    quat_to_mat(s->oq, k->oR);
+    for (int c = 0; c < 3; c++) k->op[c] = s->op[c];
+  }
   /* velocities */
   for (int c = 0; c < 6; c++) k->V[0][c] = m->fixed_base ? 0.0 : s->nu0[c];
   for (int i = 1; i < m->num_nodes; i++)
     for (int c = 0; c < 6; c++) k->V[i][c] = k->V[m->parent[i]][c] + k->S[i][c] * s->qd[i];
 }
 
+/* per-DOF implicit spring/damper of the substep: tau = tadd - b qd - k (q - ref + h qd),
+ * diagonal += armature + h b + h^2 k.  Drives (drive_kp > 0): k = kp toward the target, b = joint
+ * damping, unless the explicit estimate kp (tgt - q) - b qd exceeds the effort limit: then a constant
+ * +-limit force and no implicit terms (PhysX clamps the drive force, shadow_hand.py:241-242). */
+typedef struct {
+  double k, b, ref, tadd;
+  int sat;
+} dofterm;
+
+static dofterm dof_term(const mg_model* m, const astate* s, int i) {
+  dofterm t = {m->stiffness[i], m->damping[i], 0.0, 0.0, 0};
+  double kp = m->drive_kp[i];
+  if (kp > 0.0) {
+    double tgt = s->tgt ? s->tgt[i - 1] : 0.0;
+    double fe = kp * (tgt - s->qj[i]) - m->damping[i] * s->qd[i];
+    double F = m->effort_limit[i];
+    if (fabs(fe) > F) {
+      t.k = 0.0; t.b = 0.0; t.tadd = fe > 0 ? F : -F; t.sat = 1;
+    } else {
+      t.k = kp; t.ref = tgt;
+    }
+  }
+  return t;
+}
+
+/* fixed tendons: length L = sum c q, force f = -ks (L - clamp(L, lo, hi)) - kd dL/dt (explicit) */
+static void tendon_forces(const mg_model* m, const astate* s, double* tau /* per node */) {
+  for (int i = 0; i < m->num_nodes; i++) tau[i] = 0.0;
+  for (int t = 0; t < m->num_tendons; t++) {
+    int n0 = m->tendon_dof[t][0] + 1, n1 = m->tendon_dof[t][1] + 1;
+    double c0 = m->tendon_coef[t][0], c1 = m->tendon_coef[t][1];
+    double L = c0 * s->qj[n0] + c1 * s->qj[n1];
+    double Ld = c0 * s->qd[n0] + c1 * s->qd[n1];
+    double lo = m->tendon_range[t][0], hi = m->tendon_range[t][1];
+    double cl = L < lo ? lo : (L > hi ? hi : L);
+    double f = -m->tendon_limit_stiffness[t] * (L - cl) - m->tendon_damping[t] * Ld;
+    tau[n0] += c0 * f;
+    tau[n1] += c1 * f;
+  }
+}
+
 /* joint-space inertia (CRBA) incl. implicit diagonal, h = substep */
-static void mass_matrix(const mg_model* m, const kin* k, double h, double* M) {
-  int nv = nv_of(m), nn = m->num_nodes;
+static void mass_matrix(const mg_model* m, const kin* k, double h, double* M, const double* diag, int ld) {
+  int nv = ld, nn = m->num_nodes;
   double Ic[MAXN][6][6];
   memcpy(Ic, k->I, sizeof(double) * 36 * nn);
   for (int i = nn - 1; i >= 1; i--) {
@@ -268,7 +327,7 @@ static void mass_matrix(const mg_model* m, const kin* k, double h, double* M) {
     double F[6];
     mat6vec(Ic[i], k->S[i], F);
     int ci = dof_col(m, i);
-    M[ci * nv + ci] = dot6(k->S[i], F) + m->armature[i] + h * m->damping[i] + h * h * m->stiffness[i];
+    M[ci * nv + ci] = dot6(k->S[i], F) + (diag ? diag[i] : m->armature[i] + h * m->damping[i] + h * h * m->stiffness[i]);
     int j = m->parent[i];
     while (j > 0) {
       int cj = dof_col(m, j);
@@ -284,7 +343,7 @@ static void mass_matrix(const mg_model* m, const kin* k, double h, double* M) {
 
 /* bias forces C(q,v) incl. gravity (RNEA with qdd = 0) */
 static void bias_forces(const mg_model* m, const kin* k, const astate* s, const double* g, double* C) {
-  int nn = m->num_nodes, nv = nv_of(m);
+  int nn = m->num_nodes, nv = nv_of(m); /* C has at least nv entries */
   double A[MAXN][6], f[MAXN][6];
   for (int c = 0; c < 6; c++) A[0][c] = 0;
   for (int i = 1; i < nn; i++) {
@@ -416,10 +475,171 @@ static int geom_segment(const mg_model* m, const kin* k, int g, double* a, doubl
   return 0;
 }
 
+/* ---- narrowphase against the free object's box (object frame: R = oR, center = op) */
+
+/* signed distance of point pl (box frame) to a box of half extents hb: outside -> distance to the
+ * closest point cb, normal away from the box; inside -> minus the smallest face depth (ties: x, y, z
+ * order), normal = that face's outward normal, cb = the projection onto that face */
+static double point_box(const double* pl, const double* hb, double* nb, double* cb) {
+  double q[3];
+  int out = 0;
+  for (int a = 0; a < 3; a++) {
+    q[a] = pl[a] < -hb[a] ? -hb[a] : (pl[a] > hb[a] ? hb[a] : pl[a]);
+    if (q[a] != pl[a]) out = 1;
+  }
+  if (out) {
+    double d[3] = {pl[0] - q[0], pl[1] - q[1], pl[2] - q[2]};
+    double l = sqrt(dot3(d, d));
+    for (int a = 0; a < 3; a++) { nb[a] = d[a] / l; cb[a] = q[a]; }
+    return l;
+  }
+  int kmin = 0;
+  double dmin = hb[0] - fabs(pl[0]);
+  for (int a = 1; a < 3; a++) {
+    double dd = hb[a] - fabs(pl[a]);
+    if (dd < dmin) { dmin = dd; kmin = a; }
+  }
+  for (int a = 0; a < 3; a++) { nb[a] = 0.0; cb[a] = pl[a]; }
+  double sg = pl[kmin] < 0 ? -1.0 : 1.0;
+  nb[kmin] = sg;
+  cb[kmin] = sg * hb[kmin];
+  return -dmin;
+}
+
+/* closest parameter t in [0,1] of segment a + t u (box frame) to the box: f(t) = sum_k
+ * max(|a_k + t u_k| - h_k, 0)^2 is convex piecewise quadratic; it is minimised exactly on each
+ * interval between the (sorted) slab crossings.  If the segment passes through the box
+ * (Liang-Barsky), returns the middle of the inside portion and *inside = 1. */
+static double seg_box_t(const double* a, const double* u, const double* hb, int* inside) {
+  double t0 = 0.0, t1 = 1.0;
+  int hit = 1;
+  for (int k = 0; k < 3 && hit; k++) {
+    if (fabs(u[k]) < 1e-12) {
+      if (a[k] < -hb[k] || a[k] > hb[k]) hit = 0;
+    } else {
+      double ta = (-hb[k] - a[k]) / u[k], tb = (hb[k] - a[k]) / u[k];
+      if (ta > tb) { double x = ta; ta = tb; tb = x; }
+      if (ta > t0) t0 = ta;
+      if (tb < t1) t1 = tb;
+      if (t0 > t1) hit = 0;
+    }
+  }
+  if (hit) { *inside = 1; return 0.5 * (t0 + t1); }
+  *inside = 0;
+  double bp[8];
+  int nb = 0;
+  bp[nb++] = 0.0;
+  for (int k = 0; k < 3; k++) {
+    if (fabs(u[k]) < 1e-12) continue;
+    for (int sgn = -1; sgn <= 1; sgn += 2) {
+      double t = (sgn * hb[k] - a[k]) / u[k];
+      if (t > 0.0 && t < 1.0) bp[nb++] = t;
+    }
+  }
+  bp[nb++] = 1.0;
+  for (int i = 1; i < nb; i++) /* insertion sort */
+    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { double x = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = x; }
+  double best_t = 0.0, best_f = 1e300;
+  for (int i = 0; i + 1 < nb; i++) {
+    double lo = bp[i], hi = bp[i + 1], mid = 0.5 * (lo + hi), num = 0.0, den = 0.0;
+    for (int k = 0; k < 3; k++) {
+      double x = a[k] + mid * u[k];
+      if (x > hb[k]) { num += (a[k] - hb[k]) * u[k]; den += u[k] * u[k]; }
+      else if (x < -hb[k]) { num += (a[k] + hb[k]) * u[k]; den += u[k] * u[k]; }
+    }
+    double t = den > 0.0 ? -num / den : lo;
+    t = t < lo ? lo : (t > hi ? hi : t);
+    double f = 0.0;
+    for (int k = 0; k < 3; k++) {
+      double x = fabs(a[k] + t * u[k]) - hb[k];
+      if (x > 0) f += x * x;
+    }
+    if (f < best_f) { best_f = f; best_t = t; }
+  }
+  return best_t;
+}
+
+static void to_obj(const kin* k, const double* pw, double* pl) {
+  double d[3] = {pw[0] - k->op[0], pw[1] - k->op[1], pw[2] - k->op[2]};
+  mattvec3((double(*)[3])k->oR, d, pl);
+}
+static void from_obj_dir(const kin* k, const double* dl, double* dw) { matvec3((double(*)[3])k->oR, dl, dw); }
+static void from_obj_pt(const kin* k, const double* pl, double* pw) {
+  matvec3((double(*)[3])k->oR, pl, pw);
+  for (int a = 0; a < 3; a++) pw[a] += k->op[a];
+}
+
+/* hand geom g (A) vs the object box (B); normal points from the object to the geom */
+static int geom_object(const mg_model* m, const kin* k, int g, double off, contact* out, int n, int cap) {
+  const double hb[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
+  int nd = m->geom_node[g], ty = m->geom_type[g];
+  double c[3], R[3][3];
+  geom_world(m, k, g, c, R);
+  if (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) {
+    double r = m->geom_size[g][0], hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0;
+    double aw[3], bw[3], al[3], bl[3], u[3];
+    for (int a = 0; a < 3; a++) { aw[a] = c[a] - R[a][2] * hl; bw[a] = c[a] + R[a][2] * hl; }
+    to_obj(k, aw, al);
+    to_obj(k, bw, bl);
+    for (int a = 0; a < 3; a++) u[a] = bl[a] - al[a];
+    int inside;
+    double t = seg_box_t(al, u, hb, &inside), P[3], nb[3], cb[3];
+    for (int a = 0; a < 3; a++) P[a] = al[a] + t * u[a];
+    double sd = point_box(P, hb, nb, cb), d = sd - r;
+    if (d < off) {
+      double pm[3], pw[3], nw[3];
+      for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - r * nb[a]) + cb[a]);
+      from_obj_pt(k, pm, pw);
+      from_obj_dir(k, nb, nw);
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+    return n;
+  }
+  if (ty != MG_GT_BOX) return n;
+  const double hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
+  /* the geom's vertices against the object */
+  for (int v = 0; v < 8; v++) {
+    double l[3] = {(v & 1 ? 1 : -1) * hg[0], (v & 2 ? 1 : -1) * hg[1], (v & 4 ? 1 : -1) * hg[2]}, w[3], pl[3];
+    matvec3(R, l, w);
+    for (int a = 0; a < 3; a++) w[a] += c[a];
+    to_obj(k, w, pl);
+    double nb[3], cb[3], d = point_box(pl, hb, nb, cb);
+    if (d < off) {
+      double pm[3], pw[3], nw[3];
+      for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
+      from_obj_pt(k, pm, pw);
+      from_obj_dir(k, nb, nw);
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+  }
+  /* the object's vertices against the geom box (normal flipped: geom -> object is -n) */
+  for (int v = 0; v < 8; v++) {
+    double l[3] = {(v & 1 ? 1 : -1) * hb[0], (v & 2 ? 1 : -1) * hb[1], (v & 4 ? 1 : -1) * hb[2]}, w[3], d3[3], pl[3];
+    from_obj_pt(k, l, w);
+    for (int a = 0; a < 3; a++) d3[a] = w[a] - c[a];
+    mattvec3(R, d3, pl);
+    double nb[3], cb[3], d = point_box(pl, hg, nb, cb);
+    if (d < off) {
+      double pm[3], pw[3], nw[3];
+      for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
+      matvec3(R, pm, pw);
+      for (int a = 0; a < 3; a++) pw[a] += c[a];
+      matvec3(R, nb, nw);
+      for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+  }
+  return n;
+}
+
+/* contact order (the HIP kernel emits the same list): ground contacts of the articulation's geoms
+ * in geom order, the object's box corners on the ground, self-collision pairs in pair order, then
+ * articulation geoms against the object in geom order */
 static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, contact* out, int cap) {
   int n = 0;
   double off = p->contact_offset;
   for (int g = 0; g < m->num_geoms; g++) {
+    if (!(m->geom_filter[g] & MG_COLLIDE_GROUND)) continue;
     int nd = m->geom_node[g], ty = m->geom_type[g];
     double c[3], R[3][3];
     geom_world(m, k, g, c, R);
@@ -442,6 +662,14 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       }
     }
   }
+  if (m->obj_type == MG_GT_BOX) {
+    for (int corner = 0; corner < 8; corner++) {
+      double l[3] = {(corner & 1 ? 1 : -1) * m->obj_size[0], (corner & 2 ? 1 : -1) * m->obj_size[1],
+                     (corner & 4 ? 1 : -1) * m->obj_size[2]}, e[3];
+      from_obj_pt(k, l, e);
+      n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
+    }
+  }
   for (int pi = 0; pi < m->num_pairs; pi++) {
     int ga = m->pair[pi][0], gb = m->pair[pi][1];
     double a0[3], a1[3], b0[3], b1[3], ra, rb;
@@ -461,6 +689,9 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pt, nrm, d);
     }
   }
+  if (m->obj_type == MG_GT_BOX)
+    for (int g = 0; g < m->num_geoms; g++)
+      if (m->geom_filter[g] & MG_COLLIDE_OBJECT) n = geom_object(m, k, g, off, out, n, cap);
   return n;
 }
 
@@ -473,11 +704,12 @@ static void tangent_basis(const double* n, double* t1, double* t2) {
   cross3(n, t1, t2);
 }
 
-/* generalized Jacobian row of a unit force `dir` at point p on nodeA (minus on nodeB) */
+/* generalized Jacobian row of a unit force `dir` at point p on nodeA (minus on nodeB); a side
+ * equal to OBJ_NODE acts on the free object's columns [w; v_com] (after the articulation's) */
 static void jac_row(const mg_model* m, const kin* k, int nodeA, int nodeB, const double* p, const double* dir,
                     double* J) {
-  int nv = nv_of(m);
-  memset(J, 0, sizeof(double) * nv);
+  int nv = nv_of(m), nvt = nvt_of(m);
+  memset(J, 0, sizeof(double) * nvt);
   double r[3], w[6];
   for (int a = 0; a < 3; a++) r[a] = p[a] - k->o[a];
   cross3(r, dir, w);
@@ -485,6 +717,13 @@ static void jac_row(const mg_model* m, const kin* k, int nodeA, int nodeB, const
   for (int side = 0; side < 2; side++) {
     int node = side == 0 ? nodeA : nodeB;
     double sg = side == 0 ? 1.0 : -1.0;
+    if (node == OBJ_NODE) {
+      double ro[3], rxd[3];
+      for (int a = 0; a < 3; a++) ro[a] = p[a] - k->op[a];
+      cross3(ro, dir, rxd);
+      for (int a = 0; a < 3; a++) { J[nv + a] += sg * rxd[a]; J[nv + 3 + a] += sg * dir[a]; }
+      continue;
+    }
     if (node < 0) continue;
     if (!m->fixed_base)
       for (int c = 0; c < 6; c++) J[c] += sg * w[c];
@@ -504,15 +743,23 @@ typedef struct {
 } substep_out;
 
 static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const double* tau_act, substep_out* so) {
-  int nv = nv_of(m), nn = m->num_nodes;
+  int nv = nv_of(m), nvt = nvt_of(m), nn = m->num_nodes;
   double h = p->dt / p->substeps;
   so->h = h;
   kin k;
   forward_kinematics(m, s, &k);
-  double M[MAXV * MAXV], C[MAXV], g[3] = {p->gravity[0], p->gravity[1], p->gravity[2]};
-  mass_matrix(m, &k, h, M);
+  static __thread double M[MAXV * MAXV];
+  double C[MAXV], diag[MAXN], tadd[MAXN], kk[MAXN], bb[MAXN], ref[MAXN];
+  double ga = m->gravity_off ? 0.0 : 1.0;
+  double g[3] = {ga * p->gravity[0], ga * p->gravity[1], ga * p->gravity[2]};
+  tendon_forces(m, s, s->ttend);
+  for (int i = 1; i < nn; i++) {
+    dofterm t = dof_term(m, s, i);
+    kk[i] = t.k; bb[i] = t.b; ref[i] = t.ref; tadd[i] = t.tadd; s->sat[i] = t.sat;
+    diag[i] = m->armature[i] + h * t.b + h * h * t.k;
+  }
+  mass_matrix(m, &k, h, M, diag, nvt);
   bias_forces(m, &k, s, g, C);
-  if (cholesky(M, nv) != 0) return;
   double nu[MAXV], rhs[MAXV];
   for (int c = 0; c < 6 && !m->fixed_base; c++) nu[c] = s->nu0[c];
   for (int i = 1; i < nn; i++) nu[dof_col(m, i)] = s->qd[i];
@@ -520,10 +767,37 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   for (int i = 1; i < nn; i++) {
     int ci = dof_col(m, i);
     double t = tau_act ? tau_act[i - 1] : 0.0;
-    rhs[ci] += t - m->damping[i] * s->qd[i] - m->stiffness[i] * (s->qj[i] + h * s->qd[i]);
+    rhs[ci] += t + tadd[i] + s->ttend[i] - bb[i] * s->qd[i] - kk[i] * (s->qj[i] - ref[i] + h * s->qd[i]);
   }
-  chol_solve(M, nv, rhs);
-  for (int c = 0; c < nv; c++) nu[c] += h * rhs[c];
+  if (m->obj_type) {
+    /* object block: diag(I_world, m 1); bias = [w x I w; -m g] */
+    double Iw[3][3], Rt[3][3], T[3][3], Il[3][3] = {{m->obj_inertia[0], 0, 0}, {0, m->obj_inertia[1], 0},
+                                                      {0, 0, m->obj_inertia[2]}};
+    matmul3(k.oR, Il, T);
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) Rt[a][b] = k.oR[b][a];
+    matmul3(T, Rt, Iw);
+    for (int a = 0; a < 3; a++) {
+      for (int b = 0; b < 3; b++) M[(nv + a) * nvt + nv + b] = Iw[a][b];
+      M[(nv + 3 + a) * nvt + nv + 3 + a] = m->obj_mass;
+    }
+    double Iwv[3], gyro[3];
+    matvec3(Iw, s->ow, Iwv);
+    cross3(s->ow, Iwv, gyro);
+    for (int a = 0; a < 3; a++) {
+      nu[nv + a] = s->ow[a];
+      nu[nv + 3 + a] = s->ov[a];
+      rhs[nv + a] = -gyro[a];
+      rhs[nv + 3 + a] = m->obj_mass * m->obj_gravity * p->gravity[a];
+    }
+  }
+  if (cholesky(M, nvt) != 0) return;
+  chol_solve(M, nvt, rhs);
+  for (int c = 0; c < nvt; c++) nu[c] += h * rhs[c];
+  if (m->obj_type) { /* velocity damping of the free body (gym AssetOptions angular/linear_damping) */
+    double fa = 1.0 / (1.0 + h * m->obj_ang_damping), fl = 1.0 / (1.0 + h * m->obj_lin_damping);
+    for (int a = 0; a < 3; a++) { nu[nv + a] *= fa; nu[nv + 3 + a] *= fl; }
+  }
 
   /* constraint rows */
   int cap = p->max_contacts < MAXC ? p->max_contacts : MAXC;
@@ -552,7 +826,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     for (int side = 0; side < 2; side++) {
       double d = side == 0 ? dl : du;
       if (d >= p->limit_margin) continue;
-      memset(J[nr], 0, sizeof(double) * nv);
+      memset(J[nr], 0, sizeof(double) * nvt);
       J[nr][dof_col(m, i)] = side == 0 ? 1.0 : -1.0;
       b[nr] = d >= 0 ? -d / h : fmin(-p->baumgarte * d / h, p->max_depen_vel);
       so->row_kind[nr] = 2 + side;
@@ -562,10 +836,10 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   }
   so->nrows = nr;
   for (int r = 0; r < nr; r++) {
-    for (int c = 0; c < nv; c++) Y[r][c] = J[r][c];
-    chol_solve(M, nv, Y[r]);
+    for (int c = 0; c < nvt; c++) Y[r][c] = J[r][c];
+    chol_solve(M, nvt, Y[r]);
     double w = 0;
-    for (int c = 0; c < nv; c++) w += J[r][c] * Y[r][c];
+    for (int c = 0; c < nvt; c++) w += J[r][c] * Y[r][c];
     W[r] = w;
     so->lam[r] = 0;
   }
@@ -573,7 +847,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     for (int r = 0; r < nr; r++) {
       if (W[r] <= 1e-12) continue;
       double v = 0;
-      for (int c = 0; c < nv; c++) v += J[r][c] * nu[c];
+      for (int c = 0; c < nvt; c++) v += J[r][c] * nu[c];
       double lnew = so->lam[r] + (b[r] - v) / W[r];
       if (so->row_kind[r] == 1) {
         double lim = p->friction * so->lam[3 * so->row_ref[r]];  /* normal row of this contact */
@@ -583,7 +857,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       }
       double dl = lnew - so->lam[r];
       so->lam[r] = lnew;
-      for (int c = 0; c < nv; c++) nu[c] += Y[r][c] * dl;
+      for (int c = 0; c < nvt; c++) nu[c] += Y[r][c] * dl;
     }
   }
   /* integrate */
@@ -610,6 +884,24 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     s->qd[i] = nu[dof_col(m, i)];
     s->qj[i] += h * s->qd[i];
   }
+  if (m->obj_type) {
+    double w[3] = {nu[nv], nu[nv + 1], nu[nv + 2]}, dq[4], qn[4];
+    double wn = sqrt(dot3(w, w));
+    if (wn * h > 1e-12) {
+      double ha = 0.5 * wn * h, sn = sin(ha) / wn;
+      dq[0] = w[0] * sn; dq[1] = w[1] * sn; dq[2] = w[2] * sn; dq[3] = cos(ha);
+    } else {
+      dq[0] = 0.5 * h * w[0]; dq[1] = 0.5 * h * w[1]; dq[2] = 0.5 * h * w[2]; dq[3] = 1.0;
+    }
+    quat_mul_d(dq, s->oq, qn);
+    double l = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+    for (int a = 0; a < 4; a++) s->oq[a] = qn[a] / l;
+    for (int a = 0; a < 3; a++) {
+      s->ow[a] = w[a];
+      s->ov[a] = nu[nv + 3 + a];
+      s->op[a] += h * s->ov[a];
+    }
+  }
 }
 
 /* sensor wrench and dof force from the last substep's impulses */
@@ -631,7 +923,7 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
       for (int c = 0; c < so->ncon; c++) {
         const contact* ct = &so->con[c];
         double sg = 0;
-        if (m->geom_body[ct->geomA] == body) sg = 1;
+        if (ct->geomA >= 0 && m->geom_body[ct->geomA] == body) sg = 1;
         else if (ct->geomB >= 0 && m->geom_body[ct->geomB] == body) sg = -1;
         if (sg == 0) continue;
         double t1[3], t2[3];
@@ -650,8 +942,18 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
     }
   }
   if (dof_force) {
+    /* drive / passive force at the post-step state (saturated drives report +-effort), tendon force
+     * of the last substep, plus the joint-limit impulses / h */
     for (int i = 1; i < m->num_nodes; i++) {
-      double t = (tau_act ? tau_act[i - 1] : 0.0) - m->damping[i] * s->qd[i] - m->stiffness[i] * s->qj[i];
+      double t = (tau_act ? tau_act[i - 1] : 0.0) + s->ttend[i];
+      if (m->drive_kp[i] > 0.0) {
+        double tgt = s->tgt ? s->tgt[i - 1] : 0.0;
+        t += s->sat[i] ? (m->drive_kp[i] * (tgt - s->qj[i]) - m->damping[i] * s->qd[i] > 0 ? m->effort_limit[i]
+                                                                                                 : -m->effort_limit[i])
+                       : m->drive_kp[i] * (tgt - s->qj[i]) - m->damping[i] * s->qd[i];
+      } else {
+        t += -m->damping[i] * s->qd[i] - m->stiffness[i] * s->qj[i];
+      }
       for (int r = 0; r < so->nrows; r++) {
         if (so->row_ref[r] != i) continue;
         if (so->row_kind[r] == 2) t += so->lam[r] / so->h;
@@ -662,89 +964,26 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
   }
 }
 
-static void simulate_actor(const mg_model* m, const mg_sim_params* p, float* root, float* dof, const float* act,
-                           float* sensors, float* dof_force) {
-  astate s;
-  load_state(m, root, dof, &s);
-  double tau[MAXN];
-  for (int i = 0; i < m->num_dofs; i++) tau[i] = act ? act[i] : 0.0;
-  substep_out* so = (substep_out*)malloc(sizeof(substep_out));
-  memset(so, 0, sizeof(*so));
-  for (int st = 0; st < p->substeps; st++) substep(m, p, &s, tau, so);
-  store_state(m, &s, root, dof);
-  sensor_outputs(m, &s, so, tau, sensors, dof_force);
-  free(so);
+static void load_object(astate* s, const float* row) {
+  double nq = 0;
+  for (int a = 0; a < 3; a++) { s->op[a] = row[a]; s->ov[a] = row[7 + a]; s->ow[a] = row[10 + a]; }
+  for (int a = 0; a < 4; a++) { s->oq[a] = row[3 + a]; nq += s->oq[a] * s->oq[a]; }
+  nq = sqrt(nq);
+  for (int a = 0; a < 4; a++) s->oq[a] /= nq;
 }
-
-int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* root_states, float* dof_state,
-                 const float* dof_actuation, float* sensors, float* dof_force, int32_t threads) {
-  int nd = m->num_dofs, ns = m->num_sensors;
-#ifdef _OPENMP
-  if (threads > 0) omp_set_num_threads(threads);
-#pragma omp parallel for schedule(dynamic, 16)
-#endif
-  for (int e = 0; e < n; e++) {
-    simulate_actor(m, p, root_states + 13 * e, dof_state + 2 * nd * e, dof_actuation ? dof_actuation + nd * e : 0,
-                   sensors ? sensors + 6 * ns * e : 0, dof_force ? dof_force + nd * e : 0);
+static void store_object(const astate* s, float* row) {
+  for (int a = 0; a < 3; a++) {
+    row[a] = (float)s->op[a];
+    row[7 + a] = (float)s->ov[a];
+    row[10 + a] = (float)s->ow[a];
   }
-  (void)threads;
-  return 0;
+  for (int a = 0; a < 4; a++) row[3 + a] = (float)s->oq[a];
 }
 
-int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
-                    double* M_out) {
-  astate s;
+/* gym rigid-body states of the articulation (body origin pose, COM linear velocity, angular velocity) */
+static void body_states(const mg_model* m, const astate* s, float* out) {
   kin k;
-  load_state(m, root13, dof2, &s);
-  forward_kinematics(m, &s, &k);
-  mass_matrix(m, &k, p->dt / p->substeps, M_out);
-  return nv_of(m);
-}
-
-int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
-                          const float* tau, double* qacc_out) {
-  astate s;
-  kin k;
-  load_state(m, root13, dof2, &s);
-  forward_kinematics(m, &s, &k);
-  int nv = nv_of(m);
-  double h = p->dt / p->substeps, M[MAXV * MAXV], C[MAXV], g[3] = {p->gravity[0], p->gravity[1], p->gravity[2]};
-  mass_matrix(m, &k, h, M);
-  bias_forces(m, &k, &s, g, C);
-  if (cholesky(M, nv) != 0) return -1;
-  for (int c = 0; c < nv; c++) qacc_out[c] = -C[c];
-  for (int i = 1; i < m->num_nodes; i++)
-    qacc_out[dof_col(m, i)] += (tau ? tau[i - 1] : 0.0) - m->damping[i] * s.qd[i] -
-                               m->stiffness[i] * (s.qj[i] + h * s.qd[i]);
-  chol_solve(M, nv, qacc_out);
-  return nv;
-}
-
-int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, double* out,
-                 int32_t cap) {
-  astate s;
-  kin k;
-  load_state(m, root13, dof2, &s);
-  forward_kinematics(m, &s, &k);
-  contact con[MAXC];
-  int c = cap < MAXC ? cap : MAXC;
-  int nc = collide(m, p, &k, con, c);
-  for (int i = 0; i < nc; i++) {
-    double* o = out + 9 * i;
-    o[0] = con[i].nodeA;
-    o[1] = con[i].p[0]; o[2] = con[i].p[1]; o[3] = con[i].p[2];
-    o[4] = con[i].n[0]; o[5] = con[i].n[1]; o[6] = con[i].n[2];
-    o[7] = con[i].d;
-    o[8] = con[i].nodeB;
-  }
-  return nc;
-}
-
-int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out) {
-  astate s;
-  kin k;
-  load_state(m, root13, dof2, &s);
-  forward_kinematics(m, &s, &k);
+  forward_kinematics(m, s, &k);
   for (int b = 0; b < m->num_bodies; b++) {
     int nd = m->body_node[b];
     double bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]}, Rl[3][3],
@@ -767,5 +1006,121 @@ int orc_rigid_body_states(const mg_model* m, const float* root13, const float* d
     }
     for (int a = 0; a < 4; a++) o[3 + a] = (float)q[a];
   }
+}
+
+/* one env: root rows [articulation, (object, goal)], dof rows, PD targets, sensors, dof forces,
+ * rigid-body rows [articulation bodies, (object, goal)] */
+static void simulate_env(const mg_model* m, const mg_sim_params* p, float* root, float* dof, const float* act,
+                         const float* tgt, float* sensors, float* dof_force, float* rbs) {
+  astate s;
+  memset(&s, 0, sizeof(s));
+  load_state(m, root, dof, &s);
+  s.tgt = tgt;
+  if (m->obj_type) load_object(&s, root + 13);
+  double tau[MAXN];
+  for (int i = 0; i < m->num_dofs; i++) tau[i] = act ? act[i] : 0.0;
+  substep_out* so = (substep_out*)malloc(sizeof(substep_out));
+  memset(so, 0, sizeof(*so));
+  for (int st = 0; st < p->substeps; st++) substep(m, p, &s, tau, so);
+  store_state(m, &s, root, dof);
+  if (m->obj_type) store_object(&s, root + 13);
+  sensor_outputs(m, &s, so, tau, sensors, dof_force);
+  if (rbs) {
+    body_states(m, &s, rbs);
+    if (m->obj_type) {
+      memcpy(rbs + 13 * m->num_bodies, root + 13, 13 * sizeof(float));
+      memcpy(rbs + 13 * (m->num_bodies + 1), root + 26, 13 * sizeof(float));
+    }
+  }
+  free(so);
+}
+
+int orc_simulate_views(const mg_model* m, const mg_sim_params* p, int32_t n, const mg_state_views* v,
+                       int32_t threads) {
+  int nd = m->num_dofs, ns = m->num_sensors;
+  int rows = m->obj_type ? 3 : 1, nb = m->num_bodies + (m->obj_type ? 2 : 0);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+  for (int e = 0; e < n; e++) {
+    simulate_env(m, p, v->root_states + (size_t)13 * rows * e, v->dof_state + (size_t)2 * nd * e,
+                 v->dof_actuation ? v->dof_actuation + (size_t)nd * e : 0,
+                 v->dof_targets ? v->dof_targets + (size_t)nd * e : 0, v->sensors ? v->sensors + (size_t)6 * ns * e : 0,
+                 v->dof_force ? v->dof_force + (size_t)nd * e : 0,
+                 v->rigid_body_states ? v->rigid_body_states + (size_t)13 * nb * e : 0);
+  }
+  (void)threads;
+  return 0;
+}
+
+int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* root_states, float* dof_state,
+                 const float* dof_actuation, float* sensors, float* dof_force, int32_t threads) {
+  mg_state_views v;
+  memset(&v, 0, sizeof(v));
+  v.root_states = root_states;
+  v.dof_state = dof_state;
+  v.dof_actuation = dof_actuation;
+  v.sensors = sensors;
+  v.dof_force = dof_force;
+  return orc_simulate_views(m, p, n, &v, threads);
+}
+
+int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
+                    double* M_out) {
+  astate s;
+  kin k;
+  load_state(m, root13, dof2, &s);
+  forward_kinematics(m, &s, &k);
+  mass_matrix(m, &k, p->dt / p->substeps, M_out, 0, nv_of(m));
+  return nv_of(m);
+}
+
+int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
+                          const float* tau, double* qacc_out) {
+  astate s;
+  kin k;
+  load_state(m, root13, dof2, &s);
+  forward_kinematics(m, &s, &k);
+  int nv = nv_of(m);
+  double h = p->dt / p->substeps, M[MAXV * MAXV], C[MAXV], g[3] = {p->gravity[0], p->gravity[1], p->gravity[2]};
+  mass_matrix(m, &k, h, M, 0, nv);
+  bias_forces(m, &k, &s, g, C);
+  if (cholesky(M, nv) != 0) return -1;
+  for (int c = 0; c < nv; c++) qacc_out[c] = -C[c];
+  for (int i = 1; i < m->num_nodes; i++)
+    qacc_out[dof_col(m, i)] += (tau ? tau[i - 1] : 0.0) - m->damping[i] * s.qd[i] -
+                               m->stiffness[i] * (s.qj[i] + h * s.qd[i]);
+  chol_solve(M, nv, qacc_out);
+  return nv;
+}
+
+int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, double* out,
+                 int32_t cap) {
+  astate s;
+  kin k;
+  memset(&s, 0, sizeof(s));
+  load_state(m, root13, dof2, &s);
+  if (m->obj_type) load_object(&s, root13 + 13); /* env root rows [articulation, object, goal] */
+  forward_kinematics(m, &s, &k);
+  contact con[MAXC];
+  int c = cap < MAXC ? cap : MAXC;
+  int nc = collide(m, p, &k, con, c);
+  for (int i = 0; i < nc; i++) {
+    double* o = out + 9 * i;
+    o[0] = con[i].nodeA;
+    o[1] = con[i].p[0]; o[2] = con[i].p[1]; o[3] = con[i].p[2];
+    o[4] = con[i].n[0]; o[5] = con[i].n[1]; o[6] = con[i].n[2];
+    o[7] = con[i].d;
+    o[8] = con[i].nodeB;
+  }
+  return nc;
+}
+
+int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out) {
+  astate s;
+  memset(&s, 0, sizeof(s));
+  load_state(m, root13, dof2, &s);
+  body_states(m, &s, out);
   return m->num_bodies;
 }

@@ -9,15 +9,66 @@ them from migym/assets/*.json.
   Humanoid  assets/mjcf/nv_humanoid.xml   (tasks/humanoid.py:142-196; foot sensors :163-168;
                                            self-collision filter 0 :194)
   Cartpole  assets/urdf/cartpole.urdf     (tasks/cartpole.py:78-113; fix_base_link :88)
+  ShadowHand assets/mjcf/open_ai_assets/hand/shadow_hand.xml + assets/urdf/objects/cube_multicolor.urdf
+            (tasks/shadow_hand.py:220-396: fix_base_link, collapse_fixed_joints, disable_gravity,
+             tendon limit_stiffness 30 / damping 0.1 on the four T_*J1c tendons, fingertip force
+             sensors; the object keeps gym's default AssetOptions: angular_damping 0.5, gravity on).
+            The forearm's convex collision mesh is replaced by its bounding box.
 """
 import os
+import struct
 import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "isaacgymenvs-ma_amd"))
 from migym import model as M  # noqa: E402
 
 REF = os.environ.get("MIGYM_REFERENCE", "/root/reference")
+
+
+def stl_bounds(path, scale=(1.0, 1.0, 1.0)):
+    """axis-aligned bounds of an STL mesh (binary or ASCII), mesh frame, scaled."""
+    data = open(path, "rb").read()
+    n = struct.unpack("<I", data[80:84])[0] if len(data) >= 84 else 0
+    if len(data) == 84 + 50 * n:
+        rec = np.frombuffer(data[84:], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
+        v = rec["v"].reshape(-1, 3).astype(np.float64)
+    else:
+        v = np.array([[float(x) for x in ln.split()[1:4]] for ln in data.decode().splitlines()
+                      if ln.strip().startswith("vertex")])
+    v = v * np.asarray(scale)
+    return v.min(0), v.max(0)
+
+
+HAND_FINGERTIPS = ["robot0:ffdistal", "robot0:mfdistal", "robot0:rfdistal", "robot0:lfdistal", "robot0:thdistal"]
+HAND_TENDONS = ["robot0:T_FFJ1c", "robot0:T_MFJ1c", "robot0:T_RFJ1c", "robot0:T_LFJ1c"]
+
+
+def shadow_hand():
+    hand_dir = os.path.join(REF, "assets/mjcf/open_ai_assets/hand")
+    mesh_dir = os.path.join(hand_dir, "../stls/hand")
+    boxes = {}
+    for m in ET.parse(os.path.join(hand_dir, "shared_asset.xml")).getroot().iter("mesh"):
+        if "cvx" not in m.get("file", ""):
+            continue
+        sc = [float(x) for x in m.get("scale", "1 1 1").split()]
+        lo, hi = stl_bounds(os.path.join(mesh_dir, m.get("file")), sc)
+        boxes[m.get("name")] = ((lo + hi) / 2, (hi - lo) / 2)
+    hand = M.load_mjcf(os.path.join(hand_dir, "shadow_hand.xml"), "shadow_hand", collapse_fixed=True,
+                       mesh_boxes=boxes)
+    hand.sensors = [hand.body_index(n) for n in HAND_FINGERTIPS]
+    hand.gravity_off = 1
+    for t in hand.tendons:
+        if t["name"] in HAND_TENDONS:
+            t["limit_stiffness"], t["damping"] = 30.0, 0.1
+    cube = M.load_urdf(os.path.join(REF, "assets/urdf/objects/cube_multicolor.urdf"), "cube", fix_base=False)
+    g = cube.geoms[0]
+    hand.obj = dict(type=M.GT_BOX, size=list(g.size), mass=cube.nodes[0].mass, inertia=cube.nodes[0].inertia[:3],
+                    lin_damping=0.0, ang_damping=0.5, gravity=1)
+    return hand
 
 
 def main():
@@ -30,7 +81,9 @@ def main():
     hum.to_json(os.path.join(out, "humanoid.json"))
     cp = M.load_urdf(os.path.join(REF, "assets/urdf/cartpole.urdf"), "cartpole", fix_base=True)
     cp.to_json(os.path.join(out, "cartpole.json"))
-    for s in (ant, hum, cp):
+    sh = shadow_hand()
+    sh.to_json(os.path.join(out, "shadow_hand.json"))
+    for s in (ant, hum, cp, sh):
         print(f"{s.name}: nodes={len(s.nodes)} dofs={s.num_dofs} bodies={len(s.bodies)} geoms={len(s.geoms)} "
               f"pairs={len(s.pairs)} mass={s.total_mass():.4f} sensors={s.sensors}")
 
