@@ -8,7 +8,7 @@ overrides written for the reference work unchanged) and interpolations are
 resolved eagerly by :func:`task_config`.
 
 Sources of the values: cfg/config.yaml:18-32 (devices, physx threads,
-solver), cfg/task/Ant.yaml, Humanoid.yaml, Cartpole.yaml.
+solver), cfg/task/Ant.yaml, Humanoid.yaml, Cartpole.yaml, ShadowHand.yaml.
 """
 from __future__ import annotations
 
@@ -84,6 +84,29 @@ TASKS = {
                     max_gpu_contact_pairs=1024 * 1024),
         "task": {"randomize": False},
     },
+}
+
+TASKS["ShadowHand"] = {
+    "name": "ShadowHand",
+    "env": {
+        "numEnvs": 16384, "envSpacing": 0.75, "episodeLength": 600, "enableDebugVis": False, "aggregateMode": 1,
+        "clipObservations": 5.0, "clipActions": 1.0, "stiffnessScale": 1.0, "forceLimitScale": 1.0,
+        "useRelativeControl": False, "dofSpeedScale": 20.0, "actionsMovingAverage": 1.0,
+        "controlFrequencyInv": 1, "startPositionNoise": 0.01, "startRotationNoise": 0.0,
+        "resetPositionNoise": 0.01, "resetRotationNoise": 0.0, "resetDofPosRandomInterval": 0.2,
+        "resetDofVelRandomInterval": 0.0, "forceScale": 0.0, "forceProbRange": [0.001, 0.1],
+        "forceDecay": 0.99, "forceDecayInterval": 0.08, "distRewardScale": -10.0, "rotRewardScale": 1.0,
+        "rotEps": 0.1, "actionPenaltyScale": -0.0002, "reachGoalBonus": 250, "fallDistance": 0.24,
+        "fallPenalty": 0.0, "objectType": "block", "observationType": "full_state",
+        "asymmetric_observations": False, "successTolerance": 0.1, "printNumSuccesses": False,
+        "maxConsecutiveSuccesses": 0,
+        "asset": {"assetFileName": "mjcf/open_ai_assets/hand/shadow_hand.xml",
+                  "assetFileNameBlock": "urdf/objects/cube_multicolor.urdf"},
+        "enableCameraSensors": False,
+    },
+    "sim": _sim(dt=0.01667, num_position_iterations=8, contact_offset=0.002, rest_offset=0.0,
+                bounce_threshold_velocity=0.2, max_depenetration_velocity=1000.0),
+    "task": {"randomize": False},
 }
 
 # Multi-agent Ant (build-defined, SURVEY.md §8(a) row A-MA): A ant actors per env.

@@ -2,7 +2,8 @@
 
 What the reference task constructors compute once at setup
 (tasks/ant.py:43-114 + 135-212, tasks/humanoid.py:43-117 + 138-217,
-tasks/cartpole.py:36-113) and then pass to their jit functions every step.
+tasks/cartpole.py:36-113, tasks/shadow_hand.py:40-400) and then pass to their jit
+functions every step.
 """
 from __future__ import annotations
 
@@ -16,7 +17,9 @@ TASK_INFO = {
     "Cartpole": (_abi.MG_TASK_CARTPOLE, "cartpole", 4, 1, 2.0, 4),
     "Ant": (_abi.MG_TASK_ANT, "ant", 60, 8, 0.44, 16),
     "Humanoid": (_abi.MG_TASK_HUMANOID, "humanoid", 108, 21, 1.34, 32),
+    "ShadowHand": (_abi.MG_TASK_SHADOW_HAND, "shadow_hand", 211, 20, 0.5, 24),
 }
+HAND_OBS = {"full_state": (0, 211)}    # shadow_hand.py:108-113 (the other obs types: DESIGN.md, out of scope)
 TASK_INFO["MAAnt"] = TASK_INFO["Ant"]   # per-agent physics/obs of the multi-agent Ant are the Ant's
 
 # build-defined solver constants
@@ -68,7 +71,67 @@ def agent_offsets(A: int, spacing: float):
     return out
 
 
+def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
+    """ShadowHand constants (shadow_hand.py:46-118, 220-330)."""
+    env = cfg["env"]
+    obs_type = env.get("observationType", "full_state")
+    if obs_type not in HAND_OBS:
+        raise ValueError(f"observationType {obs_type!r} not supported (full_state only)")
+    if env.get("objectType", "block") != "block":
+        raise ValueError("objectType must be 'block' (egg/pen meshes are out of scope)")
+    if env.get("asymmetric_observations", False):
+        raise ValueError("asymmetric_observations is not supported")
+    tp = _abi.TaskParams()
+    tp.task_id = _abi.MG_TASK_SHADOW_HAND
+    tp.num_agents = 1
+    tp.obs_type, tp.num_obs = HAND_OBS[obs_type]
+    tp.num_actions = len(spec.actuators)
+    tp.dt = float(cfg["sim"]["dt"])
+    tp.clip_actions = float(env.get("clipActions", math.inf))
+    tp.clip_obs = float(env.get("clipObservations", math.inf))
+    tp.max_episode_length = int(env["episodeLength"])
+    if env.get("resetTime", -1.0) > 0.0:   # shadow_hand.py:127-131
+        tp.max_episode_length = int(round(env["resetTime"] / (env.get("controlFrequencyInv", 1) * tp.dt)))
+    nd = spec.num_dofs
+    for j, n in enumerate(spec.nodes[1:]):
+        tp.dof_lower[j], tp.dof_upper[j], tp.initial_dof_pos[j] = n.lower, n.upper, 0.0
+    for i, a in enumerate(spec.actuators):
+        tp.actuated_dof[i] = spec.dof_index(a["joint"])
+    tp.num_fingertips = len(spec.sensors)
+    for i, b in enumerate(spec.sensors):
+        tp.fingertip_body[i] = b
+    tp.max_consecutive_successes = int(env.get("maxConsecutiveSuccesses", 0))
+    tp.use_relative_control = int(bool(env.get("useRelativeControl", False)))
+    tp.ignore_z_rot = 0
+    tp.dof_speed_scale = float(env["dofSpeedScale"])
+    tp.act_moving_average = float(env["actionsMovingAverage"])
+    tp.dist_reward_scale = float(env["distRewardScale"])
+    tp.rot_reward_scale = float(env["rotRewardScale"])
+    tp.rot_eps = float(env["rotEps"])
+    tp.action_penalty_scale = float(env["actionPenaltyScale"])
+    tp.success_tolerance = float(env["successTolerance"])
+    tp.reach_goal_bonus = float(env["reachGoalBonus"])
+    tp.fall_dist = float(env["fallDistance"])
+    tp.fall_penalty = float(env["fallPenalty"])
+    tp.av_factor = float(env.get("averFactor", 0.1))
+    tp.vel_obs_scale = 0.2
+    tp.force_torque_obs_scale = 10.0
+    tp.reset_position_noise = float(env["resetPositionNoise"])
+    tp.reset_dof_pos_noise = float(env["resetDofPosRandomInterval"])
+    tp.reset_dof_vel_noise = float(env["resetDofVelRandomInterval"])
+    # hand at (0, 0, 0.5); object at hand + (0, -0.39, 0.10); goal = object - 0.04 z, drawn displaced
+    tp.start_pos[:] = (0.0, 0.0, 0.5)
+    tp.start_rot[:] = (0.0, 0.0, 0.0, 1.0)
+    tp.object_start[:] = (0.0, 0.0 + -0.39, 0.5 + 0.10)
+    tp.goal_displacement[:] = (-0.2, -0.06, 0.12)
+    tp.goal_dz = -0.04
+    del nd
+    return tp
+
+
 def task_params(task: str, cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
+    if task == "ShadowHand":
+        return hand_task_params(cfg, spec)
     base = "Ant" if task == "MAAnt" else task
     task_id, _, nobs, nact, z0, _ = TASK_INFO[base]
     env = cfg["env"]

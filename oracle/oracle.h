@@ -66,6 +66,19 @@ int orc_post_physics(const mg_task_params* tp, const mg_state_views* v, const mg
 int orc_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp, const mg_state_views* v,
                  const mg_task_buffers* tb, int32_t n, int32_t threads);
 
+/* in-hand manipulation task layer (oracle_hand.c): ShadowHand full_state */
+void orc_randomize_rotation(float r0, float r1, float* q);
+int orc_hand_reward(const mg_task_params* tp, int32_t n, float max_episode_length, const float* object_pos,
+                    const float* object_rot, const float* target_pos, const float* target_rot, const float* actions,
+                    int64_t* reset, int64_t* reset_goal, int64_t* progress, float* successes, float* cons,
+                    float* rew);
+int orc_hand_pre_physics(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
+                         const mg_task_buffers* tb, int32_t n);
+int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
+                          const mg_task_buffers* tb, int32_t n);
+int orc_hand_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp,
+                      const mg_state_views* v, const mg_task_buffers* tb, int32_t n, int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,6 +44,17 @@ def lib():
                                        C.POINTER(_abi.TaskBuffers), C.c_int32]
         l.orc_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
                                    C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32, C.c_int32]
+        l.orc_simulate_views.argtypes = [P, C.POINTER(_abi.SimParams), C.c_int32, C.POINTER(_abi.StateViews),
+                                         C.c_int32]
+        l.orc_randomize_rotation.restype = None
+        l.orc_randomize_rotation.argtypes = [C.c_float, C.c_float, P]
+        l.orc_hand_reward.argtypes = [C.POINTER(_abi.TaskParams), C.c_int32, C.c_float] + [P] * 11
+        for f in ("orc_hand_pre_physics", "orc_hand_post_physics"):
+            getattr(l, f).argtypes = [P, C.POINTER(_abi.TaskParams), C.POINTER(_abi.StateViews),
+                                      C.POINTER(_abi.TaskBuffers), C.c_int32]
+        l.orc_hand_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
+                                        C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32,
+                                        C.c_int32]
         _lib = l
     return _lib
 
@@ -100,6 +111,25 @@ def compute_observations(tp, root, dof, dof_force, sensors, actions, potentials,
 def compute_reward(tp, obs, actions, potentials, prev_potentials, progress, reset, rew):
     lib().orc_compute_reward(C.byref(tp), obs.shape[0], p(obs), p(actions), p(potentials), p(prev_potentials),
                              p(progress), p(reset), p(rew))
+
+
+def randomize_rotation(r0, r1):
+    out = np.zeros((len(r0), 4), np.float32)
+    for i, (a, b) in enumerate(zip(r0, r1)):
+        lib().orc_randomize_rotation(float(a), float(b), out[i].ctypes.data)
+    return out
+
+
+def hand_reward(tp, max_episode_length, object_pos, object_rot, target_pos, target_rot, actions, reset, reset_goal,
+                progress, successes, cons):
+    """compute_hand_reward (shadow_hand.py:746-800); buffers updated in place, returns (rew, cons)."""
+    n = object_pos.shape[0]
+    rew = np.zeros(n, np.float32)
+    c = np.array([cons], np.float32)
+    lib().orc_hand_reward(C.byref(tp), n, max_episode_length, p(f32(object_pos)), p(f32(object_rot)),
+                          p(f32(target_pos)), p(f32(target_rot)), p(f32(actions)), p(reset), p(reset_goal),
+                          p(progress), p(successes), p(c), p(rew))
+    return rew, float(c[0])
 
 
 def uniform(seed, env, counter, k):
@@ -164,3 +194,78 @@ class HostEnv:
     def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0):
         v, b = self.views(), self.buffers(seed, step, env_offset)
         lib().orc_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v), C.byref(b), self.n, threads)
+
+
+class HandHostEnv:
+    """Host buffers of one ShadowHand shard (layouts the GPU path binds: root rows
+    [hand, object, goal] per env, rigid bodies [hand bodies, object, goal])."""
+
+    def __init__(self, tp, spec, n):
+        nd, na, no = spec.num_dofs, tp.num_actions, tp.num_obs
+        nb = len(spec.bodies) + 2
+        self.n, self.nd = n, nd
+        self.root = np.zeros((n, 3, 13), np.float32)
+        self.root[:, 0, 0:3] = np.array(tp.start_pos[:3], np.float32)
+        self.root[:, 0, 3:7] = np.array(tp.start_rot[:4], np.float32)
+        obj = np.array(tp.object_start[:3], np.float32)
+        self.root[:, 1, 0:3] = obj
+        self.root[:, 1, 6] = 1.0
+        self.goal_states = np.zeros((n, 13), np.float32)
+        self.goal_states[:, 0:3] = obj
+        self.goal_states[:, 2] += np.float32(tp.goal_dz)
+        self.goal_states[:, 6] = 1.0
+        self.root[:, 2, 0:3] = self.goal_states[:, 0:3] + np.array(tp.goal_displacement[:3], np.float32)
+        self.root[:, 2, 6] = 1.0
+        self.dof = np.zeros((n, nd, 2), np.float32)
+        self.targets = np.zeros((n, nd), np.float32)
+        self.prev_targets = np.zeros((n, nd), np.float32)
+        self.sensors = np.zeros((n, len(spec.sensors) * 6), np.float32)
+        self.dof_force = np.zeros((n, nd), np.float32)
+        self.rbs = np.zeros((n, nb, 13), np.float32)
+        self.actions = np.zeros((n, na), np.float32)
+        self.actions_out = np.zeros((n, na), np.float32)
+        self.obs = np.zeros((n, no), np.float32)
+        self.obs_clamped = np.zeros((n, no), np.float32)
+        self.rew = np.zeros(n, np.float32)
+        self.reset = np.ones(n, np.int64)
+        self.reset_goal = np.ones(n, np.int64)
+        self.progress = np.zeros(n, np.int64)
+        self.timeout = np.zeros(n, np.uint8)
+        self.successes = np.zeros(n, np.float32)
+        self.cons = np.zeros(1, np.float32)
+        self.noise = None
+
+    def views(self):
+        v = _abi.StateViews()
+        v.root_states, v.dof_state, v.dof_actuation = p(self.root), p(self.dof), None
+        v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), p(self.rbs)
+        v.dof_targets = p(self.targets)
+        return v
+
+    def buffers(self, seed=0, step=0, env_offset=0):
+        b = _abi.TaskBuffers()
+        b.actions, b.actions_out, b.obs, b.obs_clamped = p(self.actions), p(self.actions_out), p(self.obs), \
+            p(self.obs_clamped)
+        b.rew, b.reset, b.progress, b.timeout = p(self.rew), p(self.reset), p(self.progress), p(self.timeout)
+        b.noise = p(self.noise)
+        b.seed, b.step_counter, b.env_offset = seed, step, env_offset
+        b.prev_targets, b.goal_states, b.reset_goal = p(self.prev_targets), p(self.goal_states), p(self.reset_goal)
+        b.successes, b.consecutive_successes = p(self.successes), p(self.cons)
+        return b
+
+    def pre_physics(self, model_np, tp, seed=0, step=0, env_offset=0):
+        v, b = self.views(), self.buffers(seed, step, env_offset)
+        lib().orc_hand_pre_physics(model_np.ctypes.data, C.byref(tp), C.byref(v), C.byref(b), self.n)
+
+    def post_physics(self, model_np, tp, seed=0, step=0, env_offset=0):
+        v, b = self.views(), self.buffers(seed, step, env_offset)
+        lib().orc_hand_post_physics(model_np.ctypes.data, C.byref(tp), C.byref(v), C.byref(b), self.n)
+
+    def simulate(self, model_np, sp, threads=0):
+        v = self.views()
+        lib().orc_simulate_views(model_np.ctypes.data, C.byref(sp), self.n, C.byref(v), threads)
+
+    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0):
+        v, b = self.views(), self.buffers(seed, step, env_offset)
+        lib().orc_hand_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v), C.byref(b), self.n,
+                                threads)

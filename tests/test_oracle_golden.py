@@ -138,3 +138,60 @@ def test_cartpole_trace_matches_reference():
         a = np.clip(d["actions"][t][:, 0], -1, 1) * 400.0
         np.testing.assert_allclose(d["actuation"][t][:, 0], a, rtol=1e-6)
         assert np.all(d["actuation"][t][:, 1] == 0)
+
+
+def test_shadowhand_reward_and_rotation_match_reference():
+    """compute_hand_reward incl. the global running mean, randomize_rotation (shadow_hand.py:746-806)."""
+    d = load("jit_shadowhand.npz")
+    tp, _ = tparams("ShadowHand")
+    np.testing.assert_allclose(O.randomize_rotation(d["r0"], d["r1"]), d["rand_rot"], rtol=RTOL, atol=ATOL)
+    reset, rg = O.i64(d["reset_buf"]).copy(), O.i64(d["reset_goal_buf"]).copy()
+    prog, succ = O.i64(d["progress"]).copy(), O.f32(d["successes"]).copy()
+    rew, cons = O.hand_reward(tp, 600.0, d["object_pos"], d["object_rot"], d["target_pos"], d["target_rot"],
+                              d["actions"], reset, rg, prog, succ, float(d["cons_in"]))
+    np.testing.assert_allclose(rew, d["rew"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_array_equal(reset, d["reset"])
+    np.testing.assert_array_equal(rg, d["goal_reset"])
+    np.testing.assert_array_equal(prog, d["progress_out"])
+    np.testing.assert_array_equal(succ, d["successes_out"])
+    np.testing.assert_allclose(cons, d["cons_out"], rtol=1e-6)
+
+
+def test_shadowhand_trace_matches_reference():
+    """Whole physics-free ShadowHand VecTask.step (pre_physics resets + PD targets, full_state obs,
+    reward, running mean, timeouts) replayed with the reference's own reset draws injected."""
+    d = load("trace_shadowhand.npz")
+    tp, spec = tparams("ShadowHand")
+    tp.max_episode_length = int(d["episode_length"])
+    mnp = M.pack_model(spec)
+    T, N = d["actions"].shape[:2]
+    h = O.HandHostEnv(tp, spec, N)
+    h.root[:] = d["init_root"]
+    h.goal_states[:] = d["init_goal_states"]
+    for t in range(T):
+        h.actions[:] = d["actions"][t]
+        h.noise = O.f32(d["noise"][t])
+        np.testing.assert_array_equal(h.reset, d["reset_in"][t])
+        np.testing.assert_array_equal(h.reset_goal, d["reset_goal_in"][t])
+        np.testing.assert_array_equal(h.progress, d["progress_in"][t])
+        h.pre_physics(mnp, tp)
+        np.testing.assert_allclose(h.root, d["root_pre"][t], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(h.dof, d["dof_pre"][t], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(h.targets, d["targets"][t], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(h.prev_targets, d["prev_targets"][t], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(h.goal_states, d["goal_states"][t], rtol=1e-6, atol=1e-7)
+        # "physics": the trace's injected post-simulate state
+        h.root[:] = d["phys_root"][t]
+        h.dof[:] = d["phys_dof"][t]
+        h.rbs[:] = d["phys_rbs"][t]
+        h.sensors[:] = d["phys_sensors"][t]
+        h.dof_force[:] = d["phys_dof_force"][t]
+        h.post_physics(mnp, tp)
+        np.testing.assert_allclose(h.obs_clamped, d["obs"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(h.rew, d["rew"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_array_equal(h.reset, d["reset"][t])
+        np.testing.assert_array_equal(h.reset_goal, d["reset_goal"][t])
+        np.testing.assert_array_equal(h.progress, d["progress"][t])
+        np.testing.assert_array_equal(h.successes, d["successes"][t])
+        np.testing.assert_allclose(h.cons, d["cons"][t], rtol=1e-6)
+        np.testing.assert_array_equal(h.timeout, d["timeouts"][t])
