@@ -1,0 +1,111 @@
+"""Known-answer tests of the oracle's hand-task physics (PD drives, tendons, free object).
+
+PARITY UNPINNED vs PhysX (closed): these pin the build's own documented
+semantics (hand tasks) with analytic answers, the way
+tests/test_oracle_physics.py pins the articulation core.
+"""
+import numpy as np
+
+import pyoracle as O
+from migym import configs, model as M, taskdefs
+
+G = 9.81
+
+
+def setup(n=2):
+    cfg = configs.task_config("ShadowHand", n)
+    spec = M.load_builtin("shadow_hand")
+    tp = taskdefs.task_params("ShadowHand", cfg, spec)
+    sp = taskdefs.sim_params(cfg, 24)
+    h = O.HandHostEnv(tp, spec, n)
+    return spec, tp, sp, M.pack_model(spec), h
+
+
+def park_object(h, pos=(5.0, 5.0, 3.0)):
+    h.root[:, 1, 0:3] = pos
+    h.root[:, 1, 3:7] = (0, 0, 0, 1)
+    h.root[:, 1, 7:] = 0
+
+
+def test_object_free_fall_and_spin():
+    spec, tp, sp, mnp, h = setup()
+    park_object(h)
+    h.root[:, 1, 10:13] = (1.0, 2.0, 3.0)
+    z0 = float(h.root[0, 1, 2])
+    h.simulate(mnp, sp)
+    hstep = sp.dt / sp.substeps
+    # semi-implicit Euler, 2 substeps: v = -g dt, z = z0 - 3 g h^2
+    np.testing.assert_allclose(h.root[0, 1, 9], -G * 2 * hstep, rtol=1e-6)
+    np.testing.assert_allclose(h.root[0, 1, 2], z0 - 3 * G * hstep ** 2, rtol=0, atol=2e-6)
+    # isotropic inertia: no gyroscopic torque; only the angular damping 1/(1 + h c) per substep
+    f = (1.0 / (1.0 + hstep * 0.5)) ** 2
+    np.testing.assert_allclose(h.root[0, 1, 10:13], np.array([1.0, 2.0, 3.0]) * f, rtol=1e-6)
+    assert np.linalg.norm(h.root[0, 1, 3:7]) == np.float32(1.0) or abs(np.linalg.norm(h.root[0, 1, 3:7]) - 1) < 1e-6
+
+
+def test_cube_settles_on_the_palm():
+    spec, tp, sp, mnp, h = setup()
+    h.root[:, 1, 0:3] = tp.object_start[:3]
+    h.root[:, 1, 3:7] = (0, 0, 0, 1)
+    for _ in range(60):
+        h.simulate(mnp, sp)
+    obj = h.root[0, 1]
+    assert np.abs(obj[7:13]).max() < 1e-3, obj
+    # resting on the palm / finger bases: palm top at z = 0.501, cube half size 0.025
+    assert 0.50 < obj[2] < 0.54, obj
+    assert len(O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)) >= 3
+    # the force sensors of fingertips that do not touch the cube read zero
+    assert np.all(np.isfinite(h.sensors))
+
+
+def test_drives_track_targets():
+    spec, tp, sp, mnp, h = setup()
+    park_object(h)
+    act = [tp.actuated_dof[i] for i in range(tp.num_actions)]
+    lo = np.array([tp.dof_lower[j] for j in range(24)])
+    hi = np.array([tp.dof_upper[j] for j in range(24)])
+    tgt = (0.3 * lo + 0.7 * hi).astype(np.float32)
+    h.targets[:] = tgt
+    for _ in range(300):
+        park_object(h)
+        h.simulate(mnp, sp)
+    err = np.abs(h.dof[0, act, 0] - tgt[act])
+    assert err.max() < 2e-2, err
+
+
+def test_saturated_drive_reports_effort_limit():
+    spec, tp, sp, mnp, h = setup()
+    park_object(h)
+    j = spec.dof_index("robot0:FFJ2")                        # kp 1, forcerange 0.9
+    h.dof[:, :, 0] = 0.5 * (np.array([n.lower for n in spec.nodes[1:]]) +
+                            np.array([n.upper for n in spec.nodes[1:]]))
+    h.targets[:] = h.dof[:, :, 0]
+    h.targets[:, j] = spec.nodes[1 + j].upper              # error ~0.79 rad + damping: unsaturated
+    h.simulate(mnp, sp)
+    assert abs(h.dof_force[0, j]) < 0.9
+    h.dof[:, j, 0] = 0.3                                     # error 1.27 rad, moving away: saturated
+    h.dof[:, j, 1] = -5.0                                    # in both substeps
+    h.dof_force[:] = 0
+    h.simulate(mnp, sp)
+    assert h.dof_force[0, j] == np.float32(0.9)
+
+
+def test_tendon_couples_distal_joint():
+    """T_FFJ1c: L = 0.00705 q(FFJ0) - 0.00805 q(FFJ1), soft limit |L| <= 0.001 with k = 30."""
+    spec, tp, sp, mnp, h = setup()
+    park_object(h)
+    j0, j1 = spec.dof_index("robot0:FFJ0"), spec.dof_index("robot0:FFJ1")
+    h.dof[:, :, 0] = 0.5 * (np.array([n.lower for n in spec.nodes[1:]]) +
+                            np.array([n.upper for n in spec.nodes[1:]]))
+    h.targets[:] = h.dof[:, :, 0]
+    h.dof[:, j0, 0], h.dof[:, j1, 0] = 0.5, 1.2
+    h.targets[:, j1] = 1.2
+    h.simulate(mnp, sp)
+    q0, q1, qd0, qd1 = h.dof[0, j0, 0], h.dof[0, j1, 0], h.dof[0, j0, 1], h.dof[0, j1, 1]
+    # the tendon pulls FFJ0 (undriven) towards flexion: positive velocity after one step
+    assert qd0 > 0
+    L = 0.00705 * 0.5 - 0.00805 * 1.2
+    f = -30.0 * (L - (-0.001))
+    # reported force on FFJ0 = c0 f (last substep's state: within 2 %) - damping * qd
+    np.testing.assert_allclose(h.dof_force[0, j0] + 0.1 * qd0, 0.00705 * f, rtol=2e-2)
+    del q0, q1, qd1
