@@ -201,6 +201,8 @@ typedef struct mg_task_params {
   int32_t use_relative_control;
   int32_t ignore_z_rot;               /* pen */
   int32_t obs_type;                   /* 0 = full_state (211) */
+  int32_t rb_per_env;                 /* rigid-body rows per env (articulation bodies + object + goal) */
+  int32_t num_dofs;                   /* hand DOFs (dof_state rows per env) */
   float dof_speed_scale;
   float act_moving_average;
   float dist_reward_scale;
@@ -280,6 +282,13 @@ int mg_compute_observations(const mg_task_params* tp, int32_t n, const float* ro
 int mg_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, const float* actions,
                       const float* potentials, const float* prev_potentials, const int64_t* progress,
                       int64_t* reset, float* rew, void* stream);
+
+/* Task-layer half of VecTask.step before the physics (pre_physics_step after the action
+ * clamp): locomotion -> dof_actuation = clamp(a) * gear * power_scale (ant.py:281-285);
+ * ShadowHand -> masked goal/env resets + PD targets into views->dof_targets
+ * (shadow_hand.py:670-698).  sim == NULL: `views` are used. */
+int mg_pre_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views,
+                   const mg_task_buffers* tb, int32_t n, void* stream);
 
 /* Task-layer half of VecTask.step after the physics (post_physics_step +
  * timeout + obs clamp).  With `sim`==NULL the state views in `views` are used

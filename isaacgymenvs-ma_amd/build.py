@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "migym.hip")
 OUT = os.path.join(HERE, "migym", "_lib", "libmigym.so")
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("team_physics.hpp", "task.hpp", "device_math.hpp")] + [
+HEADERS = [os.path.join(HERE, "csrc", f) for f in ("team_physics.hpp", "hand_task.hpp", "task.hpp", "device_math.hpp")] + [
     os.path.join(HERE, "..", "include", "migym.h")]
 ARCH = os.environ.get("MIGYM_ARCH", "gfx950")
 

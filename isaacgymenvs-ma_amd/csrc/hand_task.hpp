@@ -1,0 +1,125 @@
+// hand_task.hpp — the ShadowHand task layer on gfx950:
+// the reference's @torch.jit.script reward, randomize_rotation and the tensor code of
+// pre_physics_step / reset_idx / compute_full_state, per env.  fp32 with FMA contraction off,
+// in the reference's operation order (same rules as task.hpp).
+//
+//   quat_from_angle_axis / quat_conjugate   utils/torch_jit_utils.py:107-123
+//   scale / tensor_clamp / unscale          utils/torch_jit_utils.py:229-240
+//   randomize_rotation                      tasks/shadow_hand.py:803-806
+//   compute_hand_reward                     tasks/shadow_hand.py:746-800
+//   compute_full_state                      tasks/shadow_hand.py:528-584
+//   reset_target_pose / reset_idx           tasks/shadow_hand.py:586-668
+//   pre_physics_step                        tasks/shadow_hand.py:670-698
+#pragma once
+#include "../../include/migym.h"
+#include "device_math.hpp"
+#include "task.hpp"
+
+namespace mg {
+
+#pragma clang fp contract(off)
+
+constexpr int HAND_NOISE = 61;  // [goal-only 4 | reset_idx 53 | reset_target_pose 4]
+
+__device__ __forceinline__ void h_quat_from_angle_axis(float angle, int k, float* q) {
+  const float theta = angle / 2.0f;
+  const float sn = sinf(theta), c = cosf(theta);
+  float v[4] = {0.0f, 0.0f, 0.0f, c};
+  v[k] = 1.0f * sn;
+  float n = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
+  n = n < 1e-9f ? 1e-9f : n;
+  for (int i = 0; i < 4; i++) q[i] = v[i] / n;
+}
+
+__device__ __forceinline__ void h_randomize_rotation(float r0, float r1, float* q) {
+  const float pi = 3.14159265358979323846f;
+  float qa[4], qb[4];
+  h_quat_from_angle_axis(r0 * pi, 0, qa);
+  h_quat_from_angle_axis(r1 * pi, 1, qb);
+  t_quat_mul(qa, qb, q);
+}
+
+__device__ __forceinline__ float h_rand_pm1(float u) { return 2.0f * u + -1.0f; }
+
+// uniform k of env `gid` for this control step: injected noise row or the counter-based RNG
+__device__ __forceinline__ float h_uniform(const mg_task_buffers& tb, int e, uint64_t gid, int k) {
+  return tb.noise ? tb.noise[(size_t)HAND_NOISE * e + k] : uniform01(tb.seed, gid, tb.step_counter, (uint32_t)k);
+}
+
+// reset_target_pose: goal_states (13) and the goal actor's root row (13)
+__device__ __forceinline__ void h_reset_goal(const mg_task_params& tp, float g0, float g1, float* gs, float* groot) {
+  float q[4];
+  h_randomize_rotation(g0, g1, q);
+  gs[0] = tp.object_start[0];
+  gs[1] = tp.object_start[1];
+  gs[2] = tp.object_start[2] + tp.goal_dz;
+  for (int k = 0; k < 4; k++) gs[3 + k] = q[k];
+  for (int k = 0; k < 3; k++) groot[k] = gs[k] + tp.goal_displacement[k];
+  for (int k = 0; k < 4; k++) groot[3 + k] = q[k];
+  for (int k = 7; k < 13; k++) groot[k] = 0.0f;
+}
+
+// compute_hand_reward for one env (the global running mean is reduced by the caller)
+__device__ __forceinline__ void h_reward(const mg_task_params& tp, const float* opos, const float* orot,
+                                         const float* tpos, const float* trot, const float* act, int64_t reset_in,
+                                         int64_t goal_in, int64_t* progress, float* successes, float* rew,
+                                         int64_t* reset_out, int64_t* goal_out) {
+  const float max_episode_length = (float)tp.max_episode_length;
+  const float d0 = opos[0] - tpos[0], d1 = opos[1] - tpos[1], d2 = opos[2] - tpos[2];
+  const float goal_dist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+  float tol = tp.success_tolerance;
+  if (tp.ignore_z_rot) tol = 2.0f * tol;
+  const float tc[4] = {-trot[0], -trot[1], -trot[2], trot[3]};
+  float qd[4];
+  t_quat_mul(orot, tc, qd);
+  float qn = sqrtf(qd[0] * qd[0] + qd[1] * qd[1] + qd[2] * qd[2]);
+  qn = qn > 1.0f ? 1.0f : qn;
+  const float rot_dist = 2.0f * asinf(qn);
+  const float dist_rew = goal_dist * tp.dist_reward_scale;
+  const float rot_rew = 1.0f / (fabsf(rot_dist) + tp.rot_eps) * tp.rot_reward_scale;
+  float pen = 0.0f;
+  for (int i = 0; i < tp.num_actions; i++) pen += act[i] * act[i];
+  float reward = dist_rew + rot_rew + pen * tp.action_penalty_scale;
+  const int64_t goal_resets = fabsf(rot_dist) <= tol ? 1 : goal_in;
+  const float succ = *successes + (float)goal_resets;
+  if (goal_resets == 1) reward = reward + tp.reach_goal_bonus;
+  if (goal_dist >= tp.fall_dist) reward = reward + tp.fall_penalty;
+  int64_t resets = goal_dist >= tp.fall_dist ? 1 : reset_in;
+  int64_t prog = *progress;
+  if (tp.max_consecutive_successes > 0) {
+    if (fabsf(rot_dist) <= tol) prog = 0;
+    if (succ >= (float)tp.max_consecutive_successes) resets = 1;
+  }
+  if ((float)prog >= max_episode_length - 1.0f) resets = 1;
+  if (tp.max_consecutive_successes > 0 && (float)prog >= max_episode_length - 1.0f)
+    reward = reward + 0.5f * tp.fall_penalty;
+  *rew = reward;
+  *reset_out = resets;
+  *goal_out = goal_resets;
+  *progress = prog;
+  *successes = succ;
+}
+
+// action -> PD target of DOF d (shadow_hand.py:677-693); returns the new target
+__device__ __forceinline__ float h_target(const mg_task_params& tp, int d, float a, float prev) {
+  const float lo = tp.dof_lower[d], hi = tp.dof_upper[d];
+  float t;
+  if (tp.use_relative_control) {
+    t = prev + (float)((double)tp.dof_speed_scale * (double)tp.dt) * a;
+  } else {
+    t = 0.5f * (a + 1.0f) * (hi - lo) + lo;
+    t = tp.act_moving_average * t + (1.0f - tp.act_moving_average) * prev;
+  }
+  t = t < hi ? t : hi;
+  t = t > lo ? t : lo;
+  return t;
+}
+
+// running mean of consecutive successes (shadow_hand.py:795-798)
+__device__ __forceinline__ float h_cons_update(const mg_task_params& tp, int64_t num_resets, float finished,
+                                               float cons) {
+  if (num_resets > 0) return tp.av_factor * finished / (float)num_resets + (1.0f - tp.av_factor) * cons;
+  return cons;
+}
+
+}  // namespace mg

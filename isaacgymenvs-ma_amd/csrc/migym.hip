@@ -7,8 +7,9 @@
 #include <string>
 
 #include "../../include/migym.h"
-#include "team_physics.hpp"
+#include "hand_task.hpp"
 #include "task.hpp"
+#include "team_physics.hpp"
 
 namespace {
 thread_local std::string g_err;
@@ -37,14 +38,14 @@ struct mg_sim {
 };
 
 // ------------------------------------------------------------------------------------------------ kernels
-// gym.simulate: one team of T lanes per actor (team_physics.hpp)
-template <int T, int MN, int MC, int MG, int MP>
-__global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p, int n,
-                                                     float* __restrict__ root, float* __restrict__ dof,
-                                                     const float* __restrict__ act, float* __restrict__ sensors,
-                                                     float* __restrict__ dof_force) {
+// gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
+// rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
+template <int T, int MN, int MC, int MG, int MP, bool OBJ>
+__global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
+                                                     mg_state_views v, int n) {
   constexpr int E = kBlock / T;
-  __shared__ mg::TeamLDS<T, MN, MC> lds[E];
+  constexpr int ROWS = OBJ ? 3 : 1;
+  __shared__ mg::TeamLDS<T, MN, MC, OBJ> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   mg::load_tile(&tile, m);
   __syncthreads();
@@ -53,23 +54,34 @@ __global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict_
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors;
-  mg::Team<T, MN, MC, MG, MP> t;
+  mg::Team<T, MN, MC, MG, MP, OBJ> t;
   t.init(&lds[team], &tile, m, &p);
   __syncthreads();
-  t.load(root + (size_t)13 * ac, dof + (size_t)2 * nd * ac, act ? act + (size_t)nd * ac : nullptr);
+  float* root = v.root_states + (size_t)13 * ROWS * ac;
+  t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
+         OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
   t.outputs(lds[team].sens, lds[team].dforce);
   t.stage_state();
   __syncthreads();
   if (valid) {
-    mg::TeamLDS<T, MN, MC>& L = lds[team];
+    mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team];
     if (!m->fixed_base)
-      for (int k = t.tl; k < 13; k += T) root[(size_t)13 * a + k] = L.root[k];
-    for (int k = t.tl; k < 2 * nd; k += T) dof[(size_t)2 * nd * a + k] = L.dof[k];
-    if (sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) sensors[(size_t)6 * ns * a + k] = L.sens[k];
-    if (dof_force)
-      for (int k = t.tl; k < nd; k += T) dof_force[(size_t)nd * a + k] = L.dforce[k];
+      for (int k = t.tl; k < 13; k += T) root[k] = L.root[k];
+    if (OBJ)
+      for (int k = t.tl; k < 13; k += T) root[13 + k] = L.oroot[k];
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.dof[k];
+    if (v.sensors)
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.sens[k];
+    if (v.dof_force)
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.dforce[k];
+    if (v.rigid_body_states) {
+      const int nb = m->num_bodies, nbe = nb + (OBJ ? 2 : 0);
+      float* rb = v.rigid_body_states + (size_t)13 * nbe * a;
+      for (int b = t.tl; b < nb; b += T) t.body_state(b, rb + 13 * b);
+      if (OBJ)
+        for (int k = t.tl; k < 26; k += T) rb[13 * nb + k] = k < 13 ? L.oroot[k] : root[26 + k - 13];
+    }
   }
 }
 
@@ -294,65 +306,390 @@ __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict_
   }
 }
 
+// pre_physics_step of the locomotion tasks: effort = clamp(a) * gear * power_scale
+// (ant.py:281-285, humanoid.py:281-285; cartpole.py:159-163: DOF 0 only)
+__global__ __launch_bounds__(kBlock) void k_pre_loco(mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n,
+                                                     int nd) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * nd) return;
+  const int a = t / nd, d = t % nd, na = tp.num_actions;
+  float tau;
+  if (tp.task_id == MG_TASK_CARTPOLE) {
+    tau = d == 0 ? mg::clampf(tb.actions[(size_t)na * a], tp.clip_actions) * tp.power_scale : 0.0f;
+  } else {
+    const float act = d < na ? mg::clampf(tb.actions[(size_t)na * a + d], tp.clip_actions) : 0.0f;
+    tau = act * tp.motor_effort[d] * tp.power_scale;
+  }
+  const_cast<float*>(v.dof_actuation)[t] = tau;
+}
+
+// ------------------------------------------------------------------------------------------------ hand tasks
+// index of DOF d in the actuated list (action column), -1 if not actuated
+__device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
+  for (int i = 0; i < tp.num_actions; i++)
+    if (tp.actuated_dof[i] == d) return i;
+  return -1;
+}
+
+// pre_physics_step of one env on one lane (physics-free path, shadow_hand.py:670-698)
+__global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                     int n, int nd) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint64_t gid = (uint64_t)(tb.env_offset + e);
+  float* root = v.root_states + (size_t)39 * e;
+  float* gs = tb.goal_states + (size_t)13 * e;
+  const bool goal_reset = tb.reset_goal[e] != 0, env_reset = tb.reset[e] != 0;
+  if (goal_reset)
+    mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 0)), mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 1)),
+                     gs, root + 26);
+  float* tgt = const_cast<float*>(v.dof_targets) + (size_t)nd * e;
+  float* prev = tb.prev_targets + (size_t)nd * e;
+  if (env_reset) {
+    mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 57)),
+                     mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 58)), gs, root + 26);
+    float r[5];
+    for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 4 + k));
+    float* ob = root + 13;
+    for (int k = 0; k < 3; k++) ob[k] = tp.object_start[k] + tp.reset_position_noise * r[k];
+    mg::h_randomize_rotation(r[3], r[4], ob + 3);
+    for (int k = 7; k < 13; k++) ob[k] = 0.0f;
+    float* dof = v.dof_state + (size_t)2 * nd * e;
+    for (int j = 0; j < nd; j++) {
+      const float rp = mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 9 + j));
+      const float rv = mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 9 + nd + j));
+      const float dmax = tp.dof_upper[j] - tp.initial_dof_pos[j], dmin = tp.dof_lower[j] - tp.initial_dof_pos[j];
+      const float pos = tp.initial_dof_pos[j] + tp.reset_dof_pos_noise * (dmin + (dmax - dmin) * 0.5f * (rp + 1.0f));
+      dof[2 * j] = pos;
+      dof[2 * j + 1] = 0.0f + tp.reset_dof_vel_noise * rv;
+      prev[j] = pos;
+      tgt[j] = pos;
+    }
+    tb.progress[e] = 0;
+    tb.reset[e] = 0;
+    tb.successes[e] = 0.0f;
+  }
+  if (goal_reset || env_reset) tb.reset_goal[e] = 0;
+  const int na = tp.num_actions;
+  for (int i = 0; i < na; i++) {
+    const int d = tp.actuated_dof[i];
+    const float a = mg::clampf(tb.actions[(size_t)na * e + i], tp.clip_actions);
+    if (tb.actions_out) tb.actions_out[(size_t)na * e + i] = a;
+    const float t = mg::h_target(tp, d, a, prev[d]);
+    tgt[d] = t;
+    prev[d] = t;
+  }
+}
+
+// full_state observation value k of one env from its state rows (compute_full_state order)
+__device__ __forceinline__ float hand_obs_value(const mg_task_params& tp, int k, int nd, const float* dof,
+                                                const float* dforce, const float* orow, const float* gs,
+                                                const float* qdiff, const float* rbs, const float* sens,
+                                                const float* act) {
+  if (k < nd) return (2.0f * dof[2 * k] - tp.dof_upper[k] - tp.dof_lower[k]) / (tp.dof_upper[k] - tp.dof_lower[k]);
+  k -= nd;
+  if (k < nd) return tp.vel_obs_scale * dof[2 * k + 1];
+  k -= nd;
+  if (k < nd) return tp.force_torque_obs_scale * dforce[k];
+  k -= nd;
+  if (k < 10) return orow[k];
+  if (k < 13) return tp.vel_obs_scale * orow[k];
+  k -= 13;
+  if (k < 7) return gs[k];
+  k -= 7;
+  if (k < 4) return qdiff[k];
+  k -= 4;
+  const int nf = tp.num_fingertips;
+  if (k < 13 * nf) return rbs[(size_t)13 * tp.fingertip_body[k / 13] + k % 13];
+  k -= 13 * nf;
+  if (k < 6 * nf) return tp.force_torque_obs_scale * sens[k];
+  k -= 6 * nf;
+  return act[k];
+}
+
+// post_physics_step of one env on one lane (physics-free path): progress, full_state obs, reward,
+// the running-mean partial sums, timeout, obs clamp
+__global__ __launch_bounds__(kBlock) void k_hand_post(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                      int n, int nd) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t ro = 0;
+  float fin = 0.0f;
+  if (e < n) {
+    const int na = tp.num_actions, no = tp.num_obs;
+    const float* orow = v.root_states + (size_t)39 * e + 13;
+    const float* gs = tb.goal_states + (size_t)13 * e;
+    const float* act = tb.actions_out + (size_t)na * e;
+    float qdiff[4];
+    const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
+    mg::t_quat_mul(orow + 3, gc, qdiff);
+    int64_t prog = tb.progress[e] + 1;
+    float* o = tb.obs + (size_t)no * e;
+    const float* rbs = v.rigid_body_states + (size_t)13 * tp.rb_per_env * e;
+    for (int k = 0; k < no; k++) {
+      const float x = hand_obs_value(tp, k, nd, v.dof_state + (size_t)2 * nd * e, v.dof_force + (size_t)nd * e,
+                                     orow, gs, qdiff, rbs, v.sensors + (size_t)6 * tp.num_fingertips * e, act);
+      o[k] = x;
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(x, tp.clip_obs);
+    }
+    float succ = tb.successes[e], rew;
+    int64_t go;
+    mg::h_reward(tp, orow, orow + 3, gs, gs + 3, act, tb.reset[e], tb.reset_goal[e], &prog, &succ, &rew, &ro, &go);
+    tb.rew[e] = rew;
+    tb.reset[e] = ro;
+    tb.reset_goal[e] = go;
+    tb.progress[e] = prog;
+    tb.successes[e] = succ;
+    tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
+    fin = succ * (float)ro;
+  }
+  // partial sums of compute_hand_reward's global reduction (integer-valued: exact in any order)
+  unsigned long long cr = (unsigned long long)ro, cf = (unsigned long long)fin;
+  for (int off = 32; off >= 1; off >>= 1) {
+    cr += __shfl_xor(cr, off);
+    cf += __shfl_xor(cf, off);
+  }
+  if ((threadIdx.x & 63) == 0 && (cr | cf)) {
+    atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
+    atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
+  }
+}
+
+// consecutive_successes running mean (shadow_hand.py:795-798) from the step's sums; clears them
+__global__ void k_hand_finalize(mg_task_params tp, mg_task_buffers tb) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t nres = (int64_t)tb.reduce_scratch[0];
+  const float fin = (float)tb.reduce_scratch[1];
+  tb.consecutive_successes[0] = mg::h_cons_update(tp, nres, fin, tb.consecutive_successes[0]);
+  tb.reduce_scratch[0] = 0;
+  tb.reduce_scratch[1] = 0;
+}
+
+// The whole ShadowHand VecTask.step for one env, fused: pre_physics_step (masked goal / env resets,
+// PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
+// the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
+template <int T, int MN, int MC, int MG, int MP>
+__global__ __launch_bounds__(kBlock) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
+                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                      int n) {
+  constexpr int E = kBlock / T;
+  __shared__ mg::TeamLDS<T, MN, MC, true> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  mg::load_tile(&tile, m);
+  __syncthreads();
+  const int team = threadIdx.x / T;
+  const int e = blockIdx.x * E + team;
+  const bool valid = e < n;
+  const int ec = valid ? e : n - 1;
+  const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
+  const int nb = m->num_bodies, nbe = nb + 2;
+  mg::TeamLDS<T, MN, MC, true>& L = lds[team];
+  mg::Team<T, MN, MC, MG, MP, true> t;
+  t.init(&L, &tile, m, &p);
+  const uint64_t gid = (uint64_t)(tb.env_offset + ec);
+  const bool env_reset = tb.reset[ec] != 0, goal_reset = tb.reset_goal[ec] != 0;
+  float* root = v.root_states + (size_t)39 * ec;
+  // ---- pre_physics_step: goal / object resets staged in LDS by the team leader
+  if (t.tl == 0) {
+    float* gr = L.goal;
+    float* gs = L.goal + 13;
+    if (env_reset || goal_reset) {
+      const int c0 = env_reset ? 57 : 0;  // env reset: reset_idx's own reset_target_pose draw wins
+      mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, c0)),
+                       mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, c0 + 1)), gs, gr);
+      for (int k = 7; k < 13; k++) gs[k] = tb.goal_states[(size_t)13 * ec + k];
+    } else {
+      for (int k = 0; k < 13; k++) { gr[k] = root[26 + k]; gs[k] = tb.goal_states[(size_t)13 * ec + k]; }
+    }
+    if (env_reset) {
+      float r[5];
+      for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 4 + k));
+      for (int k = 0; k < 3; k++) L.oroot[k] = tp.object_start[k] + tp.reset_position_noise * r[k];
+      mg::h_randomize_rotation(r[3], r[4], L.oroot + 3);
+      for (int k = 7; k < 13; k++) L.oroot[k] = 0.0f;
+    } else {
+      for (int k = 0; k < 13; k++) L.oroot[k] = root[13 + k];
+    }
+  }
+  __syncthreads();
+  t.load(root, v.dof_state + (size_t)2 * nd * ec, nullptr, L.oroot, nullptr);
+  float prev = 0.0f;
+  if (t.node > 0) {  // DOF lanes: reset_idx's DOF draw, then actions -> PD targets
+    const int d = t.node - 1;
+    float cur;
+    if (env_reset) {
+      const float rp = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 9 + d));
+      const float rv = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 9 + nd + d));
+      const float dmax = tp.dof_upper[d] - tp.initial_dof_pos[d], dmin = tp.dof_lower[d] - tp.initial_dof_pos[d];
+      const float pos = tp.initial_dof_pos[d] + tp.reset_dof_pos_noise * (dmin + (dmax - dmin) * 0.5f * (rp + 1.0f));
+      t.qj = pos;
+      t.nu = 0.0f + tp.reset_dof_vel_noise * rv;
+      prev = pos;
+      cur = pos;
+    } else {
+      prev = tb.prev_targets[(size_t)nd * ec + d];
+      cur = v.dof_targets[(size_t)nd * ec + d];
+    }
+    const int ai = hand_action_of(tp, d);
+    if (ai >= 0) {
+      const float a = mg::clampf(tb.actions[(size_t)na * ec + ai], tp.clip_actions);
+      cur = mg::h_target(tp, d, a, prev);
+      prev = cur;
+    }
+    t.tgt = cur;
+  }
+  // ---- gym.simulate
+  for (int st = 0; st < p.substeps; st++) t.substep();
+  t.outputs(L.sens, L.dforce);
+  t.stage_state();
+  __syncthreads();
+  // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
+  const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
+  float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
+  {
+    const float* gs = L.goal + 13;
+    float qdiff[4];
+    const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
+    mg::t_quat_mul(L.oroot + 3, gc, qdiff);
+    const int nf = tp.num_fingertips;
+    const int ft0 = 3 * nd + 24;  // first fingertip value
+    for (int k = t.tl; k < no; k += T) {
+      float x;
+      if (k >= no - na) {  // self.actions (clamped)
+        x = mg::clampf(tb.actions[(size_t)na * ec + (k - (no - na))], tp.clip_actions);
+      } else if (k >= ft0 && k < ft0 + 13 * nf) {  // fingertip body state from the post-step FK
+        float b13[13];
+        t.body_state(tp.fingertip_body[(k - ft0) / 13], b13);
+        x = b13[(k - ft0) % 13];
+      } else {
+        x = hand_obs_value(tp, k, nd, L.dof, L.dforce, L.oroot, gs, qdiff, nullptr, L.sens, nullptr);
+      }
+      L.obs[k] = x;
+    }
+  }
+  __syncthreads();
+  int64_t ro = 0;
+  float fin = 0.0f;
+  if (t.tl == 0) {
+    const float* gs = L.goal + 13;
+    float succ = env_reset ? 0.0f : tb.successes[ec], rew;
+    int64_t prog = progress_in + 1, go;
+    mg::h_reward(tp, L.oroot, L.oroot + 3, gs, gs + 3, L.obs + (no - na), 0, 0, &prog, &succ, &rew, &ro, &go);
+    if (valid) {
+      tb.rew[e] = rew;
+      tb.reset[e] = ro;
+      tb.reset_goal[e] = go;
+      tb.progress[e] = prog;
+      tb.successes[e] = succ;
+      tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
+      fin = succ * (float)ro;
+    } else {
+      ro = 0;
+    }
+  }
+  // partial sums of the global running mean: wave reduce, one atomic pair per wave
+  unsigned long long cr = (unsigned long long)ro, cf = (unsigned long long)fin;
+  for (int off = 32; off >= 1; off >>= 1) {
+    cr += __shfl_xor(cr, off);
+    cf += __shfl_xor(cf, off);
+  }
+  if (threadIdx.x == 0 && (cr | cf)) {
+    atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
+    atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
+  }
+  if (valid) {  // write-back (gym layouts), team-cooperative
+    float* o = tb.obs + (size_t)no * e;
+    for (int k = t.tl; k < no; k += T) {
+      o[k] = L.obs[k];
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(L.obs[k], tp.clip_obs);
+    }
+    if (tb.actions_out)
+      for (int k = t.tl; k < na; k += T) tb.actions_out[(size_t)na * e + k] = L.obs[no - na + k];
+    for (int k = t.tl; k < 13; k += T) {
+      root[13 + k] = L.oroot[k];
+      root[26 + k] = L.goal[k];
+      tb.goal_states[(size_t)13 * e + k] = L.goal[13 + k];
+    }
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.dof[k];
+    if (t.node > 0) {
+      const int d = t.node - 1;
+      const_cast<float*>(v.dof_targets)[(size_t)nd * e + d] = t.tgt;
+      tb.prev_targets[(size_t)nd * e + d] = prev;
+    }
+    if (v.sensors)
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.sens[k];
+    if (v.dof_force)
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.dforce[k];
+    for (int b = t.tl; b < nb; b += T) t.body_state(b, rbs + 13 * b);
+    for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
+  }
+}
+
 __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
-                              int nidx, int row) {
+                              int nidx, int row, int div) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nidx * row) return;
   const int r = t / row, c = t % row;
-  const size_t a = (size_t)idx[r] * row + c;
+  const size_t a = (size_t)(idx[r] / div) * row + c;
   dst[a] = src[a];
 }
 
 // ------------------------------------------------------------------------------------------------ dispatch
 // Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
-// contacts MC.  The smallest instance that fits the model is launched.
-#define MG_INSTANCES(X) \
-  X(8, 4, 8, 4, 0) X(16, 9, 16, 16, 0) X(16, 16, 24, 24, 32) X(32, 24, 32, 24, 160) X(32, 32, 48, 48, 192) \
-  X(64, 40, 48, 48, 192)
+// contacts MC, geoms MG, self pairs MP, OBJ = hand-task envs with a free object.  The smallest
+// instance that fits the model is launched.
+#define MG_INSTANCES(X)                                                                                     \
+  X(8, 4, 8, 4, 0, false) X(16, 9, 16, 16, 0, false) X(16, 16, 24, 24, 32, false) X(32, 24, 32, 24, 160, false) \
+  X(32, 32, 48, 48, 192, false) X(64, 40, 48, 48, 192, false) X(32, 25, 24, 24, 0, true)
+
+static int model_lanes(const mg_model& m) {
+  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs + (m.obj_type ? 6 : 0);
+  return nv > m.num_sensors ? nv : m.num_sensors;
+}
+#define MG_FITS(T, MN, MC, MG, MP, OBJ)                                                                    \
+  (m.num_nodes <= MN && max_contacts <= MC && model_lanes(m) <= T && (m.fixed_base || T >= 6) &&        \
+   m.num_geoms <= MG && m.num_pairs <= MP && (m.obj_type != 0) == OBJ)
 
 // team size the dispatcher picks for a model (0: none fits)
 static int team_size(const mg_model& m, int max_contacts) {
-  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
-  const int lanes = nv > m.num_sensors ? nv : m.num_sensors;
-#define MG_T(T, MN, MC, MG, MP)                                                                 \
-  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6) &&        \
-      m.num_geoms <= MG && m.num_pairs <= MP)                                                      \
-    return T;
+#define MG_T(T, MN, MC, MG, MP, OBJ) \
+  if (MG_FITS(T, MN, MC, MG, MP, OBJ)) return T;
   MG_INSTANCES(MG_T)
 #undef MG_T
   return 0;
 }
 
-template <template <int, int, int, int, int> class F, typename... A>
+template <template <int, int, int, int, int, bool> class F, typename... A>
 static int dispatch(const mg_model& m, int max_contacts, A... args) {
-  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs;
-  const int lanes = nv > m.num_sensors ? nv : m.num_sensors;
-#define MG_TRY(T, MN, MC, MG, MP)                                                              \
-  if (m.num_nodes <= MN && max_contacts <= MC && lanes <= T && (m.fixed_base || T >= 6) &&       \
-      m.num_geoms <= MG && m.num_pairs <= MP) {                                                   \
-    F<T, MN, MC, MG, MP>::run(args...);                                                          \
-    return MG_OK;                                                                                 \
+#define MG_TRY(T, MN, MC, MG, MP, OBJ)             \
+  if (MG_FITS(T, MN, MC, MG, MP, OBJ)) {           \
+    F<T, MN, MC, MG, MP, OBJ>::run(args...);       \
+    return MG_OK;                                  \
   }
   MG_INSTANCES(MG_TRY)
 #undef MG_TRY
   return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
 }
 
-template <int T, int MN, int MC, int MG, int MP>
+template <int T, int MN, int MC, int MG, int MP, bool OBJ>
 struct RunSimulate {
   static void run(hipStream_t s, const mg_sim* sim) {
-    const mg_state_views& v = sim->views;
     const int E = kBlock / T;
-    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
-                       sim->params, sim->n, v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force);
+    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                       sim->d_model, sim->params, sim->views, sim->n);
   }
 };
-template <int T, int MN, int MC, int MG, int MP>
+template <int T, int MN, int MC, int MG, int MP, bool OBJ>
 struct RunEnvStep {
   static void run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
     const int E = kBlock / T;
-    hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s, sim->d_model,
-                       sim->params, *tp, sim->views, *tb, sim->n);
+    if constexpr (OBJ) {
+      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                         sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
+      hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, s, *tp, *tb);
+    } else {
+      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                         sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
+    }
   }
 };
 
@@ -434,13 +771,19 @@ int mg_set_indexed(mg_sim* sim, int32_t which, const float* src, const int32_t* 
   } else if (which == MG_SET_DOF_STATE) {
     dst = sim->views.dof_state;
     row = 2 * sim->host_model.num_dofs;
+  } else if (which == MG_SET_DOF_TARGET) {
+    dst = const_cast<float*>(sim->views.dof_targets);
+    row = sim->host_model.num_dofs;
+    if (!dst) return fail(MG_EINVAL, "mg_set_indexed: no dof_targets bound");
   } else {
     return fail(MG_EINVAL, "mg_set_indexed: unknown target");
   }
   if (dst == src) return MG_OK;  // caller wrote into the bound buffer itself (gym views alias sim memory)
   const int total = n * row;
+  // hand-task envs: actor ids are global (3 per env: hand, object, goal); DOF rows belong to the hand
+  const int div = (which != MG_SET_ROOT_STATE && sim->host_model.obj_type) ? 3 : 1;
   hipLaunchKernelGGL(k_set_indexed, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, dst, src, idx, n,
-                     row);
+                     row, div);
   return check_launch("mg_set_indexed");
 }
 
@@ -468,6 +811,46 @@ int mg_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, con
   return check_launch("mg_compute_reward");
 }
 
+static int hand_args_ok(const mg_task_params* tp, const mg_state_views& v, const mg_task_buffers* tb,
+                        const char* who) {
+  if (!v.dof_targets || !v.rigid_body_states || !v.sensors || !v.dof_force || !tb->prev_targets ||
+      !tb->goal_states || !tb->reset_goal || !tb->successes || !tb->consecutive_successes ||
+      !tb->reduce_scratch || !tb->actions_out)
+    return fail(MG_EINVAL, std::string(who) + ": ShadowHand needs dof_targets, rigid_body_states, sensors, "
+                                              "dof_force and the hand task buffers");
+  if (tp->num_dofs <= 0 || tp->num_dofs > MG_MAX_HAND_DOFS || tp->num_actions > MG_MAX_HAND_DOFS)
+    return fail(MG_EINVAL, std::string(who) + ": bad hand DOF / action count");
+  return MG_OK;
+}
+
+int mg_pre_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views, const mg_task_buffers* tb,
+                   int32_t n, void* stream) {
+  if (!tp || !tb || !tb->actions) return fail(MG_EINVAL, "mg_pre_physics: bad args");
+  mg_state_views v;
+  int nd;
+  if (sim) {
+    if (!sim->bound) return fail(MG_EINVAL, "mg_pre_physics: sim not bound");
+    v = sim->views;
+    n = sim->n;
+    nd = sim->host_model.num_dofs;
+  } else {
+    if (!views) return fail(MG_EINVAL, "mg_pre_physics: need views without a sim");
+    v = *views;
+    nd = tp->task_id == MG_TASK_SHADOW_HAND ? tp->num_dofs : (tp->task_id == MG_TASK_CARTPOLE ? 2 : tp->num_actions);
+  }
+  if (n == 0) return MG_OK;
+  if (tp->task_id == MG_TASK_SHADOW_HAND) {
+    int rc = hand_args_ok(tp, v, tb, "mg_pre_physics");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_hand_pre, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n, nd);
+  } else {
+    if (!v.dof_actuation) return fail(MG_EINVAL, "mg_pre_physics: locomotion task needs dof_actuation");
+    hipLaunchKernelGGL(k_pre_loco, dim3(grid_for(n * nd)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n,
+                       nd);
+  }
+  return check_launch("mg_pre_physics");
+}
+
 int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views, const mg_task_buffers* tb,
                     int32_t n, void* stream) {
   if (!tp || !tb) return fail(MG_EINVAL, "mg_post_physics: bad args");
@@ -484,6 +867,14 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
     v = *views;
   }
   if (n == 0) return MG_OK;
+  if (tp->task_id == MG_TASK_SHADOW_HAND) {
+    int rc = hand_args_ok(tp, v, tb, "mg_post_physics");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_hand_post, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n,
+                       tp->num_dofs);
+    hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
+    return check_launch("mg_post_physics");
+  }
   hipLaunchKernelGGL(k_post_physics, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n);
   return check_launch("mg_post_physics");
 }
@@ -492,10 +883,20 @@ int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb
   if (!sim || !sim->bound || !tp || !tb || !tb->actions || !tb->obs || !tb->rew || !tb->reset || !tb->progress ||
       !tb->timeout)
     return fail(MG_EINVAL, "mg_env_step: bad arguments");
-  if (tp->task_id != MG_TASK_CARTPOLE && (!tb->potentials || !tb->prev_potentials || !tb->up_vec || !tb->heading_vec))
-    return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
-  if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
-    return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
+  const bool hand = tp->task_id == MG_TASK_SHADOW_HAND;
+  if (hand != (sim->host_model.obj_type != 0))
+    return fail(MG_EINVAL, "mg_env_step: ShadowHand needs a model with a free object (and only it does)");
+  if (hand) {
+    int rc = hand_args_ok(tp, sim->views, tb, "mg_env_step");
+    if (rc) return rc;
+    if (tp->num_dofs != sim->host_model.num_dofs || tp->rb_per_env != sim->host_model.num_bodies + 2)
+      return fail(MG_EINVAL, "mg_env_step: task DOF / rigid-body counts do not match the model");
+  } else {
+    if (tp->task_id != MG_TASK_CARTPOLE && (!tb->potentials || !tb->prev_potentials || !tb->up_vec || !tb->heading_vec))
+      return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
+    if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
+      return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
+  }
   if (tp->num_agents > 1) {
     // the agents of an env must be teams of one wave (ballot/shuffle exchange): A | 64/T
     const int T = team_size(sim->host_model, sim->params.max_contacts);

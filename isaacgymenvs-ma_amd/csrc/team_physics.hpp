@@ -21,6 +21,13 @@
 //   product (butterfly shuffles) plus one FMA per lane.
 // All lanes of a wave run every phase (teams never diverge on barriers);
 // the block is one wave, so __syncthreads() is a cheap wave barrier.
+//
+// Hand tasks (OBJ = true, SURVEY.md §8(a) A4-A8 for ShadowHand): PD position drives
+// (implicit toward the target, +-effort when saturated), fixed tendons (explicit soft
+// limits), and a free rigid box whose 6 velocity columns [w; v_com] live on the lanes
+// right after the articulation's; contacts between articulation geoms and the box
+// couple the two blocks only through the PGS rows (response = ABA test solve on the
+// articulation lanes + the box's closed-form inverse inertia on the object lanes).
 #pragma once
 #include "../../include/migym.h"
 #include "device_math.hpp"
@@ -34,9 +41,12 @@ template <int MN, int MG, int MP>
 struct ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
-  float nf[MN][31];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
-                      // 27 stiff, 28 lower, 29 upper
-  int gtype[MG], gnode[MG], gbody[MG];
+  float nf[MN][33];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
+                      // 27 stiff, 28 lower, 29 upper, 30 drive kp, 31 effort limit
+  int gtype[MG], gnode[MG], gbody[MG], gfil[MG];
+  int tdof[MG_MAX_TENDONS][2];
+  float tf[MG_MAX_TENDONS][6];   // coef0, coef1, lo, hi, limit stiffness, damping
+  int nten;
   float gf[MG][17];   // 0-2 pos, 3-11 R, 12-14 size
   int pairs[MP > 0 ? MP : 1][2];
   int nn, ng, np;
@@ -63,11 +73,21 @@ __device__ void load_tile(ModelTile<MN, MG, MP>* t, const mg_model* m) {
     for (int k = 0; k < 6; k++) f[18 + k] = m->inertia[i][k];
     f[24] = m->mass[i]; f[25] = m->armature[i]; f[26] = m->damping[i]; f[27] = m->stiffness[i];
     f[28] = m->lower[i]; f[29] = m->upper[i];
+    f[30] = m->drive_kp[i]; f[31] = m->effort_limit[i];
+  }
+  const int nten = m->num_tendons < MG_MAX_TENDONS ? m->num_tendons : MG_MAX_TENDONS;
+  for (int q = tid; q < nten; q += nt) {
+    t->tdof[q][0] = m->tendon_dof[q][0];
+    t->tdof[q][1] = m->tendon_dof[q][1];
+    t->tf[q][0] = m->tendon_coef[q][0]; t->tf[q][1] = m->tendon_coef[q][1];
+    t->tf[q][2] = m->tendon_range[q][0]; t->tf[q][3] = m->tendon_range[q][1];
+    t->tf[q][4] = m->tendon_limit_stiffness[q]; t->tf[q][5] = m->tendon_damping[q];
   }
   for (int g = tid; g < ng; g += nt) {
     t->gtype[g] = m->geom_type[g];
     t->gnode[g] = m->geom_node[g];
     t->gbody[g] = m->geom_body[g];
+    t->gfil[g] = m->geom_filter[g];
     float* f = t->gf[g];
     M3 Rg = quat_to_mat(m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]);
     for (int k = 0; k < 3; k++) { f[k] = m->geom_pos[g][k]; f[12 + k] = m->geom_size[g][k]; }
@@ -78,12 +98,13 @@ __device__ void load_tile(ModelTile<MN, MG, MP>* t, const mg_model* m) {
     t->pairs[q][0] = m->pair[q][0];
     t->pairs[q][1] = m->pair[q][1];
   }
-  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; }
+  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; }
 }
 
-template <int T, int MN, int MC>
+template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
+  static constexpr int MRO = OBJ ? MR : 1;
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -108,6 +129,11 @@ struct TeamLDS {
   float dof[2 * MN];
   float sens[6 * MG_MAX_SENSORS];
   float dforce[MN];
+  // free object (OBJ): Jacobian rows on its columns, staged root row, obs staging
+  float rwo[MRO][6];
+  float oroot[OBJ ? 13 : 1];
+  float goal[OBJ ? 26 : 1];   // goal actor root row, goal_states row
+  float obs[OBJ ? 212 : 1];
 };
 
 // Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + ds_swizzle xor 16 and
@@ -148,10 +174,95 @@ __device__ __forceinline__ void tangent_basis_t(V3 n, V3* t1, V3* t2) {
   *t2 = cross(n, t);
 }
 
+constexpr int OBJ_NODE = -2;  // contact side on the free object
+
+// signed distance of point p (box frame) to a box of half extents hb (same rule as the oracle's
+// point_box): outside -> distance to the closest point cb, normal away from the box; inside ->
+// minus the smallest face depth (ties x, y, z), that face's normal, cb = projection onto it
+__device__ __forceinline__ float point_box(V3 p, V3 hb, V3* nb, V3* cb) {
+  V3 q = v3(fminf(fmaxf(p.x, -hb.x), hb.x), fminf(fmaxf(p.y, -hb.y), hb.y), fminf(fmaxf(p.z, -hb.z), hb.z));
+  if (q.x != p.x || q.y != p.y || q.z != p.z) {
+    V3 d = p - q;
+    float l = sqrtf(dot(d, d));
+    *nb = d * (1.0f / l);
+    *cb = q;
+    return l;
+  }
+  float dx = hb.x - fabsf(p.x), dy = hb.y - fabsf(p.y), dz = hb.z - fabsf(p.z);
+  int k = 0;
+  float dm = dx;
+  if (dy < dm) { dm = dy; k = 1; }
+  if (dz < dm) { dm = dz; k = 2; }
+  V3 c = p, n = v3(0, 0, 0);
+  if (k == 0) { float sg = p.x < 0 ? -1.f : 1.f; n.x = sg; c.x = sg * hb.x; }
+  else if (k == 1) { float sg = p.y < 0 ? -1.f : 1.f; n.y = sg; c.y = sg * hb.y; }
+  else { float sg = p.z < 0 ? -1.f : 1.f; n.z = sg; c.z = sg * hb.z; }
+  *nb = n;
+  *cb = c;
+  return -dm;
+}
+
+// closest parameter of segment a + t u (box frame) to the box (oracle seg_box_t): exact minimum of
+// the convex piecewise-quadratic squared distance over the sorted slab crossings; middle of the
+// inside portion when the segment passes through the box
+__device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
+  const float av[3] = {a.x, a.y, a.z}, uv[3] = {u.x, u.y, u.z}, hv[3] = {hb.x, hb.y, hb.z};
+  float t0 = 0.0f, t1 = 1.0f;
+  bool hit = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (fabsf(uv[k]) < 1e-12f) {
+      if (av[k] < -hv[k] || av[k] > hv[k]) hit = false;
+    } else {
+      float ta = (-hv[k] - av[k]) / uv[k], tb = (hv[k] - av[k]) / uv[k];
+      if (ta > tb) { float x = ta; ta = tb; tb = x; }
+      t0 = fmaxf(t0, ta);
+      t1 = fminf(t1, tb);
+    }
+  }
+  if (hit && t0 <= t1) return 0.5f * (t0 + t1);
+  float bp[8];
+  int nb = 0;
+  bp[nb++] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (fabsf(uv[k]) < 1e-12f) continue;
+#pragma unroll
+    for (int sg = -1; sg <= 1; sg += 2) {
+      float t = ((float)sg * hv[k] - av[k]) / uv[k];
+      if (t > 0.0f && t < 1.0f) bp[nb++] = t;
+    }
+  }
+  bp[nb++] = 1.0f;
+  for (int i = 1; i < nb; i++)
+    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { float x = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = x; }
+  float best_t = 0.0f, best_f = 3.0e38f;
+  for (int i = 0; i + 1 < nb; i++) {
+    const float lo = bp[i], hi = bp[i + 1], mid = 0.5f * (lo + hi);
+    float num = 0.0f, den = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float x = av[k] + mid * uv[k];
+      if (x > hv[k]) { num += (av[k] - hv[k]) * uv[k]; den += uv[k] * uv[k]; }
+      else if (x < -hv[k]) { num += (av[k] + hv[k]) * uv[k]; den += uv[k] * uv[k]; }
+    }
+    float t = den > 0.0f ? -num / den : lo;
+    t = fminf(fmaxf(t, lo), hi);
+    float f = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float x = fabsf(av[k] + t * uv[k]) - hv[k];
+      if (x > 0.0f) f += x * x;
+    }
+    if (f < best_f) { best_f = f; best_t = t; }
+  }
+  return best_t;
+}
+
 // Per-lane context of one team.
-template <int T, int MN, int MC, int MG, int MP>
+template <int T, int MN, int MC, int MG, int MP, bool OBJ = false>
 struct Team {
-  using L = TeamLDS<T, MN, MC>;
+  using L = TeamLDS<T, MN, MC, OBJ>;
   using MT = ModelTile<MN, MG, MP>;
   static constexpr int MR = L::MR;
   L* s;
@@ -176,6 +287,16 @@ struct Team {
   Sym6 IA;
   float Dinv, u;
   float h;
+  // drives / tendons (node lanes)
+  float tgt;           // PD target of the own DOF
+  float ttend;         // tendon generalized force (current substep)
+  int sat;             // drive saturated (current substep)
+  // free object (OBJ): pose replicated on every lane, velocity column on lanes ob0..ob0+5
+  int ob0;
+  bool objl;
+  V3 op;
+  float oq[4];
+  M3 oR;
 
   __device__ int col_of(int i) const { return ncol0 - 1 + i; }
 
@@ -210,11 +331,21 @@ struct Team {
     nu = 0.0f;
     qj = 0.0f;
     tau = 0.0f;
+    tgt = 0.0f;
+    ttend = 0.0f;
+    sat = 0;
+    ob0 = nv;
+    objl = OBJ && tl >= nv && tl < nv + 6;
+    op = v3(0, 0, 0);
+    oq[0] = oq[1] = oq[2] = 0.0f;
+    oq[3] = 1.0f;
   }
+  __device__ float gscale() const { return m->gravity_off ? 0.0f : 1.0f; }
   __device__ bool in_path(int target, int k) const { return target >= 0 && ((s->anc[target] >> k) & 1ull); }
 
   // ---------------------------------------------------------------- FK (level-synchronous)
   __device__ void fk() {
+    if (OBJ) oR = quat_to_mat(oq[0], oq[1], oq[2], oq[3]);
     if (tl == 0) {
       M3 R0 = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
       for (int a = 0; a < 3; a++)
@@ -288,7 +419,7 @@ struct Team {
       const float mass = nf[24];
       IA = body_inertia(mass, cc, Iw);
       SV IV = mul(IA, V);
-      V3 mg = ld3(p->gravity) * mass;
+      V3 mg = ld3(p->gravity) * (mass * gscale());
       pA = crf(V, IV) - sv(cross(cc, mg), mg);
       c = node == 0 ? szero() : crm(V, S * nu);
     }
@@ -296,9 +427,21 @@ struct Team {
       if (node > 0 && depth == lev) {
         U = mul(IA, S);
         const float* nf = mt->nf[node];
-        float D = dot(S, U) + nf[25] + h * nf[26] + h * h * nf[27];
+        // implicit spring/damper; PD drives toward the target unless the explicit estimate
+        // exceeds the effort limit (then a constant +-limit force, no implicit terms)
+        float kk = nf[27], bb = nf[26], ref = 0.0f, tadd = 0.0f;
+        sat = 0;
+        if (nf[30] > 0.0f) {
+          const float fe = nf[30] * (tgt - qj) - nf[26] * nu;
+          if (fabsf(fe) > nf[31]) {
+            kk = 0.0f; bb = 0.0f; tadd = fe > 0.0f ? nf[31] : -nf[31]; sat = 1;
+          } else {
+            kk = nf[30]; ref = tgt;
+          }
+        }
+        float D = dot(S, U) + nf[25] + h * bb + h * h * kk;
         Dinv = 1.0f / D;
-        float t = tau - nf[26] * nu - nf[27] * (qj + h * nu);
+        float t = tau + tadd + ttend - bb * nu - kk * (qj - ref + h * nu);
         u = t - dot(S, pA);
         Sym6 Ia = IA;
         rank1_sub(Ia, U, Dinv);
@@ -367,6 +510,52 @@ struct Team {
     }
   }
 
+  // ---------------------------------------------------------------- fixed tendons (explicit soft limits)
+  __device__ void tendons() {
+    ttend = 0.0f;
+    for (int q = 0; q < mt->nten; q++) {
+      const int d0 = mt->tdof[q][0], d1 = mt->tdof[q][1];
+      const int l0 = tb + ncol0 + d0, l1 = tb + ncol0 + d1;
+      const float q0 = __shfl(qj, l0), q1 = __shfl(qj, l1), v0 = __shfl(nu, l0), v1 = __shfl(nu, l1);
+      const float* f = mt->tf[q];
+      const float Lt = f[0] * q0 + f[1] * q1, Ld = f[0] * v0 + f[1] * v1;
+      const float cl = fminf(fmaxf(Lt, f[2]), f[3]);
+      const float F = -f[4] * (Lt - cl) - f[5] * Ld;
+      if (node > 0 && node - 1 == d0) ttend += f[0] * F;
+      if (node > 0 && node - 1 == d1) ttend += f[1] * F;
+    }
+  }
+
+  // ---------------------------------------------------------------- free object: unconstrained step
+  // I_w = R diag(I) R^T; every lane evaluates the 3-vectors, object lane k keeps component k.
+  __device__ V3 obj_inv_inertia(V3 x) const {
+    const float* I = m->obj_inertia;
+    V3 b = mulT(oR, x);
+    return mul(oR, v3(b.x / I[0], b.y / I[1], b.z / I[2]));
+  }
+  __device__ void obj_free() {
+    if (!OBJ) return;
+    const V3 w = v3(__shfl(nu, tb + ob0), __shfl(nu, tb + ob0 + 1), __shfl(nu, tb + ob0 + 2));
+    const float* I = m->obj_inertia;
+    const V3 b = mulT(oR, w);
+    const V3 Iw = mul(oR, v3(I[0] * b.x, I[1] * b.y, I[2] * b.z));
+    const V3 aw = obj_inv_inertia(cross(w, Iw) * -1.0f);
+    if (objl) {
+      const int k = tl - ob0;
+      const float a = k == 0 ? aw.x : k == 1 ? aw.y : k == 2 ? aw.z : m->obj_gravity * p->gravity[k - 3];
+      nu += h * a;
+      nu *= k < 3 ? 1.0f / (1.0f + h * m->obj_ang_damping) : 1.0f / (1.0f + h * m->obj_lin_damping);
+    }
+  }
+  // object part of the response column Y_r = M^-1 J_r^T (object lanes)
+  __device__ float obj_response(int r) const {
+    const float* J = s->rwo[r];
+    const int k = tl - ob0;
+    if (k >= 3) return J[k] / m->obj_mass;
+    const V3 y = obj_inv_inertia(v3(J[0], J[1], J[2]));
+    return k == 0 ? y.x : k == 1 ? y.y : y.z;
+  }
+
   // ---------------------------------------------------------------- test solve: Y = M~^-1 (J^T) column into lane regs
   // generalized force: spatial force fw on nodeA (and -fw on nodeB), plus unit joint force sg on node jn.
   __device__ float test_solve(int nodeA, int nodeB, SV fw, int jn, float sg) {
@@ -423,6 +612,7 @@ struct Team {
   // J_r[tl] for row r (contacts: root twist part / path projection; limits: unit on the dof column)
   __device__ float jac_entry(int r) const {
     const int kind = s->rkind[r];
+    if (OBJ && objl) return kind >= 2 ? 0.0f : s->rwo[r][tl - ob0];
     if (tl >= nv) return 0.0f;
     if (kind >= 2) return (node > 0 && node == s->rref[r]) ? (kind == 2 ? 1.0f : -1.0f) : 0.0f;
     const float* w = s->rw[r];
@@ -465,6 +655,56 @@ struct Team {
     return false;
   }
 
+  // candidate q of articulation geom g against the object box (oracle geom_object): sphere/capsule
+  // -> one closest-point candidate; box -> its 8 vertices vs the object, then the object's 8 vertices
+  // vs the geom (normal flipped).  Normal points from the object (B) to the geom (A).
+  __device__ bool obj_candidate(int g, int q, V3* pt, V3* nrm, float* dist) const {
+    const V3 hb = ld3(m->obj_size);
+    V3 c;
+    M3 Rg;
+    geom_world(g, &c, &Rg);
+    const int ty = mt->gtype[g];
+    const float* gs = mt->gf[g] + 12;
+    if (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) {
+      const float r = gs[0], hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
+      const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
+      const V3 al = mulT(oR, (c - ax) - op), bl = mulT(oR, (c + ax) - op), u = bl - al;
+      const float t = seg_box_t(al, u, hb);
+      const V3 P = al + u * t;
+      V3 nb, cb;
+      const float d = point_box(P, hb, &nb, &cb) - r;
+      *pt = mul(oR, ((P - nb * r) + cb) * 0.5f) + op;
+      *nrm = mul(oR, nb);
+      *dist = d;
+      return true;
+    }
+    const V3 hg = v3(gs[0], gs[1], gs[2]);
+    const int v = q & 7;
+    if (q < 8) {
+      const V3 l = v3((v & 1 ? 1.f : -1.f) * hg.x, (v & 2 ? 1.f : -1.f) * hg.y, (v & 4 ? 1.f : -1.f) * hg.z);
+      const V3 pl = mulT(oR, (c + mul(Rg, l)) - op);
+      V3 nb, cb;
+      *dist = point_box(pl, hb, &nb, &cb);
+      *pt = mul(oR, (pl + cb) * 0.5f) + op;
+      *nrm = mul(oR, nb);
+    } else {
+      const V3 l = v3((v & 1 ? 1.f : -1.f) * hb.x, (v & 2 ? 1.f : -1.f) * hb.y, (v & 4 ? 1.f : -1.f) * hb.z);
+      const V3 pl = mulT(Rg, (mul(oR, l) + op) - c);
+      V3 nb, cb;
+      *dist = point_box(pl, hg, &nb, &cb);
+      *pt = mul(Rg, (pl + cb) * 0.5f) + c;
+      *nrm = mul(Rg, nb) * -1.0f;
+    }
+    return true;
+  }
+
+  __device__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
+    s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
+    s->cn[slot][0] = n.x; s->cn[slot][1] = n.y; s->cn[slot][2] = n.z;
+    s->cd[slot] = d;
+    s->cA[slot] = A; s->cgA[slot] = gA; s->cB[slot] = B; s->cgB[slot] = gB;
+  }
+
   __device__ void collide() {
     const int cap = p->max_contacts < MC ? p->max_contacts : MC;
     const float off = p->contact_offset;
@@ -477,7 +717,7 @@ struct Team {
       V3 c = v3(0, 0, 0);
       M3 Rg;
       int ty = -1;
-      if (g < G) {
+      if (g < G && (mt->gfil[g] & MG_COLLIDE_GROUND)) {
         geom_world(g, &c, &Rg);
         ty = mt->gtype[g];
       }
@@ -512,16 +752,27 @@ struct Team {
             cnt++;
           } else {
             const int slot = slot0 + k;
-            if (slot < cap) {
-              s->cp[slot][0] = e.x; s->cp[slot][1] = e.y; s->cp[slot][2] = e.z - r;
-              s->cn[slot][0] = 0.0f; s->cn[slot][1] = 0.0f; s->cn[slot][2] = 1.0f;
-              s->cd[slot] = d;
-              s->cA[slot] = mt->gnode[g]; s->cgA[slot] = g; s->cB[slot] = -1; s->cgB[slot] = -1;
-            }
+            if (slot < cap) put_contact(slot, v3(e.x, e.y, e.z - r), v3(0, 0, 1), d, mt->gnode[g], g, -1, -1);
             k++;
           }
         }
       }
+    }
+    if (OBJ && m->obj_type == MG_GT_BOX) {  // the object's corners on the ground: lane per corner
+      int cnt = 0;
+      V3 e = v3(0, 0, 0);
+      if (tl < 8) {
+        const V3 hb = ld3(m->obj_size);
+        e = mul(oR, v3((tl & 1 ? 1.f : -1.f) * hb.x, (tl & 2 ? 1.f : -1.f) * hb.y, (tl & 4 ? 1.f : -1.f) * hb.z)) + op;
+        cnt = e.z < off ? 1 : 0;
+      }
+      const int incl = team_incl_scan<T>(cnt);
+      const int tot = __shfl(incl, tb + T - 1);
+      if (cnt) {
+        const int slot = base + incl - 1;
+        if (slot < cap) put_contact(slot, e, v3(0, 0, 1), e.z, OBJ_NODE, -2, -1, -1);
+      }
+      base += tot;
     }
     // self-collision pairs: lane per pair, pair order preserved
     const int P = mt->np;
@@ -558,14 +809,41 @@ struct Team {
       const int tot = __shfl(incl, tb + T - 1);
       if (cnt) {
         const int slot = base + incl - 1;
-        if (slot < cap) {
-          s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
-          s->cn[slot][0] = nrm.x; s->cn[slot][1] = nrm.y; s->cn[slot][2] = nrm.z;
-          s->cd[slot] = d;
-          s->cA[slot] = mt->gnode[ga]; s->cgA[slot] = ga; s->cB[slot] = mt->gnode[gb]; s->cgB[slot] = gb;
-        }
+        if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[ga], ga, mt->gnode[gb], gb);
       }
       base += tot;
+    }
+    if (OBJ && m->obj_type == MG_GT_BOX) {  // articulation geoms vs the object: lane per geom, geom order
+      for (int g0 = 0; g0 < G; g0 += T) {
+        const int g = g0 + tl;
+        int nc = 0;
+        if (g < G && (mt->gfil[g] & MG_COLLIDE_OBJECT)) {
+          const int ty = mt->gtype[g];
+          nc = (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) ? 1 : (ty == MG_GT_BOX ? 16 : 0);
+        }
+        int cnt = 0;
+        for (int pass = 0; pass < 2; pass++) {
+          int k = 0, slot0 = 0;
+          if (pass == 1) {
+            const int incl = team_incl_scan<T>(cnt);
+            slot0 = base + incl - cnt;
+            base += __shfl(incl, tb + T - 1);
+          }
+          for (int q = 0; q < nc; q++) {
+            V3 pt, nrm;
+            float d;
+            obj_candidate(g, q, &pt, &nrm, &d);
+            if (!(d < off)) continue;
+            if (pass == 0) {
+              cnt++;
+            } else {
+              const int slot = slot0 + k;
+              if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
+              k++;
+            }
+          }
+        }
+      }
     }
     if (tl == 0) s->ncon = base < cap ? base : cap;
     __syncthreads();
@@ -624,6 +902,12 @@ struct Team {
         s->rref[row] = c;
         s->rA[row] = s->cA[c];
         s->rB[row] = s->cB[c];
+        if (OBJ) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
+          const float so = (s->cA[c] == OBJ_NODE ? 1.0f : 0.0f) - (s->cB[c] == OBJ_NODE ? 1.0f : 0.0f);
+          const V3 wo = cross(pt - op, dirs[r]) * so, d = dirs[r] * so;
+          s->rwo[row][0] = wo.x; s->rwo[row][1] = wo.y; s->rwo[row][2] = wo.z;
+          s->rwo[row][3] = d.x; s->rwo[row][4] = d.y; s->rwo[row][5] = d.z;
+        }
       }
     }
     // joint-limit rows in DOF order (lower, then upper)
@@ -659,7 +943,9 @@ struct Team {
   // ---------------------------------------------------------------- one substep
   __device__ void substep() {
     fk();
+    if (OBJ) tendons();
     aba();
+    obj_free();
     collide();
     build_rows();
     const int nrows = s->nrows;
@@ -682,7 +968,8 @@ struct Team {
           fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
         }
       }
-      const float y = test_solve(A, B, fw, jn, sg);
+      float y = test_solve(A, B, fw, jn, sg);
+      if (OBJ && objl) y = (active && kind < 2) ? obj_response(r) : 0.0f;
       Ycol[r] = active ? y : 0.0f;
       const float Wr = team_sum<T>(active ? jac_entry(r) * y : 0.0f, tb);
       if (tl == 0 && active) {
@@ -750,6 +1037,27 @@ struct Team {
       if (tl == 5) nu = vn.z;
     }
     if (node > 0) qj += h * nu;
+    if (OBJ) {  // free object: pose replicated on every lane (exponential map, like the root)
+      const V3 om = v3(__shfl(nu, tb + ob0), __shfl(nu, tb + ob0 + 1), __shfl(nu, tb + ob0 + 2));
+      const V3 vc = v3(__shfl(nu, tb + ob0 + 3), __shfl(nu, tb + ob0 + 4), __shfl(nu, tb + ob0 + 5));
+      const float wn = sqrtf(dot(om, om));
+      float dq[4];
+      if (wn * h > 1e-12f) {
+        const float ha = 0.5f * wn * h, sn = sinf(ha) / wn;
+        dq[0] = om.x * sn; dq[1] = om.y * sn; dq[2] = om.z * sn; dq[3] = cosf(ha);
+      } else {
+        dq[0] = 0.5f * h * om.x; dq[1] = 0.5f * h * om.y; dq[2] = 0.5f * h * om.z; dq[3] = 1.0f;
+      }
+      const float* a = dq;
+      const float* b = oq;
+      float qn[4] = {a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1],
+                     a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0],
+                     a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3],
+                     a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2]};
+      const float l = 1.0f / sqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+      for (int k = 0; k < 4; k++) oq[k] = qn[k] * l;
+      op = op + vc * h;
+    }
   }
 
   // ---------------------------------------------------------------- sensors & DOF forces (last substep)
@@ -767,7 +1075,7 @@ struct Team {
       V3 F = v3(0, 0, 0), Tq = v3(0, 0, 0);
       for (int c = 0; c < s->ncon; c++) {
         float sg = 0.0f;
-        if (mt->gbody[s->cgA[c]] == body) sg = 1.0f;
+        if (s->cgA[c] >= 0 && mt->gbody[s->cgA[c]] == body) sg = 1.0f;
         else if (s->cgB[c] >= 0 && mt->gbody[s->cgB[c]] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
         V3 n = ld3(s->cn[c]), t1, t2;
@@ -781,7 +1089,14 @@ struct Team {
       o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
     }
     if (dforce_out && node > 0) {
-      float t = tau - mt->nf[node][26] * nu - mt->nf[node][27] * qj;
+      const float* nf = mt->nf[node];
+      float t = tau + ttend;
+      if (nf[30] > 0.0f) {
+        const float fe = nf[30] * (tgt - qj) - nf[26] * nu;
+        t += sat ? (fe > 0.0f ? nf[31] : -nf[31]) : fe;
+      } else {
+        t += -nf[26] * nu - nf[27] * qj;
+      }
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
         if (s->rref[r] != node) continue;
         if (s->rkind[r] == 2) t += s->rlam[r] / h;
@@ -792,7 +1107,8 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- state I/O (gym layouts)
-  __device__ void load(const float* root, const float* dof, const float* act_tau) {
+  __device__ void load(const float* root, const float* dof, const float* act_tau, const float* orow = nullptr,
+                       const float* tg = nullptr) {
     // root pose/twist: every lane reads the 13 floats (one cache line pair per actor)
     if (tl == 0) {
       p0 = ld3(root);
@@ -813,6 +1129,16 @@ struct Team {
       qj = dof[2 * (node - 1)];
       nu = dof[2 * (node - 1) + 1];
       tau = act_tau ? act_tau[node - 1] : 0.0f;
+      tgt = tg ? tg[node - 1] : 0.0f;
+    }
+    if (OBJ && orow) {  // object row [p, q, v_com, w]: pose on every lane, twist on the object lanes
+      op = ld3(orow);
+      const float n = sqrtf(orow[3] * orow[3] + orow[4] * orow[4] + orow[5] * orow[5] + orow[6] * orow[6]);
+      for (int k = 0; k < 4; k++) oq[k] = orow[3 + k] / n;
+      if (objl) {
+        const int k = tl - ob0;
+        nu = k < 3 ? orow[10 + k] : orow[7 + k - 3];
+      }
     }
   }
 
@@ -836,6 +1162,36 @@ struct Team {
       s->dof[2 * (node - 1)] = qj;
       s->dof[2 * (node - 1) + 1] = nu;
     }
+    if (OBJ) {
+      const float o0 = __shfl(nu, tb + ob0), o1 = __shfl(nu, tb + ob0 + 1), o2 = __shfl(nu, tb + ob0 + 2);
+      const float o3 = __shfl(nu, tb + ob0 + 3), o4 = __shfl(nu, tb + ob0 + 4), o5 = __shfl(nu, tb + ob0 + 5);
+      if (tl == 0) {
+        s->oroot[0] = op.x; s->oroot[1] = op.y; s->oroot[2] = op.z;
+        for (int k = 0; k < 4; k++) s->oroot[3 + k] = oq[k];
+        s->oroot[7] = o3; s->oroot[8] = o4; s->oroot[9] = o5;
+        s->oroot[10] = o0; s->oroot[11] = o1; s->oroot[12] = o2;
+      }
+    }
+  }
+
+  // gym rigid-body state of articulation body `b` (post-step FK in LDS): body-origin pose, COM linear
+  // velocity, angular velocity (oracle body_states)
+  __device__ void body_state(int b, float* o) const {
+    const int nd = m->body_node[b];
+    M3 Rn;
+    for (int a = 0; a < 3; a++)
+      for (int c2 = 0; c2 < 3; c2++) Rn.m[a][c2] = s->R[nd][3 * a + c2];
+    const M3 Rb = mul(Rn, quat_to_mat(m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]));
+    const V3 xb = ld3(s->x[nd]) + mul(Rn, ld3(m->body_pos[b]));
+    const V3 r = xb + mul(Rb, ld3(m->body_com[b])) - ld3(s->x[0]);
+    const V3 w = ld3(s->V[nd]), vo = ld3(s->V[nd] + 3);
+    const V3 vc = vo + cross(w, r);
+    float q[4];
+    mat_to_quat(Rb, q);
+    o[0] = xb.x; o[1] = xb.y; o[2] = xb.z;
+    o[3] = q[0]; o[4] = q[1]; o[5] = q[2]; o[6] = q[3];
+    o[7] = vc.x; o[8] = vc.y; o[9] = vc.z;
+    o[10] = w.x; o[11] = w.y; o[12] = w.z;
   }
 };
 

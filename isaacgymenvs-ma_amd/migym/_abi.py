@@ -51,6 +51,7 @@ class TaskParams(C.Structure):
                 ("num_fingertips", C.c_int32), ("fingertip_body", C.c_int32 * 8),
                 ("actuated_dof", C.c_int32 * MG_MAX_HAND_DOFS), ("max_consecutive_successes", C.c_int32),
                 ("use_relative_control", C.c_int32), ("ignore_z_rot", C.c_int32), ("obs_type", C.c_int32),
+                ("rb_per_env", C.c_int32), ("num_dofs", C.c_int32),
                 ("dof_speed_scale", C.c_float), ("act_moving_average", C.c_float),
                 ("dist_reward_scale", C.c_float), ("rot_reward_scale", C.c_float), ("rot_eps", C.c_float),
                 ("action_penalty_scale", C.c_float), ("success_tolerance", C.c_float),
@@ -104,6 +105,8 @@ EXPORTS = {
     "mg_compute_reward": (C.c_int, [C.POINTER(TaskParams), C.c_int32] + [C.c_void_p] * 7 + [C.c_void_p]),
     "mg_post_physics": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(StateViews),
                                   C.POINTER(TaskBuffers), C.c_int32, C.c_void_p]),
+    "mg_pre_physics": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(StateViews),
+                                 C.POINTER(TaskBuffers), C.c_int32, C.c_void_p]),
     "mg_env_step": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p]),
 }
 

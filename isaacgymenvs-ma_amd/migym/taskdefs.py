@@ -97,6 +97,8 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
         tp.dof_lower[j], tp.dof_upper[j], tp.initial_dof_pos[j] = n.lower, n.upper, 0.0
     for i, a in enumerate(spec.actuators):
         tp.actuated_dof[i] = spec.dof_index(a["joint"])
+    tp.rb_per_env = len(spec.bodies) + 2
+    tp.num_dofs = spec.num_dofs
     tp.num_fingertips = len(spec.sensors)
     for i, b in enumerate(spec.sensors):
         tp.fingertip_body[i] = b

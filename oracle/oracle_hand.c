@@ -207,7 +207,7 @@ int orc_hand_pre_physics(const mg_model* m, const mg_task_params* tp, const mg_s
 /* ---------------------------------------------------------------- observations (full_state) */
 static void hand_obs_one(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
                          const mg_task_buffers* tb, const float* act, int e, float* o) {
-  const int nd = m->num_dofs, nb = m->num_bodies + 2, nf = tp->num_fingertips;
+  const int nd = m->num_dofs, nb = tp->rb_per_env, nf = tp->num_fingertips;
   const float* dof = v->dof_state + (size_t)2 * nd * e;
   const float* ob = v->root_states + (size_t)39 * e + 13;
   const float* gs = tb->goal_states + (size_t)13 * e;

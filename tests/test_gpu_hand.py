@@ -1,0 +1,254 @@
+"""GPU parity of the ShadowHand path through the C ABI.
+
+  * task layer vs the reference's own physics-free trace (tests/golden/trace_shadowhand.npz):
+    mg_pre_physics (masked goal/env resets, PD targets) and mg_post_physics (full_state obs,
+    compute_hand_reward, the running mean) with the reference's reset draws injected;
+    rtol/atol 1e-4 on floats, exact on ints.
+  * physics step and the fused mg_env_step vs the fp64 oracle from identical states.  Contacts
+    are decided by fp32 vs fp64 distance tests, so an env whose candidate sits within rounding of
+    the contact offset may differ; the bar is per-env agreement on >= 97 % of envs with the
+    tolerances of tests/test_gpu_parity.py (positions 2e-4, velocities 2e-3 + 2e-3 |v|).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import pyoracle as O
+from migym import _abi, configs, model as M, taskdefs
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def lib():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return _abi.lib()
+
+
+def T(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(DEV, dtype).contiguous()
+
+
+def P(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def setup(n=16):
+    cfg = configs.task_config("ShadowHand", n)
+    spec = M.load_builtin("shadow_hand")
+    return spec, taskdefs.sim_params(cfg, 24), taskdefs.task_params("ShadowHand", cfg, spec)
+
+
+class DevHandEnv:
+    """Device mirror of pyoracle.HandHostEnv."""
+
+    def __init__(self, h):
+        self.h = h
+        for k in ("root", "dof", "targets", "prev_targets", "sensors", "dof_force", "rbs", "actions", "actions_out",
+                  "obs", "obs_clamped", "rew", "successes", "cons", "goal_states"):
+            setattr(self, k, T(getattr(h, k)))
+        for k in ("reset", "reset_goal", "progress"):
+            setattr(self, k, T(getattr(h, k), torch.int64))
+        self.timeout = torch.zeros(h.n, dtype=torch.bool, device=DEV)
+        self.scratch = torch.zeros(2, dtype=torch.int64, device=DEV)
+        self.noise = None
+
+    def views(self):
+        v = _abi.StateViews()
+        v.root_states, v.dof_state, v.dof_actuation = P(self.root), P(self.dof), None
+        v.sensors, v.dof_force, v.rigid_body_states = P(self.sensors), P(self.dof_force), P(self.rbs)
+        v.dof_targets = P(self.targets)
+        return v
+
+    def buffers(self, seed=0, step=0):
+        b = _abi.TaskBuffers()
+        b.actions, b.actions_out, b.obs, b.obs_clamped = P(self.actions), P(self.actions_out), P(self.obs), \
+            P(self.obs_clamped)
+        b.rew, b.reset, b.progress, b.timeout = P(self.rew), P(self.reset), P(self.progress), P(self.timeout)
+        b.noise = P(self.noise)
+        b.seed, b.step_counter, b.env_offset = seed, step, 0
+        b.prev_targets, b.goal_states, b.reset_goal = P(self.prev_targets), P(self.goal_states), P(self.reset_goal)
+        b.successes, b.consecutive_successes, b.reduce_scratch = P(self.successes), P(self.cons), P(self.scratch)
+        return b
+
+
+def np_(t):
+    return t.cpu().numpy()
+
+
+def test_hand_task_layer_replays_reference_trace(lib):
+    d = dict(np.load(os.path.join(G, "trace_shadowhand.npz")))
+    spec, sp, tp = setup()
+    tp.max_episode_length = int(d["episode_length"])
+    Tn, N = d["actions"].shape[:2]
+    h = O.HandHostEnv(tp, spec, N)
+    h.root[:] = d["init_root"]
+    h.goal_states[:] = d["init_goal_states"]
+    e = DevHandEnv(h)
+    for t in range(Tn):
+        e.actions.copy_(T(d["actions"][t]))
+        e.noise = T(d["noise"][t])
+        _abi.check(lib.mg_pre_physics(None, C.byref(tp), C.byref(e.views()), C.byref(e.buffers()), N, stream()), lib)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(np_(e.root), d["root_pre"][t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(np_(e.dof), d["dof_pre"][t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(np_(e.targets), d["targets"][t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(np_(e.goal_states), d["goal_states"][t], rtol=1e-5, atol=1e-6)
+        e.root.copy_(T(d["phys_root"][t]))
+        e.dof.copy_(T(d["phys_dof"][t]))
+        e.rbs.copy_(T(d["phys_rbs"][t]))
+        e.sensors.copy_(T(d["phys_sensors"][t]))
+        e.dof_force.copy_(T(d["phys_dof_force"][t]))
+        _abi.check(lib.mg_post_physics(None, C.byref(tp), C.byref(e.views()), C.byref(e.buffers()), N, stream()),
+                   lib)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(np_(e.obs_clamped), d["obs"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(np_(e.rew), d["rew"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_array_equal(np_(e.reset), d["reset"][t])
+        np.testing.assert_array_equal(np_(e.reset_goal), d["reset_goal"][t])
+        np.testing.assert_array_equal(np_(e.progress), d["progress"][t])
+        np.testing.assert_array_equal(np_(e.successes), d["successes"][t])
+        np.testing.assert_allclose(np_(e.cons), d["cons"][t], rtol=1e-6)
+        np.testing.assert_array_equal(np_(e.timeout).astype(np.int64), d["timeouts"][t])
+        assert int(e.scratch.abs().sum()) == 0  # the finishing kernel clears the partial sums
+
+
+def hand_states(spec, tp, n, rng):
+    """Cube on / just above the palm with random orientation and twist, random hand pose and targets."""
+    h = O.HandHostEnv(tp, spec, n)
+    lo = np.array([x.lower for x in spec.nodes[1:]])
+    hi = np.array([x.upper for x in spec.nodes[1:]])
+    h.dof[:, :, 0] = lo + (hi - lo) * rng.uniform(0.0, 0.6, (n, spec.num_dofs))
+    h.dof[:, :, 1] = rng.normal(0, 0.5, (n, spec.num_dofs))
+    h.targets[:] = lo + (hi - lo) * rng.uniform(0, 1, (n, spec.num_dofs))
+    ob = h.root[:, 1]
+    ob[:, 0:3] = np.array(tp.object_start[:3]) + rng.normal(0, 0.01, (n, 3)) - np.array([0, 0, 0.07])
+    q = rng.normal(0, 1, (n, 4))
+    ob[:, 3:7] = q / np.linalg.norm(q, axis=-1, keepdims=True)
+    ob[:, 7:13] = rng.normal(0, 0.2, (n, 6))
+    return h
+
+
+def env_agreement(a, b, atol, rtol):
+    """fraction of envs whose rows agree within atol + rtol |b|"""
+    a = a.reshape(a.shape[0], -1)
+    b = b.reshape(b.shape[0], -1)
+    ok = (np.abs(a - b) <= atol + rtol * np.abs(b)).all(axis=1)
+    return ok.mean()
+
+
+def test_hand_physics_step_matches_oracle(lib):
+    spec, sp, tp = setup()
+    n = 256
+    rng = np.random.default_rng(5)
+    h = hand_states(spec, tp, n, rng)
+    e = DevHandEnv(h)
+    mnp = M.pack_model(spec)
+    h.simulate(mnp, sp, threads=8)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    _abi.check(lib.mg_sim_simulate(sim, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    rg, dg = np_(e.root), np_(e.dof)
+    assert np.isfinite(rg).all() and np.isfinite(dg).all()
+    np.testing.assert_array_equal(rg[:, 0], h.root[:, 0])       # fixed hand root untouched
+    np.testing.assert_array_equal(rg[:, 2], h.root[:, 2])       # goal actor untouched
+    assert env_agreement(rg[:, 1, 0:7], h.root[:, 1, 0:7], 2e-4, 0) >= 0.97
+    assert env_agreement(rg[:, 1, 7:13], h.root[:, 1, 7:13], 2e-3, 2e-3) >= 0.97
+    assert env_agreement(dg[..., 0], h.dof[..., 0], 2e-4, 0) >= 0.97
+    assert env_agreement(dg[..., 1], h.dof[..., 1], 2e-3, 2e-3) >= 0.97
+    assert env_agreement(np_(e.dof_force), h.dof_force, 1e-2, 1e-2) >= 0.97
+    assert env_agreement(np_(e.rbs), h.rbs, 2e-3, 2e-3) >= 0.97
+    scale = max(1.0, np.abs(h.sensors).max())
+    assert env_agreement(np_(e.sensors), h.sensors, 1e-2 * scale, 0) >= 0.97
+    # the states exercise the object contacts
+    ncon = [len(O.contacts(mnp, sp, h.root[i].ravel(), h.dof[i], 64)) for i in range(32)]
+    assert max(ncon) >= 3
+
+
+def test_hand_fused_env_step_matches_oracle(lib):
+    """mg_env_step (the bench path) vs orc_hand_env_step over 3 control steps, device RNG resets."""
+    spec, sp, tp = setup()
+    n = 192
+    h = O.HandHostEnv(tp, spec, n)
+    e = DevHandEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    rng = np.random.default_rng(3)
+    for t in range(3):
+        a = rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32)
+        h.actions[:] = a
+        e.actions.copy_(T(a))
+        h.env_step(mnp, sp, tp, seed=5, step=t, threads=8)
+        _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=5, step=t)), stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    np.testing.assert_array_equal(np_(e.progress), h.progress)
+    assert (np_(e.reset) == h.reset).mean() >= 0.97
+    np.testing.assert_allclose(np_(e.targets), h.targets, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np_(e.prev_targets), h.prev_targets, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(np_(e.goal_states), h.goal_states, rtol=1e-5, atol=1e-6)
+    assert env_agreement(np_(e.obs), h.obs, 2e-2, 2e-2) >= 0.97
+    assert env_agreement(np_(e.rew), h.rew, 5e-2, 5e-2) >= 0.97
+    np.testing.assert_allclose(np_(e.cons), h.cons, atol=2e-2)
+
+
+def test_hand_set_indexed_maps_actor_ids(lib):
+    spec, sp, tp = setup()
+    n = 50
+    h = O.HandHostEnv(tp, spec, n)
+    e = DevHandEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    src = torch.randn((n, 24, 2), device=DEV)
+    tsrc = torch.randn((n, 24), device=DEV)
+    rsrc = torch.randn((n * 3, 13), device=DEV)
+    envs = torch.tensor([1, 7, 30], device=DEV)
+    hand_ids = (3 * envs).to(torch.int32)
+    obj_ids = (3 * envs + 1).to(torch.int32)
+    _abi.check(lib.mg_set_indexed(sim, _abi.MG_SET_DOF_STATE, P(src), P(hand_ids), 3, stream()), lib)
+    _abi.check(lib.mg_set_indexed(sim, _abi.MG_SET_DOF_TARGET, P(tsrc), P(hand_ids), 3, stream()), lib)
+    _abi.check(lib.mg_set_indexed(sim, _abi.MG_SET_ROOT_STATE, P(rsrc), P(obj_ids), 3, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    assert torch.equal(e.dof[envs], src[envs]) and torch.equal(e.targets[envs], tsrc[envs])
+    assert torch.equal(e.root.view(n * 3, 13)[obj_ids.long()], rsrc[obj_ids.long()])
+    mask = torch.ones(n, dtype=torch.bool, device=DEV)
+    mask[envs] = False
+    assert float(e.dof[mask].abs().sum()) == 0.0
+
+
+def test_hand_make_full_size():
+    import migym
+    n = 4096
+    env = migym.make(seed=0, task="ShadowHand", num_envs=n, sim_device=DEV, rl_device=DEV, headless=True)
+    assert env.num_obs == 211 and env.num_actions == 20
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(40):
+        a = torch.rand((n, 20), device=DEV, generator=g) * 2 - 1
+        obs, rew, reset, extras = env.step(a)
+    torch.cuda.synchronize()
+    o = obs["obs"]
+    assert o.shape == (n, 211) and torch.isfinite(o).all() and torch.isfinite(rew).all()
+    assert float(o.abs().max()) <= 5.0
+    assert "consecutive_successes" in extras and torch.isfinite(extras["consecutive_successes"])
+    obj = env.root_state_tensor.view(n, 3, 13)[:, 1]
+    assert torch.isfinite(obj).all() and float(obj[:, 7:13].abs().max()) < 100.0
+    # the cube stays with the hand for most envs (falls reset them; fall distance 0.24)
+    assert float((obj[:, 2] > 0.2).float().mean()) > 0.9
+    env.close()
