@@ -21,7 +21,11 @@ sys.path.insert(0, os.path.join(ROOT, "isaacgymenvs-ma_amd"))
 
 # algorithmic (compulsory) HBM bytes per env-step: every gym/VecTask-visible tensor
 # read and written once per control step; model tables amortised to 0.
-ALGO_BYTES = {"Ant": 673, "Humanoid": 1161, "Cartpole": 89, "MAAnt": 4 * 709}
+ALGO_BYTES = {"Ant": 673, "Humanoid": 1161, "Cartpole": 89, "MAAnt": 4 * 709,
+              # ShadowHand: R actions 80, prev targets 96, dof 192, object+goal 104, bufs 28 = 500;
+              # W targets 192, dof 192, 3 root rows 156, 27 rigid bodies 1404, dof_force 96, sensors 120,
+              # obs 844, scalars 32 = 3036 (full rigid-body tensor materialised)
+              "ShadowHand": 3536}
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md (spec)
 
 
@@ -33,13 +37,17 @@ def cpu_baseline(task, seconds=12.0, n=4096):
     from migym import configs, model as M, taskdefs
     cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
     cfg = configs.task_config(task, n)
-    spec = M.load_builtin(taskdefs.TASK_INFO[task][1])
-    sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[task][5])
+    base = "Ant" if task == "MAAnt" else task
+    spec = M.load_builtin(taskdefs.TASK_INFO[base][1])
+    A = int(cfg["env"].get("numAgents", 1)) if task == "MAAnt" else 1
+    sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[base][5], A)
     tp = taskdefs.task_params(task, cfg, spec)
     mnp = M.pack_model(spec)
-    h = O.HostEnv(tp, spec, n)
+    if task == "ShadowHand":
+        n = min(n, 1024)
+    h = O.HandHostEnv(tp, spec, n) if task == "ShadowHand" else O.HostEnv(tp, spec, n * A)
     rng = np.random.default_rng(0)
-    acts = rng.uniform(-1, 1, (8, n, tp.num_actions)).astype(np.float32)
+    acts = rng.uniform(-1, 1, (8,) + h.actions.shape).astype(np.float32)
     h.actions[:] = acts[0]
     h.env_step(mnp, sp, tp, 0, 0, cores)  # warm-up (first step resets every env)
     steps, t0 = 0, time.perf_counter()
