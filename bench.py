@@ -141,14 +141,16 @@ def main():
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (U(-1,1) actions, device-resident)",
-            "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, 2 substeps, PGS x4",
+            "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, {env.sim_params.substeps} substeps, "
+                                   f"PGS x{env.sim_params.pos_iters}",
                        "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
                        "agents_per_env": env.num_agents, "agent_steps_per_s": value * env.num_agents,
                        "obs_allgather": bool(gather is not None),
                        "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": None,
-                         "kernel": "k_env_step", "kernel_ms": kern_ms,
+                         "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",
+                         "kernel_ms": kern_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES[args.task]},
         }
         if not args.no_cpu_baseline and world == 1:

@@ -200,7 +200,7 @@ typedef struct mg_task_params {
   int32_t max_consecutive_successes;
   int32_t use_relative_control;
   int32_t ignore_z_rot;               /* pen */
-  int32_t obs_type;                   /* 0 = full_state (211) */
+  int32_t obs_type;                   /* 0 full_state (211), 1 full (157), 2 full_no_vel (77), 3 openai (42) */
   int32_t rb_per_env;                 /* rigid-body rows per env (articulation bodies + object + goal) */
   int32_t num_dofs;                   /* hand DOFs (dof_state rows per env) */
   float dof_speed_scale;

@@ -21,6 +21,70 @@ namespace mg {
 
 constexpr int HAND_NOISE = 61;  // [goal-only 4 | reset_idx 53 | reset_target_pose 4]
 
+// observation layouts of observationType (shadow_hand.py:108-113, 473-584): segment lists
+enum HandSeg {
+  HS_DOF_POS, HS_DOF_VEL, HS_DOF_FORCE, HS_OBJ_POSE, HS_OBJ_POS, HS_OBJ_LINVEL, HS_OBJ_ANGVEL, HS_GOAL_POSE,
+  HS_QUAT_DIFF, HS_FT_STATE, HS_FT_POS, HS_FT_FORCE, HS_ACTIONS, HS_END
+};
+// 0 full_state (compute_full_state, 211), 1 full (157), 2 full_no_vel (77), 3 openai (42)
+__constant__ const int8_t kHandLayout[4][12] = {
+    {HS_DOF_POS, HS_DOF_VEL, HS_DOF_FORCE, HS_OBJ_POSE, HS_OBJ_LINVEL, HS_OBJ_ANGVEL, HS_GOAL_POSE, HS_QUAT_DIFF,
+     HS_FT_STATE, HS_FT_FORCE, HS_ACTIONS, HS_END},
+    {HS_DOF_POS, HS_DOF_VEL, HS_OBJ_POSE, HS_OBJ_LINVEL, HS_OBJ_ANGVEL, HS_GOAL_POSE, HS_QUAT_DIFF, HS_FT_STATE,
+     HS_ACTIONS, HS_END, HS_END, HS_END},
+    {HS_DOF_POS, HS_OBJ_POSE, HS_GOAL_POSE, HS_QUAT_DIFF, HS_FT_POS, HS_ACTIONS, HS_END, HS_END, HS_END, HS_END,
+     HS_END, HS_END},
+    {HS_FT_POS, HS_OBJ_POS, HS_QUAT_DIFF, HS_ACTIONS, HS_END, HS_END, HS_END, HS_END, HS_END, HS_END, HS_END, HS_END}};
+
+__device__ __forceinline__ int h_seg_size(int seg, int nd, int nf, int na) {
+  switch (seg) {
+    case HS_DOF_POS: case HS_DOF_VEL: case HS_DOF_FORCE: return nd;
+    case HS_OBJ_POSE: case HS_GOAL_POSE: return 7;
+    case HS_OBJ_POS: case HS_OBJ_LINVEL: case HS_OBJ_ANGVEL: return 3;
+    case HS_QUAT_DIFF: return 4;
+    case HS_FT_STATE: return 13 * nf;
+    case HS_FT_POS: return 3 * nf;
+    case HS_FT_FORCE: return 6 * nf;
+    case HS_ACTIONS: return na;
+    default: return 0;
+  }
+}
+// observation column k -> (segment, index within the segment)
+__device__ __forceinline__ int h_locate(const mg_task_params& tp, int nd, int k, int* idx) {
+  const int8_t* lay = kHandLayout[tp.obs_type & 3];
+  for (int i = 0; i < 12 && lay[i] != HS_END; i++) {
+    const int n = h_seg_size(lay[i], nd, tp.num_fingertips, tp.num_actions);
+    if (k < n) { *idx = k; return lay[i]; }
+    k -= n;
+  }
+  *idx = 0;
+  return HS_END;
+}
+// fingertip body / component of an HS_FT_STATE or HS_FT_POS index
+__device__ __forceinline__ void h_ft_ref(const mg_task_params& tp, int seg, int idx, int* body, int* comp) {
+  const int w = seg == HS_FT_STATE ? 13 : 3;
+  *body = tp.fingertip_body[idx / w];
+  *comp = idx % w;
+}
+// value of a non-fingertip segment entry
+__device__ __forceinline__ float h_obs_value(const mg_task_params& tp, int seg, int i, const float* dof,
+                                             const float* dforce, const float* orow, const float* gs,
+                                             const float* qdiff, const float* sens, const float* act) {
+  switch (seg) {
+    case HS_DOF_POS: return (2.0f * dof[2 * i] - tp.dof_upper[i] - tp.dof_lower[i]) / (tp.dof_upper[i] - tp.dof_lower[i]);
+    case HS_DOF_VEL: return tp.vel_obs_scale * dof[2 * i + 1];
+    case HS_DOF_FORCE: return tp.force_torque_obs_scale * dforce[i];
+    case HS_OBJ_POSE: case HS_OBJ_POS: return orow[i];
+    case HS_OBJ_LINVEL: return orow[7 + i];
+    case HS_OBJ_ANGVEL: return tp.vel_obs_scale * orow[10 + i];
+    case HS_GOAL_POSE: return gs[i];
+    case HS_QUAT_DIFF: return qdiff[i];
+    case HS_FT_FORCE: return tp.force_torque_obs_scale * sens[i];
+    case HS_ACTIONS: return act[i];
+    default: return 0.0f;
+  }
+}
+
 __device__ __forceinline__ void h_quat_from_angle_axis(float angle, int k, float* q) {
   const float theta = angle / 2.0f;
   const float sn = sinf(theta), c = cosf(theta);

@@ -381,30 +381,19 @@ __global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state
   }
 }
 
-// full_state observation value k of one env from its state rows (compute_full_state order)
+// observation value k of one env from its state rows (observationType layout, hand_task.hpp)
 __device__ __forceinline__ float hand_obs_value(const mg_task_params& tp, int k, int nd, const float* dof,
                                                 const float* dforce, const float* orow, const float* gs,
                                                 const float* qdiff, const float* rbs, const float* sens,
                                                 const float* act) {
-  if (k < nd) return (2.0f * dof[2 * k] - tp.dof_upper[k] - tp.dof_lower[k]) / (tp.dof_upper[k] - tp.dof_lower[k]);
-  k -= nd;
-  if (k < nd) return tp.vel_obs_scale * dof[2 * k + 1];
-  k -= nd;
-  if (k < nd) return tp.force_torque_obs_scale * dforce[k];
-  k -= nd;
-  if (k < 10) return orow[k];
-  if (k < 13) return tp.vel_obs_scale * orow[k];
-  k -= 13;
-  if (k < 7) return gs[k];
-  k -= 7;
-  if (k < 4) return qdiff[k];
-  k -= 4;
-  const int nf = tp.num_fingertips;
-  if (k < 13 * nf) return rbs[(size_t)13 * tp.fingertip_body[k / 13] + k % 13];
-  k -= 13 * nf;
-  if (k < 6 * nf) return tp.force_torque_obs_scale * sens[k];
-  k -= 6 * nf;
-  return act[k];
+  int i;
+  const int seg = mg::h_locate(tp, nd, k, &i);
+  if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
+    int b, c;
+    mg::h_ft_ref(tp, seg, i, &b, &c);
+    return rbs[(size_t)13 * b + c];
+  }
+  return mg::h_obs_value(tp, seg, i, dof, dforce, orow, gs, qdiff, sens, act);
 }
 
 // post_physics_step of one env on one lane (physics-free path): progress, full_state obs, reward,
@@ -550,18 +539,20 @@ __global__ __launch_bounds__(kBlock) void k_hand_step(const mg_model* __restrict
     float qdiff[4];
     const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
     mg::t_quat_mul(L.oroot + 3, gc, qdiff);
-    const int nf = tp.num_fingertips;
-    const int ft0 = 3 * nd + 24;  // first fingertip value
     for (int k = t.tl; k < no; k += T) {
+      int i;
+      const int seg = mg::h_locate(tp, nd, k, &i);
       float x;
-      if (k >= no - na) {  // self.actions (clamped)
-        x = mg::clampf(tb.actions[(size_t)na * ec + (k - (no - na))], tp.clip_actions);
-      } else if (k >= ft0 && k < ft0 + 13 * nf) {  // fingertip body state from the post-step FK
+      if (seg == mg::HS_ACTIONS) {  // self.actions (clamped)
+        x = mg::clampf(tb.actions[(size_t)na * ec + i], tp.clip_actions);
+      } else if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {  // fingertip state from the post-step FK
+        int b, c;
+        mg::h_ft_ref(tp, seg, i, &b, &c);
         float b13[13];
-        t.body_state(tp.fingertip_body[(k - ft0) / 13], b13);
-        x = b13[(k - ft0) % 13];
+        t.body_state(b, b13);
+        x = b13[c];
       } else {
-        x = hand_obs_value(tp, k, nd, L.dof, L.dforce, L.oroot, gs, qdiff, nullptr, L.sens, nullptr);
+        x = mg::h_obs_value(tp, seg, i, L.dof, L.dforce, L.oroot, gs, qdiff, L.sens, nullptr);
       }
       L.obs[k] = x;
     }

@@ -19,7 +19,8 @@ TASK_INFO = {
     "Humanoid": (_abi.MG_TASK_HUMANOID, "humanoid", 108, 21, 1.34, 32),
     "ShadowHand": (_abi.MG_TASK_SHADOW_HAND, "shadow_hand", 211, 20, 0.5, 24),
 }
-HAND_OBS = {"full_state": (0, 211)}    # shadow_hand.py:108-113 (the other obs types: DESIGN.md, out of scope)
+# observationType -> (layout id, obs size) (shadow_hand.py:108-113; layouts in csrc/hand_task.hpp)
+HAND_OBS = {"full_state": (0, 211), "full": (1, 157), "full_no_vel": (2, 77), "openai": (3, 42)}
 TASK_INFO["MAAnt"] = TASK_INFO["Ant"]   # per-agent physics/obs of the multi-agent Ant are the Ant's
 
 # build-defined solver constants
@@ -76,7 +77,7 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     env = cfg["env"]
     obs_type = env.get("observationType", "full_state")
     if obs_type not in HAND_OBS:
-        raise ValueError(f"observationType {obs_type!r} not supported (full_state only)")
+        raise ValueError(f"Unknown type of observations! observationType should be one of: {sorted(HAND_OBS)}")
     if env.get("objectType", "block") != "block":
         raise ValueError("objectType must be 'block' (egg/pen meshes are out of scope)")
     if env.get("asymmetric_observations", False):

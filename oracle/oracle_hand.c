@@ -14,7 +14,8 @@
  *   scale / tensor_clamp / unscale                      utils/torch_jit_utils.py:229-240
  *   randomize_rotation                                  tasks/shadow_hand.py:803-806
  *   compute_hand_reward (incl. the global running mean) tasks/shadow_hand.py:746-800
- *   compute_full_state (full_state, 211 values)         tasks/shadow_hand.py:528-584
+ *   compute_full_state / compute_full_observations /
+ *   compute_fingertip_observations (observationType)    tasks/shadow_hand.py:473-584
  *   reset_target_pose / reset_idx                       tasks/shadow_hand.py:586-668
  *   pre_physics_step (goal/env resets, PD targets)      tasks/shadow_hand.py:670-698
  *   post_physics_step + VecTask.step tail               tasks/shadow_hand.py:710-716,
@@ -204,31 +205,51 @@ int orc_hand_pre_physics(const mg_model* m, const mg_task_params* tp, const mg_s
   return 0;
 }
 
-/* ---------------------------------------------------------------- observations (full_state) */
+/* ---------------------------------------------------------------- observations */
+/* observationType layouts (shadow_hand.py:473-584): compute_full_state (211),
+ * compute_full_observations (157; no_vel: 77), compute_fingertip_observations(no_vel) (42) */
+enum { DOFP, DOFV, DOFF, OPOSE, OPOS, OLIN, OANG, GPOSE, QDIFF, FTS, FTP, FTF, ACTS, END };
+static const int LAYOUT[4][12] = {
+    {DOFP, DOFV, DOFF, OPOSE, OLIN, OANG, GPOSE, QDIFF, FTS, FTF, ACTS, END},
+    {DOFP, DOFV, OPOSE, OLIN, OANG, GPOSE, QDIFF, FTS, ACTS, END, END, END},
+    {DOFP, OPOSE, GPOSE, QDIFF, FTP, ACTS, END, END, END, END, END, END},
+    {FTP, OPOS, QDIFF, ACTS, END, END, END, END, END, END, END, END}};
+
 static void hand_obs_one(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
                          const mg_task_buffers* tb, const float* act, int e, float* o) {
   const int nd = m->num_dofs, nb = tp->rb_per_env, nf = tp->num_fingertips;
   const float* dof = v->dof_state + (size_t)2 * nd * e;
   const float* ob = v->root_states + (size_t)39 * e + 13;
   const float* gs = tb->goal_states + (size_t)13 * e;
+  const float* rbs = v->rigid_body_states + (size_t)13 * nb * e;
+  float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]}, qdiff[4];
+  h_quat_mul(ob + 3, gc, qdiff);
   int k = 0;
-  for (int j = 0; j < nd; j++) o[k++] = (2.0f * dof[2 * j] - tp->dof_upper[j] - tp->dof_lower[j]) /
-                                        (tp->dof_upper[j] - tp->dof_lower[j]);
-  for (int j = 0; j < nd; j++) o[k++] = tp->vel_obs_scale * dof[2 * j + 1];
-  for (int j = 0; j < nd; j++) o[k++] = tp->force_torque_obs_scale * v->dof_force[(size_t)nd * e + j];
-  for (int c = 0; c < 7; c++) o[k++] = ob[c];
-  for (int c = 7; c < 10; c++) o[k++] = ob[c];
-  for (int c = 10; c < 13; c++) o[k++] = tp->vel_obs_scale * ob[c];
-  for (int c = 0; c < 7; c++) o[k++] = gs[c];
-  float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
-  h_quat_mul(ob + 3, gc, o + k);
-  k += 4;
-  for (int f = 0; f < nf; f++) {
-    const float* rb = v->rigid_body_states + ((size_t)nb * e + tp->fingertip_body[f]) * 13;
-    for (int c = 0; c < 13; c++) o[k++] = rb[c];
+  for (int s = 0; s < 12 && LAYOUT[tp->obs_type & 3][s] != END; s++) {
+    switch (LAYOUT[tp->obs_type & 3][s]) {
+      case DOFP:
+        for (int j = 0; j < nd; j++)
+          o[k++] = (2.0f * dof[2 * j] - tp->dof_upper[j] - tp->dof_lower[j]) / (tp->dof_upper[j] - tp->dof_lower[j]);
+        break;
+      case DOFV: for (int j = 0; j < nd; j++) o[k++] = tp->vel_obs_scale * dof[2 * j + 1]; break;
+      case DOFF: for (int j = 0; j < nd; j++) o[k++] = tp->force_torque_obs_scale * v->dof_force[(size_t)nd * e + j]; break;
+      case OPOSE: for (int c = 0; c < 7; c++) o[k++] = ob[c]; break;
+      case OPOS: for (int c = 0; c < 3; c++) o[k++] = ob[c]; break;
+      case OLIN: for (int c = 7; c < 10; c++) o[k++] = ob[c]; break;
+      case OANG: for (int c = 10; c < 13; c++) o[k++] = tp->vel_obs_scale * ob[c]; break;
+      case GPOSE: for (int c = 0; c < 7; c++) o[k++] = gs[c]; break;
+      case QDIFF: for (int c = 0; c < 4; c++) o[k++] = qdiff[c]; break;
+      case FTS:
+      case FTP: {
+        const int w = LAYOUT[tp->obs_type & 3][s] == FTS ? 13 : 3;
+        for (int f = 0; f < nf; f++)
+          for (int c = 0; c < w; c++) o[k++] = rbs[(size_t)13 * tp->fingertip_body[f] + c];
+        break;
+      }
+      case FTF: for (int c = 0; c < 6 * nf; c++) o[k++] = tp->force_torque_obs_scale * v->sensors[(size_t)6 * nf * e + c]; break;
+      case ACTS: for (int i = 0; i < tp->num_actions; i++) o[k++] = act[i]; break;
+    }
   }
-  for (int c = 0; c < 6 * nf; c++) o[k++] = tp->force_torque_obs_scale * v->sensors[(size_t)6 * nf * e + c];
-  for (int i = 0; i < tp->num_actions; i++) o[k++] = act[i];
 }
 
 int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,

@@ -467,7 +467,7 @@ class FakeHandGym(FakeGym):
         self.record = rec
 
 
-def run_shadowhand(N=32, T=8, ep_len=4):
+def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state"):
     import importlib
     sys.path.insert(0, os.path.join(HERE, "..", "..", "isaacgymenvs-ma_amd"))
     from migym import model as M
@@ -483,6 +483,7 @@ def run_shadowhand(N=32, T=8, ep_len=4):
     rec = RandRecorder()
     mod.torch_rand_float = rec
     cfg = load_task_cfg("ShadowHand", N, ep_len)
+    cfg["env"]["observationType"] = obs_type
     torch.manual_seed(0)
     env = mod.ShadowHand(cfg, "cpu", "cpu", -1, True, False, False)
     fake.env = env
@@ -531,6 +532,7 @@ def run_shadowhand(N=32, T=8, ep_len=4):
         out["timeouts"].append(extras["time_outs"].clone().long())
     res = {k: (torch.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
     res["episode_length"] = torch.tensor(ep_len)
+    res["obs_type"] = np.array(obs_type)
     return res
 
 
@@ -546,7 +548,7 @@ def main():
     # one task per process: vec_task keeps a process-global sim (vec_task.py:55-64)
     if which == "all":
         import subprocess
-        for t in ("ant", "humanoid", "cartpole", "shadowhand"):
+        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs"):
             subprocess.check_call([sys.executable, __file__, t])
         return
     if which == "ant":
@@ -557,6 +559,9 @@ def main():
         save("trace_cartpole.npz", run_cartpole())
     elif which == "shadowhand":
         save("trace_shadowhand.npz", run_shadowhand())
+    elif which == "shadowhand_obs":  # the other observationType layouts, smaller traces
+        for ot in ("full", "full_no_vel", "openai"):
+            save(f"trace_shadowhand_{ot}.npz", run_shadowhand(N=16, T=4, ep_len=3, obs_type=ot))
 
 
 if __name__ == "__main__":

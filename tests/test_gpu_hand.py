@@ -85,9 +85,14 @@ def np_(t):
     return t.cpu().numpy()
 
 
-def test_hand_task_layer_replays_reference_trace(lib):
-    d = dict(np.load(os.path.join(G, "trace_shadowhand.npz")))
-    spec, sp, tp = setup()
+@pytest.mark.parametrize("trace", ["trace_shadowhand.npz", "trace_shadowhand_full.npz",
+                                   "trace_shadowhand_full_no_vel.npz", "trace_shadowhand_openai.npz"])
+def test_hand_task_layer_replays_reference_trace(lib, trace):
+    d = dict(np.load(os.path.join(G, trace)))
+    cfg = configs.task_config("ShadowHand", 16)
+    cfg["env"]["observationType"] = str(d["obs_type"])
+    spec = M.load_builtin("shadow_hand")
+    tp = taskdefs.task_params("ShadowHand", cfg, spec)
     tp.max_episode_length = int(d["episode_length"])
     Tn, N = d["actions"].shape[:2]
     h = O.HandHostEnv(tp, spec, N)
@@ -231,6 +236,32 @@ def test_hand_set_indexed_maps_actor_ids(lib):
     mask = torch.ones(n, dtype=torch.bool, device=DEV)
     mask[envs] = False
     assert float(e.dof[mask].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("obs_type", ["full", "openai"])
+def test_hand_fused_obs_types_match_oracle(lib, obs_type):
+    cfg = configs.task_config("ShadowHand", 16)
+    cfg["env"]["observationType"] = obs_type
+    spec = M.load_builtin("shadow_hand")
+    sp, tp = taskdefs.sim_params(cfg, 24), taskdefs.task_params("ShadowHand", cfg, spec)
+    n = 64
+    h = O.HandHostEnv(tp, spec, n)
+    e = DevHandEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    rng = np.random.default_rng(8)
+    for t in range(2):
+        a = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+        h.actions[:] = a
+        e.actions.copy_(T(a))
+        h.env_step(mnp, sp, tp, seed=2, step=t, threads=8)
+        _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=2, step=t)), stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    assert np_(e.obs).shape[1] == taskdefs.HAND_OBS[obs_type][1]
+    assert env_agreement(np_(e.obs), h.obs, 2e-2, 2e-2) >= 0.97
 
 
 def test_hand_make_full_size():

@@ -157,11 +157,17 @@ def test_shadowhand_reward_and_rotation_match_reference():
     np.testing.assert_allclose(cons, d["cons_out"], rtol=1e-6)
 
 
-def test_shadowhand_trace_matches_reference():
-    """Whole physics-free ShadowHand VecTask.step (pre_physics resets + PD targets, full_state obs,
-    reward, running mean, timeouts) replayed with the reference's own reset draws injected."""
-    d = load("trace_shadowhand.npz")
-    tp, spec = tparams("ShadowHand")
+@pytest.mark.parametrize("trace", ["trace_shadowhand.npz", "trace_shadowhand_full.npz",
+                                   "trace_shadowhand_full_no_vel.npz", "trace_shadowhand_openai.npz"])
+def test_shadowhand_trace_matches_reference(trace):
+    """Whole physics-free ShadowHand VecTask.step (pre_physics resets + PD targets, observations of
+    every observationType, reward, running mean, timeouts) replayed with the reference's own reset
+    draws injected."""
+    d = load(trace)
+    cfg = configs.task_config("ShadowHand", 16)
+    cfg["env"]["observationType"] = str(d["obs_type"])
+    spec = M.load_builtin("shadow_hand")
+    tp = taskdefs.task_params("ShadowHand", cfg, spec)
     tp.max_episode_length = int(d["episode_length"])
     mnp = M.pack_model(spec)
     T, N = d["actions"].shape[:2]
