@@ -260,6 +260,8 @@ size_t mg_task_params_sizeof(void);
 size_t mg_task_buffers_sizeof(void);
 size_t mg_sim_params_sizeof(void);
 size_t mg_state_views_sizeof(void);
+/* profiling aid (phase-timing build only, see isaacgymenvs-ma_amd/build.py --timing) */
+int mg_debug_phase_cycles(uint64_t* out16, int32_t reset);
 
 typedef struct mg_sim mg_sim;
 

@@ -27,6 +27,15 @@ constexpr int kBlock = 64;
 inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
 }  // namespace
 
+#ifdef MG_PHASE_TIMING
+__device__ unsigned long long g_phase[16];  // summed over waves (team leader of lane 0)
+#define MG_PHASE_FLUSH(t)                                                          \
+  if (threadIdx.x == 0)                                                            \
+    for (int i_ = 0; i_ < 16; i_++) atomicAdd(&g_phase[i_], (t).ph[i_]);
+#else
+#define MG_PHASE_FLUSH(t)
+#endif
+
 struct mg_sim {
   mg_model host_model;
   mg_model* d_model;
@@ -41,7 +50,7 @@ struct mg_sim {
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
 template <int T, int MN, int MC, int MG, int MP, bool OBJ>
-__global__ __launch_bounds__(kBlock) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_state_views v, int n) {
   constexpr int E = kBlock / T;
   constexpr int ROWS = OBJ ? 3 : 1;
@@ -191,8 +200,10 @@ __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_s
 // state, the team writes it back to HBM.  Multi-agent: the agents of an env are consecutive
 // teams of one wave, so the AND-filter is a ballot over team leaders and the others-block a
 // shuffle from the other agents' leaders.
+// amdgpu_waves_per_eu(2): the register budget that lets two waves share a SIMD (the team kernels
+// are latency-bound; occupancy is the lever — DESIGN.md §3)
 template <int T, int MN, int MC, int MG, int MP>
-__global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
   constexpr int E = kBlock / T;
   __shared__ mg::TeamLDS<T, MN, MC> lds[E];
@@ -209,6 +220,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict_
   t.init(&L, &tile, m, &p);
   __syncthreads();
   const int64_t reset_in = tb.reset[ac];
+  t.ph_start();
   // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
   t.load(v.root_states + (size_t)13 * ac, v.dof_state + (size_t)2 * nd * ac, nullptr);
   if (t.node > 0) {
@@ -223,10 +235,12 @@ __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict_
     t.tau = tau;
     if (valid && v.dof_actuation) const_cast<float*>(v.dof_actuation)[(size_t)nd * a + d] = tau;
   }
+  t.ph_mark(14);
   for (int st = 0; st < p.substeps; st++) t.substep();
   t.outputs(L.sens, L.dforce);
   t.stage_state();
   __syncthreads();
+  t.ph_mark(8);
 
   // ---------------- post_physics_step (ant.py:287-297) on the staged state
   const int A = tp.num_agents > 1 ? tp.num_agents : 1;
@@ -304,6 +318,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(const mg_model* __restrict_
     if (v.dof_force)
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.dforce[q];
   }
+  t.ph_mark(9);
+  MG_PHASE_FLUSH(t)
 }
 
 // pre_physics_step of the locomotion tasks: effort = clamp(a) * gear * power_scale
@@ -457,7 +473,7 @@ __global__ void k_hand_finalize(mg_task_params tp, mg_task_buffers tb) {
 // PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
 // the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
 template <int T, int MN, int MC, int MG, int MP>
-__global__ __launch_bounds__(kBlock) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                       mg_task_params tp, mg_state_views v, mg_task_buffers tb,
                                                       int n) {
   constexpr int E = kBlock / T;
@@ -474,6 +490,7 @@ __global__ __launch_bounds__(kBlock) void k_hand_step(const mg_model* __restrict
   mg::TeamLDS<T, MN, MC, true>& L = lds[team];
   mg::Team<T, MN, MC, MG, MP, true> t;
   t.init(&L, &tile, m, &p);
+  t.ph_start();
   const uint64_t gid = (uint64_t)(tb.env_offset + ec);
   const bool env_reset = tb.reset[ec] != 0, goal_reset = tb.reset_goal[ec] != 0;
   float* root = v.root_states + (size_t)39 * ec;
@@ -527,10 +544,12 @@ __global__ __launch_bounds__(kBlock) void k_hand_step(const mg_model* __restrict
     t.tgt = cur;
   }
   // ---- gym.simulate
+  t.ph_mark(14);
   for (int st = 0; st < p.substeps; st++) t.substep();
   t.outputs(L.sens, L.dforce);
   t.stage_state();
   __syncthreads();
+  t.ph_mark(8);
   // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
   const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
   float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
@@ -613,6 +632,8 @@ __global__ __launch_bounds__(kBlock) void k_hand_step(const mg_model* __restrict
     for (int b = t.tl; b < nb; b += T) t.body_state(b, rbs + 13 * b);
     for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
   }
+  t.ph_mark(9);
+  MG_PHASE_FLUSH(t)
 }
 
 __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
@@ -694,6 +715,28 @@ size_t mg_task_params_sizeof(void) { return sizeof(mg_task_params); }
 size_t mg_task_buffers_sizeof(void) { return sizeof(mg_task_buffers); }
 size_t mg_sim_params_sizeof(void) { return sizeof(mg_sim_params); }
 size_t mg_state_views_sizeof(void) { return sizeof(mg_state_views); }
+
+// Profiling aid: per-phase shader cycles summed over all waves since the last reset (phase-timing
+// build only; returns MG_EINVAL otherwise).  Phases: 0 FK, 1 ABA (+tendons), 2 collide (+object
+// free step), 3 rows, 4 M~^-1, 5 row responses, 6 PGS, 7 integrate, 8 outputs, 9 task layer +
+// write-back, 13 constraint rows (count), 14 load + pre-physics, 15 substep entry.
+int mg_debug_phase_cycles(uint64_t* out16, int32_t reset) {
+#ifdef MG_PHASE_TIMING
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
+  if (out16 && hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase), 16 * sizeof(uint64_t)) != hipSuccess)
+    return fail(MG_EDEVICE, "mg_debug_phase_cycles: copy failed");
+  if (reset) {
+    uint64_t z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess)
+      return fail(MG_EDEVICE, "mg_debug_phase_cycles: reset failed");
+  }
+  return MG_OK;
+#else
+  (void)out16;
+  (void)reset;
+  return fail(MG_EINVAL, "mg_debug_phase_cycles: library built without MG_PHASE_TIMING");
+#endif
+}
 
 int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
                   mg_sim** out) {

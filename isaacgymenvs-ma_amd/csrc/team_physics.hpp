@@ -32,6 +32,8 @@
 #include "../../include/migym.h"
 #include "device_math.hpp"
 
+#include <type_traits>
+
 namespace mg {
 
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
@@ -105,25 +107,34 @@ template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
   static constexpr int MRO = OBJ ? MR : 1;
+  using mask_t = typename std::conditional<(T <= 32), unsigned int, unsigned long long>::type;
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
   float S[MN][6];
   float U[MN][6];
   float Dinv[MN];
-  float slot[MN][27];
   float acc[MN][6];
   float ut[MN];
   unsigned long long anc[MN];
   float L0[21];
   float proot[6];
-  int ncon, nrows;
-  float cp[MC][3], cn[MC][3], cd[MC];
-  int cA[MC], cB[MC], cgA[MC], cgB[MC];
-  float rw[MR][6];
-  float rb[MR], rW[MR], rlam[MR];
   float Iinv[36];
-  int rkind[MR], rref[MR], rA[MR], rB[MR];
+  int ncon, nrows;
+  // contacts: point, frame (normal + tangent basis), gap, sides (nodes / geoms)
+  float cp[MC][3], cn[MC][3], ct1[MC][3], ct2[MC][3], cd[MC];
+  int cA[MC], cB[MC], cgA[MC], cgB[MC];
+  // joint-limit rows (after the 3 rows per contact): kind | node << 4
+  int lmeta[2 * (MN - 1)];
+  // The ABA's child slots are dead once the tree pass is done; the constraint rows reuse them:
+  // per-lane Jacobian codes (two bit masks: 0 none, 1 +Sl.w, 2 -Sl.w, 3 unit), target, 1/W, impulse.
+  union {
+    float slot[MN][27];
+    struct {
+      mask_t sg[MR][2];
+      float b[MR], invW[MR], lam[MR];
+    } rows;
+  } u;
   // task-layer staging (root / dof state of the actor after the physics)
   float root[13];
   float dof[2 * MN];
@@ -287,6 +298,26 @@ struct Team {
   Sym6 IA;
   float Dinv, u;
   float h;
+  float Sl[6];         // Jacobian axis of the lane: S (joint lanes) or e_tl (root-twist lanes)
+  int ncr;             // contacts of this substep (rows 0 .. 3 ncr - 1 are contact rows)
+  V3 org;              // team origin o (root position at the start of the substep)
+#ifdef MG_PHASE_TIMING
+  // shader-clock cycles per solver phase (profiling build only, see build.py --timing)
+  unsigned long long ph[16];
+  unsigned long long tmark;
+  __device__ void ph_start() {
+    for (int i = 0; i < 16; i++) ph[i] = 0;
+    tmark = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void ph_mark(int i) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    ph[i] += t1 - tmark;
+    tmark = t1;
+  }
+#else
+  __device__ void ph_start() {}
+  __device__ void ph_mark(int) {}
+#endif
   // drives / tendons (node lanes)
   float tgt;           // PD target of the own DOF
   float ttend;         // tendon generalized force (current substep)
@@ -400,6 +431,14 @@ struct Team {
     }
   }
 
+  __device__ void set_axis() {
+    if (freeb && tl < 6) {
+      for (int k = 0; k < 6; k++) Sl[k] = k == tl ? 1.0f : 0.0f;
+    } else {
+      Sl[0] = S.a.x; Sl[1] = S.a.y; Sl[2] = S.a.z; Sl[3] = S.l.x; Sl[4] = S.l.y; Sl[5] = S.l.z;
+    }
+  }
+
   // ---------------------------------------------------------------- ABA (unconstrained step)
   __device__ void aba() {
     if (node >= 0) {
@@ -446,7 +485,7 @@ struct Team {
         Sym6 Ia = IA;
         rank1_sub(Ia, U, Dinv);
         SV pa = pA + mul(Ia, c) + U * (u * Dinv);
-        float* sl = s->slot[node];
+        float* sl = s->u.slot[node];
         for (int k = 0; k < 6; k++) { sl[k] = Ia.a[k]; sl[15 + k] = Ia.c[k]; }
         for (int k = 0; k < 9; k++) sl[6 + k] = Ia.b[k];
         sl[21] = pa.a.x; sl[22] = pa.a.y; sl[23] = pa.a.z;
@@ -461,7 +500,7 @@ struct Team {
         while (ch) {
           const int k = __builtin_ctzll(ch);
           ch &= ch - 1;
-          const float* sl = s->slot[k];
+          const float* sl = s->u.slot[k];
           for (int q = 0; q < 6; q++) { IA.a[q] += sl[q]; IA.c[q] += sl[15 + q]; }
           for (int q = 0; q < 9; q++) IA.b[q] += sl[6 + q];
           pA = pA + sv(v3(sl[21], sl[22], sl[23]), v3(sl[24], sl[25], sl[26]));
@@ -609,22 +648,39 @@ struct Team {
     return tl < nv ? y : 0.0f;
   }
 
-  // J_r[tl] for row r (contacts: root twist part / path projection; limits: unit on the dof column)
-  __device__ float jac_entry(int r) const {
-    const int kind = s->rkind[r];
-    if (OBJ && objl) return kind >= 2 ? 0.0f : s->rwo[r][tl - ob0];
-    if (tl >= nv) return 0.0f;
-    if (kind >= 2) return (node > 0 && node == s->rref[r]) ? (kind == 2 ? 1.0f : -1.0f) : 0.0f;
-    const float* w = s->rw[r];
-    const int A = s->rA[r], B = s->rB[r];
-    if (freeb && tl < 6) {
-      float sgn = (A >= 0 ? 1.0f : 0.0f) - (B >= 0 ? 1.0f : 0.0f);
-      return sgn * w[tl];
-    }
-    if (node <= 0) return 0.0f;
-    float sgn = (in_path(A, node) ? 1.0f : 0.0f) - (in_path(B, node) ? 1.0f : 0.0f);
-    if (sgn == 0.0f) return 0.0f;
-    return sgn * (S.a.x * w[0] + S.a.y * w[1] + S.a.z * w[2] + S.l.x * w[3] + S.l.y * w[4] + S.l.z * w[5]);
+  // row r -> kind (0 normal, 1 friction, 2 lower limit, 3 upper limit) and ref (contact / node).
+  // Rows are [n, t1, t2] per contact, then the joint limits (oracle order).
+  __device__ int row_kind(int r) const { return r < 3 * ncr ? (r % 3 == 0 ? 0 : 1) : (s->lmeta[r - 3 * ncr] & 3); }
+  __device__ int row_ref(int r) const { return r < 3 * ncr ? r / 3 : (s->lmeta[r - 3 * ncr] >> 4); }
+  // spatial direction of contact row r at the team origin: w = [(p - o) x d; d]
+  __device__ void row_w(int r, float* w) const {
+    const int c = r / 3, k = r - 3 * c;
+    const float* dp = k == 0 ? s->cn[c] : (k == 1 ? s->ct1[c] : s->ct2[c]);
+    const V3 d = ld3(dp), q = ld3(s->cp[c]) - org, mo = cross(q, d);
+    w[0] = mo.x; w[1] = mo.y; w[2] = mo.z; w[3] = d.x; w[4] = d.y; w[5] = d.z;
+  }
+  // Jacobian code of this lane for row r: 0 none, 1 +, 2 - (contact rows: +-Sl.w; limit rows: +-1
+  // on the DOF's lane)
+  __device__ int jac_code(int r) const {
+    if (tl >= nv || (OBJ && objl)) return 0;
+    const int kind = row_kind(r);
+    if (kind >= 2) return (node > 0 && node == row_ref(r)) ? (kind == 2 ? 1 : 2) : 0;
+    const int c = r / 3, A = s->cA[c], B = s->cB[c];
+    float sgn;
+    if (freeb && tl < 6) sgn = (A >= 0 ? 1.0f : 0.0f) - (B >= 0 ? 1.0f : 0.0f);
+    else if (node <= 0) return 0;
+    else sgn = (in_path(A, node) ? 1.0f : 0.0f) - (in_path(B, node) ? 1.0f : 0.0f);
+    return sgn > 0.0f ? 1 : (sgn < 0.0f ? 2 : 0);
+  }
+  // J_r[tl] from the lane's code (object lanes: the stored object part)
+  __device__ float jac_value(int r, int code) const {
+    if (OBJ && objl) return r >= 3 * ncr ? 0.0f : s->rwo[r][tl - ob0];
+    if (code == 0) return 0.0f;
+    if (r >= 3 * ncr) return code == 1 ? 1.0f : -1.0f;
+    float w[6];
+    row_w(r, w);
+    const float d = Sl[0] * w[0] + Sl[1] * w[1] + Sl[2] * w[2] + Sl[3] * w[3] + Sl[4] * w[4] + Sl[5] * w[5];
+    return code == 1 ? d : -d;
   }
 
   // ---------------------------------------------------------------- collision -> LDS contact list
@@ -884,26 +940,22 @@ struct Team {
 
   // ---------------------------------------------------------------- constraint rows
   __device__ void build_rows() {
-    const int ncon = s->ncon;
-    const V3 o = ld3(s->x[0]);
+    const int ncon = ncr;
     for (int c = tl; c < ncon; c += T) {
       V3 n = ld3(s->cn[c]), pt = ld3(s->cp[c]), t1, t2;
       tangent_basis_t(n, &t1, &t2);
+      s->ct1[c][0] = t1.x; s->ct1[c][1] = t1.y; s->ct1[c][2] = t1.z;
+      s->ct2[c][0] = t2.x; s->ct2[c][1] = t2.y; s->ct2[c][2] = t2.z;
       float deff = s->cd[c] - p->rest_offset;
       float bn = deff >= 0.0f ? -deff / h : fminf(-p->baumgarte * deff / h, p->max_depen_vel);
-      V3 dirs[3] = {n, t1, t2};
-      for (int r = 0; r < 3; r++) {
-        const int row = 3 * c + r;
-        V3 w = cross(pt - o, dirs[r]);
-        s->rw[row][0] = w.x; s->rw[row][1] = w.y; s->rw[row][2] = w.z;
-        s->rw[row][3] = dirs[r].x; s->rw[row][4] = dirs[r].y; s->rw[row][5] = dirs[r].z;
-        s->rb[row] = r == 0 ? bn : 0.0f;
-        s->rkind[row] = r == 0 ? 0 : 1;
-        s->rref[row] = c;
-        s->rA[row] = s->cA[c];
-        s->rB[row] = s->cB[c];
-        if (OBJ) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
-          const float so = (s->cA[c] == OBJ_NODE ? 1.0f : 0.0f) - (s->cB[c] == OBJ_NODE ? 1.0f : 0.0f);
+      s->u.rows.b[3 * c] = bn;
+      s->u.rows.b[3 * c + 1] = 0.0f;
+      s->u.rows.b[3 * c + 2] = 0.0f;
+      if (OBJ) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
+        const float so = (s->cA[c] == OBJ_NODE ? 1.0f : 0.0f) - (s->cB[c] == OBJ_NODE ? 1.0f : 0.0f);
+        V3 dirs[3] = {n, t1, t2};
+        for (int r = 0; r < 3; r++) {
+          const int row = 3 * c + r;
           const V3 wo = cross(pt - op, dirs[r]) * so, d = dirs[r] * so;
           s->rwo[row][0] = wo.x; s->rwo[row][1] = wo.y; s->rwo[row][2] = wo.z;
           s->rwo[row][3] = d.x; s->rwo[row][4] = d.y; s->rwo[row][5] = d.z;
@@ -923,18 +975,14 @@ struct Team {
     }
     const int incl = team_incl_scan<T>(cnt);
     const int tot = __shfl(incl, tb + T - 1);
-    int row = 3 * ncon + incl - cnt;
+    int li = incl - cnt;
     for (int side = 0; side < 2; side++) {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
       float d = side == 0 ? dl : du;
-      s->rb[row] = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
-      s->rkind[row] = 2 + side;
-      s->rref[row] = node;
-      s->rA[row] = -1;
-      s->rB[row] = -1;
-      for (int k = 0; k < 6; k++) s->rw[row][k] = 0.0f;
-      row++;
+      s->u.rows.b[3 * ncon + li] = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
+      s->lmeta[li] = (2 + side) | (node << 4);
+      li++;
     }
     if (tl == 0) s->nrows = 3 * ncon + tot;
     __syncthreads();
@@ -942,68 +990,100 @@ struct Team {
 
   // ---------------------------------------------------------------- one substep
   __device__ void substep() {
+    ph_mark(15);
     fk();
+    set_axis();
+    ph_mark(0);
     if (OBJ) tendons();
     aba();
+    ph_mark(1);
     obj_free();
     collide();
+    ncr = s->ncon;
+    org = ld3(s->x[0]);
+    ph_mark(2);
     build_rows();
+    ph_mark(3);
     const int nrows = s->nrows;
     const int wave_rows = __builtin_amdgcn_readfirstlane(wave_max<T>(nrows));
+#ifdef MG_PHASE_TIMING
+    ph[13] += wave_rows;
+#endif
+    // row responses Y_r = M~^-1 J_r^T by test-force ABA solves (column distributed over the lanes),
+    // W_r = J_r . Y_r, and the rows' lane codes for the sweeps
+    const unsigned long long tmask = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
     float Ycol[MR];
     for (int r = 0; r < wave_rows; r++) {
       const bool active = r < nrows;
-      const int kind = active ? s->rkind[r] : 0;
+      const int kind = active ? row_kind(r) : 0;
       int A = -1, B = -1, jn = -1;
       float sg = 0.0f;
       SV fw = szero();
       if (active) {
         if (kind >= 2) {
-          jn = s->rref[r];
+          jn = row_ref(r);
           sg = kind == 2 ? 1.0f : -1.0f;
         } else {
-          A = s->rA[r];
-          B = s->rB[r];
-          const float* w = s->rw[r];
+          const int c = r / 3;
+          A = s->cA[c];
+          B = s->cB[c];
+          float w[6];
+          row_w(r, w);
           fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
         }
       }
       float y = test_solve(A, B, fw, jn, sg);
       if (OBJ && objl) y = (active && kind < 2) ? obj_response(r) : 0.0f;
-      Ycol[r] = active ? y : 0.0f;
-      const float Wr = team_sum<T>(active ? jac_entry(r) * y : 0.0f, tb);
+      y = active ? y : 0.0f;
+      Ycol[r] = y;
+      const int code = active ? jac_code(r) : 0;
+      const float J = active ? jac_value(r, code) : 0.0f;
+      const float Wr = team_sum<T>(J * y, tb);
+      const unsigned long long m0 = (__ballot(code & 1) >> tb) & tmask, m1 = (__ballot(code & 2) >> tb) & tmask;
       if (tl == 0 && active) {
-        s->rW[r] = Wr;
-        s->rlam[r] = 0.0f;
+        s->u.rows.invW[r] = Wr > 1e-12f ? 1.0f / Wr : 0.0f;
+        s->u.rows.lam[r] = 0.0f;
+        s->u.rows.sg[r][0] = (typename L::mask_t)m0;
+        s->u.rows.sg[r][1] = (typename L::mask_t)m1;
       }
     }
     __syncthreads();
+    ph_mark(5);
+    // PGS sweeps: per row one team dot product (DPP), a clamped scalar update, one FMA per lane.
+    // Row data do not depend on the sweep's chain (the next row's response is prefetched); the
+    // friction bound uses the contact's normal impulse of this sweep, carried in a register.
+    const float mu = p->friction;
     for (int it = 0; it < p->pos_iters; it++) {
+      float lamn = 0.0f;
+      float ynext = Ycol[0];
       for (int r = 0; r < wave_rows; r++) {
+        const float y = ynext;
+        ynext = Ycol[r + 1 < MR ? r + 1 : r];
         const bool active = r < nrows;
-        const float Jr = active ? jac_entry(r) : 0.0f;
-        const float v = team_sum<T>(Jr * nu, tb);
-        float dl = 0.0f;
-        if (active) {
-          const float W = s->rW[r];
-          if (W > 1e-12f) {
-            const float lam = s->rlam[r];
-            float lnew = lam + (s->rb[r] - v) / W;
-            if (s->rkind[r] == 1) {
-              const float lim = p->friction * s->rlam[3 * s->rref[r]];
-              lnew = fminf(fmaxf(lnew, -lim), lim);
-            } else {
-              lnew = fmaxf(lnew, 0.0f);
-            }
-            dl = lnew - lam;
-          }
+        const unsigned long long c0 = s->u.rows.sg[r][0], c1 = s->u.rows.sg[r][1];
+        const float b = s->u.rows.b[r], iw = s->u.rows.invW[r], lam = s->u.rows.lam[r];
+        const int kind = row_kind(r);
+        const int code = (int)((c0 >> tl) & 1ull) | ((int)((c1 >> tl) & 1ull) << 1);
+        const float J = active ? jac_value(r, code) : 0.0f;
+        const float v = team_sum<T>(J * nu, tb);
+        float lnew = lam + (b - v) * iw;
+        if (kind == 1) {
+          const float lim = mu * lamn;
+          lnew = fminf(fmaxf(lnew, -lim), lim);
+        } else {
+          lnew = fmaxf(lnew, 0.0f);
         }
-        if (tl == 0 && active) s->rlam[r] += dl;
-        nu += Ycol[r] * dl;
+        if (iw == 0.0f) lnew = lam;  // W <= 1e-12: row skipped (oracle)
+        if (kind == 0) lamn = lnew;
+        const float dl = active ? lnew - lam : 0.0f;
+        if (tl == 0 && active) s->u.rows.lam[r] = lnew;
+        nu += y * dl;
       }
     }
     __syncthreads();
+    ph_mark(6);
     integrate();
+    ph_mark(7);
   }
 
   __device__ void integrate() {
@@ -1080,7 +1160,7 @@ struct Team {
         if (sg == 0.0f) continue;
         V3 n = ld3(s->cn[c]), t1, t2;
         tangent_basis_t(n, &t1, &t2);
-        V3 f = (n * s->rlam[3 * c] + t1 * s->rlam[3 * c + 1] + t2 * s->rlam[3 * c + 2]) * (sg / h);
+        V3 f = (n * s->u.rows.lam[3 * c] + t1 * s->u.rows.lam[3 * c + 1] + t2 * s->u.rows.lam[3 * c + 2]) * (sg / h);
         F = F + f;
         Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
       }
@@ -1098,9 +1178,10 @@ struct Team {
         t += -nf[26] * nu - nf[27] * qj;
       }
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
-        if (s->rref[r] != node) continue;
-        if (s->rkind[r] == 2) t += s->rlam[r] / h;
-        if (s->rkind[r] == 3) t -= s->rlam[r] / h;
+        const int meta = s->lmeta[r - 3 * s->ncon];
+        if ((meta >> 4) != node) continue;
+        if ((meta & 3) == 2) t += s->u.rows.lam[r] / h;
+        if ((meta & 3) == 3) t -= s->u.rows.lam[r] / h;
       }
       dforce_out[node - 1] = t;
     }
