@@ -257,41 +257,76 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   float pot = 0.0f, prev = 0.0f, up[3] = {0, 0, 0}, hd[3] = {0, 0, 0};
   int64_t progress = tb.progress[ac] + 1;
   int64_t reset = reset_in;
-  float act[64];
-  if (t.tl == 0) {
-    for (int i = 0; i < na; i++) {
-      act[i] = mg::clampf(tb.actions[(size_t)na * ac + i], tp.clip_actions);
-      if (valid && tb.actions_out) tb.actions_out[(size_t)na * a + i] = act[i];
-    }
-    if (tb.potentials) { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
-    if (do_reset) {
-      mg::reset_env(&tp, off, tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr, tb.seed,
-                    (uint64_t)(tb.env_offset + a), tb.step_counter, L.root, L.dof, &pot, &prev);
-      progress = 0;
-      reset = 0;
-    }
+  // self.actions: one lane per action column (na <= T, checked by mg_env_step)
+  const bool alane = t.tl < na;
+  const float act_l = alane ? mg::clampf(tb.actions[(size_t)na * ac + t.tl], tp.clip_actions) : 0.0f;
+  if (valid && alane && tb.actions_out) tb.actions_out[(size_t)na * a + t.tl] = act_l;
+  if (tb.potentials) { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
+  if (do_reset) {  // reset_idx: one lane per DOF draws its noise; the leader resets root and potentials
+    const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr;
+    for (int i = t.tl; i < nd; i += T)
+      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset + a), tb.step_counter, L.dof);
+    if (t.tl == 0) mg::reset_root(&tp, off, L.root, &pot, &prev);
+    progress = 0;
+    reset = 0;
   }
   __syncthreads();
+  // observations staged in the row storage (dead after outputs()), then stored coalesced
   const int no = tp.num_obs;
-  float* o = tb.obs + (size_t)no * ac;
-  if (t.tl == 0 && valid)
-    mg::obs_env(&tp, off, L.root, L.dof, L.dforce, L.sens, act, &pot, &prev, up, hd, o);
+  float* ost = &L.u.slot[0][0];
+  if (tp.task_id == MG_TASK_CARTPOLE) {
+    if (t.tl < 4) ost[t.tl] = L.dof[t.tl];
+  } else {
+    if (t.tl == 0) mg::obs_head(&tp, off, L.root, &pot, &prev, up, hd, ost);
+    const bool hum = tp.task_id == MG_TASK_HUMANOID;
+    for (int q = t.tl; q < nd; q += T) {
+      ost[12 + q] = mg::t_unscale(L.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
+      ost[12 + nd + q] = L.dof[2 * q + 1] * tp.dof_vel_scale;
+      if (hum) ost[12 + 2 * nd + q] = L.dforce[q] * tp.contact_force_scale;
+    }
+    const int bs = 12 + (hum ? 3 : 2) * nd, nss = mg::t_sensors(&tp);
+    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.sens[q] * tp.contact_force_scale;
+    if (alane) ost[bs + 6 * nss + t.tl] = act_l;
+  }
   if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
     const float px = L.root[0], py = L.root[1], pz = L.root[2];
     const int base = no - 3 * (A - 1);
     for (int j = 1; j < A; j++) {
       const int src = (team - k + (k + j) % A) * T;
       const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
-      if (t.tl == 0 && valid) {
-        o[base + 3 * (j - 1) + 0] = qx - px;
-        o[base + 3 * (j - 1) + 1] = qy - py;
-        o[base + 3 * (j - 1) + 2] = qz - pz;
+      if (t.tl == 0) {
+        ost[base + 3 * (j - 1) + 0] = qx - px;
+        ost[base + 3 * (j - 1) + 1] = qy - py;
+        ost[base + 3 * (j - 1) + 2] = qz - pz;
       }
     }
   }
+  __syncthreads();
+  // reward: per-action terms as team sums (DPP), the rest on the leader
+  float rew = 0.0f;
+  if (tp.task_id == MG_TASK_CARTPOLE) {
+    if (t.tl == 0) mg::reward_env(&tp, ost, &act_l, pot, prev, progress, &reset, &rew);
+  } else {
+    float ac2 = act_l * act_l, el = 0.0f, lim = 0.0f;
+    if (alane) {
+      if (tp.task_id == MG_TASK_ANT) {
+        el = fabsf(act_l * ost[12 + nd + t.tl]);
+        lim = ost[12 + t.tl] > 0.99f ? 1.0f : 0.0f;
+      } else {
+        const float ratio = tp.motor_effort[t.tl] / tp.max_motor_effort;
+        const float ab = fabsf(ost[12 + t.tl]);
+        const float scaled = tp.joints_at_limit_cost_scale * (ab - 0.98f) / 0.02f;
+        lim = (ab > 0.98f ? 1.0f : 0.0f) * scaled * ratio;
+        el = fabsf(act_l * ost[12 + nd + t.tl]) * ratio;
+      }
+    }
+    ac2 = mg::team_sum<T>(ac2, t.tb);
+    el = mg::team_sum<T>(el, t.tb);
+    lim = mg::team_sum<T>(lim, t.tb);
+    if (tp.task_id == MG_TASK_ANT) lim = lim * tp.joints_at_limit_cost_scale;
+    if (t.tl == 0) mg::reward_from_sums(&tp, ost, ac2, el, lim, pot, prev, progress, &reset, &rew);
+  }
   if (t.tl == 0 && valid) {
-    float rew;
-    mg::reward_env(&tp, o, act, pot, prev, progress, &reset, &rew);
     const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
     tb.rew[a] = rew;
     tb.reset[a] = reset;
@@ -305,8 +340,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         tb.heading_vec[3 * (size_t)a + c] = hd[c];
       }
     }
-    if (tb.obs_clamped)
-      for (int i = 0; i < no; i++) tb.obs_clamped[(size_t)no * a + i] = mg::clampf(o[i], tp.clip_obs);
+  }
+  if (valid) {
+    float* o = tb.obs + (size_t)no * a;
+    for (int q = t.tl; q < no; q += T) {
+      o[q] = ost[q];
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(ost[q], tp.clip_obs);
+    }
   }
   __syncthreads();
   if (valid) {  // state write-back (gym layouts), team-cooperative
@@ -930,6 +970,8 @@ int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb
       return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
     if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
       return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
+    if (tp->num_actions > team_size(sim->host_model, sim->params.max_contacts))
+      return fail(MG_EINVAL, "mg_env_step: more actions than lanes per actor");
   }
   if (tp->num_agents > 1) {
     // the agents of an env must be teams of one wave (ballot/shuffle exchange): A | 64/T

@@ -183,35 +183,87 @@ __device__ void reward_env(const mg_task_params* tp, const float* o, const float
   *reset = rs;
 }
 
-// reset_idx for one env.  noise: row of 2*nD U(0,1) (or NULL: device counter RNG)
+// reset_idx for DOF i of one env (ant.py:257-266; cartpole.py:146-151).  noise: row of 2*nD U(0,1)
+// (or NULL: device counter RNG)
+__device__ __forceinline__ void reset_dof(const mg_task_params* tp, int i, int nd, const float* noise, uint64_t seed,
+                                          uint64_t env_gid, uint64_t counter, float* dof) {
+  float up = noise ? noise[i] : uniform01(seed, env_gid, counter, (uint32_t)i);
+  float uv = noise ? noise[nd + i] : uniform01(seed, env_gid, counter, (uint32_t)(nd + i));
+  if (tp->task_id == MG_TASK_CARTPOLE) {
+    dof[2 * i] = 0.2f * (up - 0.5f);
+    dof[2 * i + 1] = 0.5f * (uv - 0.5f);
+  } else {
+    float pos = 0.4f * up + -0.2f;
+    float vel = 0.2f * uv + -0.1f;
+    float q = tp->initial_dof_pos[i] + pos;
+    q = q < tp->dof_upper[i] ? q : tp->dof_upper[i];
+    q = q > tp->dof_lower[i] ? q : tp->dof_lower[i];
+    dof[2 * i] = q;
+    dof[2 * i + 1] = vel;
+  }
+}
+// root / potentials part of reset_idx (ant.py:268-279)
+__device__ __forceinline__ void reset_root(const mg_task_params* tp, const float* off, float* root, float* pot,
+                                           float* prev_pot) {
+  if (tp->task_id == MG_TASK_CARTPOLE) return;
+  for (int k = 0; k < 3; k++) root[k] = tp->start_pos[k] + off[k];
+  for (int k = 0; k < 4; k++) root[3 + k] = tp->start_rot[k];
+  for (int k = 7; k < 13; k++) root[k] = 0.0f;
+  float t0 = (tp->target[0] + off[0]) - root[0], t1 = (tp->target[1] + off[1]) - root[1], t2 = 0.0f;
+  float nrm = sqrtf(t0 * t0 + t1 * t1 + t2 * t2);
+  *prev_pot = -nrm / tp->dt;
+  *pot = *prev_pot;
+}
 __device__ void reset_env(const mg_task_params* tp, const float* off, const float* noise, uint64_t seed,
                           uint64_t env_gid, uint64_t counter, float* root, float* dof, float* pot, float* prev_pot) {
   const int nd = t_dofs(tp);
-  for (int i = 0; i < nd; i++) {
-    float up = noise ? noise[i] : uniform01(seed, env_gid, counter, (uint32_t)i);
-    float uv = noise ? noise[nd + i] : uniform01(seed, env_gid, counter, (uint32_t)(nd + i));
-    if (tp->task_id == MG_TASK_CARTPOLE) {
-      dof[2 * i] = 0.2f * (up - 0.5f);
-      dof[2 * i + 1] = 0.5f * (uv - 0.5f);
-    } else {
-      float pos = 0.4f * up + -0.2f;
-      float vel = 0.2f * uv + -0.1f;
-      float q = tp->initial_dof_pos[i] + pos;
-      q = q < tp->dof_upper[i] ? q : tp->dof_upper[i];
-      q = q > tp->dof_lower[i] ? q : tp->dof_lower[i];
-      dof[2 * i] = q;
-      dof[2 * i + 1] = vel;
-    }
+  for (int i = 0; i < nd; i++) reset_dof(tp, i, nd, noise, seed, env_gid, counter, dof);
+  reset_root(tp, off, root, pot, prev_pot);
+}
+
+// the first 12 observation values of compute_{ant,humanoid}_observations (ant.py:401-406,
+// humanoid.py:401-413) + the potentials / basis vectors
+__device__ __forceinline__ void obs_head(const mg_task_params* tp, const float* off, const float* root, float* pot,
+                                         float* prev_pot, float* up, float* heading, float* o) {
+  LocoFeat f;
+  loco_features(tp, root, off, f);
+  *prev_pot = *pot;
+  *pot = f.potential;
+  for (int i = 0; i < 3; i++) { up[i] = f.up_vec[i]; heading[i] = f.heading_vec[i]; }
+  int k = 0;
+  o[k++] = root[2];
+  for (int i = 0; i < 3; i++) o[k++] = f.vel_loc[i];
+  if (tp->task_id == MG_TASK_ANT) {
+    for (int i = 0; i < 3; i++) o[k++] = f.angvel_loc[i];
+    o[k++] = f.yaw;
+    o[k++] = f.roll;
+    o[k++] = f.angle_to_target;
+  } else {
+    for (int i = 0; i < 3; i++) o[k++] = f.angvel_loc[i] * tp->angular_velocity_scale;
+    o[k++] = t_normalize_angle(f.yaw);
+    o[k++] = t_normalize_angle(f.roll);
+    o[k++] = t_normalize_angle(f.angle_to_target);
   }
-  if (tp->task_id != MG_TASK_CARTPOLE) {
-    for (int k = 0; k < 3; k++) root[k] = tp->start_pos[k] + off[k];
-    for (int k = 0; k < 4; k++) root[3 + k] = tp->start_rot[k];
-    for (int k = 7; k < 13; k++) root[k] = 0.0f;
-    float t0 = (tp->target[0] + off[0]) - root[0], t1 = (tp->target[1] + off[1]) - root[1], t2 = 0.0f;
-    float nrm = sqrtf(t0 * t0 + t1 * t1 + t2 * t2);
-    *prev_pot = -nrm / tp->dt;
-    *pot = *prev_pot;
-  }
+  o[k++] = f.up_proj;
+  o[k++] = f.heading_proj;
+}
+
+// reward given the team sums of the per-action terms (compute_{ant,humanoid}_reward, ant.py:325-371,
+// humanoid.py:323-375); ac = sum a^2, el = energy term, lim = joints-at-limit term
+__device__ __forceinline__ void reward_from_sums(const mg_task_params* tp, const float* o, float ac, float el,
+                                                 float lim, float pot, float prev_pot, int64_t progress,
+                                                 int64_t* reset, float* rew) {
+  const float max_ep_m1 = (float)tp->max_episode_length - 1.0f;
+  float heading = o[11] > 0.8f ? tp->heading_weight : tp->heading_weight * o[11] / 0.8f;
+  float up = o[10] > 0.93f ? 0.0f + tp->up_weight : 0.0f;
+  float alive = tp->task_id == MG_TASK_ANT ? 0.5f : 2.0f;
+  float progress_reward = pot - prev_pot;
+  float total = progress_reward + alive + up + heading - tp->actions_cost_scale * ac - tp->energy_cost_scale * el - lim;
+  int64_t rs = *reset;
+  if (o[0] < tp->termination_height) { total = tp->death_cost; rs = 1; }
+  if ((float)progress >= max_ep_m1) rs = 1;
+  *rew = total;
+  *reset = rs;
 }
 
 __device__ __forceinline__ float clampf(float x, float lim) {
