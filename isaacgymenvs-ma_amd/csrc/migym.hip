@@ -714,8 +714,7 @@ template <template <int, int, int, int, int, bool> class F, typename... A>
 static int dispatch(const mg_model& m, int max_contacts, A... args) {
 #define MG_TRY(T, MN, MC, MG, MP, OBJ)             \
   if (MG_FITS(T, MN, MC, MG, MP, OBJ)) {           \
-    F<T, MN, MC, MG, MP, OBJ>::run(args...);       \
-    return MG_OK;                                  \
+    return F<T, MN, MC, MG, MP, OBJ>::run(args...); \
   }
   MG_INSTANCES(MG_TRY)
 #undef MG_TRY
@@ -724,16 +723,20 @@ static int dispatch(const mg_model& m, int max_contacts, A... args) {
 
 template <int T, int MN, int MC, int MG, int MP, bool OBJ>
 struct RunSimulate {
-  static void run(hipStream_t s, const mg_sim* sim) {
+  static int run(hipStream_t s, const mg_sim* sim) {
     const int E = kBlock / T;
     hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                        sim->d_model, sim->params, sim->views, sim->n);
+    return MG_OK;
   }
 };
 template <int T, int MN, int MC, int MG, int MP, bool OBJ>
 struct RunEnvStep {
-  static void run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
+  static int run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
     const int E = kBlock / T;
+    // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
+    if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u))
+      return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
     if constexpr (OBJ) {
       hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                          sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
@@ -742,6 +745,7 @@ struct RunEnvStep {
       hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                          sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
     }
+    return MG_OK;
   }
 };
 

@@ -103,11 +103,12 @@ __device__ void load_tile(ModelTile<MN, MG, MP>* t, const mg_model* m) {
   if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; }
 }
 
+static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
+
 template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
   static constexpr int MRO = OBJ ? MR : 1;
-  using mask_t = typename std::conditional<(T <= 32), unsigned int, unsigned long long>::type;
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -123,17 +124,15 @@ struct TeamLDS {
   int ncon, nrows;
   // contacts: point, frame (normal + tangent basis), gap, sides (nodes / geoms)
   float cp[MC][3], cn[MC][3], ct1[MC][3], ct2[MC][3], cd[MC];
-  int cA[MC], cB[MC], cgA[MC], cgB[MC];
+  int cside[MC];  // packed int8 [node A, node B, geom A, geom B] (-1 none, -2 the free object)
   // joint-limit rows (after the 3 rows per contact): kind | node << 4
   int lmeta[2 * (MN - 1)];
   // The ABA's child slots are dead once the tree pass is done; the constraint rows reuse them:
-  // per-lane Jacobian codes (two bit masks: 0 none, 1 +Sl.w, 2 -Sl.w, 3 unit), target, 1/W, impulse.
+  // per row {target b, 1/W, impulse, kind (0 normal, 1 friction, 2 limit)}, one 16-byte LDS read.
+  struct alignas(16) Row { float b, iw, lam, kind; };
   union {
     float slot[MN][27];
-    struct {
-      mask_t sg[MR][2];
-      float b[MR], invW[MR], lam[MR];
-    } rows;
+    Row rows[MR];
   } u;
   // task-layer staging (root / dof state of the actor after the physics)
   float root[13];
@@ -648,6 +647,8 @@ struct Team {
     return tl < nv ? y : 0.0f;
   }
 
+  // side k of contact c: 0 node A, 1 node B, 2 geom A, 3 geom B
+  __device__ int cside(int c, int k) const { return (int)(int8_t)(s->cside[c] >> (8 * k)); }
   // row r -> kind (0 normal, 1 friction, 2 lower limit, 3 upper limit) and ref (contact / node).
   // Rows are [n, t1, t2] per contact, then the joint limits (oracle order).
   __device__ int row_kind(int r) const { return r < 3 * ncr ? (r % 3 == 0 ? 0 : 1) : (s->lmeta[r - 3 * ncr] & 3); }
@@ -665,7 +666,7 @@ struct Team {
     if (tl >= nv || (OBJ && objl)) return 0;
     const int kind = row_kind(r);
     if (kind >= 2) return (node > 0 && node == row_ref(r)) ? (kind == 2 ? 1 : 2) : 0;
-    const int c = r / 3, A = s->cA[c], B = s->cB[c];
+    const int c = r / 3, A = cside(c, 0), B = cside(c, 1);
     float sgn;
     if (freeb && tl < 6) sgn = (A >= 0 ? 1.0f : 0.0f) - (B >= 0 ? 1.0f : 0.0f);
     else if (node <= 0) return 0;
@@ -758,7 +759,7 @@ struct Team {
     s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
     s->cn[slot][0] = n.x; s->cn[slot][1] = n.y; s->cn[slot][2] = n.z;
     s->cd[slot] = d;
-    s->cA[slot] = A; s->cgA[slot] = gA; s->cB[slot] = B; s->cgB[slot] = gB;
+    s->cside[slot] = (A & 0xff) | ((B & 0xff) << 8) | ((gA & 0xff) << 16) | ((gB & 0xff) << 24);
   }
 
   __device__ void collide() {
@@ -948,11 +949,11 @@ struct Team {
       s->ct2[c][0] = t2.x; s->ct2[c][1] = t2.y; s->ct2[c][2] = t2.z;
       float deff = s->cd[c] - p->rest_offset;
       float bn = deff >= 0.0f ? -deff / h : fminf(-p->baumgarte * deff / h, p->max_depen_vel);
-      s->u.rows.b[3 * c] = bn;
-      s->u.rows.b[3 * c + 1] = 0.0f;
-      s->u.rows.b[3 * c + 2] = 0.0f;
+      s->u.rows[3 * c].b = bn;
+      s->u.rows[3 * c + 1].b = 0.0f;
+      s->u.rows[3 * c + 2].b = 0.0f;
       if (OBJ) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
-        const float so = (s->cA[c] == OBJ_NODE ? 1.0f : 0.0f) - (s->cB[c] == OBJ_NODE ? 1.0f : 0.0f);
+        const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
         V3 dirs[3] = {n, t1, t2};
         for (int r = 0; r < 3; r++) {
           const int row = 3 * c + r;
@@ -980,7 +981,7 @@ struct Team {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
       float d = side == 0 ? dl : du;
-      s->u.rows.b[3 * ncon + li] = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
+      s->u.rows[3 * ncon + li].b = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
       s->lmeta[li] = (2 + side) | (node << 4);
       li++;
     }
@@ -1010,9 +1011,9 @@ struct Team {
     ph[13] += wave_rows;
 #endif
     // row responses Y_r = M~^-1 J_r^T by test-force ABA solves (column distributed over the lanes),
-    // W_r = J_r . Y_r, and the rows' lane codes for the sweeps
-    const unsigned long long tmask = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
-    float Ycol[MR];
+    // W_r = J_r . Y_r.  Lane j keeps (J_r[j], Y_r[j]) of every row in private arrays for the sweeps;
+    // rows past this team's count get J = Y = 0 and zero scalars, so the sweeps need no row mask.
+    float Jcol[MR], Ycol[MR];
     for (int r = 0; r < wave_rows; r++) {
       const bool active = r < nrows;
       const int kind = active ? row_kind(r) : 0;
@@ -1025,8 +1026,8 @@ struct Team {
           sg = kind == 2 ? 1.0f : -1.0f;
         } else {
           const int c = r / 3;
-          A = s->cA[c];
-          B = s->cB[c];
+          A = cside(c, 0);
+          B = cside(c, 1);
           float w[6];
           row_w(r, w);
           fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
@@ -1035,49 +1036,72 @@ struct Team {
       float y = test_solve(A, B, fw, jn, sg);
       if (OBJ && objl) y = (active && kind < 2) ? obj_response(r) : 0.0f;
       y = active ? y : 0.0f;
-      Ycol[r] = y;
       const int code = active ? jac_code(r) : 0;
       const float J = active ? jac_value(r, code) : 0.0f;
+      Ycol[r] = y;
+      Jcol[r] = J;
       const float Wr = team_sum<T>(J * y, tb);
-      const unsigned long long m0 = (__ballot(code & 1) >> tb) & tmask, m1 = (__ballot(code & 2) >> tb) & tmask;
-      if (tl == 0 && active) {
-        s->u.rows.invW[r] = Wr > 1e-12f ? 1.0f / Wr : 0.0f;
-        s->u.rows.lam[r] = 0.0f;
-        s->u.rows.sg[r][0] = (typename L::mask_t)m0;
-        s->u.rows.sg[r][1] = (typename L::mask_t)m1;
+      if (tl == 0) {
+        typename L::Row& rw = s->u.rows[r];
+        rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
+        rw.lam = 0.0f;
+        rw.kind = kind >= 2 ? 2.0f : (float)kind;
+        if (!active) rw.b = 0.0f;
       }
+    }
+    // a sweep shorter than the prefetch depth would read a row's impulse before its previous visit
+    // wrote it: pad it with zero rows (J = Y = 0, 1/W = 0: skipped, as the oracle skips W = 0 rows)
+    constexpr int PF = 4;
+    const int prow = (wave_rows > 0 && wave_rows < PF) ? PF : wave_rows;
+    for (int r = wave_rows; r < prow; r++) {
+      Ycol[r] = 0.0f;
+      Jcol[r] = 0.0f;
+      if (tl == 0) s->u.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, 0.0f};
     }
     __syncthreads();
     ph_mark(5);
-    // PGS sweeps: per row one team dot product (DPP), a clamped scalar update, one FMA per lane.
-    // Row data do not depend on the sweep's chain (the next row's response is prefetched); the
-    // friction bound uses the contact's normal impulse of this sweep, carried in a register.
+    // PGS sweeps as one stream of pos_iters * wave_rows row visits: per visit one team dot product
+    // (DPP), the clamp, one FMA per lane.  A visit's data (private J/Y, LDS row scalars) do not
+    // depend on the sweep's chain; they sit in PF rotating registers loaded PF visits ahead, each load
+    // issued after the previous occupant's last use.  The friction bound uses the contact's normal
+    // impulse of this sweep (the normal row precedes its two friction rows), carried in a register.
     const float mu = p->friction;
-    for (int it = 0; it < p->pos_iters; it++) {
-      float lamn = 0.0f;
-      float ynext = Ycol[0];
-      for (int r = 0; r < wave_rows; r++) {
-        const float y = ynext;
-        ynext = Ycol[r + 1 < MR ? r + 1 : r];
-        const bool active = r < nrows;
-        const unsigned long long c0 = s->u.rows.sg[r][0], c1 = s->u.rows.sg[r][1];
-        const float b = s->u.rows.b[r], iw = s->u.rows.invW[r], lam = s->u.rows.lam[r];
-        const int kind = row_kind(r);
-        const int code = (int)((c0 >> tl) & 1ull) | ((int)((c1 >> tl) & 1ull) << 1);
-        const float J = active ? jac_value(r, code) : 0.0f;
-        const float v = team_sum<T>(J * nu, tb);
-        float lnew = lam + (b - v) * iw;
-        if (kind == 1) {
+    const int nvis = p->pos_iters * prow;
+    float pJ[PF], pY[PF];
+    typename L::Row pR[PF];
+    int rq = 0;  // row of the next prefetch
+#pragma unroll
+    for (int k = 0; k < PF; k++) {
+      if (k < nvis) {
+        pJ[k] = Jcol[rq];
+        pY[k] = Ycol[rq];
+        pR[k] = s->u.rows[rq];
+        rq = rq + 1 == prow ? 0 : rq + 1;
+      }
+    }
+    float lamn = 0.0f;
+    int r = 0;
+    for (int v0 = 0; v0 < nvis; v0 += PF) {
+#pragma unroll
+      for (int k = 0; k < PF; k++) {
+        if (v0 + k < nvis) {
+          const float v = team_sum<T>(pJ[k] * nu, tb);
+          const float lam = pR[k].lam, iw = pR[k].iw, kd = pR[k].kind;
+          float lnew = lam + (pR[k].b - v) * iw;
           const float lim = mu * lamn;
-          lnew = fminf(fmaxf(lnew, -lim), lim);
-        } else {
-          lnew = fmaxf(lnew, 0.0f);
+          lnew = kd == 1.0f ? fminf(fmaxf(lnew, -lim), lim) : fmaxf(lnew, 0.0f);
+          if (iw == 0.0f) lnew = lam;  // W <= 1e-12 (or a padding row): skipped (oracle)
+          if (kd == 0.0f) lamn = lnew;
+          if (tl == 0) s->u.rows[r].lam = lnew;
+          nu += pY[k] * (lnew - lam);
+          r = r + 1 == prow ? 0 : r + 1;
+          if (v0 + k + PF < nvis) {
+            pJ[k] = Jcol[rq];
+            pY[k] = Ycol[rq];
+            pR[k] = s->u.rows[rq];
+            rq = rq + 1 == prow ? 0 : rq + 1;
+          }
         }
-        if (iw == 0.0f) lnew = lam;  // W <= 1e-12: row skipped (oracle)
-        if (kind == 0) lamn = lnew;
-        const float dl = active ? lnew - lam : 0.0f;
-        if (tl == 0 && active) s->u.rows.lam[r] = lnew;
-        nu += y * dl;
       }
     }
     __syncthreads();
@@ -1155,12 +1179,12 @@ struct Team {
       V3 F = v3(0, 0, 0), Tq = v3(0, 0, 0);
       for (int c = 0; c < s->ncon; c++) {
         float sg = 0.0f;
-        if (s->cgA[c] >= 0 && mt->gbody[s->cgA[c]] == body) sg = 1.0f;
-        else if (s->cgB[c] >= 0 && mt->gbody[s->cgB[c]] == body) sg = -1.0f;
+        if (cside(c, 2) >= 0 && mt->gbody[cside(c, 2)] == body) sg = 1.0f;
+        else if (cside(c, 3) >= 0 && mt->gbody[cside(c, 3)] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
         V3 n = ld3(s->cn[c]), t1, t2;
         tangent_basis_t(n, &t1, &t2);
-        V3 f = (n * s->u.rows.lam[3 * c] + t1 * s->u.rows.lam[3 * c + 1] + t2 * s->u.rows.lam[3 * c + 2]) * (sg / h);
+        V3 f = (n * s->u.rows[3 * c].lam + t1 * s->u.rows[3 * c + 1].lam + t2 * s->u.rows[3 * c + 2].lam) * (sg / h);
         F = F + f;
         Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
       }
@@ -1180,8 +1204,8 @@ struct Team {
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
         const int meta = s->lmeta[r - 3 * s->ncon];
         if ((meta >> 4) != node) continue;
-        if ((meta & 3) == 2) t += s->u.rows.lam[r] / h;
-        if ((meta & 3) == 3) t -= s->u.rows.lam[r] / h;
+        if ((meta & 3) == 2) t += s->u.rows[r].lam / h;
+        if ((meta & 3) == 3) t -= s->u.rows[r].lam / h;
       }
       dforce_out[node - 1] = t;
     }
