@@ -3,8 +3,10 @@
 // asynchronous on the caller's stream; no entry point synchronises.
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "../../include/migym.h"
 #include "hand_task.hpp"
@@ -28,10 +30,17 @@ inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
 }  // namespace
 
 #ifdef MG_PHASE_TIMING
-__device__ unsigned long long g_phase[16];  // summed over waves (team leader of lane 0)
-#define MG_PHASE_FLUSH(t)                                                          \
-  if (threadIdx.x == 0)                                                            \
-    for (int i_ = 0; i_ < 16; i_++) atomicAdd(&g_phase[i_], (t).ph[i_]);
+// per-wave accumulators (one row of 16 per block; plain read-modify-writes by the block's own wave,
+// so the profiling build adds no atomic traffic that would slow the solver's memory path)
+constexpr int kPhaseCap = 1 << 16;  // blocks tracked
+__device__ unsigned long long* g_phase_buf;
+#define MG_PHASE_FLUSH(t)                                                              \
+  if (g_phase_buf && blockIdx.x < kPhaseCap && threadIdx.x < 16) {                     \
+    unsigned int v_ = 0;                                                               \
+    for (int i_ = 0; i_ < 16; i_++)                                                    \
+      if ((int)threadIdx.x == i_) v_ = (t).ph[i_];                                     \
+    g_phase_buf[16 * (size_t)blockIdx.x + threadIdx.x] += v_;                          \
+  }
 #else
 #define MG_PHASE_FLUSH(t)
 #endif
@@ -760,20 +769,33 @@ size_t mg_task_buffers_sizeof(void) { return sizeof(mg_task_buffers); }
 size_t mg_sim_params_sizeof(void) { return sizeof(mg_sim_params); }
 size_t mg_state_views_sizeof(void) { return sizeof(mg_state_views); }
 
-// Profiling aid: per-phase shader cycles summed over all waves since the last reset (phase-timing
+// Profiling aid: per-phase shader cycles summed over all waves (blocks < 65536) since the last reset (phase-timing
 // build only; returns MG_EINVAL otherwise).  Phases: 0 FK, 1 ABA (+tendons), 2 collide (+object
 // free step), 3 rows, 4 M~^-1, 5 row responses, 6 PGS, 7 integrate, 8 outputs, 9 task layer +
 // write-back, 13 constraint rows (count), 14 load + pre-physics, 15 substep entry.
 int mg_debug_phase_cycles(uint64_t* out16, int32_t reset) {
 #ifdef MG_PHASE_TIMING
-  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
-  if (out16 && hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase), 16 * sizeof(uint64_t)) != hipSuccess)
-    return fail(MG_EDEVICE, "mg_debug_phase_cycles: copy failed");
-  if (reset) {
-    uint64_t z[16] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess)
-      return fail(MG_EDEVICE, "mg_debug_phase_cycles: reset failed");
+  static unsigned long long* buf = nullptr;
+  const size_t bytes = (size_t)kPhaseCap * 16 * sizeof(unsigned long long);
+  if (!buf) {  // first call: allocate + zero the per-wave rows and publish them to the kernels
+    if (hipMalloc(&buf, bytes) != hipSuccess || hipMemset(buf, 0, bytes) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(g_phase_buf), &buf, sizeof(buf)) != hipSuccess)
+      return fail(MG_EDEVICE, "mg_debug_phase_cycles: buffer setup failed");
+    if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
+    if (out16) memset(out16, 0, 16 * sizeof(uint64_t));
+    return MG_OK;
   }
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
+  if (out16) {
+    std::vector<unsigned long long> h((size_t)kPhaseCap * 16);
+    if (hipMemcpy(h.data(), buf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(MG_EDEVICE, "mg_debug_phase_cycles: copy failed");
+    for (int i = 0; i < 16; i++) out16[i] = 0;
+    for (size_t w = 0; w < (size_t)kPhaseCap; w++)
+      for (int i = 0; i < 16; i++) out16[i] += h[16 * w + i];
+  }
+  if (reset && hipMemset(buf, 0, bytes) != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: reset failed");
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
   return MG_OK;
 #else
   (void)out16;

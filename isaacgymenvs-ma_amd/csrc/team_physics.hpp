@@ -301,16 +301,17 @@ struct Team {
   int ncr;             // contacts of this substep (rows 0 .. 3 ncr - 1 are contact rows)
   V3 org;              // team origin o (root position at the start of the substep)
 #ifdef MG_PHASE_TIMING
-  // shader-clock cycles per solver phase (profiling build only, see build.py --timing)
-  unsigned long long ph[16];
+  // shader-clock cycles per solver phase (profiling build only, see build.py --timing); wave-uniform
+  // 32-bit accumulators so they stay in SGPRs and do not disturb the vector register budget
+  unsigned int ph[16];
   unsigned long long tmark;
   __device__ void ph_start() {
-    for (int i = 0; i < 16; i++) ph[i] = 0;
+    for (int i = 0; i < 16; i++) ph[i] = 0u;
     tmark = __builtin_amdgcn_s_memtime();
   }
   __device__ void ph_mark(int i) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    ph[i] += t1 - tmark;
+    ph[i] = __builtin_amdgcn_readfirstlane(ph[i] + (unsigned int)(t1 - tmark));
     tmark = t1;
   }
 #else
