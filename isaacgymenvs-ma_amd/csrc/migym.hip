@@ -79,20 +79,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
          OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(lds[team].sens, lds[team].dforce);
+  t.outputs(lds[team].u.sv.st.sens, lds[team].u.sv.st.dforce);
   t.stage_state();
   __syncthreads();
   if (valid) {
     mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team];
     if (!m->fixed_base)
-      for (int k = t.tl; k < 13; k += T) root[k] = L.root[k];
+      for (int k = t.tl; k < 13; k += T) root[k] = L.u.sv.st.root[k];
     if (OBJ)
       for (int k = t.tl; k < 13; k += T) root[13 + k] = L.oroot[k];
-    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.dof[k];
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.u.sv.st.dof[k];
     if (v.sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.sens[k];
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.u.sv.st.sens[k];
     if (v.dof_force)
-      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.dforce[k];
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.u.sv.st.dforce[k];
     if (v.rigid_body_states) {
       const int nb = m->num_bodies, nbe = nb + (OBJ ? 2 : 0);
       float* rb = v.rigid_body_states + (size_t)13 * nbe * a;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   }
   t.ph_mark(14);
   for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(L.sens, L.dforce);
+  t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
   t.stage_state();
   __syncthreads();
   t.ph_mark(8);
@@ -274,31 +274,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   if (do_reset) {  // reset_idx: one lane per DOF draws its noise; the leader resets root and potentials
     const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr;
     for (int i = t.tl; i < nd; i += T)
-      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset + a), tb.step_counter, L.dof);
-    if (t.tl == 0) mg::reset_root(&tp, off, L.root, &pot, &prev);
+      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset + a), tb.step_counter, L.u.sv.st.dof);
+    if (t.tl == 0) mg::reset_root(&tp, off, L.u.sv.st.root, &pot, &prev);
     progress = 0;
     reset = 0;
   }
   __syncthreads();
   // observations staged in the row storage (dead after outputs()), then stored coalesced
   const int no = tp.num_obs;
-  float* ost = &L.u.slot[0][0];
+  float* ost = &L.u.sv.rows[0].b;
   if (tp.task_id == MG_TASK_CARTPOLE) {
-    if (t.tl < 4) ost[t.tl] = L.dof[t.tl];
+    if (t.tl < 4) ost[t.tl] = L.u.sv.st.dof[t.tl];
   } else {
-    if (t.tl == 0) mg::obs_head(&tp, off, L.root, &pot, &prev, up, hd, ost);
+    if (t.tl == 0) mg::obs_head(&tp, off, L.u.sv.st.root, &pot, &prev, up, hd, ost);
     const bool hum = tp.task_id == MG_TASK_HUMANOID;
     for (int q = t.tl; q < nd; q += T) {
-      ost[12 + q] = mg::t_unscale(L.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
-      ost[12 + nd + q] = L.dof[2 * q + 1] * tp.dof_vel_scale;
-      if (hum) ost[12 + 2 * nd + q] = L.dforce[q] * tp.contact_force_scale;
+      ost[12 + q] = mg::t_unscale(L.u.sv.st.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
+      ost[12 + nd + q] = L.u.sv.st.dof[2 * q + 1] * tp.dof_vel_scale;
+      if (hum) ost[12 + 2 * nd + q] = L.u.sv.st.dforce[q] * tp.contact_force_scale;
     }
     const int bs = 12 + (hum ? 3 : 2) * nd, nss = mg::t_sensors(&tp);
-    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.sens[q] * tp.contact_force_scale;
+    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.u.sv.st.sens[q] * tp.contact_force_scale;
     if (alane) ost[bs + 6 * nss + t.tl] = act_l;
   }
   if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
-    const float px = L.root[0], py = L.root[1], pz = L.root[2];
+    const float px = L.u.sv.st.root[0], py = L.u.sv.st.root[1], pz = L.u.sv.st.root[2];
     const int base = no - 3 * (A - 1);
     for (int j = 1; j < A; j++) {
       const int src = (team - k + (k + j) % A) * T;
@@ -360,12 +360,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   __syncthreads();
   if (valid) {  // state write-back (gym layouts), team-cooperative
     if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
-      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.root[q];
-    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.dof[q];
+      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
+    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.u.sv.st.dof[q];
     if (v.sensors)
-      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.sens[q];
+      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.u.sv.st.sens[q];
     if (v.dof_force)
-      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.dforce[q];
+      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t)
@@ -595,7 +595,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   // ---- gym.simulate
   t.ph_mark(14);
   for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(L.sens, L.dforce);
+  t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
   t.stage_state();
   __syncthreads();
   t.ph_mark(8);
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         t.body_state(b, b13);
         x = b13[c];
       } else {
-        x = mg::h_obs_value(tp, seg, i, L.dof, L.dforce, L.oroot, gs, qdiff, L.sens, nullptr);
+        x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
       }
       L.obs[k] = x;
     }
@@ -668,16 +668,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       root[26 + k] = L.goal[k];
       tb.goal_states[(size_t)13 * e + k] = L.goal[13 + k];
     }
-    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.dof[k];
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.u.sv.st.dof[k];
     if (t.node > 0) {
       const int d = t.node - 1;
       const_cast<float*>(v.dof_targets)[(size_t)nd * e + d] = t.tgt;
       tb.prev_targets[(size_t)nd * e + d] = prev;
     }
     if (v.sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.sens[k];
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.u.sv.st.sens[k];
     if (v.dof_force)
-      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.dforce[k];
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.u.sv.st.dforce[k];
     for (int b = t.tl; b < nb; b += T) t.body_state(b, rbs + 13 * b);
     for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
   }
@@ -744,7 +744,7 @@ struct RunEnvStep {
   static int run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
     const int E = kBlock / T;
     // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
-    if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u))
+    if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
       return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
     if constexpr (OBJ) {
       hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
@@ -771,7 +771,7 @@ size_t mg_state_views_sizeof(void) { return sizeof(mg_state_views); }
 
 // Profiling aid: per-phase shader cycles summed over all waves (blocks < 65536) since the last reset (phase-timing
 // build only; returns MG_EINVAL otherwise).  Phases: 0 FK, 1 ABA (+tendons), 2 collide (+object
-// free step), 3 rows, 4 M~^-1, 5 row responses, 6 PGS, 7 integrate, 8 outputs, 9 task layer +
+// free step), 3 rows, 4 row Jacobians / W, 5 test solves, 6 PGS, 7 integrate, 8 outputs, 9 task layer +
 // write-back, 13 constraint rows (count), 14 load + pre-physics, 15 substep entry.
 int mg_debug_phase_cycles(uint64_t* out16, int32_t reset) {
 #ifdef MG_PHASE_TIMING

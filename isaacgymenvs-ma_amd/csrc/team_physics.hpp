@@ -109,17 +109,15 @@ template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
   static constexpr int MRO = OBJ ? MR : 1;
+  static constexpr int RB = 3;  // right-hand sides per test solve (the 3 rows of a contact)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
   float S[MN][6];
   float U[MN][6];
   float Dinv[MN];
-  float acc[MN][6];
-  float ut[MN];
   unsigned long long anc[MN];
   float L0[21];
-  float proot[6];
   float Iinv[36];
   int ncon, nrows;
   // contacts: point, frame (normal + tangent basis), gap, sides (nodes / geoms)
@@ -127,18 +125,35 @@ struct TeamLDS {
   int cside[MC];  // packed int8 [node A, node B, geom A, geom B] (-1 none, -2 the free object)
   // joint-limit rows (after the 3 rows per contact): kind | node << 4
   int lmeta[2 * (MN - 1)];
-  // The ABA's child slots are dead once the tree pass is done; the constraint rows reuse them:
-  // per row {target b, 1/W, impulse, kind (0 normal, 1 friction, 2 limit)}, one 16-byte LDS read.
+  // The ABA's child slots are dead once its backward pass is done.  The same storage then holds the
+  // forward-pass / test-solve accelerations (RB right-hand sides; slab 0 is the ABA's), and behind
+  // them the constraint rows: per row {target b, 1/W, impulse, kind (0 normal, 1 friction, 2 limit)},
+  // one 16-byte LDS read.  After the last substep the post-step staging (root row, DOF state, sensor
+  // and DOF forces) takes the accelerations' place; the rows region becomes the observation staging
+  // once the outputs have read the impulses.
   struct alignas(16) Row { float b, iw, lam, kind; };
+  struct Solve {
+    float acc[RB][MN][6];
+    float ut[RB][MN];
+    float proot[RB][6];
+  };
+  struct Stage {
+    float root[13];
+    float dof[2 * MN];
+    float sens[6 * MG_MAX_SENSORS];
+    float dforce[MN];
+  };
+  static_assert(sizeof(Stage) <= sizeof(Solve), "staging must fit the test-solve storage");
   union {
     float slot[MN][27];
-    Row rows[MR];
+    struct {
+      union {
+        Solve ts;
+        Stage st;
+      };
+      Row rows[MR];
+    } sv;
   } u;
-  // task-layer staging (root / dof state of the actor after the physics)
-  float root[13];
-  float dof[2 * MN];
-  float sens[6 * MG_MAX_SENSORS];
-  float dforce[MN];
   // free object (OBJ): Jacobian rows on its columns, staged root row, obs staging
   float rwo[MRO][6];
   float oroot[OBJ ? 13 : 1];
@@ -510,10 +525,10 @@ struct Team {
     if (tl == 0) {
       if (freeb) {
         chol6(IA, s->L0);
-        s->proot[0] = pA.a.x; s->proot[1] = pA.a.y; s->proot[2] = pA.a.z;
-        s->proot[3] = pA.l.x; s->proot[4] = pA.l.y; s->proot[5] = pA.l.z;
+        s->u.sv.ts.proot[0][0] = pA.a.x; s->u.sv.ts.proot[0][1] = pA.a.y; s->u.sv.ts.proot[0][2] = pA.a.z;
+        s->u.sv.ts.proot[0][3] = pA.l.x; s->u.sv.ts.proot[0][4] = pA.l.y; s->u.sv.ts.proot[0][5] = pA.l.z;
       } else {
-        for (int k = 0; k < 6; k++) s->acc[0][k] = 0.0f;
+        for (int k = 0; k < 6; k++) s->u.sv.ts.acc[0][0][k] = 0.0f;
       }
     }
     __syncthreads();
@@ -526,25 +541,25 @@ struct Team {
       float a = 0.0f;
       for (int k = 0; k < 6; k++) {
         s->Iinv[6 * k + tl] = cv[k];
-        a -= cv[k] * s->proot[k];
+        a -= cv[k] * s->u.sv.ts.proot[0][k];
       }
-      s->acc[0][tl] = a;
+      s->u.sv.ts.acc[0][0][tl] = a;
     }
     __syncthreads();
     float qdd = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
-        SV ap = sv(ld3(s->acc[par]), ld3(s->acc[par] + 3)) + c;
+        SV ap = sv(ld3(s->u.sv.ts.acc[0][par]), ld3(s->u.sv.ts.acc[0][par] + 3)) + c;
         qdd = (u - dot(U, ap)) * Dinv;
         SV a = ap + S * qdd;
-        s->acc[node][0] = a.a.x; s->acc[node][1] = a.a.y; s->acc[node][2] = a.a.z;
-        s->acc[node][3] = a.l.x; s->acc[node][4] = a.l.y; s->acc[node][5] = a.l.z;
+        s->u.sv.ts.acc[0][node][0] = a.a.x; s->u.sv.ts.acc[0][node][1] = a.a.y; s->u.sv.ts.acc[0][node][2] = a.a.z;
+        s->u.sv.ts.acc[0][node][3] = a.l.x; s->u.sv.ts.acc[0][node][4] = a.l.y; s->u.sv.ts.acc[0][node][5] = a.l.z;
       }
       __syncthreads();
     }
     // nu* = nu + h * acc
     if (tl < nv) {
-      float a = (freeb && tl < 6) ? s->acc[0][tl] : qdd;
+      float a = (freeb && tl < 6) ? s->u.sv.ts.acc[0][0][tl] : qdd;
       nu += h * a;
     }
   }
@@ -595,57 +610,92 @@ struct Team {
     return k == 0 ? y.x : k == 1 ? y.y : y.z;
   }
 
-  // ---------------------------------------------------------------- test solve: Y = M~^-1 (J^T) column into lane regs
-  // generalized force: spatial force fw on nodeA (and -fw on nodeB), plus unit joint force sg on node jn.
-  __device__ float test_solve(int nodeA, int nodeB, SV fw, int jn, float sg) {
-    if (node > 0) s->ut[node] = 0.0f;
+  // ---------------------------------------------------------------- test solves: Y = M~^-1 J^T, RB rows at once
+  // Right-hand side q is row r0 + q: spatial force -fw on its node A and +fw on node B (contact rows) or a
+  // unit joint force +-1 on node jn (limit rows).  Lane q < RB walks its own paths to the root (private
+  // ut / proot slabs, so the walks run in parallel); the root solve and the level-synchronous forward
+  // pass then carry the RB columns together.  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
+  __device__ void test_solve(int r0, int nrows_, float* y) {
+    typename L::Solve& ts = s->u.sv.ts;
+    for (int i = tl; i < L::RB * MN; i += T) (&ts.ut[0][0])[i] = 0.0f;
     __syncthreads();
-    if (tl == 0) {
+    if (tl < L::RB) {
+      const int r = r0 + tl;
       SV proot = szero();
-      for (int side = 0; side < 3; side++) {
-        int k;
-        SV pv;
-        float tq = 0.0f;
-        if (side == 0) { k = nodeA; pv = fw * -1.0f; }
-        else if (side == 1) { k = nodeB; pv = fw; }
-        else { k = jn; pv = szero(); tq = sg; }
-        if (k < 0 || (side == 2 && k == 0)) continue;
-        while (k > 0) {
-          SV Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3));
-          SV Uk = sv(ld3(s->U[k]), ld3(s->U[k] + 3));
-          float uk = tq - dot(Sk, pv);
-          s->ut[k] += uk;
-          pv = pv + Uk * (uk * s->Dinv[k]);
-          tq = 0.0f;
-          k = mt->parent[k];
+      if (r < nrows_) {
+        const int kind = row_kind(r);
+        int nodeA = -1, nodeB = -1, jn = -1;
+        float sg = 0.0f;
+        SV fw = szero();
+        if (kind >= 2) {
+          jn = row_ref(r);
+          sg = kind == 2 ? 1.0f : -1.0f;
+        } else {
+          const int c = r / 3;
+          nodeA = cside(c, 0);
+          nodeB = cside(c, 1);
+          float w[6];
+          row_w(r, w);
+          fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
         }
-        proot = proot + pv;
+        float* ut = ts.ut[tl];
+        for (int side = 0; side < 3; side++) {
+          int k;
+          SV pv;
+          float tq = 0.0f;
+          if (side == 0) { k = nodeA; pv = fw * -1.0f; }
+          else if (side == 1) { k = nodeB; pv = fw; }
+          else { k = jn; pv = szero(); tq = sg; }
+          if (k < 0 || (side == 2 && k == 0)) continue;
+          while (k > 0) {
+            SV Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3));
+            SV Uk = sv(ld3(s->U[k]), ld3(s->U[k] + 3));
+            float uk = tq - dot(Sk, pv);
+            ut[k] += uk;
+            pv = pv + Uk * (uk * s->Dinv[k]);
+            tq = 0.0f;
+            k = mt->parent[k];
+          }
+          proot = proot + pv;
+        }
       }
-      s->proot[0] = proot.a.x; s->proot[1] = proot.a.y; s->proot[2] = proot.a.z;
-      s->proot[3] = proot.l.x; s->proot[4] = proot.l.y; s->proot[5] = proot.l.z;
-      if (!freeb)
-        for (int q = 0; q < 6; q++) s->acc[0][q] = 0.0f;
+      float* pr = ts.proot[tl];
+      pr[0] = proot.a.x; pr[1] = proot.a.y; pr[2] = proot.a.z;
+      pr[3] = proot.l.x; pr[4] = proot.l.y; pr[5] = proot.l.z;
     }
     __syncthreads();
-    if (freeb && tl < 6) {
+    for (int i = tl; i < 6 * L::RB; i += T) {  // root: a0 = -IA0^-1 p0 (free base) or 0
+      const int q = i / 6, c = i - 6 * q;
       float a = 0.0f;
-      for (int q = 0; q < 6; q++) a -= s->Iinv[6 * tl + q] * s->proot[q];
-      s->acc[0][tl] = a;
+      if (freeb)
+        for (int j = 0; j < 6; j++) a -= s->Iinv[6 * c + j] * ts.proot[q][j];
+      ts.acc[q][0][c] = a;
     }
     __syncthreads();
-    float y = 0.0f;
+    float yv[L::RB];
+#pragma unroll
+    for (int q = 0; q < L::RB; q++) yv[q] = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
-        SV ap = sv(ld3(s->acc[par]), ld3(s->acc[par] + 3));
-        y = (s->ut[node] - dot(U, ap)) * Dinv;
-        SV a = ap + S * y;
-        s->acc[node][0] = a.a.x; s->acc[node][1] = a.a.y; s->acc[node][2] = a.a.z;
-        s->acc[node][3] = a.l.x; s->acc[node][4] = a.l.y; s->acc[node][5] = a.l.z;
+#pragma unroll
+        for (int q = 0; q < L::RB; q++) {
+          const float* ac = ts.acc[q][par];
+          SV ap = sv(ld3(ac), ld3(ac + 3));
+          const float yq = (ts.ut[q][node] - dot(U, ap)) * Dinv;
+          SV a = ap + S * yq;
+          float* an = ts.acc[q][node];
+          an[0] = a.a.x; an[1] = a.a.y; an[2] = a.a.z;
+          an[3] = a.l.x; an[4] = a.l.y; an[5] = a.l.z;
+          yv[q] = yq;
+        }
       }
       __syncthreads();
     }
-    if (freeb && tl < 6) y = s->acc[0][tl];
-    return tl < nv ? y : 0.0f;
+#pragma unroll
+    for (int q = 0; q < L::RB; q++) {
+      float v = (freeb && tl < 6) ? ts.acc[q][0][tl] : yv[q];
+      y[q] = tl < nv ? v : 0.0f;
+    }
   }
 
   // side k of contact c: 0 node A, 1 node B, 2 geom A, 3 geom B
@@ -950,9 +1000,9 @@ struct Team {
       s->ct2[c][0] = t2.x; s->ct2[c][1] = t2.y; s->ct2[c][2] = t2.z;
       float deff = s->cd[c] - p->rest_offset;
       float bn = deff >= 0.0f ? -deff / h : fminf(-p->baumgarte * deff / h, p->max_depen_vel);
-      s->u.rows[3 * c].b = bn;
-      s->u.rows[3 * c + 1].b = 0.0f;
-      s->u.rows[3 * c + 2].b = 0.0f;
+      s->u.sv.rows[3 * c].b = bn;
+      s->u.sv.rows[3 * c + 1].b = 0.0f;
+      s->u.sv.rows[3 * c + 2].b = 0.0f;
       if (OBJ) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
         const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
         V3 dirs[3] = {n, t1, t2};
@@ -982,7 +1032,7 @@ struct Team {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
       float d = side == 0 ? dl : du;
-      s->u.rows[3 * ncon + li].b = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
+      s->u.sv.rows[3 * ncon + li].b = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
       s->lmeta[li] = (2 + side) | (node << 4);
       li++;
     }
@@ -1015,40 +1065,34 @@ struct Team {
     // W_r = J_r . Y_r.  Lane j keeps (J_r[j], Y_r[j]) of every row in private arrays for the sweeps;
     // rows past this team's count get J = Y = 0 and zero scalars, so the sweeps need no row mask.
     float Jcol[MR], Ycol[MR];
-    for (int r = 0; r < wave_rows; r++) {
-      const bool active = r < nrows;
-      const int kind = active ? row_kind(r) : 0;
-      int A = -1, B = -1, jn = -1;
-      float sg = 0.0f;
-      SV fw = szero();
-      if (active) {
-        if (kind >= 2) {
-          jn = row_ref(r);
-          sg = kind == 2 ? 1.0f : -1.0f;
-        } else {
-          const int c = r / 3;
-          A = cside(c, 0);
-          B = cside(c, 1);
-          float w[6];
-          row_w(r, w);
-          fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
+    for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
+      float yb[L::RB];
+      test_solve(r0, nrows, yb);
+      ph_mark(5);
+#pragma unroll
+      for (int q = 0; q < L::RB; q++) {
+        const int r = r0 + q;
+        if (r < wave_rows) {
+          const bool active = r < nrows;
+          const int kind = active ? row_kind(r) : 0;
+          float y = yb[q];
+          if (OBJ && objl) y = (active && kind < 2) ? obj_response(r) : 0.0f;
+          y = active ? y : 0.0f;
+          const int code = active ? jac_code(r) : 0;
+          const float J = active ? jac_value(r, code) : 0.0f;
+          Ycol[r] = y;
+          Jcol[r] = J;
+          const float Wr = team_sum<T>(J * y, tb);
+          if (tl == 0) {
+            typename L::Row& rw = s->u.sv.rows[r];
+            rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
+            rw.lam = 0.0f;
+            rw.kind = kind >= 2 ? 2.0f : (float)kind;
+            if (!active) rw.b = 0.0f;
+          }
         }
       }
-      float y = test_solve(A, B, fw, jn, sg);
-      if (OBJ && objl) y = (active && kind < 2) ? obj_response(r) : 0.0f;
-      y = active ? y : 0.0f;
-      const int code = active ? jac_code(r) : 0;
-      const float J = active ? jac_value(r, code) : 0.0f;
-      Ycol[r] = y;
-      Jcol[r] = J;
-      const float Wr = team_sum<T>(J * y, tb);
-      if (tl == 0) {
-        typename L::Row& rw = s->u.rows[r];
-        rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
-        rw.lam = 0.0f;
-        rw.kind = kind >= 2 ? 2.0f : (float)kind;
-        if (!active) rw.b = 0.0f;
-      }
+      ph_mark(4);
     }
     // a sweep shorter than the prefetch depth would read a row's impulse before its previous visit
     // wrote it: pad it with zero rows (J = Y = 0, 1/W = 0: skipped, as the oracle skips W = 0 rows)
@@ -1057,7 +1101,7 @@ struct Team {
     for (int r = wave_rows; r < prow; r++) {
       Ycol[r] = 0.0f;
       Jcol[r] = 0.0f;
-      if (tl == 0) s->u.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, 0.0f};
+      if (tl == 0) s->u.sv.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, 0.0f};
     }
     __syncthreads();
     ph_mark(5);
@@ -1076,7 +1120,7 @@ struct Team {
       if (k < nvis) {
         pJ[k] = Jcol[rq];
         pY[k] = Ycol[rq];
-        pR[k] = s->u.rows[rq];
+        pR[k] = s->u.sv.rows[rq];
         rq = rq + 1 == prow ? 0 : rq + 1;
       }
     }
@@ -1093,13 +1137,13 @@ struct Team {
           lnew = kd == 1.0f ? fminf(fmaxf(lnew, -lim), lim) : fmaxf(lnew, 0.0f);
           if (iw == 0.0f) lnew = lam;  // W <= 1e-12 (or a padding row): skipped (oracle)
           if (kd == 0.0f) lamn = lnew;
-          if (tl == 0) s->u.rows[r].lam = lnew;
+          if (tl == 0) s->u.sv.rows[r].lam = lnew;
           nu += pY[k] * (lnew - lam);
           r = r + 1 == prow ? 0 : r + 1;
           if (v0 + k + PF < nvis) {
             pJ[k] = Jcol[rq];
             pY[k] = Ycol[rq];
-            pR[k] = s->u.rows[rq];
+            pR[k] = s->u.sv.rows[rq];
             rq = rq + 1 == prow ? 0 : rq + 1;
           }
         }
@@ -1185,7 +1229,7 @@ struct Team {
         if (sg == 0.0f) continue;
         V3 n = ld3(s->cn[c]), t1, t2;
         tangent_basis_t(n, &t1, &t2);
-        V3 f = (n * s->u.rows[3 * c].lam + t1 * s->u.rows[3 * c + 1].lam + t2 * s->u.rows[3 * c + 2].lam) * (sg / h);
+        V3 f = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) * (sg / h);
         F = F + f;
         Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
       }
@@ -1205,8 +1249,8 @@ struct Team {
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
         const int meta = s->lmeta[r - 3 * s->ncon];
         if ((meta >> 4) != node) continue;
-        if ((meta & 3) == 2) t += s->u.rows[r].lam / h;
-        if ((meta & 3) == 3) t -= s->u.rows[r].lam / h;
+        if ((meta & 3) == 2) t += s->u.sv.rows[r].lam / h;
+        if ((meta & 3) == 3) t -= s->u.sv.rows[r].lam / h;
       }
       dforce_out[node - 1] = t;
     }
@@ -1253,20 +1297,20 @@ struct Team {
     float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
     float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
     if (tl == 0) {
-      s->root[0] = p0.x; s->root[1] = p0.y; s->root[2] = p0.z;
-      for (int k = 0; k < 4; k++) s->root[3 + k] = q0[k];
+      s->u.sv.st.root[0] = p0.x; s->u.sv.st.root[1] = p0.y; s->u.sv.st.root[2] = p0.z;
+      for (int k = 0; k < 4; k++) s->u.sv.st.root[3 + k] = q0[k];
       if (freeb) {
         M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
         V3 cw = mul(Rr, ld3(m->body_com[0]));
         V3 om = v3(w0, w1, w2);
         V3 vc = v3(v0, v1, v2) + cross(om, cw);
-        s->root[7] = vc.x; s->root[8] = vc.y; s->root[9] = vc.z;
-        s->root[10] = om.x; s->root[11] = om.y; s->root[12] = om.z;
+        s->u.sv.st.root[7] = vc.x; s->u.sv.st.root[8] = vc.y; s->u.sv.st.root[9] = vc.z;
+        s->u.sv.st.root[10] = om.x; s->u.sv.st.root[11] = om.y; s->u.sv.st.root[12] = om.z;
       }
     }
     if (node > 0) {
-      s->dof[2 * (node - 1)] = qj;
-      s->dof[2 * (node - 1) + 1] = nu;
+      s->u.sv.st.dof[2 * (node - 1)] = qj;
+      s->u.sv.st.dof[2 * (node - 1) + 1] = nu;
     }
     if (OBJ) {
       const float o0 = __shfl(nu, tb + ob0), o1 = __shfl(nu, tb + ob0 + 1), o2 = __shfl(nu, tb + ob0 + 2);
