@@ -640,21 +640,40 @@ struct Team {
         }
         float* ut = ts.ut[tl];
         for (int side = 0; side < 3; side++) {
-          int k;
+          int k0;
           SV pv;
           float tq = 0.0f;
-          if (side == 0) { k = nodeA; pv = fw * -1.0f; }
-          else if (side == 1) { k = nodeB; pv = fw; }
-          else { k = jn; pv = szero(); tq = sg; }
-          if (k < 0 || (side == 2 && k == 0)) continue;
-          while (k > 0) {
-            SV Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3));
-            SV Uk = sv(ld3(s->U[k]), ld3(s->U[k] + 3));
-            float uk = tq - dot(Sk, pv);
-            ut[k] += uk;
-            pv = pv + Uk * (uk * s->Dinv[k]);
+          if (side == 0) { k0 = nodeA; pv = fw * -1.0f; }
+          else if (side == 1) { k0 = nodeB; pv = fw; }
+          else { k0 = jn; pv = szero(); tq = sg; }
+          if (k0 < 0 || (side == 2 && k0 == 0)) continue;
+          if (k0 == 0) {  // force on the root body: straight into the root's bias
+            proot = proot + pv;
+            continue;
+          }
+          // the path to the root is the ancestor mask (parents precede children, checked at sim
+          // creation), so the next node's S / U / D^-1 are loaded while this one is processed; the
+          // ut accumulations are fire-and-forget LDS adds (program order per lane, as the oracle)
+          unsigned long long path = s->anc[k0] & ~1ull;
+          int k = 63 - __builtin_clzll(path);
+          SV Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3)), Uk = sv(ld3(s->U[k]), ld3(s->U[k] + 3));
+          float Dk = s->Dinv[k];
+          while (true) {
+            path &= ~(1ull << k);
+            const int kn = path ? 63 - __builtin_clzll(path) : 0;
+            SV Sn = Sk, Un = Uk;
+            float Dn = Dk;
+            if (kn > 0) {
+              Sn = sv(ld3(s->S[kn]), ld3(s->S[kn] + 3));
+              Un = sv(ld3(s->U[kn]), ld3(s->U[kn] + 3));
+              Dn = s->Dinv[kn];
+            }
+            const float uk = tq - dot(Sk, pv);
+            atomicAdd(&ut[k], uk);
+            pv = pv + Uk * (uk * Dk);
             tq = 0.0f;
-            k = mt->parent[k];
+            if (kn == 0) break;
+            k = kn; Sk = Sn; Uk = Un; Dk = Dn;
           }
           proot = proot + pv;
         }
@@ -733,6 +752,42 @@ struct Team {
     row_w(r, w);
     const float d = Sl[0] * w[0] + Sl[1] * w[1] + Sl[2] * w[2] + Sl[3] * w[3] + Sl[4] * w[4] + Sl[5] * w[5];
     return code == 1 ? d : -d;
+  }
+
+  // J_r[lane] for the RB rows r0 .. r0 + RB - 1 of a test-solve batch.  Contact rows come in aligned
+  // triples (n, t1, t2 of contact r0 / 3): they share the lane's sign and the point-velocity vector
+  // g = Sl_ang x (p - o) + Sl_lin, so J_r = sign (d_r . g) (= sign Sl . [(p - o) x d_r; d_r]).
+  // Limit rows: +-1 on the DOF's lane.  Object lanes: the stored object part of the contact rows.
+  __device__ void batch_jacobians(int r0, int nrows_, float* J) const {
+#pragma unroll
+    for (int q = 0; q < L::RB; q++) J[q] = 0.0f;
+    if (OBJ && objl) {
+      if (r0 < 3 * ncr)
+        for (int q = 0; q < L::RB; q++) J[q] = s->rwo[r0 + q][tl - ob0];
+      return;
+    }
+    if (tl >= nv) return;
+    if (r0 < 3 * ncr) {
+      const int c = r0 / 3, A = cside(c, 0), B = cside(c, 1);
+      float sgn;
+      if (freeb && tl < 6) sgn = (A >= 0 ? 1.0f : 0.0f) - (B >= 0 ? 1.0f : 0.0f);
+      else if (node <= 0) return;
+      else sgn = (in_path(A, node) ? 1.0f : 0.0f) - (in_path(B, node) ? 1.0f : 0.0f);
+      if (sgn == 0.0f) return;
+      const V3 g = cross(v3(Sl[0], Sl[1], Sl[2]), ld3(s->cp[c]) - org) + v3(Sl[3], Sl[4], Sl[5]);
+      J[0] = sgn * dot(ld3(s->cn[c]), g);
+      J[1] = sgn * dot(ld3(s->ct1[c]), g);
+      J[2] = sgn * dot(ld3(s->ct2[c]), g);
+    } else {
+#pragma unroll
+      for (int q = 0; q < L::RB; q++) {
+        const int r = r0 + q;
+        if (r < nrows_ && node > 0) {
+          const int meta = s->lmeta[r - 3 * ncr];
+          if ((meta >> 4) == node) J[q] = (meta & 3) == 2 ? 1.0f : -1.0f;
+        }
+      }
+    }
   }
 
   // ---------------------------------------------------------------- collision -> LDS contact list
@@ -1066,7 +1121,8 @@ struct Team {
     // rows past this team's count get J = Y = 0 and zero scalars, so the sweeps need no row mask.
     float Jcol[MR], Ycol[MR];
     for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
-      float yb[L::RB];
+      float jb[L::RB], yb[L::RB];
+      batch_jacobians(r0, nrows, jb);
       test_solve(r0, nrows, yb);
       ph_mark(5);
 #pragma unroll
@@ -1074,12 +1130,11 @@ struct Team {
         const int r = r0 + q;
         if (r < wave_rows) {
           const bool active = r < nrows;
-          const int kind = active ? row_kind(r) : 0;
+          const bool contact = r < 3 * ncr;
           float y = yb[q];
-          if (OBJ && objl) y = (active && kind < 2) ? obj_response(r) : 0.0f;
+          if (OBJ && objl) y = contact ? obj_response(r) : 0.0f;
           y = active ? y : 0.0f;
-          const int code = active ? jac_code(r) : 0;
-          const float J = active ? jac_value(r, code) : 0.0f;
+          const float J = jb[q];
           Ycol[r] = y;
           Jcol[r] = J;
           const float Wr = team_sum<T>(J * y, tb);
@@ -1087,7 +1142,7 @@ struct Team {
             typename L::Row& rw = s->u.sv.rows[r];
             rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
             rw.lam = 0.0f;
-            rw.kind = kind >= 2 ? 2.0f : (float)kind;
+            rw.kind = contact ? (q == 0 ? 0.0f : 1.0f) : 2.0f;
             if (!active) rw.b = 0.0f;
           }
         }
