@@ -127,11 +127,11 @@ struct TeamLDS {
   int lmeta[2 * (MN - 1)];
   // The ABA's child slots are dead once its backward pass is done.  The same storage then holds the
   // forward-pass / test-solve accelerations (RB right-hand sides; slab 0 is the ABA's), and behind
-  // them the constraint rows: per row {target b, 1/W, impulse, kind (0 normal, 1 friction, 2 limit)},
+  // them the constraint rows: per row {target b, 1/W, impulse, mu (friction: the coefficient; -1 normal, -2 limit)},
   // one 16-byte LDS read.  After the last substep the post-step staging (root row, DOF state, sensor
   // and DOF forces) takes the accelerations' place; the rows region becomes the observation staging
   // once the outputs have read the impulses.
-  struct alignas(16) Row { float b, iw, lam, kind; };
+  struct alignas(16) Row { float b, iw, lam, mu; };
   struct Solve {
     float acc[RB][MN][6];
     float ut[RB][MN];
@@ -1142,7 +1142,7 @@ struct Team {
             typename L::Row& rw = s->u.sv.rows[r];
             rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
             rw.lam = 0.0f;
-            rw.kind = contact ? (q == 0 ? 0.0f : 1.0f) : 2.0f;
+            rw.mu = contact ? (q == 0 ? -1.0f : p->friction) : -2.0f;
             if (!active) rw.b = 0.0f;
           }
         }
@@ -1156,7 +1156,7 @@ struct Team {
     for (int r = wave_rows; r < prow; r++) {
       Ycol[r] = 0.0f;
       Jcol[r] = 0.0f;
-      if (tl == 0) s->u.sv.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, 0.0f};
+      if (tl == 0) s->u.sv.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};
     }
     __syncthreads();
     ph_mark(5);
@@ -1186,12 +1186,13 @@ struct Team {
       for (int k = 0; k < PF; k++) {
         if (v0 + k < nvis) {
           const float v = team_sum<T>(pJ[k] * nu, tb);
-          const float lam = pR[k].lam, iw = pR[k].iw, kd = pR[k].kind;
-          float lnew = lam + (pR[k].b - v) * iw;
-          const float lim = mu * lamn;
-          lnew = kd == 1.0f ? fminf(fmaxf(lnew, -lim), lim) : fmaxf(lnew, 0.0f);
-          if (iw == 0.0f) lnew = lam;  // W <= 1e-12 (or a padding row): skipped (oracle)
-          if (kd == 0.0f) lamn = lnew;
+          const float lam = pR[k].lam, m = pR[k].mu;
+          // friction rows (m = mu >= 0): clamp to +-mu lambda_n; normal / limit rows (m < 0): >= 0.
+          // Rows with 1/W = 0 keep lambda = 0 without a test: lam + (b - v) * 0 = 0 clamps to 0.
+          const float t = fmaxf(m, 0.0f) * lamn;
+          float lnew = fmaxf(lam + (pR[k].b - v) * pR[k].iw, -t);
+          lnew = m >= 0.0f ? fminf(lnew, t) : lnew;
+          lamn = m == -1.0f ? lnew : lamn;
           if (tl == 0) s->u.sv.rows[r].lam = lnew;
           nu += pY[k] * (lnew - lam);
           r = r + 1 == prow ? 0 : r + 1;
