@@ -109,7 +109,7 @@ template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
   static constexpr int MRO = OBJ ? MR : 1;
-  static constexpr int RB = 3;  // right-hand sides per test solve (the 3 rows of a contact)
+  static constexpr int RB = 6;  // right-hand sides per test solve (the rows of 2 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -133,9 +133,17 @@ struct TeamLDS {
   // once the outputs have read the impulses.
   struct alignas(16) Row { float b, iw, lam, mu; };
   struct Solve {
-    float acc[RB][MN][6];
-    float ut[RB][MN];
-    float proot[RB][6];
+    union {
+      struct {
+        float acc[MN][6];  // ABA forward pass
+        float proot[6];
+      } aba;
+      struct {
+        float ut[RB][MN];   // test solves: joint-space forces of the RB columns,
+        float proot[RB][6]; // their root biases and root accelerations
+        float a0[RB][6];
+      } ts;
+    };
   };
   struct Stage {
     float root[13];
@@ -525,10 +533,10 @@ struct Team {
     if (tl == 0) {
       if (freeb) {
         chol6(IA, s->L0);
-        s->u.sv.ts.proot[0][0] = pA.a.x; s->u.sv.ts.proot[0][1] = pA.a.y; s->u.sv.ts.proot[0][2] = pA.a.z;
-        s->u.sv.ts.proot[0][3] = pA.l.x; s->u.sv.ts.proot[0][4] = pA.l.y; s->u.sv.ts.proot[0][5] = pA.l.z;
+        s->u.sv.ts.aba.proot[0] = pA.a.x; s->u.sv.ts.aba.proot[1] = pA.a.y; s->u.sv.ts.aba.proot[2] = pA.a.z;
+        s->u.sv.ts.aba.proot[3] = pA.l.x; s->u.sv.ts.aba.proot[4] = pA.l.y; s->u.sv.ts.aba.proot[5] = pA.l.z;
       } else {
-        for (int k = 0; k < 6; k++) s->u.sv.ts.acc[0][0][k] = 0.0f;
+        for (int k = 0; k < 6; k++) s->u.sv.ts.aba.acc[0][k] = 0.0f;
       }
     }
     __syncthreads();
@@ -541,25 +549,25 @@ struct Team {
       float a = 0.0f;
       for (int k = 0; k < 6; k++) {
         s->Iinv[6 * k + tl] = cv[k];
-        a -= cv[k] * s->u.sv.ts.proot[0][k];
+        a -= cv[k] * s->u.sv.ts.aba.proot[k];
       }
-      s->u.sv.ts.acc[0][0][tl] = a;
+      s->u.sv.ts.aba.acc[0][tl] = a;
     }
     __syncthreads();
     float qdd = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
-        SV ap = sv(ld3(s->u.sv.ts.acc[0][par]), ld3(s->u.sv.ts.acc[0][par] + 3)) + c;
+        SV ap = sv(ld3(s->u.sv.ts.aba.acc[par]), ld3(s->u.sv.ts.aba.acc[par] + 3)) + c;
         qdd = (u - dot(U, ap)) * Dinv;
         SV a = ap + S * qdd;
-        s->u.sv.ts.acc[0][node][0] = a.a.x; s->u.sv.ts.acc[0][node][1] = a.a.y; s->u.sv.ts.acc[0][node][2] = a.a.z;
-        s->u.sv.ts.acc[0][node][3] = a.l.x; s->u.sv.ts.acc[0][node][4] = a.l.y; s->u.sv.ts.acc[0][node][5] = a.l.z;
+        s->u.sv.ts.aba.acc[node][0] = a.a.x; s->u.sv.ts.aba.acc[node][1] = a.a.y; s->u.sv.ts.aba.acc[node][2] = a.a.z;
+        s->u.sv.ts.aba.acc[node][3] = a.l.x; s->u.sv.ts.aba.acc[node][4] = a.l.y; s->u.sv.ts.aba.acc[node][5] = a.l.z;
       }
       __syncthreads();
     }
     // nu* = nu + h * acc
     if (tl < nv) {
-      float a = (freeb && tl < 6) ? s->u.sv.ts.acc[0][0][tl] : qdd;
+      float a = (freeb && tl < 6) ? s->u.sv.ts.aba.acc[0][tl] : qdd;
       nu += h * a;
     }
   }
@@ -613,10 +621,12 @@ struct Team {
   // ---------------------------------------------------------------- test solves: Y = M~^-1 J^T, RB rows at once
   // Right-hand side q is row r0 + q: spatial force -fw on its node A and +fw on node B (contact rows) or a
   // unit joint force +-1 on node jn (limit rows).  Lane q < RB walks its own paths to the root (private
-  // ut / proot slabs, so the walks run in parallel); the root solve and the level-synchronous forward
-  // pass then carry the RB columns together.  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
+  // ut / proot slabs, so the walks run in parallel) and the root solve gives a0 per column.  The forward
+  // pass is then written in joint space, y_j = (ut_j - U_j.a0 - sum_{i in anc(j)} (U_j.S_i) y_i) / D_j:
+  // level by level, each lane gathers its ancestor's y values with one bpermute per column (no LDS
+  // round trip or barrier per level).  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
   __device__ void test_solve(int r0, int nrows_, float* y) {
-    typename L::Solve& ts = s->u.sv.ts;
+    auto& ts = s->u.sv.ts.ts;
     for (int i = tl; i < L::RB * MN; i += T) (&ts.ut[0][0])[i] = 0.0f;
     __syncthreads();
     if (tl < L::RB) {
@@ -688,31 +698,43 @@ struct Team {
       float a = 0.0f;
       if (freeb)
         for (int j = 0; j < 6; j++) a -= s->Iinv[6 * c + j] * ts.proot[q][j];
-      ts.acc[q][0][c] = a;
+      ts.a0[q][c] = a;
     }
     __syncthreads();
-    float yv[L::RB];
+    float base[L::RB], accv[L::RB], yv[L::RB];
 #pragma unroll
-    for (int q = 0; q < L::RB; q++) yv[q] = 0.0f;
+    for (int q = 0; q < L::RB; q++) {
+      base[q] = 0.0f;
+      accv[q] = 0.0f;
+      yv[q] = 0.0f;
+      if (node > 0) {
+        const float* a0 = ts.a0[q];
+        base[q] = ts.ut[q][node] - dot(U, sv(ld3(a0), ld3(a0 + 3)));
+      }
+    }
+    // proper ancestors below the root, visited in increasing depth (= increasing index)
+    unsigned long long path = node > 0 ? (s->anc[node] & ~1ull & ~(1ull << node)) : 0ull;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
 #pragma unroll
+        for (int q = 0; q < L::RB; q++) yv[q] = (base[q] - accv[q]) * Dinv;
+      }
+      if (lev < maxdepth) {
+        const bool deeper = node > 0 && depth > lev;
+        const int an = deeper ? __builtin_ctzll(path) : 1;
+        if (deeper) path &= path - 1;
+        const int src = deeper ? tb + ncol0 + an - 1 : (int)threadIdx.x;
+        const float C = deeper ? dot(U, sv(ld3(s->S[an]), ld3(s->S[an] + 3))) : 0.0f;
+#pragma unroll
         for (int q = 0; q < L::RB; q++) {
-          const float* ac = ts.acc[q][par];
-          SV ap = sv(ld3(ac), ld3(ac + 3));
-          const float yq = (ts.ut[q][node] - dot(U, ap)) * Dinv;
-          SV a = ap + S * yq;
-          float* an = ts.acc[q][node];
-          an[0] = a.a.x; an[1] = a.a.y; an[2] = a.a.z;
-          an[3] = a.l.x; an[4] = a.l.y; an[5] = a.l.z;
-          yv[q] = yq;
+          const float ya = __shfl(yv[q], src);
+          accv[q] += C * ya;
         }
       }
-      __syncthreads();
     }
 #pragma unroll
     for (int q = 0; q < L::RB; q++) {
-      float v = (freeb && tl < 6) ? ts.acc[q][0][tl] : yv[q];
+      float v = (freeb && tl < 6) ? ts.a0[q][tl] : yv[q];
       y[q] = tl < nv ? v : 0.0f;
     }
   }
@@ -754,16 +776,16 @@ struct Team {
     return code == 1 ? d : -d;
   }
 
-  // J_r[lane] for the RB rows r0 .. r0 + RB - 1 of a test-solve batch.  Contact rows come in aligned
+  // J_r[lane] for the 3 rows r0 .. r0 + 2 of a test-solve batch (r0 a multiple of 3).  Contact rows come in aligned
   // triples (n, t1, t2 of contact r0 / 3): they share the lane's sign and the point-velocity vector
   // g = Sl_ang x (p - o) + Sl_lin, so J_r = sign (d_r . g) (= sign Sl . [(p - o) x d_r; d_r]).
   // Limit rows: +-1 on the DOF's lane.  Object lanes: the stored object part of the contact rows.
   __device__ void batch_jacobians(int r0, int nrows_, float* J) const {
 #pragma unroll
-    for (int q = 0; q < L::RB; q++) J[q] = 0.0f;
+    for (int q = 0; q < 3; q++) J[q] = 0.0f;
     if (OBJ && objl) {
       if (r0 < 3 * ncr)
-        for (int q = 0; q < L::RB; q++) J[q] = s->rwo[r0 + q][tl - ob0];
+        for (int q = 0; q < 3; q++) J[q] = s->rwo[r0 + q][tl - ob0];
       return;
     }
     if (tl >= nv) return;
@@ -780,7 +802,7 @@ struct Team {
       J[2] = sgn * dot(ld3(s->ct2[c]), g);
     } else {
 #pragma unroll
-      for (int q = 0; q < L::RB; q++) {
+      for (int q = 0; q < 3; q++) {
         const int r = r0 + q;
         if (r < nrows_ && node > 0) {
           const int meta = s->lmeta[r - 3 * ncr];
@@ -1122,7 +1144,8 @@ struct Team {
     float Jcol[MR], Ycol[MR];
     for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
       float jb[L::RB], yb[L::RB];
-      batch_jacobians(r0, nrows, jb);
+#pragma unroll
+      for (int g = 0; g < L::RB; g += 3) batch_jacobians(r0 + g, nrows, jb + g);
       test_solve(r0, nrows, yb);
       ph_mark(5);
 #pragma unroll
@@ -1142,7 +1165,7 @@ struct Team {
             typename L::Row& rw = s->u.sv.rows[r];
             rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
             rw.lam = 0.0f;
-            rw.mu = contact ? (q == 0 ? -1.0f : p->friction) : -2.0f;
+            rw.mu = contact ? (q % 3 == 0 ? -1.0f : p->friction) : -2.0f;
             if (!active) rw.b = 0.0f;
           }
         }
