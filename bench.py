@@ -61,6 +61,23 @@ def cpu_baseline(task, seconds=12.0, n=4096):
                       f"(fp64 physics, fp32 task layer), not PhysX"}
 
 
+def pmc_traffic(task, n, kern_ms):
+    """Measured HBM traffic of the dominant kernel for this workload, from the committed rocprofv3 --pmc
+    passes of the same bench command (tools/gpu_prof.sh -> tools/pmc_summary.py --json): FETCH_SIZE x2
+    (gfx950 correction) + WRITE_SIZE per launch, expressed over this run's launch time like `achieved`.
+    None when no pass was recorded for this workload."""
+    path = os.path.join(ROOT, "profiles", "r01", f"pmc_{task}_{n}.json")
+    try:
+        with open(path) as f:
+            b = json.load(f)["traffic_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return {"traffic": None}
+    if b is None:
+        return {"traffic": None}
+    return {"traffic": b / (kern_ms * 1e-3) / 1e9, "traffic_bytes_per_launch": b,
+            "traffic_source": os.path.relpath(path, ROOT)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,7 +165,7 @@ def main():
                        "obs_allgather": bool(gather is not None),
                        "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": None,
+                         "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms),
                          "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",
                          "kernel_ms": kern_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES[args.task]},

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   constexpr int E = kBlock / T;
   constexpr int ROWS = OBJ ? 3 : 1;
   __shared__ mg::TeamLDS<T, MN, MC, OBJ> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   mg::load_tile(&tile, m);
   __syncthreads();
   const int team = threadIdx.x / T;
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                                                       int n) {
   constexpr int E = kBlock / T;
   __shared__ mg::TeamLDS<T, MN, MC, true> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
   mg::load_tile(&tile, m);
   __syncthreads();
   const int team = threadIdx.x / T;

@@ -39,7 +39,7 @@ namespace mg {
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
 // loaded once per launch, so every per-node / per-geom constant is an LDS read
 // (~64 cycles) instead of a dependent global load.  Rows padded to odd strides.
-template <int MN, int MG, int MP>
+template <int MN, int MG, int MP, int OC = 1>
 struct ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
@@ -49,13 +49,14 @@ struct ModelTile {
   int tdof[MG_MAX_TENDONS][2];
   float tf[MG_MAX_TENDONS][6];   // coef0, coef1, lo, hi, limit stiffness, damping
   int nten;
-  float gf[MG][17];   // 0-2 pos, 3-11 R, 12-14 size
+  float gf[MG][17];   // 0-2 pos, 3-11 R, 12-14 size, 15 bounding radius
   int pairs[MP > 0 ? MP : 1][2];
-  int nn, ng, np;
+  unsigned short ocand[OC];  // object-collision candidates (geom << 4 | candidate), geom order
+  int nn, ng, np, noc;
 };
 
-template <int MN, int MG, int MP>
-__device__ void load_tile(ModelTile<MN, MG, MP>* t, const mg_model* m) {
+template <int MN, int MG, int MP, int OC>
+__device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nn = m->num_nodes, ng = m->num_geoms < MG ? m->num_geoms : MG;
   const int np = m->num_pairs < MP ? m->num_pairs : MP;
@@ -95,12 +96,26 @@ __device__ void load_tile(ModelTile<MN, MG, MP>* t, const mg_model* m) {
     for (int k = 0; k < 3; k++) { f[k] = m->geom_pos[g][k]; f[12 + k] = m->geom_size[g][k]; }
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) f[3 + 3 * a + b] = Rg.m[a][b];
+    const float* sz = m->geom_size[g];
+    const int ty = m->geom_type[g];
+    f[15] = ty == MG_GT_BOX ? sqrtf(sz[0] * sz[0] + sz[1] * sz[1] + sz[2] * sz[2])
+                            : (ty == MG_GT_CAPSULE ? sz[0] + sz[1] : sz[0]);
+  }
+  if (OC > 1 && tid == 0) {  // object candidates: spheres/capsules 1 (closest point), boxes 16 (vertex tests)
+    int n = 0;
+    for (int g = 0; g < ng; g++) {
+      if (!(m->geom_filter[g] & MG_COLLIDE_OBJECT)) continue;
+      const int ty = m->geom_type[g];
+      const int nc = (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) ? 1 : (ty == MG_GT_BOX ? 16 : 0);
+      for (int q = 0; q < nc && n < OC; q++) t->ocand[n++] = (unsigned short)((g << 4) | q);
+    }
+    t->noc = n;
   }
   for (int q = tid; q < np; q += nt) {
     t->pairs[q][0] = m->pair[q][0];
     t->pairs[q][1] = m->pair[q][1];
   }
-  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; }
+  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; if (OC <= 1) t->noc = 0; }
 }
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
@@ -169,7 +184,7 @@ struct TeamLDS {
   float obs[OBJ ? 212 : 1];
 };
 
-// Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + ds_swizzle xor 16 and
+// Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + v_permlane16_swap (xor 16) and
 // a bpermute xor 32.  Every step adds a lane to its partner symmetrically, so all lanes of the team
 // end with bit-identical sums (fp add is commutative) and no broadcast is needed.
 template <int T>
@@ -178,7 +193,11 @@ __device__ __forceinline__ float team_sum(float v, int) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad xor 2
   if (T >= 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
   if (T >= 16) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
-  if (T >= 32) v += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));      // xor 16
+  if (T >= 32) {  // xor 16: v_permlane16_swap exchanges the odd 16-lane rows of one copy with the even
+                  // rows of the other (gfx950), so the partner value is in the swapped copy
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+  }
   if (T >= 64) v += __shfl_xor(v, 32);
   return v;
 }
@@ -296,7 +315,7 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
 template <int T, int MN, int MC, int MG, int MP, bool OBJ = false>
 struct Team {
   using L = TeamLDS<T, MN, MC, OBJ>;
-  using MT = ModelTile<MN, MG, MP>;
+  using MT = ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>;
   static constexpr int MR = L::MR;
   L* s;
   const MT* mt;
@@ -843,11 +862,8 @@ struct Team {
   // candidate q of articulation geom g against the object box (oracle geom_object): sphere/capsule
   // -> one closest-point candidate; box -> its 8 vertices vs the object, then the object's 8 vertices
   // vs the geom (normal flipped).  Normal points from the object (B) to the geom (A).
-  __device__ bool obj_candidate(int g, int q, V3* pt, V3* nrm, float* dist) const {
+  __device__ bool obj_candidate(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
     const V3 hb = ld3(m->obj_size);
-    V3 c;
-    M3 Rg;
-    geom_world(g, &c, &Rg);
     const int ty = mt->gtype[g];
     const float* gs = mt->gf[g] + 12;
     if (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) {
@@ -998,36 +1014,37 @@ struct Team {
       }
       base += tot;
     }
-    if (OBJ && m->obj_type == MG_GT_BOX) {  // articulation geoms vs the object: lane per geom, geom order
-      for (int g0 = 0; g0 < G; g0 += T) {
-        const int g = g0 + tl;
-        int nc = 0;
-        if (g < G && (mt->gfil[g] & MG_COLLIDE_OBJECT)) {
-          const int ty = mt->gtype[g];
-          nc = (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) ? 1 : (ty == MG_GT_BOX ? 16 : 0);
-        }
-        int cnt = 0;
-        for (int pass = 0; pass < 2; pass++) {
-          int k = 0, slot0 = 0;
-          if (pass == 1) {
-            const int incl = team_incl_scan<T>(cnt);
-            slot0 = base + incl - cnt;
-            base += __shfl(incl, tb + T - 1);
-          }
-          for (int q = 0; q < nc; q++) {
-            V3 pt, nrm;
-            float d;
-            obj_candidate(g, q, &pt, &nrm, &d);
-            if (!(d < off)) continue;
-            if (pass == 0) {
-              cnt++;
-            } else {
-              const int slot = slot0 + k;
-              if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
-              k++;
-            }
+    if (OBJ && m->obj_type == MG_GT_BOX) {
+      // articulation geoms vs the object: one lane per (geom, candidate) in geom order (the oracle's
+      // emission order); a candidate whose geom's bounding sphere cannot come within the contact
+      // offset of the object's is skipped (conservative: the same contacts)
+      const float ro = sqrtf(dot(ld3(m->obj_size), ld3(m->obj_size)));
+      const int NC = mt->noc;
+      for (int f0 = 0; f0 < NC; f0 += T) {
+        const int f = f0 + tl;
+        int cnt = 0, g = 0;
+        V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
+        float d = 0.0f;
+        if (f < NC) {
+          const int e = mt->ocand[f];
+          g = e >> 4;
+          V3 c;
+          M3 Rg;
+          geom_world(g, &c, &Rg);
+          const V3 dc = c - op;
+          const float reach = mt->gf[g][15] + ro + off;
+          if (dot(dc, dc) <= reach * reach) {
+            obj_candidate(g, e & 15, c, Rg, &pt, &nrm, &d);
+            cnt = d < off ? 1 : 0;
           }
         }
+        const int incl = team_incl_scan<T>(cnt);
+        const int tot = __shfl(incl, tb + T - 1);
+        if (cnt) {
+          const int slot = base + incl - 1;
+          if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
+        }
+        base += tot;
       }
     }
     if (tl == 0) s->ncon = base < cap ? base : cap;

@@ -1,12 +1,25 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs: per-dispatch mean of each counter for one kernel."""
+"""Summarise rocprofv3 --pmc CSVs: per-dispatch median/mean of each counter for one kernel.
+
+    python tools/pmc_summary.py <dir> [kernel] [--json out.json]
+
+With --json, also writes the per-launch HBM traffic of the kernel as MI355X_MICROARCH.md's
+HBM/rocprofv3 section prescribes: FETCH_SIZE (kB) doubled (gfx950 reports half of the bytes of
+wide coalesced reads) + WRITE_SIZE (kB), medians over the dispatches.
+"""
 import collections
 import csv
 import glob
 import sys
 
-d = sys.argv[1]
-kern = sys.argv[2] if len(sys.argv) > 2 else "k_env_step"
+args = [a for a in sys.argv[1:]]
+jout = None
+if "--json" in args:
+    i = args.index("--json")
+    jout = args[i + 1]
+    del args[i:i + 2]
+d = args[0]
+kern = args[1] if len(args) > 1 else "k_env_step"
 agg = collections.defaultdict(list)
 for f in sorted(glob.glob(f"{d}/*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -15,3 +28,12 @@ for f in sorted(glob.glob(f"{d}/*counter_collection.csv")):
 for k, v in sorted(agg.items()):
     v = sorted(v)
     print(f"{k:28s} n={len(v):3d} median={v[len(v)//2]:.4g} mean={sum(v)/len(v):.4g}")
+if jout:
+    import json
+    med = {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
+    fetch, write = med.get("FETCH_SIZE"), med.get("WRITE_SIZE")
+    out = {"kernel": kern, "dispatches": len(agg.get("FETCH_SIZE", [])), "FETCH_SIZE_kB": fetch, "WRITE_SIZE_kB": write,
+           "traffic_bytes_per_launch": None if fetch is None or write is None else (2.0 * fetch + write) * 1024.0,
+           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM/rocprofv3); kB = 1024 B"}
+    json.dump(out, open(jout, "w"), indent=1)
+    print("wrote", jout)
