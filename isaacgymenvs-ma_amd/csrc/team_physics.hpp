@@ -124,7 +124,7 @@ template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
   static constexpr int MRO = OBJ ? MR : 1;
-  static constexpr int RB = 6;  // right-hand sides per test solve (the rows of 2 contacts)
+  static constexpr int RB = (T >= 32 && !OBJ) ? 12 : 6;  // right-hand sides per test solve (rows of 4 or 2 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
