@@ -602,6 +602,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
   const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
   float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
+  // rigid-body states of the hand once (one lane per body) into the dead row storage: the fingertip
+  // observations and the rigid_body_states write-back both read them
+  float* bst = &L.u.sv.rows[0].b;
+  for (int b = t.tl; b < nb; b += T) t.body_state(b, bst + 13 * b);
+  __syncthreads();
   {
     const float* gs = L.goal + 13;
     float qdiff[4];
@@ -616,9 +621,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       } else if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {  // fingertip state from the post-step FK
         int b, c;
         mg::h_ft_ref(tp, seg, i, &b, &c);
-        float b13[13];
-        t.body_state(b, b13);
-        x = b13[c];
+        x = bst[13 * b + c];
       } else {
         x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
       }
@@ -678,7 +681,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.u.sv.st.sens[k];
     if (v.dof_force)
       for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.u.sv.st.dforce[k];
-    for (int b = t.tl; b < nb; b += T) t.body_state(b, rbs + 13 * b);
+    for (int k = t.tl; k < 13 * nb; k += T) rbs[k] = bst[k];
     for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
   }
   t.ph_mark(9);
@@ -746,6 +749,9 @@ struct RunEnvStep {
     // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
     if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
       return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
+    // hand tasks stage the rigid-body states of the articulation in the same storage
+    if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
+      return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
     if constexpr (OBJ) {
       hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                          sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);

@@ -920,7 +920,8 @@ struct Team {
       int ty = -1;
       if (g < G && (mt->gfil[g] & MG_COLLIDE_GROUND)) {
         geom_world(g, &c, &Rg);
-        ty = mt->gtype[g];
+        // every candidate's gap is >= c.z - bounding radius: geoms that high cannot touch the plane
+        if (c.z - mt->gf[g][15] < off) ty = mt->gtype[g];
       }
       const float* gs = g < G ? mt->gf[g] + 12 : mt->gf[0] + 12;
       int cnt = 0;
