@@ -120,11 +120,15 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
 
+#ifndef MG_RB_WIDE
+#define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
+#endif
+
 template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
   static constexpr int MR = 3 * MC + 2 * (MN - 1);
   static constexpr int MRO = OBJ ? MR : 1;
-  static constexpr int RB = (T >= 32 && !OBJ) ? 12 : 6;  // right-hand sides per test solve (rows of 4 or 2 contacts)
+  static constexpr int RB = (T >= 32 && !OBJ) ? MG_RB_WIDE : 6;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -154,9 +158,8 @@ struct TeamLDS {
         float proot[6];
       } aba;
       struct {
-        float ut[RB][MN];   // test solves: joint-space forces of the RB columns,
-        float proot[RB][6]; // their root biases and root accelerations
-        float a0[RB][6];
+        float ut[RB][MN];   // test solves: joint-space forces of the RB columns
+        float proot[RB][6]; // and their root biases
       } ts;
     };
   };
@@ -166,7 +169,6 @@ struct TeamLDS {
     float sens[6 * MG_MAX_SENSORS];
     float dforce[MN];
   };
-  static_assert(sizeof(Stage) <= sizeof(Solve), "staging must fit the test-solve storage");
   union {
     float slot[MN][27];
     struct {
@@ -644,7 +646,7 @@ struct Team {
   // pass is then written in joint space, y_j = (ut_j - U_j.a0 - sum_{i in anc(j)} (U_j.S_i) y_i) / D_j:
   // level by level, each lane gathers its ancestor's y values with one bpermute per column (no LDS
   // round trip or barrier per level).  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
-  __device__ void test_solve(int r0, int nrows_, float* y) {
+  __device__ void test_solve(int r0, int nrows_, const float* Wv, float* y) {
     auto& ts = s->u.sv.ts.ts;
     for (int i = tl; i < L::RB * MN; i += T) (&ts.ut[0][0])[i] = 0.0f;
     __syncthreads();
@@ -712,31 +714,25 @@ struct Team {
       pr[3] = proot.l.x; pr[4] = proot.l.y; pr[5] = proot.l.z;
     }
     __syncthreads();
-    for (int i = tl; i < 6 * L::RB; i += T) {  // root: a0 = -IA0^-1 p0 (free base) or 0
-      const int q = i / 6, c = i - 6 * q;
-      float a = 0.0f;
-      if (freeb)
-        for (int j = 0; j < 6; j++) a -= s->Iinv[6 * c + j] * ts.proot[q][j];
-      ts.a0[q][c] = a;
-    }
-    __syncthreads();
-    float base[L::RB], accv[L::RB], yv[L::RB];
+    ph_mark(10);
+    // base_q = ut_j - U_j.a0 (joint lanes) or a0[tl] (root lanes), both as ut + Wv.p0 (see aba())
+    // rem_q starts at base_q and loses C_ji y_i as the ancestors' values arrive
+    float rem[L::RB], yv[L::RB];
 #pragma unroll
     for (int q = 0; q < L::RB; q++) {
-      base[q] = 0.0f;
-      accv[q] = 0.0f;
+      const float* p0 = ts.proot[q];
+      float b = node > 0 ? ts.ut[q][node] : 0.0f;
+      b += Wv[0] * p0[0] + Wv[1] * p0[1] + Wv[2] * p0[2] + Wv[3] * p0[3] + Wv[4] * p0[4] + Wv[5] * p0[5];
+      rem[q] = b;
       yv[q] = 0.0f;
-      if (node > 0) {
-        const float* a0 = ts.a0[q];
-        base[q] = ts.ut[q][node] - dot(U, sv(ld3(a0), ld3(a0 + 3)));
-      }
     }
+    ph_mark(11);
     // proper ancestors below the root, visited in increasing depth (= increasing index)
     unsigned long long path = node > 0 ? (s->anc[node] & ~1ull & ~(1ull << node)) : 0ull;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
 #pragma unroll
-        for (int q = 0; q < L::RB; q++) yv[q] = (base[q] - accv[q]) * Dinv;
+        for (int q = 0; q < L::RB; q++) yv[q] = rem[q] * Dinv;
       }
       if (lev < maxdepth) {
         const bool deeper = node > 0 && depth > lev;
@@ -747,13 +743,14 @@ struct Team {
 #pragma unroll
         for (int q = 0; q < L::RB; q++) {
           const float ya = __shfl(yv[q], src);
-          accv[q] += C * ya;
+          rem[q] -= C * ya;
         }
       }
     }
+    ph_mark(12);
 #pragma unroll
     for (int q = 0; q < L::RB; q++) {
-      float v = (freeb && tl < 6) ? ts.a0[q][tl] : yv[q];
+      float v = (freeb && tl < 6) ? rem[q] : yv[q];
       y[q] = tl < nv ? v : 0.0f;
     }
   }
@@ -1159,13 +1156,28 @@ struct Team {
     // row responses Y_r = M~^-1 J_r^T by test-force ABA solves (column distributed over the lanes),
     // W_r = J_r . Y_r.  Lane j keeps (J_r[j], Y_r[j]) of every row in private arrays for the sweeps;
     // rows past this team's count get J = Y = 0 and zero scalars, so the sweeps need no row mask.
+    // root coupling of the test solves: with a0 = -IA0^-1 p0, a joint lane's U.a0 = -(IA0^-1 U).p0
+    // and a root lane's a0[tl] = -(row tl of IA0^-1).p0, so one 6-vector per lane covers both
+    float Wv[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (freeb && wave_rows > 0) {
+      if (tl < 6) {
+        for (int k = 0; k < 6; k++) Wv[k] = -s->Iinv[6 * tl + k];
+      } else if (node > 0) {
+        const float Uv[6] = {U.a.x, U.a.y, U.a.z, U.l.x, U.l.y, U.l.z};
+        for (int k = 0; k < 6; k++) {
+          float w = 0.0f;
+          for (int c2 = 0; c2 < 6; c2++) w += s->Iinv[6 * c2 + k] * Uv[c2];
+          Wv[k] = w;
+        }
+      }
+    }
     float Jcol[MR], Ycol[MR];
     for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
       float jb[L::RB], yb[L::RB];
 #pragma unroll
       for (int g = 0; g < L::RB; g += 3) batch_jacobians(r0 + g, nrows, jb + g);
-      test_solve(r0, nrows, yb);
-      ph_mark(5);
+      ph_mark(4);
+      test_solve(r0, nrows, Wv, yb);
 #pragma unroll
       for (int q = 0; q < L::RB; q++) {
         const int r = r0 + q;
@@ -1188,7 +1200,7 @@ struct Team {
           }
         }
       }
-      ph_mark(4);
+      ph_mark(5);
     }
     // a sweep shorter than the prefetch depth would read a row's impulse before its previous visit
     // wrote it: pad it with zero rows (J = Y = 0, 1/W = 0: skipped, as the oracle skips W = 0 rows)

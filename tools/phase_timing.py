@@ -17,8 +17,8 @@ sys.path.insert(0, os.path.join(ROOT, "isaacgymenvs-ma_amd"))
 os.environ.setdefault("MIGYM_LIB", os.path.join(ROOT, "isaacgymenvs-ma_amd", "migym", "_lib",
                                                 "libmigym_timing.so"))
 
-NAMES = {0: "fk", 1: "aba", 2: "collide", 3: "rows", 4: "row_jacobians", 5: "test_solves", 6: "pgs",
-         7: "integrate", 8: "outputs", 9: "task+writeback", 13: "rows_count", 14: "load+pre", 15: "substep_entry"}
+NAMES = {0: "fk", 1: "aba", 2: "collide", 3: "rows", 4: "row_jacobians", 5: "rows_finish", 6: "pgs",
+         7: "integrate", 8: "outputs", 9: "task+writeback", 10: "ts_walks", 11: "ts_root", 12: "ts_forward", 13: "rows_count", 14: "load+pre", 15: "substep_entry"}
 
 
 def main():
