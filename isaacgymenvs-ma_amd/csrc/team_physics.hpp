@@ -120,6 +120,9 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
 
+#ifndef MG_PGS_PREFETCH
+#define MG_PGS_PREFETCH 2  // PGS visits whose data are in flight ahead of the sweep
+#endif
 #ifndef MG_RB_WIDE
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
 #endif
@@ -1202,10 +1205,13 @@ struct Team {
       }
       ph_mark(5);
     }
-    // a sweep shorter than the prefetch depth would read a row's impulse before its previous visit
-    // wrote it: pad it with zero rows (J = Y = 0, 1/W = 0: skipped, as the oracle skips W = 0 rows)
-    constexpr int PF = 4;
-    const int prow = (wave_rows > 0 && wave_rows < PF) ? PF : wave_rows;
+    // The sweep runs over prow rows, the row count rounded up to a multiple of the prefetch depth PF
+    // (so a row's impulse is never read ahead of its previous visit's write, and the unrolled loop
+    // needs no per-visit guards): the padding rows have J = Y = 0 and 1/W = 0, i.e. they are skipped
+    // as the oracle skips W = 0 rows.
+    constexpr int PF = MG_PGS_PREFETCH;
+    static_assert(MR % PF == 0, "row capacity must be a multiple of the PGS prefetch depth");
+    const int prow = wave_rows == 0 ? 0 : ((wave_rows + PF - 1) / PF) * PF;
     for (int r = wave_rows; r < prow; r++) {
       Ycol[r] = 0.0f;
       Jcol[r] = 0.0f;
@@ -1213,48 +1219,42 @@ struct Team {
     }
     __syncthreads();
     ph_mark(5);
-    // PGS sweeps as one stream of pos_iters * wave_rows row visits: per visit one team dot product
-    // (DPP), the clamp, one FMA per lane.  A visit's data (private J/Y, LDS row scalars) do not
-    // depend on the sweep's chain; they sit in PF rotating registers loaded PF visits ahead, each load
-    // issued after the previous occupant's last use.  The friction bound uses the contact's normal
-    // impulse of this sweep (the normal row precedes its two friction rows), carried in a register.
-    const float mu = p->friction;
-    const int nvis = p->pos_iters * prow;
+    // PGS sweeps: per visit one team dot product (DPP), a branch-free clamp (med3), one multiply-add
+    // per lane.  A visit's data (private J/Y, LDS row record) do not depend on the sweep's chain; they
+    // sit in PF rotating registers loaded PF visits ahead, each load issued after the previous
+    // occupant's last use.  The friction bound uses the contact's normal impulse of this sweep (the
+    // normal row precedes its two friction rows), carried in a register.  Every lane of the team
+    // computes the same impulse, so all of them store it (no exec-mask switch per visit).
     float pJ[PF], pY[PF];
     typename L::Row pR[PF];
-    int rq = 0;  // row of the next prefetch
+    if (prow > 0) {
 #pragma unroll
-    for (int k = 0; k < PF; k++) {
-      if (k < nvis) {
-        pJ[k] = Jcol[rq];
-        pY[k] = Ycol[rq];
-        pR[k] = s->u.sv.rows[rq];
-        rq = rq + 1 == prow ? 0 : rq + 1;
+      for (int k = 0; k < PF; k++) {
+        pJ[k] = Jcol[k];
+        pY[k] = Ycol[k];
+        pR[k] = s->u.sv.rows[k];
       }
     }
     float lamn = 0.0f;
-    int r = 0;
-    for (int v0 = 0; v0 < nvis; v0 += PF) {
+    for (int it = 0; it < p->pos_iters; it++) {
+      for (int r0 = 0; r0 < prow; r0 += PF) {
+        const int rn = r0 + PF == prow ? 0 : r0 + PF;  // next block of rows (wraps into the next sweep)
 #pragma unroll
-      for (int k = 0; k < PF; k++) {
-        if (v0 + k < nvis) {
+        for (int k = 0; k < PF; k++) {
           const float v = team_sum<T>(pJ[k] * nu, tb);
           const float lam = pR[k].lam, m = pR[k].mu;
-          // friction rows (m = mu >= 0): clamp to +-mu lambda_n; normal / limit rows (m < 0): >= 0.
-          // Rows with 1/W = 0 keep lambda = 0 without a test: lam + (b - v) * 0 = 0 clamps to 0.
-          const float t = fmaxf(m, 0.0f) * lamn;
-          float lnew = fmaxf(lam + (pR[k].b - v) * pR[k].iw, -t);
-          lnew = m >= 0.0f ? fminf(lnew, t) : lnew;
+          // friction rows (m = mu >= 0): [-mu lambda_n, mu lambda_n]; normal / limit rows (m < 0):
+          // [0, inf).  Rows with 1/W = 0 keep lambda = 0: lam + (b - v) * 0 = 0 clamps to 0.
+          const bool fric = m >= 0.0f;
+          const float t = fric ? m * lamn : 0.0f;
+          const float hi = fric ? t : __builtin_inff();
+          const float lnew = __builtin_amdgcn_fmed3f(lam + (pR[k].b - v) * pR[k].iw, -t, hi);
           lamn = m == -1.0f ? lnew : lamn;
-          if (tl == 0) s->u.sv.rows[r].lam = lnew;
+          s->u.sv.rows[r0 + k].lam = lnew;
           nu += pY[k] * (lnew - lam);
-          r = r + 1 == prow ? 0 : r + 1;
-          if (v0 + k + PF < nvis) {
-            pJ[k] = Jcol[rq];
-            pY[k] = Ycol[rq];
-            pR[k] = s->u.sv.rows[rq];
-            rq = rq + 1 == prow ? 0 : rq + 1;
-          }
+          pJ[k] = Jcol[rn + k];
+          pY[k] = Ycol[rn + k];
+          pR[k] = s->u.sv.rows[rn + k];
         }
       }
     }
