@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                                                      mg_state_views v, int n) {
   constexpr int E = kBlock / T;
   constexpr int ROWS = OBJ ? 3 : 1;
-  __shared__ mg::TeamLDS<T, MN, MC, OBJ> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   mg::load_tile(&tile, m);
   __syncthreads();
@@ -73,17 +73,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int ac = valid ? a : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors;
   mg::Team<T, MN, MC, MG, MP, OBJ> t;
-  t.init(&lds[team], &tile, m, &p);
+  t.init(&lds[team].v, &tile, m, &p);
   __syncthreads();
   float* root = v.root_states + (size_t)13 * ROWS * ac;
   t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
          OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(lds[team].u.sv.st.sens, lds[team].u.sv.st.dforce);
+  t.outputs(lds[team].v.u.sv.st.sens, lds[team].v.u.sv.st.dforce);
   t.stage_state();
   __syncthreads();
   if (valid) {
-    mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team];
+    mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team].v;
     if (!m->fixed_base)
       for (int k = t.tl; k < 13; k += T) root[k] = L.u.sv.st.root[k];
     if (OBJ)
@@ -215,7 +215,7 @@ template <int T, int MN, int MC, int MG, int MP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
   constexpr int E = kBlock / T;
-  __shared__ mg::TeamLDS<T, MN, MC> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   mg::load_tile(&tile, m);
   __syncthreads();
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
-  mg::TeamLDS<T, MN, MC>& L = lds[team];
+  mg::TeamLDS<T, MN, MC>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP> t;
   t.init(&L, &tile, m, &p);
   __syncthreads();
@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                                                       mg_task_params tp, mg_state_views v, mg_task_buffers tb,
                                                       int n) {
   constexpr int E = kBlock / T;
-  __shared__ mg::TeamLDS<T, MN, MC, true> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, true>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
   mg::load_tile(&tile, m);
   __syncthreads();
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
-  mg::TeamLDS<T, MN, MC, true>& L = lds[team];
+  mg::TeamLDS<T, MN, MC, true>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, true> t;
   t.init(&L, &tile, m, &p);
   t.ph_start();

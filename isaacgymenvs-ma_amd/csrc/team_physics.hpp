@@ -189,6 +189,22 @@ struct TeamLDS {
   float obs[OBJ ? 212 : 1];
 };
 
+// A team's LDS region padded so that consecutive teams start 4*T bytes apart modulo 128 B.  A
+// ds_read/write_b32 is serviced per 32-lane half with bank = dword address mod 32, so teams of
+// T < 32 lanes share a half: without the stagger (Ant's TeamLDS is 3840 B = 30 x 128 B) lane j
+// of team 0 and lane j of team 1 hit the same bank on every per-lane or broadcast access
+// (measured: SQ_LDS_BANK_CONFLICT ~ 2x SQ_INSTS_LDS for Ant).  With the stagger, per-lane
+// accesses at any odd dword stride and team-broadcast reads are conflict-free across the teams.
+template <class L, int T, int P = (T < 32) ? (int)((4 * T - (int)(sizeof(L) % 128) + 128) % 128) : 0>
+struct alignas(16) BankSlot {
+  L v;
+  char pad[P];
+};
+template <class L, int T>
+struct alignas(16) BankSlot<L, T, 0> {
+  L v;
+};
+
 // Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + v_permlane16_swap (xor 16) and
 // a bpermute xor 32.  Every step adds a lane to its partner symmetrically, so all lanes of the team
 // end with bit-identical sums (fp add is commutative) and no broadcast is needed.
