@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_VERSION 2
+#define MG_VERSION 3
 
 #define MG_MAX_NODES 40
 #define MG_MAX_BODIES 40
@@ -69,6 +69,8 @@ enum { MG_OK = 0, MG_EINVAL = -1, MG_EDEVICE = -2, MG_ENOMEM = -3, MG_ECAPACITY 
 enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2, MG_TASK_SHADOW_HAND = 3 };
 #define MG_MAX_AGENTS 8
 enum { MG_SET_ROOT_STATE = 0, MG_SET_DOF_STATE = 1, MG_SET_DOF_TARGET = 2 };
+/* coordinate space of applied rigid-body forces (gymapi.CoordinateSpace) */
+enum { MG_ENV_SPACE = 0, MG_LOCAL_SPACE = 1, MG_GLOBAL_SPACE = 2 };
 /* geom collision filter bits (mg_model.geom_filter) */
 enum { MG_COLLIDE_GROUND = 1, MG_COLLIDE_OBJECT = 2 };
 
@@ -155,6 +157,13 @@ typedef struct mg_state_views {
   float* dof_force;         /* (N*A*nD), may be NULL */
   float* rigid_body_states; /* (N*A*nB, 13), may be NULL */
   const float* dof_targets; /* (N*A*nD) PD position targets (set_dof_position_target_tensor), may be NULL */
+  /* gym.apply_rigid_body_force_tensors(sim, forces, None, space) (shadow_hand.py:700-708): forces
+   * (N*A*nB, 3) in the rigid-body layout, applied at each body's centre of mass for every substep
+   * of the next simulate.  Rows of the free object are applied; articulation rows must be zero.
+   * NULL = no forces.  The fused hand step writes this tensor (it owns the random-force update). */
+  float* rb_forces;
+  int32_t rb_force_space;   /* MG_LOCAL_SPACE: body frame at the start of each substep; else world */
+  int32_t pad_views;
 } mg_state_views;
 
 /* Task constants (cfg['env'] of the task YAML). */
@@ -222,6 +231,15 @@ typedef struct mg_task_params {
   float object_start[3];             /* object_init_state position */
   float goal_displacement[3];        /* goal actor = goal_states + displacement */
   float goal_dz;                     /* goal_init = object_init + (0, 0, goal_dz) */
+  /* asymmetric actor-critic (shadow_hand.py:125-131, 470-471): states_buf = the full_state layout */
+  int32_t num_states;                /* 0 = no states buffer, else 211 */
+  /* random object forces (shadow_hand.py:69-72, 196-199, 641-643, 700-708); force_scale 0 = off */
+  int32_t object_rb;                 /* rigid-body row of the object within an env (object_rb_handles) */
+  float force_scale;
+  float force_decay_step;            /* forceDecay ** (dt / forceDecayInterval), fp32 (torch.pow) */
+  float force_prob_lo;               /* forceProbRange */
+  float force_prob_hi;
+  float object_rb_mass;              /* object_rb_masses */
 } mg_task_params;
 
 /* Task-layer buffers (VecTask.allocate_buffers, vec_task.py:302-325). */
@@ -239,8 +257,10 @@ typedef struct mg_task_buffers {
   float* up_vec;            /* (N*A, 3) */
   float* heading_vec;       /* (N*A, 3) */
   const float* noise;       /* (N*A, 2*nD) injected U(0,1) reset noise, or NULL = device RNG;
-                             * ShadowHand: (N, 61) = [goal-only draw 4 | reset_idx draw 53 |
-                             * reset_target_pose draw 4] (shadow_hand.py:587, 610) */
+                             * ShadowHand: (N, 66) = [goal-only draw 4 | reset_idx draw 53 |
+                             * reset_target_pose draw 4 | force-probability redraw 1 (U(0,1)) |
+                             * force selection 1 (U(0,1)) | force direction 3 (N(0,1))]
+                             * (shadow_hand.py:587, 610, 642-643, 704-706) */
   uint64_t seed;            /* device RNG seed (counter-based, keyed by global env id) */
   uint64_t step_counter;    /* VecTask.control_steps: RNG counter */
   int64_t env_offset;       /* global id of this shard's first env (multi-GPU) */
@@ -251,6 +271,8 @@ typedef struct mg_task_buffers {
   float* successes;         /* (N) */
   float* consecutive_successes; /* (1) running mean (shadow_hand.py:795-798) */
   uint64_t* reduce_scratch; /* (2) device scratch: sum(resets), sum(successes * resets) */
+  float* states;            /* (N, num_states) states_buf, may be NULL */
+  float* random_force_prob; /* (N) per-env force probability, redrawn on reset; may be NULL */
 } mg_task_buffers;
 
 const char* mg_last_error(void);

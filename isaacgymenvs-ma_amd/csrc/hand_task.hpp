@@ -19,7 +19,10 @@ namespace mg {
 
 #pragma clang fp contract(off)
 
-constexpr int HAND_NOISE = 61;  // [goal-only 4 | reset_idx 53 | reset_target_pose 4]
+// injected noise row: [goal-only 4 | reset_idx 53 | reset_target_pose 4 | force-probability redraw 1 |
+// force selection 1 | force direction 3 (N(0,1))]  (shadow_hand.py:587, 610, 642-643, 704-706)
+constexpr int HAND_NOISE = 66;
+constexpr int HN_FORCE_PROB = 61, HN_FORCE_SEL = 62, HN_FORCE_DIR = 63;
 
 // observation layouts of observationType (shadow_hand.py:108-113, 473-584): segment lists
 enum HandSeg {
@@ -50,8 +53,8 @@ __device__ __forceinline__ int h_seg_size(int seg, int nd, int nf, int na) {
   }
 }
 // observation column k -> (segment, index within the segment)
-__device__ __forceinline__ int h_locate(const mg_task_params& tp, int nd, int k, int* idx) {
-  const int8_t* lay = kHandLayout[tp.obs_type & 3];
+__device__ __forceinline__ int h_locate_in(int layout, const mg_task_params& tp, int nd, int k, int* idx) {
+  const int8_t* lay = kHandLayout[layout & 3];
   for (int i = 0; i < 12 && lay[i] != HS_END; i++) {
     const int n = h_seg_size(lay[i], nd, tp.num_fingertips, tp.num_actions);
     if (k < n) { *idx = k; return lay[i]; }
@@ -59,6 +62,9 @@ __device__ __forceinline__ int h_locate(const mg_task_params& tp, int nd, int k,
   }
   *idx = 0;
   return HS_END;
+}
+__device__ __forceinline__ int h_locate(const mg_task_params& tp, int nd, int k, int* idx) {
+  return h_locate_in(tp.obs_type, tp, nd, k, idx);
 }
 // fingertip body / component of an HS_FT_STATE or HS_FT_POS index
 __device__ __forceinline__ void h_ft_ref(const mg_task_params& tp, int seg, int idx, int* body, int* comp) {
@@ -108,6 +114,35 @@ __device__ __forceinline__ float h_rand_pm1(float u) { return 2.0f * u + -1.0f; 
 // uniform k of env `gid` for this control step: injected noise row or the counter-based RNG
 __device__ __forceinline__ float h_uniform(const mg_task_buffers& tb, int e, uint64_t gid, int k) {
   return tb.noise ? tb.noise[(size_t)HAND_NOISE * e + k] : uniform01(tb.seed, gid, tb.step_counter, (uint32_t)k);
+}
+
+// N(0,1) draw k of env `gid`: injected noise column, or Box-Muller on two counter-based uniforms
+__device__ __forceinline__ float h_normal(const mg_task_buffers& tb, int e, uint64_t gid, int k) {
+  if (tb.noise) return tb.noise[(size_t)HAND_NOISE * e + k];
+  const float u1 = uniform01(tb.seed, gid, tb.step_counter, (uint32_t)(128 + 2 * k));
+  const float u2 = uniform01(tb.seed, gid, tb.step_counter, (uint32_t)(129 + 2 * k));
+  return sqrtf(-2.0f * logf(1.0f - u1)) * cosf(6.28318530717958647f * u2);
+}
+
+// random object force of one env for this step (shadow_hand.py:641-643 in reset_idx, 700-706 in
+// pre_physics_step): a reset zeroes the force and redraws the env's probability
+// exp((log lo - log hi) u + log hi); then, with forceScale > 0, the force decays by
+// forceDecay^(dt / forceDecayInterval) (tp.force_decay_step, evaluated on the host with torch.pow) and
+// with probability `prob` is replaced by N(0,1)^3 * object mass * forceScale.  f: in/out (3).
+__device__ __forceinline__ void h_object_force(const mg_task_params& tp, const mg_task_buffers& tb, int e,
+                                               uint64_t gid, bool env_reset, float* f) {
+  float prob = tb.random_force_prob ? tb.random_force_prob[e] : 0.0f;
+  if (env_reset) {
+    f[0] = f[1] = f[2] = 0.0f;
+    const float lhi = logf(tp.force_prob_hi);
+    prob = expf((logf(tp.force_prob_lo) - lhi) * h_uniform(tb, e, gid, HN_FORCE_PROB) + lhi);
+    if (tb.random_force_prob) tb.random_force_prob[e] = prob;
+  }
+  if (tp.force_scale > 0.0f) {
+    for (int k = 0; k < 3; k++) f[k] = f[k] * tp.force_decay_step;
+    if (h_uniform(tb, e, gid, HN_FORCE_SEL) < prob)
+      for (int k = 0; k < 3; k++) f[k] = h_normal(tb, e, gid, HN_FORCE_DIR + k) * tp.object_rb_mass * tp.force_scale;
+  }
 }
 
 // reset_target_pose: goal_states (13) and the goal actor's root row (13)

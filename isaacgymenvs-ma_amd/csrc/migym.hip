@@ -74,6 +74,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int nd = m->num_dofs, ns = m->num_sensors;
   mg::Team<T, MN, MC, MG, MP, OBJ> t;
   t.init(&lds[team].v, &tile, m, &p);
+  if (OBJ && t.tl < 4) {  // applied force on the object row of rb_forces (apply_rigid_body_force_tensors)
+    const float* fr = v.rb_forces ? v.rb_forces + ((size_t)(m->num_bodies + 2) * ac + m->num_bodies) * 3 : nullptr;
+    lds[team].v.oforce[t.tl] = t.tl < 3 ? (fr ? fr[t.tl] : 0.0f) : (v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f);
+  }
   __syncthreads();
   float* root = v.root_states + (size_t)13 * ROWS * ac;
   t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
@@ -444,15 +448,23 @@ __global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state
     tgt[d] = t;
     prev[d] = t;
   }
+  // random object forces (reset_idx's zeroing + probability redraw, then decay / new draws)
+  if (v.rb_forces || tb.random_force_prob) {
+    float* fr = v.rb_forces ? v.rb_forces + ((size_t)tp.rb_per_env * e + tp.object_rb) * 3 : nullptr;
+    float f[3] = {fr ? fr[0] : 0.0f, fr ? fr[1] : 0.0f, fr ? fr[2] : 0.0f};
+    mg::h_object_force(tp, tb, e, gid, env_reset, f);
+    if (fr)
+      for (int k = 0; k < 3; k++) fr[k] = f[k];
+  }
 }
 
 // observation value k of one env from its state rows (observationType layout, hand_task.hpp)
-__device__ __forceinline__ float hand_obs_value(const mg_task_params& tp, int k, int nd, const float* dof,
+__device__ __forceinline__ float hand_obs_value(int layout, const mg_task_params& tp, int k, int nd, const float* dof,
                                                 const float* dforce, const float* orow, const float* gs,
                                                 const float* qdiff, const float* rbs, const float* sens,
                                                 const float* act) {
   int i;
-  const int seg = mg::h_locate(tp, nd, k, &i);
+  const int seg = mg::h_locate_in(layout, tp, nd, k, &i);
   if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
     int b, c;
     mg::h_ft_ref(tp, seg, i, &b, &c);
@@ -480,11 +492,17 @@ __global__ __launch_bounds__(kBlock) void k_hand_post(mg_task_params tp, mg_stat
     float* o = tb.obs + (size_t)no * e;
     const float* rbs = v.rigid_body_states + (size_t)13 * tp.rb_per_env * e;
     for (int k = 0; k < no; k++) {
-      const float x = hand_obs_value(tp, k, nd, v.dof_state + (size_t)2 * nd * e, v.dof_force + (size_t)nd * e,
-                                     orow, gs, qdiff, rbs, v.sensors + (size_t)6 * tp.num_fingertips * e, act);
+      const float x = hand_obs_value(tp.obs_type, tp, k, nd, v.dof_state + (size_t)2 * nd * e,
+                                     v.dof_force + (size_t)nd * e, orow, gs, qdiff, rbs,
+                                     v.sensors + (size_t)6 * tp.num_fingertips * e, act);
       o[k] = x;
       if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(x, tp.clip_obs);
     }
+    if (tb.states)  // asymmetric_observations: states_buf = compute_full_state(asymm_obs=True)
+      for (int k = 0; k < tp.num_states; k++)
+        tb.states[(size_t)tp.num_states * e + k] =
+            hand_obs_value(0, tp, k, nd, v.dof_state + (size_t)2 * nd * e, v.dof_force + (size_t)nd * e, orow, gs,
+                           qdiff, rbs, v.sensors + (size_t)6 * tp.num_fingertips * e, act);
     float succ = tb.successes[e], rew;
     int64_t go;
     mg::h_reward(tp, orow, orow + 3, gs, gs + 3, act, tb.reset[e], tb.reset_goal[e], &prog, &succ, &rew, &ro, &go);
@@ -555,6 +573,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     } else {
       for (int k = 0; k < 13; k++) { gr[k] = root[26 + k]; gs[k] = tb.goal_states[(size_t)13 * ec + k]; }
     }
+    // random object forces: reset_idx zeroes / redraws the probability, pre_physics_step decays / draws
+    float f[3] = {0.0f, 0.0f, 0.0f};
+    if (v.rb_forces || tb.random_force_prob) {
+      const float* fr = v.rb_forces ? v.rb_forces + ((size_t)nbe * ec + nb) * 3 : nullptr;
+      if (fr)
+        for (int k = 0; k < 3; k++) f[k] = fr[k];
+      if (valid) mg::h_object_force(tp, tb, ec, gid, env_reset, f);
+    }
+    for (int k = 0; k < 3; k++) L.oforce[k] = f[k];
+    L.oforce[3] = v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f;
     if (env_reset) {
       float r[5];
       for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 4 + k));
@@ -683,6 +711,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.u.sv.st.dforce[k];
     for (int k = t.tl; k < 13 * nb; k += T) rbs[k] = bst[k];
     for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
+    if (v.rb_forces && t.tl < 3) v.rb_forces[((size_t)nbe * e + nb) * 3 + t.tl] = L.oforce[t.tl];
+    if (tb.states) {  // asymmetric_observations: the full_state layout (compute_full_state(asymm_obs=True))
+      const float* gs = L.goal + 13;
+      float qdiff[4];
+      const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
+      mg::t_quat_mul(L.oroot + 3, gc, qdiff);
+      for (int k = t.tl; k < tp.num_states; k += T) {
+        int i;
+        const int seg = mg::h_locate_in(0, tp, nd, k, &i);
+        float x;
+        if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
+          int b, c;
+          mg::h_ft_ref(tp, seg, i, &b, &c);
+          x = bst[13 * b + c];
+        } else {
+          x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
+                              L.obs + (no - na));
+        }
+        tb.states[(size_t)tp.num_states * e + k] = x;
+      }
+    }
   }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t)

@@ -187,6 +187,7 @@ struct TeamLDS {
   float oroot[OBJ ? 13 : 1];
   float goal[OBJ ? 26 : 1];   // goal actor root row, goal_states row
   float obs[OBJ ? 212 : 1];
+  float oforce[OBJ ? 4 : 1];  // external force on the object (apply_rigid_body_force_tensors), [3] = local
 };
 
 // A team's LDS region padded so that consecutive teams start 4*T bytes apart modulo 128 B.  A
@@ -644,7 +645,11 @@ struct Team {
     const V3 aw = obj_inv_inertia(cross(w, Iw) * -1.0f);
     if (objl) {
       const int k = tl - ob0;
-      const float a = k == 0 ? aw.x : k == 1 ? aw.y : k == 2 ? aw.z : m->obj_gravity * p->gravity[k - 3];
+      // applied force at the COM (LOCAL_SPACE: rotated by the orientation at the start of the substep)
+      const V3 fl = v3(s->oforce[0], s->oforce[1], s->oforce[2]);
+      const V3 fw = s->oforce[3] != 0.0f ? mul(oR, fl) : fl;
+      const float fk = k == 3 ? fw.x : k == 4 ? fw.y : fw.z;
+      const float a = k == 0 ? aw.x : k == 1 ? aw.y : k == 2 ? aw.z : m->obj_gravity * p->gravity[k - 3] + fk / m->obj_mass;
       nu += h * a;
       nu *= k < 3 ? 1.0f / (1.0f + h * m->obj_ang_damping) : 1.0f / (1.0f + h * m->obj_lin_damping);
     }

@@ -19,7 +19,10 @@ LIB_PATH = os.path.join(PKG_DIR, "_lib", "libmigym.so")
 MG_TASK_CARTPOLE, MG_TASK_ANT, MG_TASK_HUMANOID, MG_TASK_SHADOW_HAND = 0, 1, 2, 3
 MG_SET_ROOT_STATE, MG_SET_DOF_STATE, MG_SET_DOF_TARGET = 0, 1, 2
 MG_MAX_HAND_DOFS = 32
-HAND_NOISE_COLS = 61   # [goal-only 4 | reset_idx 53 | reset_target_pose 4] (shadow_hand.py:587, 610)
+# [goal-only 4 | reset_idx 53 | reset_target_pose 4 | force-prob redraw 1 | force select 1 | force dir 3]
+# (shadow_hand.py:587, 610, 642-643, 704-706)
+HAND_NOISE_COLS = 66
+MG_ENV_SPACE, MG_LOCAL_SPACE, MG_GLOBAL_SPACE = 0, 1, 2
 
 
 class SimParams(C.Structure):
@@ -32,7 +35,8 @@ class SimParams(C.Structure):
 class StateViews(C.Structure):
     _fields_ = [("root_states", C.c_void_p), ("dof_state", C.c_void_p), ("dof_actuation", C.c_void_p),
                 ("sensors", C.c_void_p), ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p),
-                ("dof_targets", C.c_void_p)]
+                ("dof_targets", C.c_void_p), ("rb_forces", C.c_void_p), ("rb_force_space", C.c_int32),
+                ("pad_views", C.c_int32)]
 
 
 class TaskParams(C.Structure):
@@ -59,7 +63,10 @@ class TaskParams(C.Structure):
                 ("av_factor", C.c_float), ("vel_obs_scale", C.c_float), ("force_torque_obs_scale", C.c_float),
                 ("reset_position_noise", C.c_float), ("reset_dof_pos_noise", C.c_float),
                 ("reset_dof_vel_noise", C.c_float), ("object_start", C.c_float * 3),
-                ("goal_displacement", C.c_float * 3), ("goal_dz", C.c_float)]
+                ("goal_displacement", C.c_float * 3), ("goal_dz", C.c_float),
+                ("num_states", C.c_int32), ("object_rb", C.c_int32), ("force_scale", C.c_float),
+                ("force_decay_step", C.c_float), ("force_prob_lo", C.c_float), ("force_prob_hi", C.c_float),
+                ("object_rb_mass", C.c_float)]
 
 
 class TaskBuffers(C.Structure):
@@ -70,7 +77,8 @@ class TaskBuffers(C.Structure):
                 ("noise", C.c_void_p), ("seed", C.c_uint64), ("step_counter", C.c_uint64),
                 ("env_offset", C.c_int64),
                 ("prev_targets", C.c_void_p), ("goal_states", C.c_void_p), ("reset_goal", C.c_void_p),
-                ("successes", C.c_void_p), ("consecutive_successes", C.c_void_p), ("reduce_scratch", C.c_void_p)]
+                ("successes", C.c_void_p), ("consecutive_successes", C.c_void_p), ("reduce_scratch", C.c_void_p),
+                ("states", C.c_void_p), ("random_force_prob", C.c_void_p)]
 
 
 def model_bytes(spec) -> np.ndarray:

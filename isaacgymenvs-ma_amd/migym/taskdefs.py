@@ -80,8 +80,6 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
         raise ValueError(f"Unknown type of observations! observationType should be one of: {sorted(HAND_OBS)}")
     if env.get("objectType", "block") != "block":
         raise ValueError("objectType must be 'block' (egg/pen meshes are out of scope)")
-    if env.get("asymmetric_observations", False):
-        raise ValueError("asymmetric_observations is not supported")
     tp = _abi.TaskParams()
     tp.task_id = _abi.MG_TASK_SHADOW_HAND
     tp.num_agents = 1
@@ -128,6 +126,19 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     tp.object_start[:] = (0.0, 0.0 + -0.39, 0.5 + 0.10)
     tp.goal_displacement[:] = (-0.2, -0.06, 0.12)
     tp.goal_dz = -0.04
+    # asymmetric actor-critic: states_buf (N, 211) = compute_full_state(asymm_obs=True) (shadow_hand.py:125-131)
+    tp.num_states = 211 if env.get("asymmetric_observations", False) else 0
+    # random object forces (shadow_hand.py:69-72, 196-199, 700-706); the per-step decay factor is
+    # torch.pow(float32 forceDecay, dt / forceDecayInterval) exactly as the reference evaluates it
+    import torch
+    tp.object_rb = len(spec.bodies)
+    tp.object_rb_mass = float(spec.obj["mass"]) if spec.obj else 0.0
+    tp.force_scale = float(env.get("forceScale", 0.0))
+    lo, hi = env.get("forceProbRange", [0.001, 0.1])
+    tp.force_prob_lo, tp.force_prob_hi = float(lo), float(hi)
+    decay = torch.tensor(float(env.get("forceDecay", 0.99)), dtype=torch.float32)
+    dt32 = float(torch.tensor(float(cfg["sim"]["dt"]), dtype=torch.float32))  # gymapi.SimParams.dt is a C float
+    tp.force_decay_step = float(torch.pow(decay, dt32 / float(env.get("forceDecayInterval", 0.08))))
     del nd
     return tp
 

@@ -31,14 +31,17 @@ class ShadowHand(VecTask):
         env = cfg["env"]
         if cfg.get("task", {}).get("randomize", False):
             raise NotImplementedError("domain randomization is not on this build's hot path (SURVEY.md §8(f))")
-        if float(env.get("forceScale", 0.0)) > 0.0:
-            raise NotImplementedError("random object forces (forceScale > 0) are not on the hot path")
         self.obs_type = env.get("observationType", "full_state")
         self.object_type = env.get("objectType", "block")
         self.max_episode_length = env["episodeLength"]
         self.num_fingertips = 5
         env["numObservations"] = taskdefs.HAND_OBS.get(self.obs_type, (0, 211))[1]
-        env["numStates"] = 0
+        self.asymmetric_obs = bool(env.get("asymmetric_observations", False))
+        env["numStates"] = 211 if self.asymmetric_obs else 0   # shadow_hand.py:125-131
+        self.force_scale = float(env.get("forceScale", 0.0))
+        self.force_prob_range = env.get("forceProbRange", [0.001, 0.1])
+        self.force_decay = env.get("forceDecay", 0.99)
+        self.force_decay_interval = env.get("forceDecayInterval", 0.08)
         env["numActions"] = 20
         self.up_axis_idx = 2
         super().__init__(cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture,
@@ -101,6 +104,12 @@ class ShadowHand(VecTask):
         v.dof_actuation, v.sensors = None, _abi.ptr(self.sensor_tensor)
         v.dof_force, v.rigid_body_states = _abi.ptr(self.dof_force_tensor), _abi.ptr(self.rigid_body_states)
         v.dof_targets = _abi.ptr(self.cur_targets)
+        # apply_rigid_body_force_tensors(sim, rb_forces, None, LOCAL_SPACE) (shadow_hand.py:708): the fused
+        # step updates and applies the object row every step (zero while forceScale is 0)
+        self.rb_forces = torch.zeros((N, self.num_bodies, 3), device=dev, dtype=f)
+        self.object_rb_handles = torch.tensor([self.num_shadow_hand_bodies], device=dev, dtype=torch.long)
+        self.object_rb_masses = torch.tensor([tp.object_rb_mass], device=dev, dtype=f)
+        v.rb_forces, v.rb_force_space = _abi.ptr(self.rb_forces), _abi.MG_LOCAL_SPACE
         self._views = v
         _abi.check(self._lib.mg_sim_bind(self.sim, _abi.C.byref(v)), self._lib)
 
@@ -116,10 +125,16 @@ class ShadowHand(VecTask):
         tb.prev_targets, tb.goal_states = _abi.ptr(self.prev_targets), _abi.ptr(self.goal_states)
         tb.reset_goal, tb.successes = _abi.ptr(self.reset_goal_buf), _abi.ptr(self.successes)
         tb.consecutive_successes, tb.reduce_scratch = _abi.ptr(self.consecutive_successes), _abi.ptr(self._reduce)
+        # random force probability per env (shadow_hand.py:196-199), redrawn on reset inside the step
+        lo, hi = (torch.tensor(float(x), device=dev) for x in self.force_prob_range)
+        self.random_force_prob = torch.exp((torch.log(lo) - torch.log(hi)) * torch.rand(N, device=dev) + torch.log(hi))
+        tb.random_force_prob = _abi.ptr(self.random_force_prob)
+        tb.states = _abi.ptr(self.states_buf) if self.num_states > 0 else None
 
     def post_step_extras(self):
         self.extras["consecutive_successes"] = self.consecutive_successes.mean()
 
     def set_reset_noise(self, noise):
-        """Inject per-env U(0,1) rows (N, 61) = [goal-only 4 | reset_idx 53 | reset_target_pose 4]."""
+        """Inject per-env rows (N, 66) = [goal-only 4 | reset_idx 53 | reset_target_pose 4 | force probability
+        redraw 1 | force selection 1 (all U(0,1)) | force direction 3 (N(0,1))]."""
         super().set_reset_noise(noise)

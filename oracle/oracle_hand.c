@@ -27,6 +27,12 @@
 #include "oracle.h"
 
 #define PI_F 3.14159265358979323846f
+/* injected noise row: [goal-only 4 | reset_idx 53 | reset_target_pose 4 | force prob 1 | force select 1 |
+ * force direction 3] (shadow_hand.py:587, 610, 642-643, 704-706) */
+#define HN_COLS 66
+#define HN_FORCE_PROB 61
+#define HN_FORCE_SEL 62
+#define HN_FORCE_DIR 63
 
 static void h_quat_mul(const float* a, const float* b, float* o) { /* torch_jit_utils.py:41-62 */
   float x1 = a[0], y1 = a[1], z1 = a[2], w1 = a[3];
@@ -127,10 +133,38 @@ int orc_hand_reward(const mg_task_params* tp, int32_t n, float max_episode_lengt
 
 /* ---------------------------------------------------------------- resets + targets */
 static float hu(const mg_task_buffers* tb, int e, int k) {
-  return tb->noise ? tb->noise[(size_t)61 * e + k]
+  return tb->noise ? tb->noise[(size_t)HN_COLS * e + k]
                    : orc_uniform(tb->seed, (uint64_t)(tb->env_offset + e), tb->step_counter, (uint32_t)k);
 }
 static float rand_pm1(float u) { return 2.0f * u + -1.0f; } /* torch_rand_float(-1, 1): (1 - -1) * u + -1 */
+
+/* N(0,1) draw k: injected column, or Box-Muller on two counter-based uniforms (same recipe as the GPU) */
+static float hn(const mg_task_buffers* tb, int e, int k) {
+  if (tb->noise) return tb->noise[(size_t)HN_COLS * e + k];
+  const uint64_t gid = (uint64_t)(tb->env_offset + e);
+  const float u1 = orc_uniform(tb->seed, gid, tb->step_counter, (uint32_t)(128 + 2 * k));
+  const float u2 = orc_uniform(tb->seed, gid, tb->step_counter, (uint32_t)(129 + 2 * k));
+  return sqrtf(-2.0f * logf(1.0f - u1)) * cosf(6.28318530717958647f * u2);
+}
+
+/* random object force of env e (shadow_hand.py:641-643 reset_idx; 700-706 pre_physics_step):
+ * a reset zeroes rb_forces[e] and redraws random_force_prob[e] = exp((log lo - log hi) u + log hi);
+ * with forceScale > 0 the force decays by forceDecay^(dt/forceDecayInterval) and, when
+ * U(0,1) < prob, becomes randn(3) * object mass * forceScale. */
+static void object_force(const mg_task_params* tp, const mg_task_buffers* tb, int e, int env_reset, float* f) {
+  float prob = tb->random_force_prob ? tb->random_force_prob[e] : 0.0f;
+  if (env_reset) {
+    f[0] = f[1] = f[2] = 0.0f;
+    const float lhi = logf(tp->force_prob_hi);
+    prob = expf((logf(tp->force_prob_lo) - lhi) * hu(tb, e, HN_FORCE_PROB) + lhi);
+    if (tb->random_force_prob) tb->random_force_prob[e] = prob;
+  }
+  if (tp->force_scale > 0.0f) {
+    for (int k = 0; k < 3; k++) f[k] = f[k] * tp->force_decay_step;
+    if (hu(tb, e, HN_FORCE_SEL) < prob)
+      for (int k = 0; k < 3; k++) f[k] = hn(tb, e, HN_FORCE_DIR + k) * tp->object_rb_mass * tp->force_scale;
+  }
+}
 
 static void reset_target_pose(const mg_task_params* tp, const mg_task_buffers* tb, float* root_env, int e,
                               float g0, float g1) {
@@ -201,6 +235,13 @@ int orc_hand_pre_physics(const mg_model* m, const mg_task_params* tp, const mg_s
       tgt[(size_t)nd * e + d] = t;
       *prev = t;
     }
+    if (v->rb_forces || tb->random_force_prob) {
+      float* fr = v->rb_forces ? v->rb_forces + ((size_t)tp->rb_per_env * e + tp->object_rb) * 3 : NULL;
+      float f[3] = {fr ? fr[0] : 0.0f, fr ? fr[1] : 0.0f, fr ? fr[2] : 0.0f};
+      object_force(tp, tb, e, env_reset, f);
+      if (fr)
+        for (int k = 0; k < 3; k++) fr[k] = f[k];
+    }
   }
   return 0;
 }
@@ -215,7 +256,7 @@ static const int LAYOUT[4][12] = {
     {DOFP, OPOSE, GPOSE, QDIFF, FTP, ACTS, END, END, END, END, END, END},
     {FTP, OPOS, QDIFF, ACTS, END, END, END, END, END, END, END, END}};
 
-static void hand_obs_one(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
+static void hand_obs_one(int layout, const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
                          const mg_task_buffers* tb, const float* act, int e, float* o) {
   const int nd = m->num_dofs, nb = tp->rb_per_env, nf = tp->num_fingertips;
   const float* dof = v->dof_state + (size_t)2 * nd * e;
@@ -225,8 +266,8 @@ static void hand_obs_one(const mg_model* m, const mg_task_params* tp, const mg_s
   float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]}, qdiff[4];
   h_quat_mul(ob + 3, gc, qdiff);
   int k = 0;
-  for (int s = 0; s < 12 && LAYOUT[tp->obs_type & 3][s] != END; s++) {
-    switch (LAYOUT[tp->obs_type & 3][s]) {
+  for (int s = 0; s < 12 && LAYOUT[layout & 3][s] != END; s++) {
+    switch (LAYOUT[layout & 3][s]) {
       case DOFP:
         for (int j = 0; j < nd; j++)
           o[k++] = (2.0f * dof[2 * j] - tp->dof_upper[j] - tp->dof_lower[j]) / (tp->dof_upper[j] - tp->dof_lower[j]);
@@ -241,7 +282,7 @@ static void hand_obs_one(const mg_model* m, const mg_task_params* tp, const mg_s
       case QDIFF: for (int c = 0; c < 4; c++) o[k++] = qdiff[c]; break;
       case FTS:
       case FTP: {
-        const int w = LAYOUT[tp->obs_type & 3][s] == FTS ? 13 : 3;
+        const int w = LAYOUT[layout & 3][s] == FTS ? 13 : 3;
         for (int f = 0; f < nf; f++)
           for (int c = 0; c < w; c++) o[k++] = rbs[(size_t)13 * tp->fingertip_body[f] + c];
         break;
@@ -262,7 +303,9 @@ int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_
     tb->progress[e] += 1;
     const float* act = tb->actions_out + (size_t)na * e;
     float* o = tb->obs + (size_t)no * e;
-    hand_obs_one(m, tp, v, tb, act, e, o);
+    hand_obs_one(tp->obs_type, m, tp, v, tb, act, e, o);
+    /* asymmetric_observations: states_buf = compute_full_state(asymm_obs=True) (shadow_hand.py:470-471) */
+    if (tb->states && tp->num_states > 0) hand_obs_one(0, m, tp, v, tb, act, e, tb->states + (size_t)tp->num_states * e);
     const float* ob = v->root_states + (size_t)39 * e + 13;
     const float* gs = tb->goal_states + (size_t)13 * e;
     int64_t ro, go;

@@ -137,6 +137,8 @@ typedef struct {
   double qj[MAXN], qd[MAXN];
   double op[3], oq[4];   /* free object pose (COM = origin) */
   double ow[3], ov[3];   /* object angular / COM linear velocity (world) */
+  double of[3];          /* applied force on the object COM (apply_rigid_body_force_tensors) */
+  int of_local;          /* LOCAL_SPACE: of is in the object frame at the start of each substep */
   const float* tgt;      /* PD targets (nD) or NULL */
   int sat[MAXN];         /* drive saturated in the last substep */
   double ttend[MAXN];    /* tendon generalized force of the last substep */
@@ -790,6 +792,10 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       rhs[nv + a] = -gyro[a];
       rhs[nv + 3 + a] = m->obj_mass * m->obj_gravity * p->gravity[a];
     }
+    double fw[3];
+    if (s->of_local) matvec3(k.oR, s->of, fw);
+    else for (int a = 0; a < 3; a++) fw[a] = s->of[a];
+    for (int a = 0; a < 3; a++) rhs[nv + 3 + a] += fw[a];
   }
   if (cholesky(M, nvt) != 0) return;
   chol_solve(M, nvt, rhs);
@@ -1011,12 +1017,16 @@ static void body_states(const mg_model* m, const astate* s, float* out) {
 /* one env: root rows [articulation, (object, goal)], dof rows, PD targets, sensors, dof forces,
  * rigid-body rows [articulation bodies, (object, goal)] */
 static void simulate_env(const mg_model* m, const mg_sim_params* p, float* root, float* dof, const float* act,
-                         const float* tgt, float* sensors, float* dof_force, float* rbs) {
+                         const float* tgt, float* sensors, float* dof_force, float* rbs, const float* oforce,
+                         int oforce_local) {
   astate s;
   memset(&s, 0, sizeof(s));
   load_state(m, root, dof, &s);
   s.tgt = tgt;
   if (m->obj_type) load_object(&s, root + 13);
+  if (oforce)
+    for (int a = 0; a < 3; a++) s.of[a] = oforce[a];
+  s.of_local = oforce_local;
   double tau[MAXN];
   for (int i = 0; i < m->num_dofs; i++) tau[i] = act ? act[i] : 0.0;
   substep_out* so = (substep_out*)malloc(sizeof(substep_out));
@@ -1048,7 +1058,9 @@ int orc_simulate_views(const mg_model* m, const mg_sim_params* p, int32_t n, con
                  v->dof_actuation ? v->dof_actuation + (size_t)nd * e : 0,
                  v->dof_targets ? v->dof_targets + (size_t)nd * e : 0, v->sensors ? v->sensors + (size_t)6 * ns * e : 0,
                  v->dof_force ? v->dof_force + (size_t)nd * e : 0,
-                 v->rigid_body_states ? v->rigid_body_states + (size_t)13 * nb * e : 0);
+                 v->rigid_body_states ? v->rigid_body_states + (size_t)13 * nb * e : 0,
+                 (m->obj_type && v->rb_forces) ? v->rb_forces + ((size_t)nb * e + m->num_bodies) * 3 : 0,
+                 v->rb_force_space == MG_LOCAL_SPACE);
   }
   (void)threads;
   return 0;

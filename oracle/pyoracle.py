@@ -234,18 +234,24 @@ class HandHostEnv:
         self.successes = np.zeros(n, np.float32)
         self.cons = np.zeros(1, np.float32)
         self.noise = None
+        # random object forces (apply_rigid_body_force_tensors, LOCAL_SPACE) and asymmetric states
+        self.rb_forces = np.zeros((n, nb, 3), np.float32)
+        self.force_prob = None
+        self.states = None
 
     def views(self):
         v = _abi.StateViews()
         v.root_states, v.dof_state, v.dof_actuation = p(self.root), p(self.dof), None
         v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), p(self.rbs)
         v.dof_targets = p(self.targets)
+        v.rb_forces, v.rb_force_space = p(self.rb_forces), _abi.MG_LOCAL_SPACE
         return v
 
     def buffers(self, seed=0, step=0, env_offset=0):
         b = _abi.TaskBuffers()
         b.actions, b.actions_out, b.obs, b.obs_clamped = p(self.actions), p(self.actions_out), p(self.obs), \
             p(self.obs_clamped)
+        b.states, b.random_force_prob = p(self.states), p(self.force_prob)
         b.rew, b.reset, b.progress, b.timeout = p(self.rew), p(self.reset), p(self.progress), p(self.timeout)
         b.noise = p(self.noise)
         b.seed, b.step_counter, b.env_offset = seed, step, env_offset

@@ -373,6 +373,13 @@ class FakeHandGym(FakeGym):
     def get_asset_rigid_shape_count(self, a):
         return 22
 
+    def load_asset(self, sim, root, path, *a):
+        return path
+
+    def get_asset_rigid_body_count(self, a):
+        # the hand MJCF has the articulation's bodies; the object and goal URDFs one body each
+        return len(self.spec["bodies"]) if str(a).endswith(".xml") else 1
+
     def get_asset_actuator_count(self, a):
         return len(self.spec["actuated"])
 
@@ -436,6 +443,9 @@ class FakeHandGym(FakeGym):
     def set_dof_position_target_tensor(self, sim, t):
         self.targets = t.clone()
 
+    def apply_rigid_body_force_tensors(self, sim, forces, torques, space):
+        self.calls.append(("rb_forces", forces.clone(), int(space)))
+
     def simulate(self, sim):
         N, nd, g = self.N, self.spec["num_dof"], self.gen
         rec = {"root_pre": self.root.view(N, 3, 13).clone(), "dof_pre": self.dof.view(N, nd, 2).clone(),
@@ -467,7 +477,28 @@ class FakeHandGym(FakeGym):
         self.record = rec
 
 
-def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state"):
+class _TorchRecorder:
+    """Stands in for a task module's ``torch``: every ``torch.rand`` / ``torch.randn`` draw is kept."""
+
+    def __init__(self):
+        self.draws = []
+
+    def __getattr__(self, k):
+        return getattr(torch, k)
+
+    def rand(self, *shape, **kw):
+        u = torch.rand(*shape, **kw)
+        self.draws.append(("rand", u.clone()))
+        return u
+
+    def randn(self, *shape, **kw):
+        u = torch.randn(*shape, **kw)
+        self.draws.append(("randn", u.clone()))
+        return u
+
+
+def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state", force_scale=0.0, asymmetric=False,
+                   force_prob_range=None):
     import importlib
     sys.path.insert(0, os.path.join(HERE, "..", "..", "isaacgymenvs-ma_amd"))
     from migym import model as M
@@ -482,16 +513,24 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state"):
     install_fake(fake)
     rec = RandRecorder()
     mod.torch_rand_float = rec
+    trec = _TorchRecorder()
+    mod.torch = trec
     cfg = load_task_cfg("ShadowHand", N, ep_len)
     cfg["env"]["observationType"] = obs_type
+    cfg["env"]["forceScale"] = force_scale
+    cfg["env"]["asymmetric_observations"] = asymmetric
+    if force_prob_range is not None:
+        cfg["env"]["forceProbRange"] = force_prob_range
     torch.manual_seed(0)
     env = mod.ShadowHand(cfg, "cpu", "cpu", -1, True, False, False)
+    init_force_prob = env.random_force_prob.clone()
     fake.env = env
     nd = spec["num_dof"]
     g = torch.Generator().manual_seed(4)
     keys = ("actions", "noise", "reset_in", "reset_goal_in", "progress_in", "root_pre", "dof_pre", "targets",
             "prev_targets", "goal_states", "phys_root", "phys_dof", "phys_rbs", "phys_sensors", "phys_dof_force",
-            "obs", "rew", "reset", "reset_goal", "progress", "successes", "cons", "timeouts")
+            "obs", "rew", "reset", "reset_goal", "progress", "successes", "cons", "timeouts", "rb_forces",
+            "force_prob", "states")
     out = {k: [] for k in keys}
     out["init_root"] = env.root_state_tensor.view(N, 3, 13).clone()
     out["init_goal_states"] = env.goal_states.clone()
@@ -500,8 +539,9 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state"):
         reset_in, goal_in = env.reset_buf.clone(), env.reset_goal_buf.clone()
         progress_in = env.progress_buf.clone()
         rec.draws.clear()
+        trec.draws.clear()
         obs_dict, rew, reset, extras = env.step(actions)
-        noise = torch.zeros(N, 61)
+        noise = torch.zeros(N, 66)
         gids = goal_in.nonzero(as_tuple=False).flatten()
         eids = reset_in.nonzero(as_tuple=False).flatten()
         k = 0
@@ -511,6 +551,23 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state"):
         if len(eids) > 0:
             noise[eids, 4:57] = rec.draws[k]
             noise[eids, 57:61] = rec.draws[k + 1]
+        # torch.rand / randn draws of the module, in call order: reset_idx's force-probability redraw
+        # (shadow_hand.py:642-643), then with forceScale > 0 the selection U(0,1) over all envs and the
+        # N(0,1) force rows of the selected envs (704-706)
+        td = list(trec.draws)
+        if len(eids) > 0:
+            kind, u = td.pop(0)
+            assert kind == "rand" and u.shape == (len(eids),)
+            noise[eids, 61] = u
+        if force_scale > 0.0:
+            kind, u = td.pop(0)
+            assert kind == "rand" and u.shape == (N,)
+            noise[:, 62] = u
+            sel = (u < env.random_force_prob).nonzero(as_tuple=False).flatten()
+            kind, gn = td.pop(0)
+            assert kind == "randn" and gn.shape[0] == len(sel)
+            noise[sel, 63:66] = gn.reshape(len(sel), 3)
+        assert not td, [d[0] for d in td]
         r = fake.record
         out["actions"].append(actions)
         out["noise"].append(noise)
@@ -530,9 +587,15 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state"):
         out["successes"].append(env.successes.clone())
         out["cons"].append(env.consecutive_successes.clone())
         out["timeouts"].append(extras["time_outs"].clone().long())
+        out["rb_forces"].append(env.rb_forces.clone())
+        out["force_prob"].append(env.random_force_prob.clone())
+        out["states"].append(obs_dict["states"].clone() if asymmetric else torch.zeros(N, 0))
     res = {k: (torch.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
     res["episode_length"] = torch.tensor(ep_len)
     res["obs_type"] = np.array(obs_type)
+    res["init_force_prob"] = init_force_prob
+    res["force_scale"] = torch.tensor(force_scale)
+    res["object_mass"] = torch.tensor(0.070875)
     return res
 
 
@@ -548,7 +611,7 @@ def main():
     # one task per process: vec_task keeps a process-global sim (vec_task.py:55-64)
     if which == "all":
         import subprocess
-        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs"):
+        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces"):
             subprocess.check_call([sys.executable, __file__, t])
         return
     if which == "ant":
@@ -559,6 +622,9 @@ def main():
         save("trace_cartpole.npz", run_cartpole())
     elif which == "shadowhand":
         save("trace_shadowhand.npz", run_shadowhand())
+    elif which == "shadowhand_forces":  # random object forces + asymmetric states (forceScale > 0)
+        save("trace_shadowhand_forces.npz", run_shadowhand(N=32, T=8, ep_len=4, force_scale=2.0, asymmetric=True,
+                                                               force_prob_range=[0.2, 0.8]))
     elif which == "shadowhand_obs":  # the other observationType layouts, smaller traces
         for ot in ("full", "full_no_vel", "openai"):
             save(f"trace_shadowhand_{ot}.npz", run_shadowhand(N=16, T=4, ep_len=3, obs_type=ot))

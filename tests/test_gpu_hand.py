@@ -18,6 +18,7 @@ import torch
 
 import pyoracle as O
 from migym import _abi, configs, model as M, taskdefs
+from test_oracle_golden import HAND_TRACES, hand_noise, hand_trace_setup
 
 pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden")
@@ -61,12 +62,16 @@ class DevHandEnv:
         self.timeout = torch.zeros(h.n, dtype=torch.bool, device=DEV)
         self.scratch = torch.zeros(2, dtype=torch.int64, device=DEV)
         self.noise = None
+        self.rb_forces = T(h.rb_forces)
+        self.force_prob = None if h.force_prob is None else T(h.force_prob)
+        self.states = None if h.states is None else T(h.states)
 
     def views(self):
         v = _abi.StateViews()
         v.root_states, v.dof_state, v.dof_actuation = P(self.root), P(self.dof), None
         v.sensors, v.dof_force, v.rigid_body_states = P(self.sensors), P(self.dof_force), P(self.rbs)
         v.dof_targets = P(self.targets)
+        v.rb_forces, v.rb_force_space = P(self.rb_forces), _abi.MG_LOCAL_SPACE
         return v
 
     def buffers(self, seed=0, step=0):
@@ -78,6 +83,7 @@ class DevHandEnv:
         b.seed, b.step_counter, b.env_offset = seed, step, 0
         b.prev_targets, b.goal_states, b.reset_goal = P(self.prev_targets), P(self.goal_states), P(self.reset_goal)
         b.successes, b.consecutive_successes, b.reduce_scratch = P(self.successes), P(self.cons), P(self.scratch)
+        b.states, b.random_force_prob = P(self.states), P(self.force_prob)
         return b
 
 
@@ -85,29 +91,31 @@ def np_(t):
     return t.cpu().numpy()
 
 
-@pytest.mark.parametrize("trace", ["trace_shadowhand.npz", "trace_shadowhand_full.npz",
-                                   "trace_shadowhand_full_no_vel.npz", "trace_shadowhand_openai.npz"])
+@pytest.mark.parametrize("trace", HAND_TRACES)
 def test_hand_task_layer_replays_reference_trace(lib, trace):
     d = dict(np.load(os.path.join(G, trace)))
-    cfg = configs.task_config("ShadowHand", 16)
-    cfg["env"]["observationType"] = str(d["obs_type"])
-    spec = M.load_builtin("shadow_hand")
-    tp = taskdefs.task_params("ShadowHand", cfg, spec)
-    tp.max_episode_length = int(d["episode_length"])
+    spec, tp = hand_trace_setup(d)
     Tn, N = d["actions"].shape[:2]
     h = O.HandHostEnv(tp, spec, N)
     h.root[:] = d["init_root"]
     h.goal_states[:] = d["init_goal_states"]
+    forces = "force_scale" in d
+    if forces:
+        h.force_prob = O.f32(d["init_force_prob"]).copy()
+        h.states = np.zeros((N, tp.num_states), np.float32)
     e = DevHandEnv(h)
     for t in range(Tn):
         e.actions.copy_(T(d["actions"][t]))
-        e.noise = T(d["noise"][t])
+        e.noise = T(hand_noise(d, t))
         _abi.check(lib.mg_pre_physics(None, C.byref(tp), C.byref(e.views()), C.byref(e.buffers()), N, stream()), lib)
         torch.cuda.synchronize()
         np.testing.assert_allclose(np_(e.root), d["root_pre"][t], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(np_(e.dof), d["dof_pre"][t], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(np_(e.targets), d["targets"][t], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(np_(e.goal_states), d["goal_states"][t], rtol=1e-5, atol=1e-6)
+        if forces:
+            np.testing.assert_allclose(np_(e.rb_forces), d["rb_forces"][t], rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(np_(e.force_prob), d["force_prob"][t], rtol=1e-5)
         e.root.copy_(T(d["phys_root"][t]))
         e.dof.copy_(T(d["phys_dof"][t]))
         e.rbs.copy_(T(d["phys_rbs"][t]))
@@ -125,6 +133,9 @@ def test_hand_task_layer_replays_reference_trace(lib, trace):
         np.testing.assert_allclose(np_(e.cons), d["cons"][t], rtol=1e-6)
         np.testing.assert_array_equal(np_(e.timeout).astype(np.int64), d["timeouts"][t])
         assert int(e.scratch.abs().sum()) == 0  # the finishing kernel clears the partial sums
+        if forces:
+            np.testing.assert_allclose(np.clip(np_(e.states), -tp.clip_obs, tp.clip_obs), d["states"][t],
+                                       rtol=1e-4, atol=1e-4)
 
 
 def hand_states(spec, tp, n, rng):
@@ -156,6 +167,8 @@ def test_hand_physics_step_matches_oracle(lib):
     n = 256
     rng = np.random.default_rng(5)
     h = hand_states(spec, tp, n, rng)
+    # applied object forces (LOCAL_SPACE) on half of the envs
+    h.rb_forces[: n // 2, len(spec.bodies)] = rng.normal(0, 0.3, (n // 2, 3))
     e = DevHandEnv(h)
     mnp = M.pack_model(spec)
     h.simulate(mnp, sp, threads=8)
@@ -209,6 +222,44 @@ def test_hand_fused_env_step_matches_oracle(lib):
     assert env_agreement(np_(e.obs), h.obs, 2e-2, 2e-2) >= 0.97
     assert env_agreement(np_(e.rew), h.rew, 5e-2, 5e-2) >= 0.97
     np.testing.assert_allclose(np_(e.cons), h.cons, atol=2e-2)
+
+
+def test_hand_fused_forces_and_states_match_oracle(lib):
+    """mg_env_step with random object forces (forceScale 2, forceProbRange [0.2, 0.8]) and asymmetric
+    states vs the oracle over 3 control steps with the device RNG: force draws, probability redraws
+    and the applied force in the object's dynamics."""
+    cfg = configs.task_config("ShadowHand", 16)
+    cfg["env"]["forceScale"] = 2.0
+    cfg["env"]["forceProbRange"] = [0.2, 0.8]
+    cfg["env"]["asymmetric_observations"] = True
+    spec = M.load_builtin("shadow_hand")
+    sp, tp = taskdefs.sim_params(cfg, 24), taskdefs.task_params("ShadowHand", cfg, spec)
+    assert tp.num_states == 211 and tp.force_scale == 2.0
+    n = 128
+    h = O.HandHostEnv(tp, spec, n)
+    h.force_prob = np.full(n, 0.5, np.float32)
+    h.states = np.zeros((n, 211), np.float32)
+    e = DevHandEnv(h)
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
+    rng = np.random.default_rng(11)
+    for t in range(3):
+        a = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+        h.actions[:] = a
+        e.actions.copy_(T(a))
+        h.env_step(mnp, sp, tp, seed=9, step=t, threads=8)
+        _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=9, step=t)), stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    nb = len(spec.bodies)
+    assert np.abs(h.rb_forces[:, nb]).sum(-1).astype(bool).mean() > 0.3   # forces were drawn
+    np.testing.assert_allclose(np_(e.rb_forces), h.rb_forces, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(np_(e.force_prob), h.force_prob, rtol=1e-5)
+    assert env_agreement(np_(e.root)[:, 1], h.root[:, 1], 2e-3, 2e-3) >= 0.97
+    assert env_agreement(np_(e.states), h.states, 2e-2, 2e-2) >= 0.97
+    np.testing.assert_allclose(np_(e.states)[:, 211 - 20:], np_(e.obs)[:, 211 - 20:])  # actions block
 
 
 def test_hand_set_indexed_maps_actor_ids(lib):
@@ -282,4 +333,32 @@ def test_hand_make_full_size():
     assert torch.isfinite(obj).all() and float(obj[:, 7:13].abs().max()) < 100.0
     # the cube stays with the hand for most envs (falls reset them; fall distance 0.24)
     assert float((obj[:, 2] > 0.2).float().mean()) > 0.9
+    env.close()
+
+
+def test_hand_make_asymmetric_with_forces():
+    """make() with asymmetric_observations and forceScale > 0: obs_dict['states'] (N, 211) clamped to
+    clipObservations, rb_forces (N, 27, 3) populated on the object row only."""
+    import migym
+    n = 512
+    cfg = configs.task_config("ShadowHand", n, sim_device=DEV)
+    cfg["env"]["asymmetric_observations"] = True
+    cfg["env"]["forceScale"] = 1.0
+    cfg["env"]["forceProbRange"] = [0.1, 0.5]
+    env = migym.make(seed=0, task="ShadowHand", num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                     cfg={"task": cfg})
+    assert env.num_states == 211 and env.states_buf.shape == (n, 211)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(10):
+        obs, rew, reset, extras = env.step(torch.rand((n, 20), device=DEV, generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    st = obs["states"]
+    assert st.shape == (n, 211) and torch.isfinite(st).all() and float(st.abs().max()) <= 5.0
+    # states = full_state layout: actions block equals the obs actions block (obs is full_state too)
+    assert torch.equal(st[:, 191:], obs["obs"][:, 191:])
+    obj = len(env.model_spec.bodies)
+    f = env.rb_forces
+    assert float(f[:, obj].abs().sum()) > 0 and float(f[:, :obj].abs().sum()) == 0.0
+    p = env.random_force_prob
+    assert float(p.min()) >= 0.1 - 1e-6 and float(p.max()) <= 0.5 + 1e-6
     env.close()

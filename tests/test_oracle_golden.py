@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import pyoracle as O
-from migym import model as M, taskdefs, configs
+from migym import _abi, model as M, taskdefs, configs
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 RTOL, ATOL = 2e-5, 2e-5
@@ -157,26 +157,54 @@ def test_shadowhand_reward_and_rotation_match_reference():
     np.testing.assert_allclose(cons, d["cons_out"], rtol=1e-6)
 
 
-@pytest.mark.parametrize("trace", ["trace_shadowhand.npz", "trace_shadowhand_full.npz",
-                                   "trace_shadowhand_full_no_vel.npz", "trace_shadowhand_openai.npz"])
-def test_shadowhand_trace_matches_reference(trace):
-    """Whole physics-free ShadowHand VecTask.step (pre_physics resets + PD targets, observations of
-    every observationType, reward, running mean, timeouts) replayed with the reference's own reset
-    draws injected."""
-    d = load(trace)
-    cfg = configs.task_config("ShadowHand", 16)
+def hand_noise(d, t):
+    """Injected noise row of step t, padded to the 66 columns of the current layout (the traces made
+    before the random-force columns existed hold the first 61)."""
+    x = O.f32(d["noise"][t])
+    return np.ascontiguousarray(np.pad(x, ((0, 0), (0, _abi.HAND_NOISE_COLS - x.shape[1]))))
+
+
+def hand_trace_setup(d, n=16):
+    """Task params of a ShadowHand trace: observation type, episode length, and for the forces trace
+    forceScale / forceProbRange / asymmetric states with the fake gym's object mass."""
+    cfg = configs.task_config("ShadowHand", n)
     cfg["env"]["observationType"] = str(d["obs_type"])
+    if "force_scale" in d:
+        cfg["env"]["forceScale"] = float(d["force_scale"])
+        cfg["env"]["forceProbRange"] = [0.2, 0.8]
+        cfg["env"]["asymmetric_observations"] = d["states"].shape[-1] > 0
     spec = M.load_builtin("shadow_hand")
     tp = taskdefs.task_params("ShadowHand", cfg, spec)
     tp.max_episode_length = int(d["episode_length"])
+    if "object_mass" in d:
+        tp.object_rb_mass = float(d["object_mass"])
+    return spec, tp
+
+
+HAND_TRACES = ["trace_shadowhand.npz", "trace_shadowhand_full.npz", "trace_shadowhand_full_no_vel.npz",
+               "trace_shadowhand_openai.npz", "trace_shadowhand_forces.npz"]
+
+
+@pytest.mark.parametrize("trace", HAND_TRACES)
+def test_shadowhand_trace_matches_reference(trace):
+    """Whole physics-free ShadowHand VecTask.step (pre_physics resets + PD targets, observations of
+    every observationType, reward, running mean, timeouts) replayed with the reference's own reset
+    draws injected.  The forces trace adds random object forces (forceScale 2, rb_forces after the
+    decay / redraw, the per-env probability redrawn on reset) and the asymmetric states buffer."""
+    d = load(trace)
+    spec, tp = hand_trace_setup(d)
     mnp = M.pack_model(spec)
     T, N = d["actions"].shape[:2]
     h = O.HandHostEnv(tp, spec, N)
     h.root[:] = d["init_root"]
     h.goal_states[:] = d["init_goal_states"]
+    forces = "force_scale" in d
+    if forces:
+        h.force_prob = O.f32(d["init_force_prob"]).copy()
+        h.states = np.zeros((N, tp.num_states), np.float32)
     for t in range(T):
         h.actions[:] = d["actions"][t]
-        h.noise = O.f32(d["noise"][t])
+        h.noise = hand_noise(d, t)
         np.testing.assert_array_equal(h.reset, d["reset_in"][t])
         np.testing.assert_array_equal(h.reset_goal, d["reset_goal_in"][t])
         np.testing.assert_array_equal(h.progress, d["progress_in"][t])
@@ -186,6 +214,9 @@ def test_shadowhand_trace_matches_reference(trace):
         np.testing.assert_allclose(h.targets, d["targets"][t], rtol=1e-6, atol=1e-7)
         np.testing.assert_allclose(h.prev_targets, d["prev_targets"][t], rtol=1e-6, atol=1e-7)
         np.testing.assert_allclose(h.goal_states, d["goal_states"][t], rtol=1e-6, atol=1e-7)
+        if forces:
+            np.testing.assert_allclose(h.rb_forces, d["rb_forces"][t], rtol=1e-6, atol=1e-7)
+            np.testing.assert_allclose(h.force_prob, d["force_prob"][t], rtol=1e-6)
         # "physics": the trace's injected post-simulate state
         h.root[:] = d["phys_root"][t]
         h.dof[:] = d["phys_dof"][t]
@@ -201,3 +232,6 @@ def test_shadowhand_trace_matches_reference(trace):
         np.testing.assert_array_equal(h.successes, d["successes"][t])
         np.testing.assert_allclose(h.cons, d["cons"][t], rtol=1e-6)
         np.testing.assert_array_equal(h.timeout, d["timeouts"][t])
+        if forces:  # get_state() = clamp(states_buf, +-clipObservations)
+            np.testing.assert_allclose(np.clip(h.states, -tp.clip_obs, tp.clip_obs), d["states"][t], rtol=RTOL,
+                                       atol=ATOL)

@@ -43,6 +43,30 @@ def test_object_free_fall_and_spin():
     assert np.linalg.norm(h.root[0, 1, 3:7]) == np.float32(1.0) or abs(np.linalg.norm(h.root[0, 1, 3:7]) - 1) < 1e-6
 
 
+def test_object_applied_force_local_space():
+    """apply_rigid_body_force_tensors(..., LOCAL_SPACE) on the object row (shadow_hand.py:708): the body-frame
+    force is rotated by the orientation at the start of each substep and accelerates the COM by F/m."""
+    spec, tp, sp, mnp, h = setup()
+    park_object(h)
+    # object turned 90 deg about z: body x -> world y
+    h.root[:, 1, 3:7] = (0.0, 0.0, np.sin(np.pi / 4), np.cos(np.pi / 4))
+    m = spec.obj["mass"]
+    h.rb_forces[:, len(spec.bodies)] = (2.0 * m, 0.0, 0.0)   # 2 m/s^2 along body x
+    h.simulate(mnp, sp)
+    dt = sp.dt
+    np.testing.assert_allclose(h.root[0, 1, 7], 0.0, atol=1e-6)
+    np.testing.assert_allclose(h.root[0, 1, 8], 2.0 * dt, rtol=1e-5)
+    np.testing.assert_allclose(h.root[0, 1, 9], -G * dt, rtol=1e-5)
+    # world-space forces are applied as given
+    park_object(h)
+    h.root[:, 1, 3:7] = (0.0, 0.0, np.sin(np.pi / 4), np.cos(np.pi / 4))
+    v = h.views()
+    v.rb_force_space = 0
+    O.lib().orc_simulate_views(mnp.ctypes.data, O.C.byref(sp), h.n, O.C.byref(v), 0)
+    np.testing.assert_allclose(h.root[0, 1, 7], 2.0 * dt, rtol=1e-5)
+    np.testing.assert_allclose(h.root[0, 1, 8], 0.0, atol=1e-6)
+
+
 def test_cube_settles_on_the_palm():
     spec, tp, sp, mnp, h = setup()
     h.root[:, 1, 0:3] = tp.object_start[:3]
