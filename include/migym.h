@@ -163,7 +163,10 @@ typedef struct mg_state_views {
    * NULL = no forces.  The fused hand step writes this tensor (it owns the random-force update). */
   float* rb_forces;
   int32_t rb_force_space;   /* MG_LOCAL_SPACE: body frame at the start of each substep; else world */
-  int32_t pad_views;
+  int32_t env_props_stride; /* floats per row of env_props (mg_env_props_layout) */
+  /* per-actor physical properties under domain randomization ((N*A, stride), see below); NULL = the
+   * model's constants for every actor */
+  const float* env_props;
 } mg_state_views;
 
 /* Task constants (cfg['env'] of the task YAML). */
@@ -275,6 +278,97 @@ typedef struct mg_task_buffers {
   float* random_force_prob; /* (N) per-env force probability, redrawn on reset; may be NULL */
 } mg_task_buffers;
 
+typedef struct mg_sim mg_sim;
+
+/* ---- domain randomization (tasks/base/vec_task.py:612-842, utils/dr_utils.py) ----
+ * The reference re-sets actor properties through the gym property setters in a per-env Python loop.
+ * Here the per-actor physical properties live in one device table, env_props (N*A rows of `stride`
+ * floats, bound through mg_state_views.env_props), which mg_dr_apply rewrites for the actors being
+ * randomized and the physics kernels read instead of the model's constants.  Row layout (offsets
+ * from mg_env_props_layout):
+ *   MG_EP_NODE    num_nodes x 8: [mass, armature, damping, stiffness, lower, upper, drive kp, effort]
+ *                 (mass of the node's body; its inertia scales with mass / model mass:
+ *                 set_actor_rigid_body_properties(..., recomputeInertia=True))
+ *   MG_EP_GEOM    num_geoms: friction of each collision shape (a contact's friction is the mean of
+ *                 its two shapes'; the ground plane's is mg_sim_params.friction)
+ *   MG_EP_TENDON  num_tendons x 2: [limit stiffness, damping]
+ *   MG_EP_OBJECT  4: [mass, friction, scale, 0] of the free object (scale: half extents x s,
+ *                 mass x s^3, inertia x s^5) */
+enum { MG_EP_NODE = 0, MG_EP_GEOM = 1, MG_EP_TENDON = 2, MG_EP_OBJECT = 3 };
+enum { MG_DR_UNIFORM = 0, MG_DR_GAUSSIAN = 1, MG_DR_LOGUNIFORM = 2 };
+enum { MG_DR_ADDITIVE = 0, MG_DR_SCALING = 1 };
+enum { MG_DR_SCHED_NONE = 0, MG_DR_SCHED_LINEAR = 1, MG_DR_SCHED_CONSTANT = 2 };
+
+/* one randomized attribute (dr_utils.generate_random_samples / apply_random_samples) */
+typedef struct mg_dr_desc {
+  int32_t distribution;     /* MG_DR_UNIFORM / GAUSSIAN (range = [mu, std]) / LOGUNIFORM */
+  int32_t operation;        /* MG_DR_ADDITIVE / MG_DR_SCALING */
+  int32_t schedule;         /* MG_DR_SCHED_* */
+  int32_t schedule_steps;
+  int32_t num_buckets;      /* > 0: get_bucketed_val over the unscheduled range */
+  int32_t after_setup;      /* 0: its property holds a setup_only attribute (randomized on the first call only) */
+  float range[2];
+} mg_dr_desc;
+/* one element of an attribute: env_props column, descriptor, original value (og_prop) */
+typedef struct mg_dr_attr {
+  int32_t slot;
+  int32_t desc;
+  float og;
+  int32_t pad;
+} mg_dr_attr;
+
+typedef struct mg_dr_apply_args {
+  const mg_dr_desc* descs;  /* device */
+  const mg_dr_attr* attrs;  /* device, nattr */
+  int32_t nattr;
+  int32_t stride;           /* env_props row length */
+  int32_t n;                /* actors */
+  int32_t frequency;        /* randomization_params.frequency */
+  int32_t first;            /* first_randomization: every actor, setup_only attributes included */
+  int32_t increment;        /* randomize_buf += 1 before the test (post_physics_step's increment) */
+  int64_t last_step;        /* gym.get_frame_count (schedules) */
+  float* env_props;         /* (n, stride) */
+  const int64_t* reset_mask;/* (n) reset_buf of the resetting step (ignored with first) */
+  int64_t* randomize_buf;   /* (n) */
+  const float* samples;     /* (n, nattr) injected samples (generate_random_samples output), or NULL */
+  uint64_t seed;            /* device RNG: counter-based, keyed by (global actor id, counter, attr) */
+  uint64_t counter;
+  int64_t env_offset;
+} mg_dr_apply_args;
+
+/* noise_lambda of randomization_params.observations / .actions (vec_task.py:684-720), in the
+ * reference's fp32 operation order:
+ *   x = op(x, ((corr * c_scale + c_shift) + z * scale) + shift)
+ * gaussian: z ~ N(0,1), scale = var, shift = mu, c_scale = var_corr, c_shift = mu_corr;
+ * uniform:  z ~ U(0,1), scale = hi - lo, shift = lo, c_scale = hi_corr - lo_corr, c_shift = lo_corr
+ * (corr is N(0,1) in both, as the reference draws it with randn_like).  Optional clamp into x_clamped. */
+typedef struct mg_dr_noise_args {
+  float* x;                 /* (n) in/out */
+  float* x_clamped;         /* (n) clamp(x, +-clip) or NULL */
+  float clip;
+  int32_t distribution;     /* MG_DR_GAUSSIAN or MG_DR_UNIFORM */
+  int32_t operation;        /* MG_DR_ADDITIVE / MG_DR_SCALING */
+  int32_t refresh_corr;     /* draw a new corr tensor first ("corr" absent from dr_randomizations) */
+  float* corr;              /* (n) persistent correlated noise */
+  int64_t n;
+  float scale, shift;       /* schedule applied by the caller */
+  float c_scale, c_shift;
+  const float* injected;    /* (n) per-call draws (randn_like / rand_like), or NULL = device RNG */
+  const float* injected_corr; /* (n) corr draws when refreshing, or NULL */
+  uint64_t seed;
+  uint64_t counter;
+  int64_t elem_offset;      /* global index of element 0 (multi-GPU shards) */
+  uint32_t key;             /* RNG stream of this tensor */
+  int32_t pad;
+} mg_dr_noise_args;
+
+int mg_env_props_layout(const mg_model* m, int32_t offsets[4]);   /* returns the row stride (floats) */
+int mg_env_props_defaults(const mg_model* m, float* row);           /* host: one row of model values */
+int mg_dr_apply(const mg_dr_apply_args* a, void* stream);
+int mg_dr_noise(const mg_dr_noise_args* a, void* stream);
+/* replace the simulation parameters (gym.set_sim_params; DR of sim_params.gravity) */
+int mg_sim_set_params(mg_sim* sim, const mg_sim_params* params);
+
 const char* mg_last_error(void);
 int mg_version(void);
 size_t mg_model_sizeof(void);
@@ -282,10 +376,11 @@ size_t mg_task_params_sizeof(void);
 size_t mg_task_buffers_sizeof(void);
 size_t mg_sim_params_sizeof(void);
 size_t mg_state_views_sizeof(void);
+size_t mg_dr_desc_sizeof(void);
+size_t mg_dr_apply_args_sizeof(void);
+size_t mg_dr_noise_args_sizeof(void);
 /* profiling aid (phase-timing build only, see isaacgymenvs-ma_amd/build.py --timing) */
 int mg_debug_phase_cycles(uint64_t* out16, int32_t reset);
-
-typedef struct mg_sim mg_sim;
 
 int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
                   mg_sim** out);

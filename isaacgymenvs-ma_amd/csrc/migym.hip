@@ -58,13 +58,14 @@ struct mg_sim {
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
-template <int T, int MN, int MC, int MG, int MP, bool OBJ>
+template <int T, int MN, int MC, int MG, int MP, bool OBJ, bool DR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_state_views v, int n) {
   constexpr int E = kBlock / T;
   constexpr int ROWS = OBJ ? 3 : 1;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::load_tile(&tile, m);
   __syncthreads();
   const int team = threadIdx.x / T;
@@ -74,6 +75,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int nd = m->num_dofs, ns = m->num_sensors;
   mg::Team<T, MN, MC, MG, MP, OBJ> t;
   t.init(&lds[team].v, &tile, m, &p);
+  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
+    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
+    t.drn = &drt[team].node[0][0];
+    t.drg = drt[team].geom;
+    t.drt = &drt[team].ten[0][0];
+    t.dro = drt[team].obj;
+  }
   if (OBJ && t.tl < 4) {  // applied force on the object row of rb_forces (apply_rigid_body_force_tensors)
     const float* fr = v.rb_forces ? v.rb_forces + ((size_t)(m->num_bodies + 2) * ac + m->num_bodies) * 3 : nullptr;
     lds[team].v.oforce[t.tl] = t.tl < 3 ? (fr ? fr[t.tl] : 0.0f) : (v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f);
@@ -215,12 +223,13 @@ __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_s
 // shuffle from the other agents' leaders.
 // amdgpu_waves_per_eu(2): the register budget that lets two waves share a SIMD (the team kernels
 // are latency-bound; occupancy is the lever — DESIGN.md §3)
-template <int T, int MN, int MC, int MG, int MP>
+template <int T, int MN, int MC, int MG, int MP, bool DR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
   constexpr int E = kBlock / T;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::load_tile(&tile, m);
   __syncthreads();
   const int team = threadIdx.x / T;
@@ -231,6 +240,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   mg::TeamLDS<T, MN, MC>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP> t;
   t.init(&L, &tile, m, &p);
+  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
+    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
+    t.drn = &drt[team].node[0][0];
+    t.drg = drt[team].geom;
+    t.drt = &drt[team].ten[0][0];
+    t.dro = drt[team].obj;
+  }
   __syncthreads();
   const int64_t reset_in = tb.reset[ac];
   t.ph_start();
@@ -539,13 +555,14 @@ __global__ void k_hand_finalize(mg_task_params tp, mg_task_buffers tb) {
 // The whole ShadowHand VecTask.step for one env, fused: pre_physics_step (masked goal / env resets,
 // PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
 // the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
-template <int T, int MN, int MC, int MG, int MP>
+template <int T, int MN, int MC, int MG, int MP, bool DR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                       mg_task_params tp, mg_state_views v, mg_task_buffers tb,
                                                       int n) {
   constexpr int E = kBlock / T;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, true>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::load_tile(&tile, m);
   __syncthreads();
   const int team = threadIdx.x / T;
@@ -557,6 +574,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   mg::TeamLDS<T, MN, MC, true>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, true> t;
   t.init(&L, &tile, m, &p);
+  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
+    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
+    t.drn = &drt[team].node[0][0];
+    t.drg = drt[team].geom;
+    t.drt = &drt[team].ten[0][0];
+    t.dro = drt[team].obj;
+  }
   t.ph_start();
   const uint64_t gid = (uint64_t)(tb.env_offset + ec);
   const bool env_reset = tb.reset[ec] != 0, goal_reset = tb.reset_goal[ec] != 0;
@@ -746,6 +770,114 @@ __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__
   dst[a] = src[a];
 }
 
+// ------------------------------------------------------------------------------------------------ domain randomization
+// dr_utils.generate_random_samples: the schedule scaling, then one draw of the descriptor's distribution
+// (gaussian: np.random.normal(mu, var) = mu + var z).  Double precision like the reference's numpy.
+__device__ double dr_sched(const mg_dr_desc& d, int64_t last_step) {
+  if (d.schedule == MG_DR_SCHED_LINEAR)
+    return 1.0 / (double)d.schedule_steps * (double)(last_step < d.schedule_steps ? last_step : d.schedule_steps);
+  if (d.schedule == MG_DR_SCHED_CONSTANT) return last_step < d.schedule_steps ? 0.0 : 1.0;
+  return 1.0;
+}
+__device__ double dr_sample(const mg_dr_desc& d, double sc, float u1, float u2) {
+  double a = d.range[0], b = d.range[1];
+  if (d.distribution == MG_DR_GAUSSIAN) {
+    if (d.operation == MG_DR_ADDITIVE) { a *= sc; b *= sc; }
+    else { b = b * sc; a = a * sc + 1.0 * (1.0 - sc); }
+    const double z = sqrt(-2.0 * log(1.0 - (double)u1)) * cos(6.283185307179586 * (double)u2);
+    return a + b * z;
+  }
+  if (d.operation == MG_DR_ADDITIVE) { a *= sc; b *= sc; }
+  else { a = a * sc + 1.0 * (1.0 - sc); b = b * sc + 1.0 * (1.0 - sc); }
+  if (d.distribution == MG_DR_LOGUNIFORM) return exp(log(a) + (log(b) - log(a)) * (double)u1);
+  return a + (b - a) * (double)u1;
+}
+// dr_utils.get_bucketed_val: floor onto num_buckets buckets of the unscheduled range (uniform: [lo, hi];
+// otherwise [mu - 2 sqrt(var), mu + 2 sqrt(var)]); below the first bucket Python's index -1 wraps to the last
+__device__ double dr_bucket(const mg_dr_desc& d, double v) {
+  double lo, hi;
+  if (d.distribution == MG_DR_UNIFORM) { lo = d.range[0]; hi = d.range[1]; }
+  else { lo = d.range[0] - 2.0 * sqrt((double)d.range[1]); hi = d.range[0] + 2.0 * sqrt((double)d.range[1]); }
+  const int nb = d.num_buckets;
+  int cnt = 0;  // bisect_right
+  for (int i = 0; i < nb; i++)
+    if ((hi - lo) * (double)i / (double)nb + lo <= v) cnt = i + 1;
+  const int idx = cnt - 1 < 0 ? nb - 1 : cnt - 1;
+  return (hi - lo) * (double)idx / (double)nb + lo;
+}
+
+// apply_randomizations' actor-property part for one actor per thread (vec_task.py:626-637, 746-842): the
+// actor is randomized on the first call, or when randomize_buf >= frequency on a resetting step (then its
+// counter restarts); each attribute element gets op(og, sample) (+ buckets) in its env_props column.
+// Properties holding a setup_only attribute are only randomized on the first call.
+__global__ __launch_bounds__(kBlock) void k_dr_apply(mg_dr_apply_args a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  bool doit = a.first != 0;
+  if (!doit) {
+    int64_t rb = a.randomize_buf[e] + (a.increment ? 1 : 0);
+    doit = rb >= (int64_t)a.frequency && a.reset_mask[e] != 0;
+    if (doit) rb = 0;
+    a.randomize_buf[e] = rb;
+  }
+  if (!doit) return;
+  const uint64_t gid = (uint64_t)(a.env_offset + e);
+  float* row = a.env_props + (size_t)a.stride * e;
+  for (int i = 0; i < a.nattr; i++) {
+    const mg_dr_attr at = a.attrs[i];
+    const mg_dr_desc d = a.descs[at.desc];
+    if (!a.first && !d.after_setup) continue;
+    double smp;
+    if (a.samples) {
+      smp = (double)a.samples[(size_t)a.nattr * e + i];
+    } else {
+      const float u1 = mg::uniform01(a.seed, gid, a.counter, (uint32_t)(8192 + 2 * i));
+      const float u2 = mg::uniform01(a.seed, gid, a.counter, (uint32_t)(8193 + 2 * i));
+      smp = dr_sample(d, dr_sched(d, a.last_step), u1, u2);
+    }
+    double v = d.operation == MG_DR_SCALING ? (double)at.og * smp : (double)at.og + smp;
+    if (d.num_buckets > 0) v = dr_bucket(d, v);
+    row[at.slot] = (float)v;
+  }
+}
+
+// noise_lambda (vec_task.py:684-720) over a flat tensor; corr is (re)drawn when refresh_corr is set
+__global__ __launch_bounds__(kBlock) void k_dr_noise(mg_dr_noise_args a) {
+#pragma clang fp contract(off)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t gid = (uint64_t)(a.elem_offset + i);
+    float c;
+    if (a.refresh_corr) {
+      if (a.injected_corr) {
+        c = a.injected_corr[i];
+      } else {
+        const float u1 = mg::uniform01(a.seed, gid, a.counter, 4 * a.key), u2 = mg::uniform01(a.seed, gid, a.counter, 4 * a.key + 1);
+        c = sqrtf(-2.0f * logf(1.0f - u1)) * cosf(6.28318530717958647f * u2);
+      }
+      a.corr[i] = c;
+    } else {
+      c = a.corr[i];
+    }
+    float z;
+    if (a.injected) {
+      z = a.injected[i];
+    } else {
+      const float u1 = mg::uniform01(a.seed, gid, a.counter, 4 * a.key + 2);
+      if (a.distribution == MG_DR_GAUSSIAN) {
+        const float u2 = mg::uniform01(a.seed, gid, a.counter, 4 * a.key + 3);
+        z = sqrtf(-2.0f * logf(1.0f - u1)) * cosf(6.28318530717958647f * u2);
+      } else {
+        z = u1;
+      }
+    }
+    const float cc = c * a.c_scale + a.c_shift;
+    const float nz = (cc + z * a.scale) + a.shift;
+    const float x = a.operation == MG_DR_SCALING ? a.x[i] * nz : a.x[i] + nz;
+    a.x[i] = x;
+    if (a.x_clamped) a.x_clamped[i] = fminf(fmaxf(x, -a.clip), a.clip);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ dispatch
 // Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
 // contacts MC, geoms MG, self pairs MP, OBJ = hand-task envs with a free object.  The smallest
@@ -786,8 +918,13 @@ template <int T, int MN, int MC, int MG, int MP, bool OBJ>
 struct RunSimulate {
   static int run(hipStream_t s, const mg_sim* sim) {
     const int E = kBlock / T;
-    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                       sim->d_model, sim->params, sim->views, sim->n);
+    // the domain-randomized instance reads each actor's env_props row (mg_dr_apply)
+    if (sim->views.env_props)
+      hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                         sim->d_model, sim->params, sim->views, sim->n);
+    else
+      hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                         sim->d_model, sim->params, sim->views, sim->n);
     return MG_OK;
   }
 };
@@ -802,12 +939,20 @@ struct RunEnvStep {
     if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
       return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
     if constexpr (OBJ) {
-      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                         sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
+      if (sim->views.env_props)
+        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
+      else
+        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
       hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, s, *tp, *tb);
     } else {
-      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                         sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
+      if (sim->views.env_props)
+        hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
+      else
+        hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
     }
     return MG_OK;
   }
@@ -823,6 +968,9 @@ size_t mg_task_params_sizeof(void) { return sizeof(mg_task_params); }
 size_t mg_task_buffers_sizeof(void) { return sizeof(mg_task_buffers); }
 size_t mg_sim_params_sizeof(void) { return sizeof(mg_sim_params); }
 size_t mg_state_views_sizeof(void) { return sizeof(mg_state_views); }
+size_t mg_dr_desc_sizeof(void) { return sizeof(mg_dr_desc); }
+size_t mg_dr_apply_args_sizeof(void) { return sizeof(mg_dr_apply_args); }
+size_t mg_dr_noise_args_sizeof(void) { return sizeof(mg_dr_noise_args); }
 
 // Profiling aid: per-phase shader cycles summed over all waves (blocks < 65536) since the last reset (phase-timing
 // build only; returns MG_EINVAL otherwise).  Phases: 0 FK, 1 ABA (+tendons), 2 collide (+object
@@ -895,6 +1043,8 @@ int mg_sim_bind(mg_sim* sim, const mg_state_views* views) {
   if (!sim || !views || !views->root_states || !views->dof_state) return fail(MG_EINVAL, "mg_sim_bind: bad views");
   if (sim->host_model.num_sensors > 0 && !views->sensors)
     return fail(MG_EINVAL, "mg_sim_bind: model has force sensors but no sensor buffer");
+  if (views->env_props && views->env_props_stride < mg_env_props_layout(&sim->host_model, nullptr))
+    return fail(MG_EINVAL, "mg_sim_bind: env_props_stride is shorter than mg_env_props_layout's row");
   sim->views = *views;
   sim->bound = true;
   return MG_OK;
@@ -906,6 +1056,60 @@ int mg_sim_simulate(mg_sim* sim, void* stream) {
                                  (const mg_sim*)sim);
   if (rc) return rc;
   return check_launch("mg_sim_simulate");
+}
+
+int mg_sim_set_params(mg_sim* sim, const mg_sim_params* params) {
+  if (!sim || !params || params->substeps < 1 || params->dt <= 0.0f || params->max_contacts < 0)
+    return fail(MG_EINVAL, "mg_sim_set_params: bad arguments");
+  if (params->max_contacts != sim->params.max_contacts || params->agents != sim->params.agents)
+    return fail(MG_EINVAL, "mg_sim_set_params: max_contacts / agents are fixed at mg_sim_create");
+  sim->params = *params;  // taken by value by every later launch
+  return MG_OK;
+}
+
+int mg_env_props_layout(const mg_model* m, int32_t offsets[4]) {
+  if (!m) return fail(MG_EINVAL, "mg_env_props_layout: bad model");
+  const int o0 = 0, o1 = 8 * m->num_nodes, o2 = o1 + m->num_geoms, o3 = o2 + 2 * m->num_tendons;
+  if (offsets) { offsets[0] = o0; offsets[1] = o1; offsets[2] = o2; offsets[3] = o3; }
+  return (o3 + 4 + 3) & ~3;
+}
+
+int mg_env_props_defaults(const mg_model* m, float* row) {
+  if (!m || !row) return fail(MG_EINVAL, "mg_env_props_defaults: bad arguments");
+  int32_t off[4];
+  const int stride = mg_env_props_layout(m, off);
+  for (int k = 0; k < stride; k++) row[k] = 0.0f;
+  for (int i = 0; i < m->num_nodes; i++) {
+    float* r = row + off[MG_EP_NODE] + 8 * i;
+    r[0] = m->mass[i]; r[1] = m->armature[i]; r[2] = m->damping[i]; r[3] = m->stiffness[i];
+    r[4] = m->lower[i]; r[5] = m->upper[i]; r[6] = m->drive_kp[i]; r[7] = m->effort_limit[i];
+  }
+  for (int g = 0; g < m->num_geoms; g++) row[off[MG_EP_GEOM] + g] = 1.0f;  // shape friction (build-defined default)
+  for (int q = 0; q < m->num_tendons; q++) {
+    row[off[MG_EP_TENDON] + 2 * q] = m->tendon_limit_stiffness[q];
+    row[off[MG_EP_TENDON] + 2 * q + 1] = m->tendon_damping[q];
+  }
+  float* o = row + off[MG_EP_OBJECT];
+  o[0] = m->obj_mass; o[1] = 1.0f; o[2] = 1.0f; o[3] = 0.0f;
+  return MG_OK;
+}
+
+int mg_dr_apply(const mg_dr_apply_args* a, void* stream) {
+  if (!a || a->n < 0 || a->nattr < 0 || (a->nattr > 0 && (!a->descs || !a->attrs)) || !a->env_props ||
+      a->stride <= 0 || (!a->first && (!a->reset_mask || !a->randomize_buf)))
+    return fail(MG_EINVAL, "mg_dr_apply: bad arguments");
+  if (a->n == 0) return MG_OK;
+  hipLaunchKernelGGL(k_dr_apply, dim3(grid_for(a->n)), dim3(kBlock), 0, (hipStream_t)stream, *a);
+  return check_launch("mg_dr_apply");
+}
+
+int mg_dr_noise(const mg_dr_noise_args* a, void* stream) {
+  if (!a || !a->x || !a->corr || a->n < 0) return fail(MG_EINVAL, "mg_dr_noise: bad arguments");
+  if (a->n == 0) return MG_OK;
+  const int64_t blocks = (a->n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_dr_noise, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(kBlock), 0,
+                     (hipStream_t)stream, *a);
+  return check_launch("mg_dr_noise");
 }
 
 int mg_sim_destroy(mg_sim* sim) {

@@ -206,6 +206,29 @@ struct alignas(16) BankSlot<L, T, 0> {
   L v;
 };
 
+// Per-actor properties under domain randomization (mg_state_views.env_props), one copy per team in
+// LDS: nodes [mass, armature, damping, stiffness, lower, upper, drive kp, effort] (rows of 9 floats:
+// a node's lane reads its own row, odd stride), geom friction, tendons [limit stiffness, damping],
+// object [mass, friction, scale].  The layout of the global row is mg_env_props_layout's.
+template <int MN, int MG>
+struct DrTile {
+  float node[MN][9];
+  float geom[MG];
+  float ten[MG_MAX_TENDONS][2];
+  float obj[4];
+};
+// copy one env_props row (global) into the team's DrTile, team-cooperative
+template <int T, int MN, int MG>
+__device__ void load_dr(DrTile<MN, MG>* d, const float* row, const mg_model* m, int tl) {
+  const int nn = m->num_nodes, ng = m->num_geoms, nt = m->num_tendons;
+  for (int k = tl; k < 8 * nn; k += T) d->node[k >> 3][k & 7] = row[k];
+  const float* g = row + 8 * nn;
+  for (int k = tl; k < ng; k += T) d->geom[k] = g[k];
+  const float* tr = g + ng;
+  for (int k = tl; k < 2 * nt; k += T) d->ten[k >> 1][k & 1] = tr[k];
+  if (tl < 4) d->obj[tl] = tr[2 * nt + tl];
+}
+
 // Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + v_permlane16_swap (xor 16) and
 // a bpermute xor 32.  Every step adds a lane to its partner symmetrically, so all lanes of the team
 // end with bit-identical sums (fp add is commutative) and no broadcast is needed.
@@ -386,6 +409,23 @@ struct Team {
   float tgt;           // PD target of the own DOF
   float ttend;         // tendon generalized force (current substep)
   int sat;             // drive saturated (current substep)
+  // domain randomization: the team's DrTile (nullptr: the model's constants)
+  const float* drn;    // node rows (stride 9)
+  const float* drg;    // geom friction
+  const float* drt;    // tendons (stride 2)
+  const float* dro;    // object [mass, friction, scale]
+  // node property row [mass, armature, damping, stiffness, lower, upper, drive kp, effort]
+  __device__ const float* nprop(int i) const { return drn ? drn + 9 * i : &mt->nf[i][24]; }
+  __device__ float omass() const { return dro ? dro[0] : m->obj_mass; }
+  __device__ float oscale() const { return dro ? dro[2] : 1.0f; }
+  __device__ V3 osize() const { return ld3(m->obj_size) * oscale(); }
+  // object principal moments: model inertia x (mass / model mass) x scale^2 (uniform density)
+  __device__ V3 oinertia() const {
+    const float f = dro ? (dro[0] / m->obj_mass) * dro[2] * dro[2] : 1.0f;
+    return ld3(m->obj_inertia) * f;
+  }
+  // friction coefficient of a contact side's geom (-1 ground plane, -2 the object)
+  __device__ float gmu(int g) const { return g >= 0 ? drg[g] : (g == -2 ? dro[1] : p->friction); }
   // free object (OBJ): pose replicated on every lane, velocity column on lanes ob0..ob0+5
   int ob0;
   bool objl;
@@ -400,6 +440,7 @@ struct Team {
     mt = tile;
     m = mm;
     p = pp;
+    drn = drg = drt = dro = nullptr;
     tl = threadIdx.x % T;
     tb = threadIdx.x - tl;
     freeb = !m->fixed_base;
@@ -510,7 +551,9 @@ struct Team {
       const float* nf = mt->nf[node];
       V3 cc = x + mul(R, ld3(nf + 15)) - o;
       const float* in = nf + 18;
-      float Il[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
+      const float isc = (drn && nf[24] > 0.0f) ? drn[9 * node] / nf[24] : 1.0f;  // DR: inertia scales with the body mass
+      float Il[3][3] = {{in[0] * isc, in[3] * isc, in[4] * isc}, {in[3] * isc, in[1] * isc, in[5] * isc},
+                        {in[4] * isc, in[5] * isc, in[2] * isc}};
       float Tm[3][3], Iw[6];
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) Tm[a][b] = R.m[a][0] * Il[0][b] + R.m[a][1] * Il[1][b] + R.m[a][2] * Il[2][b];
@@ -519,7 +562,7 @@ struct Team {
         int a = idx[k][0], b = idx[k][1];
         Iw[k] = Tm[a][0] * R.m[b][0] + Tm[a][1] * R.m[b][1] + Tm[a][2] * R.m[b][2];
       }
-      const float mass = nf[24];
+      const float mass = drn ? drn[9 * node] : nf[24];
       IA = body_inertia(mass, cc, Iw);
       SV IV = mul(IA, V);
       V3 mg = ld3(p->gravity) * (mass * gscale());
@@ -529,20 +572,20 @@ struct Team {
     for (int lev = maxdepth; lev >= 1; lev--) {
       if (node > 0 && depth == lev) {
         U = mul(IA, S);
-        const float* nf = mt->nf[node];
+        const float* np = nprop(node);  // [mass, arm, damp, stiff, lower, upper, kp, effort]
         // implicit spring/damper; PD drives toward the target unless the explicit estimate
         // exceeds the effort limit (then a constant +-limit force, no implicit terms)
-        float kk = nf[27], bb = nf[26], ref = 0.0f, tadd = 0.0f;
+        float kk = np[3], bb = np[2], ref = 0.0f, tadd = 0.0f;
         sat = 0;
-        if (nf[30] > 0.0f) {
-          const float fe = nf[30] * (tgt - qj) - nf[26] * nu;
-          if (fabsf(fe) > nf[31]) {
-            kk = 0.0f; bb = 0.0f; tadd = fe > 0.0f ? nf[31] : -nf[31]; sat = 1;
+        if (np[6] > 0.0f) {
+          const float fe = np[6] * (tgt - qj) - np[2] * nu;
+          if (fabsf(fe) > np[7]) {
+            kk = 0.0f; bb = 0.0f; tadd = fe > 0.0f ? np[7] : -np[7]; sat = 1;
           } else {
-            kk = nf[30]; ref = tgt;
+            kk = np[6]; ref = tgt;
           }
         }
-        float D = dot(S, U) + nf[25] + h * bb + h * h * kk;
+        float D = dot(S, U) + np[1] + h * bb + h * h * kk;
         Dinv = 1.0f / D;
         float t = tau + tadd + ttend - bb * nu - kk * (qj - ref + h * nu);
         u = t - dot(S, pA);
@@ -623,7 +666,8 @@ struct Team {
       const float* f = mt->tf[q];
       const float Lt = f[0] * q0 + f[1] * q1, Ld = f[0] * v0 + f[1] * v1;
       const float cl = fminf(fmaxf(Lt, f[2]), f[3]);
-      const float F = -f[4] * (Lt - cl) - f[5] * Ld;
+      const float kl = drt ? drt[2 * q] : f[4], bd = drt ? drt[2 * q + 1] : f[5];
+      const float F = -kl * (Lt - cl) - bd * Ld;
       if (node > 0 && node - 1 == d0) ttend += f[0] * F;
       if (node > 0 && node - 1 == d1) ttend += f[1] * F;
     }
@@ -632,16 +676,16 @@ struct Team {
   // ---------------------------------------------------------------- free object: unconstrained step
   // I_w = R diag(I) R^T; every lane evaluates the 3-vectors, object lane k keeps component k.
   __device__ V3 obj_inv_inertia(V3 x) const {
-    const float* I = m->obj_inertia;
+    const V3 I = oinertia();
     V3 b = mulT(oR, x);
-    return mul(oR, v3(b.x / I[0], b.y / I[1], b.z / I[2]));
+    return mul(oR, v3(b.x / I.x, b.y / I.y, b.z / I.z));
   }
   __device__ void obj_free() {
     if (!OBJ) return;
     const V3 w = v3(__shfl(nu, tb + ob0), __shfl(nu, tb + ob0 + 1), __shfl(nu, tb + ob0 + 2));
-    const float* I = m->obj_inertia;
+    const V3 I = oinertia();
     const V3 b = mulT(oR, w);
-    const V3 Iw = mul(oR, v3(I[0] * b.x, I[1] * b.y, I[2] * b.z));
+    const V3 Iw = mul(oR, v3(I.x * b.x, I.y * b.y, I.z * b.z));
     const V3 aw = obj_inv_inertia(cross(w, Iw) * -1.0f);
     if (objl) {
       const int k = tl - ob0;
@@ -649,7 +693,7 @@ struct Team {
       const V3 fl = v3(s->oforce[0], s->oforce[1], s->oforce[2]);
       const V3 fw = s->oforce[3] != 0.0f ? mul(oR, fl) : fl;
       const float fk = k == 3 ? fw.x : k == 4 ? fw.y : fw.z;
-      const float a = k == 0 ? aw.x : k == 1 ? aw.y : k == 2 ? aw.z : m->obj_gravity * p->gravity[k - 3] + fk / m->obj_mass;
+      const float a = k == 0 ? aw.x : k == 1 ? aw.y : k == 2 ? aw.z : m->obj_gravity * p->gravity[k - 3] + fk / omass();
       nu += h * a;
       nu *= k < 3 ? 1.0f / (1.0f + h * m->obj_ang_damping) : 1.0f / (1.0f + h * m->obj_lin_damping);
     }
@@ -658,7 +702,7 @@ struct Team {
   __device__ float obj_response(int r) const {
     const float* J = s->rwo[r];
     const int k = tl - ob0;
-    if (k >= 3) return J[k] / m->obj_mass;
+    if (k >= 3) return J[k] / omass();
     const V3 y = obj_inv_inertia(v3(J[0], J[1], J[2]));
     return k == 0 ? y.x : k == 1 ? y.y : y.z;
   }
@@ -884,7 +928,7 @@ struct Team {
   // -> one closest-point candidate; box -> its 8 vertices vs the object, then the object's 8 vertices
   // vs the geom (normal flipped).  Normal points from the object (B) to the geom (A).
   __device__ bool obj_candidate(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
-    const V3 hb = ld3(m->obj_size);
+    const V3 hb = osize();
     const int ty = mt->gtype[g];
     const float* gs = mt->gf[g] + 12;
     if (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) {
@@ -985,7 +1029,7 @@ struct Team {
       int cnt = 0;
       V3 e = v3(0, 0, 0);
       if (tl < 8) {
-        const V3 hb = ld3(m->obj_size);
+        const V3 hb = osize();
         e = mul(oR, v3((tl & 1 ? 1.f : -1.f) * hb.x, (tl & 2 ? 1.f : -1.f) * hb.y, (tl & 4 ? 1.f : -1.f) * hb.z)) + op;
         cnt = e.z < off ? 1 : 0;
       }
@@ -1040,7 +1084,7 @@ struct Team {
       // articulation geoms vs the object: one lane per (geom, candidate) in geom order (the oracle's
       // emission order); a candidate whose geom's bounding sphere cannot come within the contact
       // offset of the object's is skipped (conservative: the same contacts)
-      const float ro = sqrtf(dot(ld3(m->obj_size), ld3(m->obj_size)));
+      const float ro = sqrtf(dot(osize(), osize()));
       const int NC = mt->noc;
       for (int f0 = 0; f0 < NC; f0 += T) {
         const int f = f0 + tl;
@@ -1135,8 +1179,9 @@ struct Team {
     float dl = 0.0f, du = 0.0f;
     bool lo = false, hi = false;
     if (node > 0 && mt->limited[node]) {
-      dl = qj - mt->nf[node][28];
-      du = mt->nf[node][29] - qj;
+      const float* np = nprop(node);
+      dl = qj - np[4];
+      du = np[5] - qj;
       lo = dl < p->limit_margin;
       hi = du < p->limit_margin;
       cnt = (lo ? 1 : 0) + (hi ? 1 : 0);
@@ -1219,7 +1264,9 @@ struct Team {
             typename L::Row& rw = s->u.sv.rows[r];
             rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
             rw.lam = 0.0f;
-            rw.mu = contact ? (q % 3 == 0 ? -1.0f : p->friction) : -2.0f;
+            // DR: a contact's friction is the mean of its two shapes' (vec_task.py rigid_shape_properties)
+            const float muc = (drg && contact) ? 0.5f * (gmu(cside(r / 3, 2)) + gmu(cside(r / 3, 3))) : p->friction;
+            rw.mu = contact ? (q % 3 == 0 ? -1.0f : muc) : -2.0f;
             if (!active) rw.b = 0.0f;
           }
         }
@@ -1368,13 +1415,13 @@ struct Team {
       o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
     }
     if (dforce_out && node > 0) {
-      const float* nf = mt->nf[node];
+      const float* np = nprop(node);
       float t = tau + ttend;
-      if (nf[30] > 0.0f) {
-        const float fe = nf[30] * (tgt - qj) - nf[26] * nu;
-        t += sat ? (fe > 0.0f ? nf[31] : -nf[31]) : fe;
+      if (np[6] > 0.0f) {
+        const float fe = np[6] * (tgt - qj) - np[2] * nu;
+        t += sat ? (fe > 0.0f ? np[7] : -np[7]) : fe;
       } else {
-        t += -nf[26] * nu - nf[27] * qj;
+        t += -np[2] * nu - np[3] * qj;
       }
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
         const int meta = s->lmeta[r - 3 * s->ncon];

@@ -36,7 +36,40 @@ class StateViews(C.Structure):
     _fields_ = [("root_states", C.c_void_p), ("dof_state", C.c_void_p), ("dof_actuation", C.c_void_p),
                 ("sensors", C.c_void_p), ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p),
                 ("dof_targets", C.c_void_p), ("rb_forces", C.c_void_p), ("rb_force_space", C.c_int32),
-                ("pad_views", C.c_int32)]
+                ("env_props_stride", C.c_int32), ("env_props", C.c_void_p)]
+
+
+# ---- domain randomization (include/migym.h; vec_task.py:612-842, dr_utils.py)
+MG_EP_NODE, MG_EP_GEOM, MG_EP_TENDON, MG_EP_OBJECT = 0, 1, 2, 3
+MG_DR_UNIFORM, MG_DR_GAUSSIAN, MG_DR_LOGUNIFORM = 0, 1, 2
+MG_DR_ADDITIVE, MG_DR_SCALING = 0, 1
+MG_DR_SCHED_NONE, MG_DR_SCHED_LINEAR, MG_DR_SCHED_CONSTANT = 0, 1, 2
+
+
+class DrDesc(C.Structure):
+    _fields_ = [("distribution", C.c_int32), ("operation", C.c_int32), ("schedule", C.c_int32),
+                ("schedule_steps", C.c_int32), ("num_buckets", C.c_int32), ("after_setup", C.c_int32),
+                ("range", C.c_float * 2)]
+
+
+class DrAttr(C.Structure):
+    _fields_ = [("slot", C.c_int32), ("desc", C.c_int32), ("og", C.c_float), ("pad", C.c_int32)]
+
+
+class DrApplyArgs(C.Structure):
+    _fields_ = [("descs", C.c_void_p), ("attrs", C.c_void_p), ("nattr", C.c_int32), ("stride", C.c_int32),
+                ("n", C.c_int32), ("frequency", C.c_int32), ("first", C.c_int32), ("increment", C.c_int32),
+                ("last_step", C.c_int64), ("env_props", C.c_void_p), ("reset_mask", C.c_void_p),
+                ("randomize_buf", C.c_void_p), ("samples", C.c_void_p), ("seed", C.c_uint64),
+                ("counter", C.c_uint64), ("env_offset", C.c_int64)]
+
+
+class DrNoiseArgs(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("x_clamped", C.c_void_p), ("clip", C.c_float), ("distribution", C.c_int32),
+                ("operation", C.c_int32), ("refresh_corr", C.c_int32), ("corr", C.c_void_p), ("n", C.c_int64),
+                ("scale", C.c_float), ("shift", C.c_float), ("c_scale", C.c_float), ("c_shift", C.c_float),
+                ("injected", C.c_void_p), ("injected_corr", C.c_void_p), ("seed", C.c_uint64),
+                ("counter", C.c_uint64), ("elem_offset", C.c_int64), ("key", C.c_uint32), ("pad", C.c_int32)]
 
 
 class TaskParams(C.Structure):
@@ -117,6 +150,14 @@ EXPORTS = {
     "mg_pre_physics": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(StateViews),
                                  C.POINTER(TaskBuffers), C.c_int32, C.c_void_p]),
     "mg_env_step": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p]),
+    "mg_dr_desc_sizeof": (C.c_size_t, []),
+    "mg_dr_apply_args_sizeof": (C.c_size_t, []),
+    "mg_dr_noise_args_sizeof": (C.c_size_t, []),
+    "mg_env_props_layout": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mg_env_props_defaults": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mg_dr_apply": (C.c_int, [C.POINTER(DrApplyArgs), C.c_void_p]),
+    "mg_dr_noise": (C.c_int, [C.POINTER(DrNoiseArgs), C.c_void_p]),
+    "mg_sim_set_params": (C.c_int, [C.c_void_p, C.POINTER(SimParams)]),
 }
 
 _LIB = None
@@ -137,7 +178,8 @@ def _bind(lib):
 def check_layout(lib):
     sizes = {"mg_model_sizeof": _model.MODEL_DTYPE.itemsize, "mg_task_params_sizeof": C.sizeof(TaskParams),
              "mg_task_buffers_sizeof": C.sizeof(TaskBuffers), "mg_sim_params_sizeof": C.sizeof(SimParams),
-             "mg_state_views_sizeof": C.sizeof(StateViews)}
+             "mg_state_views_sizeof": C.sizeof(StateViews), "mg_dr_desc_sizeof": C.sizeof(DrDesc),
+             "mg_dr_apply_args_sizeof": C.sizeof(DrApplyArgs), "mg_dr_noise_args_sizeof": C.sizeof(DrNoiseArgs)}
     for fn, py in sizes.items():
         c = getattr(lib, fn)()
         if c != py:

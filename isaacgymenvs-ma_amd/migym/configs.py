@@ -45,6 +45,125 @@ def _sim(dt=0.0166, **physx):
 
 _LOCO_PLANE = {"staticFriction": 1.0, "dynamicFriction": 1.0, "restitution": 0.0}
 
+
+# task.randomization_params of the task YAMLs (cfg/task/Ant.yaml:63-101, Humanoid.yaml:63-129,
+# ShadowHand.yaml:64-169); applied when task.randomize is True (migym/dr.py)
+_DR_ANT = {'frequency': 600,
+ 'observations': {'range': [0, 0.002], 'operation': 'additive', 'distribution': 'gaussian'},
+ 'actions': {'range': [0.0, 0.02], 'operation': 'additive', 'distribution': 'gaussian'},
+ 'actor_params': {'ant': {'color': True,
+                          'rigid_body_properties': {'mass': {'range': [0.5, 1.5],
+                                                             'operation': 'scaling',
+                                                             'distribution': 'uniform',
+                                                             'setup_only': True}},
+                          'dof_properties': {'damping': {'range': [0.5, 1.5],
+                                                         'operation': 'scaling',
+                                                         'distribution': 'uniform'},
+                                             'stiffness': {'range': [0.5, 1.5],
+                                                           'operation': 'scaling',
+                                                           'distribution': 'uniform'},
+                                             'lower': {'range': [0, 0.01],
+                                                       'operation': 'additive',
+                                                       'distribution': 'gaussian'},
+                                             'upper': {'range': [0, 0.01],
+                                                       'operation': 'additive',
+                                                       'distribution': 'gaussian'}}}}}
+_DR_HUMANOID = {'frequency': 600,
+ 'observations': {'range': [0, 0.002], 'operation': 'additive', 'distribution': 'gaussian'},
+ 'actions': {'range': [0.0, 0.02], 'operation': 'additive', 'distribution': 'gaussian'},
+ 'sim_params': {'gravity': {'range': [0, 0.4],
+                            'operation': 'additive',
+                            'distribution': 'gaussian',
+                            'schedule': 'linear',
+                            'schedule_steps': 3000}},
+ 'actor_params': {'humanoid': {'color': True,
+                               'rigid_body_properties': {'mass': {'range': [0.5, 1.5],
+                                                                  'operation': 'scaling',
+                                                                  'distribution': 'uniform',
+                                                                  'setup_only': True,
+                                                                  'schedule': 'linear',
+                                                                  'schedule_steps': 3000}},
+                               'rigid_shape_properties': {'friction': {'num_buckets': 500,
+                                                                       'range': [0.7, 1.3],
+                                                                       'operation': 'scaling',
+                                                                       'distribution': 'uniform',
+                                                                       'schedule': 'linear',
+                                                                       'schedule_steps': 3000},
+                                                          'restitution': {'range': [0.0, 0.7],
+                                                                          'operation': 'scaling',
+                                                                          'distribution': 'uniform',
+                                                                          'schedule': 'linear',
+                                                                          'schedule_steps': 3000}},
+                               'dof_properties': {'damping': {'range': [0.5, 1.5],
+                                                              'operation': 'scaling',
+                                                              'distribution': 'uniform',
+                                                              'schedule': 'linear',
+                                                              'schedule_steps': 3000},
+                                                  'stiffness': {'range': [0.5, 1.5],
+                                                                'operation': 'scaling',
+                                                                'distribution': 'uniform',
+                                                                'schedule': 'linear',
+                                                                'schedule_steps': 3000},
+                                                  'lower': {'range': [0, 0.01],
+                                                            'operation': 'additive',
+                                                            'distribution': 'gaussian',
+                                                            'schedule': 'linear',
+                                                            'schedule_steps': 3000},
+                                                  'upper': {'range': [0, 0.01],
+                                                            'operation': 'additive',
+                                                            'distribution': 'gaussian',
+                                                            'schedule': 'linear',
+                                                            'schedule_steps': 3000}}}}}
+_DR_SHADOWHAND = {'frequency': 720,
+ 'observations': {'range': [0, 0.002],
+                  'range_correlated': [0, 0.001],
+                  'operation': 'additive',
+                  'distribution': 'gaussian'},
+ 'actions': {'range': [0.0, 0.05],
+             'range_correlated': [0, 0.015],
+             'operation': 'additive',
+             'distribution': 'gaussian'},
+ 'sim_params': {'gravity': {'range': [0, 0.4], 'operation': 'additive', 'distribution': 'gaussian'}},
+ 'actor_params': {'hand': {'color': True,
+                           'tendon_properties': {'damping': {'range': [0.3, 3.0],
+                                                             'operation': 'scaling',
+                                                             'distribution': 'loguniform'},
+                                                 'stiffness': {'range': [0.75, 1.5],
+                                                               'operation': 'scaling',
+                                                               'distribution': 'loguniform'}},
+                           'dof_properties': {'damping': {'range': [0.3, 3.0],
+                                                          'operation': 'scaling',
+                                                          'distribution': 'loguniform'},
+                                              'stiffness': {'range': [0.75, 1.5],
+                                                            'operation': 'scaling',
+                                                            'distribution': 'loguniform'},
+                                              'lower': {'range': [0, 0.01],
+                                                        'operation': 'additive',
+                                                        'distribution': 'gaussian'},
+                                              'upper': {'range': [0, 0.01],
+                                                        'operation': 'additive',
+                                                        'distribution': 'gaussian'}},
+                           'rigid_body_properties': {'mass': {'range': [0.5, 1.5],
+                                                              'operation': 'scaling',
+                                                              'distribution': 'uniform',
+                                                              'setup_only': True}},
+                           'rigid_shape_properties': {'friction': {'num_buckets': 250,
+                                                                   'range': [0.7, 1.3],
+                                                                   'operation': 'scaling',
+                                                                   'distribution': 'uniform'}}},
+                  'object': {'scale': {'range': [0.95, 1.05],
+                                       'operation': 'scaling',
+                                       'distribution': 'uniform',
+                                       'setup_only': True},
+                             'rigid_body_properties': {'mass': {'range': [0.5, 1.5],
+                                                                'operation': 'scaling',
+                                                                'distribution': 'uniform',
+                                                                'setup_only': True}},
+                             'rigid_shape_properties': {'friction': {'num_buckets': 250,
+                                                                     'range': [0.7, 1.3],
+                                                                     'operation': 'scaling',
+                                                                     'distribution': 'uniform'}}}}}
+
 TASKS = {
     "Ant": {
         "name": "Ant",
@@ -57,7 +176,7 @@ TASKS = {
             "asset": {"assetFileName": "mjcf/nv_ant.xml"}, "enableCameraSensors": False,
         },
         "sim": _sim(),
-        "task": {"randomize": False},
+        "task": {"randomize": False, "randomization_params": _DR_ANT},
     },
     "Humanoid": {
         "name": "Humanoid",
@@ -70,7 +189,7 @@ TASKS = {
             "plane": dict(_LOCO_PLANE), "enableCameraSensors": False,
         },
         "sim": _sim(),
-        "task": {"randomize": False},
+        "task": {"randomize": False, "randomization_params": _DR_HUMANOID},
     },
     "Cartpole": {
         "name": "Cartpole",
@@ -106,7 +225,7 @@ TASKS["ShadowHand"] = {
     },
     "sim": _sim(dt=0.01667, num_position_iterations=8, contact_offset=0.002, rest_offset=0.0,
                 bounce_threshold_velocity=0.2, max_depenetration_velocity=1000.0),
-    "task": {"randomize": False},
+    "task": {"randomize": False, "randomization_params": _DR_SHADOWHAND},
 }
 
 # Multi-agent Ant (build-defined, SURVEY.md §8(a) row A-MA): A ant actors per env.

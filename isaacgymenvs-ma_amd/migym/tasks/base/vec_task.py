@@ -31,6 +31,7 @@ import torch
 
 from ... import _abi
 from ... import model as M
+from ...dr import DomainRandomizationMixin
 from ... import spaces
 from ... import taskdefs
 
@@ -95,12 +96,16 @@ class Env(abc.ABC):
         pass
 
 
-class VecTask(Env):
+class VecTask(DomainRandomizationMixin, Env):
     """Base class of the MI355X tasks.  Subclasses set ``task_name`` and fill
     ``cfg['env']['numObservations'/'numActions']`` before calling ``__init__``."""
 
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 24}
     task_name = None
+    # domain randomization (migym/dr.py): actor names of task.randomization_params.actor_params, and
+    # whether the task resets (and so randomizes) in pre_physics_step (ShadowHand) or post_physics_step
+    dr_actor_names = {}
+    dr_reset_in_pre_physics = False
 
     def __init__(self, config, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
                  force_render=False):
@@ -123,6 +128,8 @@ class VecTask(Env):
         self.allocate_buffers()
         self.obs_dict = {}
         self.extras = {}
+        self._dr_init()
+        self.sim_initialized = True
 
     # ---------------------------------------------------------------------------------- setup
     def create_sim(self):
@@ -218,6 +225,13 @@ class VecTask(Env):
             a = a.to(device=self.device, dtype=torch.float32).contiguous()
         if a.shape != (self.num_actors, self.num_actions):
             raise ValueError(f"actions must be {(self.num_actors, self.num_actions)}, got {tuple(a.shape)}")
+        dr = self.randomize and self._dr is not None
+        if dr:
+            a = self._dr_actions(a)   # vec_task.py:372-374
+            if self.dr_reset_in_pre_physics:   # reset_idx in pre_physics_step (shadow_hand.py:599-607)
+                self._dr_step(self.reset_buf, pending_increment=self.control_steps > 0)
+            else:
+                self._dr["mask"].copy_(self.reset_buf)   # the resets post_physics_step will apply
         self._actions_in = a   # keep alive until the launch has consumed it
         tb = self._tb
         tb.actions = a.data_ptr()
@@ -228,12 +242,26 @@ class VecTask(Env):
             _abi.check(self._lib.mg_env_step(self.sim, _abi.C.byref(self.task_params), _abi.C.byref(tb), stream),
                        self._lib)
         self.control_steps += 1
+        self.frame_count += self.control_freq_inv
+        if dr:
+            if not self.dr_reset_in_pre_physics:   # reset_idx in post_physics_step (ant.py:287-293)
+                self._dr_step(self._dr["mask"], pending_increment=True)
+            self._dr_observations()   # vec_task.py:398-400
         self.extras["time_outs"] = self.timeout_buf.to(self.rl_device)
         self.post_step_extras()
         self.obs_dict["obs"] = self.obs_clamped.to(self.rl_device)
         if self.num_states > 0:
             self.obs_dict["states"] = self.get_state()
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    def _dr_step(self, mask, pending_increment):
+        """apply_randomizations as reset_idx calls it (only when some env resets: with dr_exact_trigger this
+        is checked with one host synchronisation, otherwise assumed), plus post_physics_step's
+        randomize_buf += 1 that precedes it."""
+        if (not self.dr_exact_trigger) or bool(mask.any()):
+            self.apply_randomizations(self.randomization_params, reset_mask=mask, increment=pending_increment)
+        elif pending_increment:
+            self.randomize_buf_actors += 1
 
     def post_step_extras(self):
         """Task-specific extras (e.g. Ant's true_objective); cheap device views only."""

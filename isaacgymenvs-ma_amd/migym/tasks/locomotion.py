@@ -29,9 +29,6 @@ class _Locomotion(VecTask):
         self.joints_at_limit_cost_scale = env["jointsAtLimitCost"]
         self.death_cost = env["deathCost"]
         self.termination_height = env["terminationHeight"]
-        self.randomize = cfg.get("task", {}).get("randomize", False)
-        if self.randomize:
-            raise NotImplementedError("domain randomization is not on this build's hot path (SURVEY.md §8(f))")
         env["numObservations"] = self.num_obs_default
         env["numActions"] = self.num_act_default
         self.up_axis_idx = 2
@@ -50,6 +47,7 @@ class Ant(_Locomotion):
     task_name = "Ant"
     num_obs_default = 60
     num_act_default = 8
+    dr_actor_names = {"ant": "articulation"}
 
     def post_step_extras(self):
         # compute_true_objective (ant.py:245-250): forward velocity of the torso
@@ -60,6 +58,7 @@ class Humanoid(_Locomotion):
     task_name = "Humanoid"
     num_obs_default = 108
     num_act_default = 21
+    dr_actor_names = {"humanoid": "articulation"}
 
 
 class MAAnt(_Locomotion):
@@ -76,6 +75,7 @@ class MAAnt(_Locomotion):
     task_name = "MAAnt"
     num_obs_default = 60
     num_act_default = 8
+    dr_actor_names = {"ant": "articulation"}
 
     def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
                  force_render=False):

@@ -25,12 +25,12 @@ from .base.vec_task import VecTask
 
 class ShadowHand(VecTask):
     task_name = "ShadowHand"
+    dr_actor_names = {"hand": "articulation", "object": "object", "goal_object": "none"}
+    dr_reset_in_pre_physics = True
 
     def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
                  force_render=False):
         env = cfg["env"]
-        if cfg.get("task", {}).get("randomize", False):
-            raise NotImplementedError("domain randomization is not on this build's hot path (SURVEY.md §8(f))")
         self.obs_type = env.get("observationType", "full_state")
         self.object_type = env.get("objectType", "block")
         self.max_episode_length = env["episodeLength"]

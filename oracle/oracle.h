@@ -79,6 +79,10 @@ int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_
 int orc_hand_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp,
                       const mg_state_views* v, const mg_task_buffers* tb, int32_t n, int32_t threads);
 
+/* domain randomization (oracle_dr.c): restatements of mg_dr_apply / mg_dr_noise on host buffers */
+int orc_dr_apply(const mg_dr_apply_args* a);
+int orc_dr_noise(const mg_dr_noise_args* a);
+
 #ifdef __cplusplus
 }
 #endif

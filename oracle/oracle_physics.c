@@ -139,6 +139,7 @@ typedef struct {
   double ow[3], ov[3];   /* object angular / COM linear velocity (world) */
   double of[3];          /* applied force on the object COM (apply_rigid_body_force_tensors) */
   int of_local;          /* LOCAL_SPACE: of is in the object frame at the start of each substep */
+  const double* gmu;     /* DR: friction per geom, [num_geoms] = the object's; NULL = sim friction */
   const float* tgt;      /* PD targets (nD) or NULL */
   int sat[MAXN];         /* drive saturated in the last substep */
   double ttend[MAXN];    /* tendon generalized force of the last substep */
@@ -856,7 +857,16 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       for (int c = 0; c < nvt; c++) v += J[r][c] * nu[c];
       double lnew = so->lam[r] + (b[r] - v) / W[r];
       if (so->row_kind[r] == 1) {
-        double lim = p->friction * so->lam[3 * so->row_ref[r]];  /* normal row of this contact */
+        double mu = p->friction;
+        if (s->gmu) { /* DR: mean of the two shapes' friction (ground plane: sim friction) */
+          const contact* ct = &so->con[so->row_ref[r]];
+          const int g2[2] = {ct->geomA, ct->geomB};
+          double sum = 0.0;
+          for (int k = 0; k < 2; k++)
+            sum += g2[k] >= 0 ? s->gmu[g2[k]] : (g2[k] == -2 ? s->gmu[m->num_geoms] : p->friction);
+          mu = 0.5 * sum;
+        }
+        double lim = mu * so->lam[3 * so->row_ref[r]];  /* normal row of this contact */
         lnew = lnew < -lim ? -lim : (lnew > lim ? lim : lnew);
       } else if (lnew < 0) {
         lnew = 0;
@@ -1016,11 +1026,48 @@ static void body_states(const mg_model* m, const astate* s, float* out) {
 
 /* one env: root rows [articulation, (object, goal)], dof rows, PD targets, sensors, dof forces,
  * rigid-body rows [articulation bodies, (object, goal)] */
-static void simulate_env(const mg_model* m, const mg_sim_params* p, float* root, float* dof, const float* act,
+/* domain randomization: the model with one env_props row applied (include/migym.h layout) */
+static void apply_env_props(const mg_model* m, const float* row, mg_model* mm, double* gmu) {
+  *mm = *m;
+  const int nn = m->num_nodes, ng = m->num_geoms, nt = m->num_tendons;
+  for (int i = 0; i < nn; i++) {
+    const float* r = row + 8 * i;
+    const double sc = m->mass[i] > 0.0f ? (double)r[0] / (double)m->mass[i] : 1.0;
+    mm->mass[i] = r[0];
+    for (int k = 0; k < 6; k++) mm->inertia[i][k] = (float)((double)m->inertia[i][k] * sc);
+    mm->armature[i] = r[1]; mm->damping[i] = r[2]; mm->stiffness[i] = r[3];
+    mm->lower[i] = r[4]; mm->upper[i] = r[5]; mm->drive_kp[i] = r[6]; mm->effort_limit[i] = r[7];
+  }
+  const float* g = row + 8 * nn;
+  for (int k = 0; k < ng; k++) gmu[k] = g[k];
+  const float* t = g + ng;
+  for (int q = 0; q < nt; q++) { mm->tendon_limit_stiffness[q] = t[2 * q]; mm->tendon_damping[q] = t[2 * q + 1]; }
+  const float* o = t + 2 * nt;
+  gmu[ng] = o[1];
+  if (m->obj_type) {
+    const double sc = (double)o[2], fm = (double)o[0] / (double)m->obj_mass;
+    mm->obj_mass = o[0];
+    for (int a = 0; a < 3; a++) {
+      mm->obj_size[a] = (float)((double)m->obj_size[a] * sc);
+      mm->obj_inertia[a] = (float)((double)m->obj_inertia[a] * fm * sc * sc);
+    }
+  }
+}
+
+static void simulate_env(const mg_model* m0, const mg_sim_params* p, float* root, float* dof, const float* act,
                          const float* tgt, float* sensors, float* dof_force, float* rbs, const float* oforce,
-                         int oforce_local) {
+                         int oforce_local, const float* props) {
   astate s;
   memset(&s, 0, sizeof(s));
+  mg_model* mdr = NULL;
+  double gmu[MG_MAX_GEOMS + 1];
+  const mg_model* m = m0;
+  if (props) {
+    mdr = (mg_model*)malloc(sizeof(mg_model));
+    apply_env_props(m0, props, mdr, gmu);
+    m = mdr;
+    s.gmu = gmu;
+  }
   load_state(m, root, dof, &s);
   s.tgt = tgt;
   if (m->obj_type) load_object(&s, root + 13);
@@ -1043,6 +1090,7 @@ static void simulate_env(const mg_model* m, const mg_sim_params* p, float* root,
     }
   }
   free(so);
+  free(mdr);
 }
 
 int orc_simulate_views(const mg_model* m, const mg_sim_params* p, int32_t n, const mg_state_views* v,
@@ -1060,7 +1108,8 @@ int orc_simulate_views(const mg_model* m, const mg_sim_params* p, int32_t n, con
                  v->dof_force ? v->dof_force + (size_t)nd * e : 0,
                  v->rigid_body_states ? v->rigid_body_states + (size_t)13 * nb * e : 0,
                  (m->obj_type && v->rb_forces) ? v->rb_forces + ((size_t)nb * e + m->num_bodies) * 3 : 0,
-                 v->rb_force_space == MG_LOCAL_SPACE);
+                 v->rb_force_space == MG_LOCAL_SPACE,
+                 v->env_props ? v->env_props + (size_t)v->env_props_stride * e : 0);
   }
   (void)threads;
   return 0;

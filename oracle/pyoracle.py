@@ -55,6 +55,8 @@ def lib():
         l.orc_hand_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
                                         C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32,
                                         C.c_int32]
+        l.orc_dr_apply.argtypes = [C.POINTER(_abi.DrApplyArgs)]
+        l.orc_dr_noise.argtypes = [C.POINTER(_abi.DrNoiseArgs)]
         _lib = l
     return _lib
 
@@ -169,11 +171,14 @@ class HostEnv:
         self.up = np.zeros((n, 3), np.float32)
         self.heading = np.zeros((n, 3), np.float32)
         self.noise = None
+        self.env_props = None   # (n, stride) domain-randomized properties, or None
 
     def views(self):
         v = _abi.StateViews()
         v.root_states, v.dof_state, v.dof_actuation = p(self.root), p(self.dof), p(self.act_eff)
         v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), None
+        if self.env_props is not None:
+            v.env_props, v.env_props_stride = p(self.env_props), self.env_props.shape[1]
         return v
 
     def buffers(self, seed=0, step=0, env_offset=0):

@@ -599,6 +599,260 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state", force_scale=0.0, 
     return res
 
 
+# ---------------------------------------------------------------------------------- domain randomization
+DR_TRACE_PARAMS = {
+    "frequency": 3,
+    "observations": {"range": [0, .002], "range_correlated": [0, .001], "operation": "additive",
+                     "distribution": "gaussian"},
+    "actions": {"range": [0., .05], "range_correlated": [0, .015], "operation": "additive", "distribution": "uniform"},
+    "sim_params": {"gravity": {"range": [0, 0.4], "operation": "additive", "distribution": "gaussian",
+                               "schedule": "linear", "schedule_steps": 6}},
+    "actor_params": {"ant": {
+        "color": True,
+        "rigid_body_properties": {"mass": {"range": [0.5, 1.5], "operation": "scaling", "distribution": "uniform",
+                                           "setup_only": True}},
+        "rigid_shape_properties": {"friction": {"num_buckets": 40, "range": [0.7, 1.3], "operation": "scaling",
+                                                "distribution": "uniform", "schedule": "linear", "schedule_steps": 6},
+                                   "restitution": {"range": [0., 0.7], "operation": "scaling",
+                                                   "distribution": "uniform"}},
+        "dof_properties": {"damping": {"range": [0.5, 1.5], "operation": "scaling", "distribution": "uniform",
+                                       "schedule": "linear", "schedule_steps": 6},
+                           "stiffness": {"range": [0.5, 1.5], "operation": "scaling", "distribution": "loguniform"},
+                           "lower": {"range": [0, 0.01], "operation": "additive", "distribution": "gaussian"},
+                           "upper": {"range": [0, 0.01], "operation": "additive", "distribution": "gaussian"}}}},
+}
+
+
+class _NpRandomRecorder:
+    """Stands in for dr_utils' ``np``: np.random.normal / uniform draws are kept in call order."""
+
+    def __init__(self):
+        self.draws = []
+        rec = self
+
+        class _R:
+            def normal(self, *a, **k):
+                x = np.random.normal(*a, **k)
+                rec.draws.append(np.array(x, dtype=np.float64).ravel())
+                return x
+
+            def uniform(self, *a, **k):
+                x = np.random.uniform(*a, **k)
+                rec.draws.append(np.array(x, dtype=np.float64).ravel())
+                return x
+        self.random = _R()
+
+    def __getattr__(self, k):
+        return getattr(np, k)
+
+
+class FakeDRGym(FakeGym):
+    """FakeGym + the property getters/setters apply_randomizations uses (vec_task.py:612-842)."""
+
+    def __init__(self, spec, num_envs, hand):
+        super().__init__(spec, num_envs)
+        from isaacgym import gymapi as ga
+        self.model = hand
+        self.frames = 0
+        self.simp = ga.SimParams()
+        self.simp.gravity = ga.Vec3(0.0, 0.0, -9.81)
+        self.simp.physx.rest_offset = 0.0
+        self.sim_param_sets = []
+        n, nd = num_envs, spec["num_dof"]
+        self.dof_set = {k: np.zeros((n, nd)) for k in ("damping", "stiffness", "lower", "upper")}
+        self.mass_set = np.zeros((n, len(hand.bodies)))
+        self.fric_set = np.zeros((n, len(hand.geoms)))
+        self._envs = 0
+
+    def create_env(self, *a):
+        self._envs += 1
+        return self._envs - 1
+
+    def get_frame_count(self, sim):
+        return self.frames
+
+    def simulate(self, sim):
+        super().simulate(sim)
+        self.frames += 1
+
+    def get_sim_params(self, sim):
+        # gym.get_sim_params returns the parameters by value (a new pybind object per call)
+        from isaacgym import gymapi as ga
+        q = ga.SimParams()
+        q.gravity = ga.Vec3(self.simp.gravity.x, self.simp.gravity.y, self.simp.gravity.z)
+        q.physx.rest_offset = self.simp.physx.rest_offset
+        return q
+
+    def set_sim_params(self, sim, p):
+        self.simp.gravity.x, self.simp.gravity.y, self.simp.gravity.z = p.gravity.x, p.gravity.y, p.gravity.z
+        self.sim_param_sets.append((p.gravity.x, p.gravity.y, p.gravity.z))
+
+    def find_actor_handle(self, env, name):
+        return 0
+
+    def get_actor_count(self, env):
+        return 1
+
+    def get_actor_handle(self, env, i):
+        return 0
+
+    def get_actor_name(self, env, h):
+        return "ant"
+
+    def get_actor_rigid_shape_count(self, env, h):
+        return len(self.model.geoms)
+
+    def get_actor_rigid_body_count(self, env, h):
+        return len(self.model.bodies)
+
+    def get_actor_dof_properties(self, env, h):
+        nd = self.spec["num_dof"]
+        dt = np.dtype([("hasLimits", "?"), ("lower", "f4"), ("upper", "f4"), ("driveMode", "i4"), ("velocity", "f4"),
+                       ("effort", "f4"), ("stiffness", "f4"), ("damping", "f4"), ("friction", "f4"),
+                       ("armature", "f4")])
+        a = np.zeros(nd, dt)
+        nodes = self.model.nodes[1:]
+        a["hasLimits"] = True
+        a["lower"] = [x.lower for x in nodes]
+        a["upper"] = [x.upper for x in nodes]
+        a["stiffness"] = [x.stiffness for x in nodes]
+        a["damping"] = [x.damping for x in nodes]
+        a["armature"] = [x.armature for x in nodes]
+        return a
+
+    def set_actor_dof_properties(self, env, h, props):
+        if isinstance(env, int):
+            for k in self.dof_set:
+                self.dof_set[k][env] = props[k]
+
+    def get_actor_rigid_body_properties(self, env, h):
+        return [_Prop(mass=float(self.model.nodes[b.node].mass)) for b in self.model.bodies]
+
+    def set_actor_rigid_body_properties(self, env, h, props, recompute=False):
+        self.mass_set[env] = [float(np.asarray(p.mass).ravel()[0]) for p in props]
+
+    def get_actor_rigid_shape_properties(self, env, h):
+        return [_Prop(friction=1.0, restitution=0.0) for _ in self.model.geoms]
+
+    def set_actor_rigid_shape_properties(self, env, h, props):
+        self.fric_set[env] = [float(np.asarray(p.friction).ravel()[0]) for p in props]
+
+    def get_actor_tendon_properties(self, env, h):
+        return []
+
+    def set_actor_tendon_properties(self, env, h, props):
+        pass
+
+
+def run_ant_dr(N=32, T=10, ep_len=3):
+    """Ant with task.randomize on the fake gym: every numpy / torch draw of apply_randomizations and of the
+    noise lambdas is recorded, with the property values the reference hands to the gym setters."""
+    import importlib
+    sys.path.insert(0, os.path.join(HERE, "..", "..", "isaacgymenvs-ma_amd"))
+    from migym import model as M
+    from isaacgymenvs.utils import dr_utils
+    import isaacgymenvs.tasks.base.vec_task as vt
+    mod = importlib.import_module("isaacgymenvs.tasks.ant")
+    ant = M.load_builtin("ant")
+    d = math.pi / 180
+    spec = dict(num_dof=8, sensors=4, start_z=0.44, gears=[15.0] * 8, bodies=[b.name for b in ant.bodies],
+                lower=[x * d for x in [-40, 30, -40, -100, -40, -100, -40, 30]],
+                upper=[x * d for x in [40, 100, 40, -30, 40, -30, 40, 100]])
+    fake = FakeDRGym(spec, N, ant)
+    install_fake(fake)
+    rec = RandRecorder()
+    mod.torch_rand_float = rec
+    nprec = _NpRandomRecorder()
+    dr_utils.np = nprec
+    trec = _TorchRecorder()
+
+    def randn_like(t, *a, **k):
+        u = torch.randn_like(t, *a, **k)
+        trec.draws.append(("randn", u.clone()))
+        return u
+
+    def rand_like(t, *a, **k):
+        u = torch.rand_like(t, *a, **k)
+        trec.draws.append(("rand", u.clone()))
+        return u
+    trec.randn_like, trec.rand_like = randn_like, rand_like
+    vt.torch = trec
+    cfg = load_task_cfg("Ant", N, ep_len)
+    cfg["task"]["randomize"] = True
+    cfg["task"]["randomization_params"] = DR_TRACE_PARAMS
+    np.random.seed(7)
+    torch.manual_seed(0)
+    env = mod.Ant(cfg, "cpu", "cpu", -1, True, False, False)
+    out = {"init_np": [np.concatenate(nprec.draws)], "init_sim": [fake.sim_param_sets[-1]],
+           "init_mass": [fake.mass_set.copy()], "init_fric": [fake.fric_set.copy()],
+           "init_dof": [np.stack([fake.dof_set[k].copy() for k in ("damping", "stiffness", "lower", "upper")])]}
+    nprec.draws.clear()
+    keys = ("actions", "act_draws", "obs_draws", "np_draws", "sim_set", "actuation", "phys_root", "phys_dof",
+            "phys_sensors", "noise", "reset_in", "progress_in", "obs", "rew", "reset", "progress", "randomize_buf",
+            "mass_set", "fric_set", "dof_set", "potentials", "prev_potentials")
+    for k in keys:
+        out[k] = []
+    nd = 8
+    lo, hi = torch.tensor(spec["lower"]), torch.tensor(spec["upper"])
+    lo, hi = torch.minimum(lo, hi), torch.maximum(lo, hi)
+    g = torch.Generator().manual_seed(5)
+    for t in range(T):
+        actions = torch.rand(N, 8, generator=g) * 2.4 - 1.2
+        root, dof, sens = physics_output(g, N, nd, lo, hi, (0.25, 0.7), 4)
+        fake.inject = (root, dof, sens, None)
+        reset_in, progress_in = env.reset_buf.clone(), env.progress_buf.clone()
+        rec.draws.clear()
+        trec.draws.clear()
+        nprec.draws.clear()
+        fake.calls.clear()
+        nsim = len(fake.sim_param_sets)
+        obs_dict, rew, reset, extras = env.step(actions)
+        ids = reset_in.nonzero(as_tuple=False).flatten()
+        noise = torch.zeros(N, 2 * nd)
+        if len(ids) > 0:
+            noise[ids, :nd] = rec.draws[0]
+            noise[ids, nd:] = rec.draws[1]
+        # torch draws: the action lambda's (N, 8) [corr?, z] then the observation lambda's (N, 60) [corr?, z]
+        act = [u for _, u in trec.draws if u.shape[-1] == 8]
+        obsd = [u for _, u in trec.draws if u.shape[-1] == 60]
+        pad = lambda lst, w: torch.stack(lst + [torch.full((N, w), float("nan"))] * (2 - len(lst)))  # noqa: E731
+        out["act_draws"].append(pad(act, 8) if len(act) == 2 else torch.stack([torch.full((N, 8), float("nan")), act[0]]))
+        out["obs_draws"].append(pad(obsd, 60) if len(obsd) == 2 else torch.stack([torch.full((N, 60), float("nan")), obsd[0]]))
+        nd_np = np.concatenate(nprec.draws) if nprec.draws else np.zeros(0)
+        out["np_draws"].append(nd_np)
+        out["sim_set"].append(np.array(fake.sim_param_sets[nsim:] or [(np.nan,) * 3]))
+        out["actions"].append(actions)
+        out["actuation"].append([c[1] for c in fake.calls if c[0] == "actuation"][0].view(N, nd).clone())
+        out["phys_root"].append(root)
+        out["phys_dof"].append(dof.view(N, nd, 2))
+        out["phys_sensors"].append(sens.view(N, 24))
+        out["noise"].append(noise)
+        out["reset_in"].append(reset_in)
+        out["progress_in"].append(progress_in)
+        out["obs"].append(obs_dict["obs"].clone())
+        out["rew"].append(rew.clone())
+        out["reset"].append(reset.clone())
+        out["progress"].append(env.progress_buf.clone())
+        out["randomize_buf"].append(env.randomize_buf.clone())
+        out["mass_set"].append(fake.mass_set.copy())
+        out["fric_set"].append(fake.fric_set.copy())
+        out["dof_set"].append(np.stack([fake.dof_set[k].copy() for k in ("damping", "stiffness", "lower", "upper")]))
+        out["potentials"].append(env.potentials.clone())
+        out["prev_potentials"].append(env.prev_potentials.clone())
+    res = {}
+    for k, v in out.items():
+        if k in ("np_draws", "sim_set", "init_np"):
+            # ragged: concatenate with per-step lengths
+            res[k + "_len"] = np.array([len(x) for x in v])
+            res[k] = np.concatenate([np.asarray(x, np.float64).reshape(len(x), -1) if k == "sim_set"
+                                     else np.asarray(x, np.float64).reshape(-1, 1) for x in v])
+        else:
+            res[k] = torch.stack(v) if isinstance(v[0], torch.Tensor) else np.stack(v)
+    res["episode_length"] = torch.tensor(ep_len)
+    res["lower"], res["upper"] = lo, hi
+    return res
+
+
 def save(name, d):
     path = os.path.join(HERE, name)
     np.savez_compressed(path, **{k: (v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
@@ -611,7 +865,7 @@ def main():
     # one task per process: vec_task keeps a process-global sim (vec_task.py:55-64)
     if which == "all":
         import subprocess
-        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces"):
+        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces", "ant_dr"):
             subprocess.check_call([sys.executable, __file__, t])
         return
     if which == "ant":
@@ -622,6 +876,8 @@ def main():
         save("trace_cartpole.npz", run_cartpole())
     elif which == "shadowhand":
         save("trace_shadowhand.npz", run_shadowhand())
+    elif which == "ant_dr":  # task.randomize: property draws, noise lambdas, gravity
+        save("trace_ant_dr.npz", run_ant_dr())
     elif which == "shadowhand_forces":  # random object forces + asymmetric states (forceScale > 0)
         save("trace_shadowhand_forces.npz", run_shadowhand(N=32, T=8, ep_len=4, force_scale=2.0, asymmetric=True,
                                                                force_prob_range=[0.2, 0.8]))
