@@ -86,8 +86,9 @@ def main():
     ap.add_argument("--task", default="Ant")
     ap.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", action="store_true",
-                    help="all-gather obs/rew/reset of every rank each step (one RCCL collective)")
+    ap.add_argument("--gather", nargs="?", const="all", default=None, choices=["all", "root"],
+                    help="concatenate obs/rew/reset of every rank each step: 'all' = one RCCL all-gather, "
+                         "'root' = point-to-point sends to rank 0 (migym.dist.OutputGather)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     args = ap.parse_args()
@@ -117,7 +118,7 @@ def main():
     gather = None
     if args.gather and world > 1 and args.backend == "nccl":
         from migym.dist import OutputGather
-        gather = OutputGather(env.num_actors, env.num_obs, dev)
+        gather = OutputGather(env.num_actors, env.num_obs, dev, mode=args.gather)
 
     def step(a):
         obs, rew, reset, _ = env.step(a)
@@ -162,7 +163,7 @@ def main():
                                    f"PGS x{env.sim_params.pos_iters}",
                        "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
                        "agents_per_env": env.num_agents, "agent_steps_per_s": value * env.num_agents,
-                       "obs_allgather": bool(gather is not None),
+                       "obs_gather": args.gather if gather is not None else None,
                        "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms),

@@ -44,16 +44,20 @@ def rollout(task, n, offset, n_total, rank_slice):
     return outs
 
 
-def _worker(rank, world, port, task, q):
+def _worker(rank, world, port, task, q, mode="all"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n_total = N_PER_RANK * world
     outs = rollout(task, N_PER_RANK, rank * N_PER_RANK, n_total, slice(rank * N_PER_RANK, (rank + 1) * N_PER_RANK))
     spec, sp, tp = _setup(task)
-    g = OutputGather(N_PER_RANK, tp.num_obs, "cpu")
+    g = OutputGather(N_PER_RANK, tp.num_obs, "cpu", mode=mode)
     res = []
     for obs, rew, reset in outs:
-        o, r, d = g(torch.from_numpy(obs), torch.from_numpy(rew), torch.from_numpy(reset))
+        got = g(torch.from_numpy(obs), torch.from_numpy(rew), torch.from_numpy(reset))
+        if got is None:
+            assert mode == "root" and rank != 0
+            continue
+        o, r, d = got
         res.append((o.numpy().copy(), r.numpy().copy(), d.numpy().copy()))
     if rank == 0:
         q.put(res)
@@ -69,13 +73,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("task", ["Ant", "Cartpole"])
-def test_sharded_rollout_equals_single_process(task):
+@pytest.mark.parametrize("task,mode", [("Ant", "all"), ("Cartpole", "all"), ("Ant", "root")])
+def test_sharded_rollout_equals_single_process(task, mode):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, task, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, task, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     gathered = q.get(timeout=120)
