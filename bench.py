@@ -74,8 +74,16 @@ def pmc_traffic(task, n, kern_ms):
         return {"traffic": None}
     if b is None:
         return {"traffic": None}
-    return {"traffic": b / (kern_ms * 1e-3) / 1e9, "traffic_bytes_per_launch": b,
-            "traffic_source": os.path.relpath(path, ROOT)}
+    out = {"traffic": b / (kern_ms * 1e-3) / 1e9, "traffic_bytes_per_launch": b,
+           "traffic_source": os.path.relpath(path, ROOT)}
+    try:
+        with open(path) as f:
+            issue = json.load(f).get("issue")
+        if issue:
+            out["pmc_issue"] = issue   # VALU-active / wait fractions of the same launches
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 def main():

@@ -121,7 +121,10 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
 
 #ifndef MG_PGS_PREFETCH
-#define MG_PGS_PREFETCH 2  // PGS visits whose data are in flight ahead of the sweep
+#define MG_PGS_PREFETCH 4  // PGS visits per block of the sweep (their data are loaded one block ahead)
+#endif
+#ifndef MG_PGS_EARLY
+#define MG_PGS_EARLY 1  // issue a block's private J/Y loads one whole block ahead (compiler barrier)
 #endif
 #ifndef MG_RB_WIDE
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
@@ -129,7 +132,8 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 
 template <int T, int MN, int MC, bool OBJ = false>
 struct TeamLDS {
-  static constexpr int MR = 3 * MC + 2 * (MN - 1);
+  // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
+  static constexpr int MR = (3 * MC + 2 * (MN - 1) + MG_PGS_PREFETCH - 1) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;
   static constexpr int MRO = OBJ ? MR : 1;
   static constexpr int RB = (T >= 32 && !OBJ) ? MG_RB_WIDE : 6;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
@@ -1307,6 +1311,17 @@ struct Team {
     for (int it = 0; it < p->pos_iters; it++) {
       for (int r0 = 0; r0 < prow; r0 += PF) {
         const int rn = r0 + PF == prow ? 0 : r0 + PF;  // next block of rows (wraps into the next sweep)
+#if MG_PGS_EARLY
+        // the next block's private J/Y (scratch, L2 latency) are issued before this block's visits; the
+        // compiler barrier keeps the scheduler from sinking them behind the first visits
+        float nJ[PF], nY[PF];
+#pragma unroll
+        for (int k = 0; k < PF; k++) {
+          nJ[k] = Jcol[rn + k];
+          nY[k] = Ycol[rn + k];
+        }
+        asm volatile("" ::: "memory");
+#endif
 #pragma unroll
         for (int k = 0; k < PF; k++) {
           const float v = team_sum<T>(pJ[k] * nu, tb);
@@ -1320,8 +1335,13 @@ struct Team {
           lamn = m == -1.0f ? lnew : lamn;
           s->u.sv.rows[r0 + k].lam = lnew;
           nu += pY[k] * (lnew - lam);
+#if MG_PGS_EARLY
+          pJ[k] = nJ[k];
+          pY[k] = nY[k];
+#else
           pJ[k] = Jcol[rn + k];
           pY[k] = Ycol[rn + k];
+#endif
           pR[k] = s->u.sv.rows[rn + k];
         }
       }

@@ -35,5 +35,14 @@ if jout:
     out = {"kernel": kern, "dispatches": len(agg.get("FETCH_SIZE", [])), "FETCH_SIZE_kB": fetch, "WRITE_SIZE_kB": write,
            "traffic_bytes_per_launch": None if fetch is None or write is None else (2.0 * fetch + write) * 1024.0,
            "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM/rocprofv3); kB = 1024 B"}
+    # issue / latency picture of the same launches (per-wave cycle fractions, medians over dispatches)
+    wc = med.get("SQ_WAVE_CYCLES")
+    if wc:
+        out["issue"] = {k: med[c] / wc for k, c in (("valu_active_frac", "SQ_ACTIVE_INST_VALU"),
+                                                     ("any_active_frac", "SQ_ACTIVE_INST_ANY"),
+                                                     ("wait_any_frac", "SQ_WAIT_ANY"),
+                                                     ("wait_inst_lds_frac", "SQ_WAIT_INST_LDS")) if c in med}
+        if "SQ_INSTS_LDS" in med and "SQ_LDS_BANK_CONFLICT" in med:
+            out["issue"]["lds_bank_conflict_cycles_per_lds_inst"] = med["SQ_LDS_BANK_CONFLICT"] / med["SQ_INSTS_LDS"]
     json.dump(out, open(jout, "w"), indent=1)
     print("wrote", jout)
