@@ -243,6 +243,11 @@ typedef struct mg_task_params {
   float force_prob_lo;               /* forceProbRange */
   float force_prob_hi;
   float object_rb_mass;              /* object_rb_masses */
+  /* observation column -> (segment << 8 | index) of the observationType layout (obs_map) and of the
+   * full_state layout (state_map).  Filled by the library before a hand-task launch; callers need
+   * not set them. */
+  uint16_t obs_map[256];
+  uint16_t state_map[256];
 } mg_task_params;
 
 /* Task-layer buffers (VecTask.allocate_buffers, vec_task.py:302-325). */

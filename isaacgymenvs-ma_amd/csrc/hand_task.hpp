@@ -66,6 +66,42 @@ __device__ __forceinline__ int h_locate_in(int layout, const mg_task_params& tp,
 __device__ __forceinline__ int h_locate(const mg_task_params& tp, int nd, int k, int* idx) {
   return h_locate_in(tp.obs_type, tp, nd, k, idx);
 }
+// host copy of the layouts: fills obs_map / state_map (column -> segment << 8 | index) once per launch,
+// so the kernels look a column up instead of walking the segment list per column
+static const int8_t kHandLayoutHost[4][12] = {
+    {HS_DOF_POS, HS_DOF_VEL, HS_DOF_FORCE, HS_OBJ_POSE, HS_OBJ_LINVEL, HS_OBJ_ANGVEL, HS_GOAL_POSE, HS_QUAT_DIFF,
+     HS_FT_STATE, HS_FT_FORCE, HS_ACTIONS, HS_END},
+    {HS_DOF_POS, HS_DOF_VEL, HS_OBJ_POSE, HS_OBJ_LINVEL, HS_OBJ_ANGVEL, HS_GOAL_POSE, HS_QUAT_DIFF, HS_FT_STATE,
+     HS_ACTIONS, HS_END, HS_END, HS_END},
+    {HS_DOF_POS, HS_OBJ_POSE, HS_GOAL_POSE, HS_QUAT_DIFF, HS_FT_POS, HS_ACTIONS, HS_END, HS_END, HS_END, HS_END,
+     HS_END, HS_END},
+    {HS_FT_POS, HS_OBJ_POS, HS_QUAT_DIFF, HS_ACTIONS, HS_END, HS_END, HS_END, HS_END, HS_END, HS_END, HS_END, HS_END}};
+inline int h_seg_size_host(int seg, int nd, int nf, int na) {
+  switch (seg) {
+    case HS_DOF_POS: case HS_DOF_VEL: case HS_DOF_FORCE: return nd;
+    case HS_OBJ_POSE: case HS_GOAL_POSE: return 7;
+    case HS_OBJ_POS: case HS_OBJ_LINVEL: case HS_OBJ_ANGVEL: return 3;
+    case HS_QUAT_DIFF: return 4;
+    case HS_FT_STATE: return 13 * nf;
+    case HS_FT_POS: return 3 * nf;
+    case HS_FT_FORCE: return 6 * nf;
+    case HS_ACTIONS: return na;
+    default: return 0;
+  }
+}
+inline void h_fill_map(uint16_t* map, int layout, int nd, int nf, int na) {
+  int k = 0;
+  for (int i = 0; i < 12 && kHandLayoutHost[layout & 3][i] != HS_END && k < 256; i++) {
+    const int seg = kHandLayoutHost[layout & 3][i], n = h_seg_size_host(seg, nd, nf, na);
+    for (int j = 0; j < n && k < 256; j++) map[k++] = (uint16_t)((seg << 8) | j);
+  }
+  for (; k < 256; k++) map[k] = (uint16_t)(HS_END << 8);
+}
+inline void h_fill_maps(mg_task_params* tp) {
+  h_fill_map(tp->obs_map, tp->obs_type, tp->num_dofs, tp->num_fingertips, tp->num_actions);
+  h_fill_map(tp->state_map, 0, tp->num_dofs, tp->num_fingertips, tp->num_actions);
+}
+
 // fingertip body / component of an HS_FT_STATE or HS_FT_POS index
 __device__ __forceinline__ void h_ft_ref(const mg_task_params& tp, int seg, int idx, int* body, int* comp) {
   const int w = seg == HS_FT_STATE ? 13 : 3;

@@ -55,6 +55,9 @@ struct mg_sim {
   bool bound;
 };
 
+#ifndef MG_EXP
+#define MG_EXP 0  // profiling experiments only (phase attribution): skip parts of the hand post-physics
+#endif
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
@@ -657,16 +660,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   // rigid-body states of the hand once (one lane per body) into the dead row storage: the fingertip
   // observations and the rigid_body_states write-back both read them
   float* bst = &L.u.sv.rows[0].b;
+#if !(MG_EXP & 1)
   for (int b = t.tl; b < nb; b += T) t.body_state(b, bst + 13 * b);
+#endif
   __syncthreads();
+#if !(MG_EXP & 2)
   {
     const float* gs = L.goal + 13;
     float qdiff[4];
     const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
     mg::t_quat_mul(L.oroot + 3, gc, qdiff);
     for (int k = t.tl; k < no; k += T) {
-      int i;
-      const int seg = mg::h_locate(tp, nd, k, &i);
+      const int mk = tp.obs_map[k], seg = mk >> 8, i = mk & 255;   // column -> (segment, index)
       float x;
       if (seg == mg::HS_ACTIONS) {  // self.actions (clamped)
         x = mg::clampf(tb.actions[(size_t)na * ec + i], tp.clip_actions);
@@ -680,10 +685,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       L.obs[k] = x;
     }
   }
+#endif
   __syncthreads();
   int64_t ro = 0;
   float fin = 0.0f;
-  if (t.tl == 0) {
+  if (!(MG_EXP & 4) && t.tl == 0) {
     const float* gs = L.goal + 13;
     float succ = env_reset ? 0.0f : tb.successes[ec], rew;
     int64_t prog = progress_in + 1, go;
@@ -710,7 +716,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
     atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
   }
-  if (valid) {  // write-back (gym layouts), team-cooperative
+  if (!(MG_EXP & 8) && valid) {  // write-back (gym layouts), team-cooperative
     float* o = tb.obs + (size_t)no * e;
     for (int k = t.tl; k < no; k += T) {
       o[k] = L.obs[k];
@@ -742,8 +748,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
       mg::t_quat_mul(L.oroot + 3, gc, qdiff);
       for (int k = t.tl; k < tp.num_states; k += T) {
-        int i;
-        const int seg = mg::h_locate_in(0, tp, nd, k, &i);
+        const int mk = tp.state_map[k], seg = mk >> 8, i = mk & 255;
         float x;
         if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
           int b, c;
@@ -939,6 +944,9 @@ struct RunEnvStep {
     if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
       return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
     if constexpr (OBJ) {
+      mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
+      mg::h_fill_maps(&tpm);
+      tp = &tpm;
       if (sim->views.env_props)
         hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                            sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);

@@ -1089,24 +1089,48 @@ struct Team {
       // emission order); a candidate whose geom's bounding sphere cannot come within the contact
       // offset of the object's is skipped (conservative: the same contacts)
       const float ro = sqrtf(dot(osize(), osize()));
-      const int NC = mt->noc;
+      // pass 1, lane per geom: bounding-sphere cull of the whole geom (its centre only: R . pos + x);
+      // the survivors' candidates are then enumerated densely, so culled boxes cost no lanes
+      unsigned long long live = 0ull;
+      for (int g0 = 0; g0 < G; g0 += T) {
+        const int g = g0 + tl;
+        bool ok = false;
+        if (g < G && (mt->gfil[g] & MG_COLLIDE_OBJECT) &&
+            (mt->gtype[g] == MG_GT_SPHERE || mt->gtype[g] == MG_GT_CAPSULE || mt->gtype[g] == MG_GT_BOX)) {
+          const int nd = mt->gnode[g];
+          const float* gp = mt->gf[g];
+          const float* Rn = s->R[nd];
+          const V3 c = ld3(s->x[nd]) + v3(Rn[0] * gp[0] + Rn[1] * gp[1] + Rn[2] * gp[2],
+                                          Rn[3] * gp[0] + Rn[4] * gp[1] + Rn[5] * gp[2],
+                                          Rn[6] * gp[0] + Rn[7] * gp[1] + Rn[8] * gp[2]);
+          const V3 dc = c - op;
+          const float reach = gp[15] + ro + off;
+          ok = dot(dc, dc) <= reach * reach;
+        }
+        const unsigned long long b = __ballot(ok);
+        live |= ((b >> tb) & (T >= 64 ? ~0ull : ((1ull << T) - 1ull))) << g0;
+      }
+      int NC = 0;
+      for (unsigned long long mm = live; mm; mm &= mm - 1) NC += mt->gtype[__builtin_ctzll(mm)] == MG_GT_BOX ? 16 : 1;
       for (int f0 = 0; f0 < NC; f0 += T) {
         const int f = f0 + tl;
         int cnt = 0, g = 0;
         V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
         float d = 0.0f;
         if (f < NC) {
-          const int e = mt->ocand[f];
-          g = e >> 4;
+          // candidate f of the survivors, in geom order: its geom and candidate index
+          int q = f;
+          for (unsigned long long mm = live; mm; mm &= mm - 1) {
+            g = __builtin_ctzll(mm);
+            const int n = mt->gtype[g] == MG_GT_BOX ? 16 : 1;
+            if (q < n) break;
+            q -= n;
+          }
           V3 c;
           M3 Rg;
           geom_world(g, &c, &Rg);
-          const V3 dc = c - op;
-          const float reach = mt->gf[g][15] + ro + off;
-          if (dot(dc, dc) <= reach * reach) {
-            obj_candidate(g, e & 15, c, Rg, &pt, &nrm, &d);
-            cnt = d < off ? 1 : 0;
-          }
+          obj_candidate(g, q, c, Rg, &pt, &nrm, &d);
+          cnt = d < off ? 1 : 0;
         }
         const int incl = team_incl_scan<T>(cnt);
         const int tot = __shfl(incl, tb + T - 1);

@@ -99,7 +99,7 @@ class TaskParams(C.Structure):
                 ("goal_displacement", C.c_float * 3), ("goal_dz", C.c_float),
                 ("num_states", C.c_int32), ("object_rb", C.c_int32), ("force_scale", C.c_float),
                 ("force_decay_step", C.c_float), ("force_prob_lo", C.c_float), ("force_prob_hi", C.c_float),
-                ("object_rb_mass", C.c_float)]
+                ("object_rb_mass", C.c_float), ("obs_map", C.c_uint16 * 256), ("state_map", C.c_uint16 * 256)]
 
 
 class TaskBuffers(C.Structure):
