@@ -913,10 +913,20 @@ struct Team {
     *cw = ld3(s->x[nd]) + mul(Rn, ld3(gf));
     *Rg = mul(Rn, Rl);
   }
+  // world frames of the geoms, staged once per substep by collide() (lane per geom) in the team's
+  // union storage (dead between the ABA and build_rows); rows of 13 floats (odd stride): centre, R
+  static constexpr int GW = 13;
+  __device__ float* gw_tile() const { return &s->u.slot[0][0]; }
+  __device__ void geom_staged(int g, V3* c, M3* Rg) const {
+    const float* w = gw_tile() + GW * g;
+    *c = v3(w[0], w[1], w[2]);
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) Rg->m[a][b] = w[3 + 3 * a + b];
+  }
   __device__ bool geom_segment(int g, V3* a, V3* b, float* r) const {
     V3 c;
     M3 Rg;
-    geom_world(g, &c, &Rg);
+    geom_staged(g, &c, &Rg);
     int ty = mt->gtype[g];
     const float* gs = mt->gf[g] + 12;
     if (ty == MG_GT_SPHERE) { *a = c; *b = c; *r = gs[0]; return true; }
@@ -980,6 +990,17 @@ struct Team {
     const float off = p->contact_offset;
     int base = 0;
     const int G = mt->ng;
+    static_assert(MN * 27 >= MG * GW, "geom frames must fit the team's union storage");
+    for (int g = tl; g < G; g += T) {
+      V3 c;
+      M3 Rg;
+      geom_world(g, &c, &Rg);
+      float* w = gw_tile() + GW * g;
+      w[0] = c.x; w[1] = c.y; w[2] = c.z;
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) w[3 + 3 * a + b] = Rg.m[a][b];
+    }
+    __syncthreads();
     // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
     // pass 1 counts, a team scan places them, pass 2 recomputes and writes (no private arrays).
     for (int g0 = 0; g0 < G; g0 += T) {
@@ -988,7 +1009,7 @@ struct Team {
       M3 Rg;
       int ty = -1;
       if (g < G && (mt->gfil[g] & MG_COLLIDE_GROUND)) {
-        geom_world(g, &c, &Rg);
+        geom_staged(g, &c, &Rg);
         // every candidate's gap is >= c.z - bounding radius: geoms that high cannot touch the plane
         if (c.z - mt->gf[g][15] < off) ty = mt->gtype[g];
       }
@@ -1097,14 +1118,9 @@ struct Team {
         bool ok = false;
         if (g < G && (mt->gfil[g] & MG_COLLIDE_OBJECT) &&
             (mt->gtype[g] == MG_GT_SPHERE || mt->gtype[g] == MG_GT_CAPSULE || mt->gtype[g] == MG_GT_BOX)) {
-          const int nd = mt->gnode[g];
-          const float* gp = mt->gf[g];
-          const float* Rn = s->R[nd];
-          const V3 c = ld3(s->x[nd]) + v3(Rn[0] * gp[0] + Rn[1] * gp[1] + Rn[2] * gp[2],
-                                          Rn[3] * gp[0] + Rn[4] * gp[1] + Rn[5] * gp[2],
-                                          Rn[6] * gp[0] + Rn[7] * gp[1] + Rn[8] * gp[2]);
+          const V3 c = ld3(gw_tile() + GW * g);
           const V3 dc = c - op;
-          const float reach = gp[15] + ro + off;
+          const float reach = mt->gf[g][15] + ro + off;
           ok = dot(dc, dc) <= reach * reach;
         }
         const unsigned long long b = __ballot(ok);
@@ -1128,7 +1144,7 @@ struct Team {
           }
           V3 c;
           M3 Rg;
-          geom_world(g, &c, &Rg);
+          geom_staged(g, &c, &Rg);
           obj_candidate(g, q, c, Rg, &pt, &nrm, &d);
           cnt = d < off ? 1 : 0;
         }
@@ -1448,8 +1464,7 @@ struct Team {
         if (cside(c, 2) >= 0 && mt->gbody[cside(c, 2)] == body) sg = 1.0f;
         else if (cside(c, 3) >= 0 && mt->gbody[cside(c, 3)] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
-        V3 n = ld3(s->cn[c]), t1, t2;
-        tangent_basis_t(n, &t1, &t2);
+        const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
         V3 f = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) * (sg / h);
         F = F + f;
         Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
