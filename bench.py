@@ -99,6 +99,8 @@ def main():
                          "'root' = point-to-point sends to rank 0 (migym.dist.OutputGather)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--object-type", default="block", choices=["block", "egg", "pen"],
+                    help="ShadowHand objectType (shadow_hand.py:86-100)")
     args = ap.parse_args()
 
     import torch
@@ -118,8 +120,14 @@ def main():
 
     import migym
     n = args.num_envs
+    mk = {}
+    if args.task == "ShadowHand" and args.object_type != "block":
+        from migym import configs
+        tcfg = configs.task_config("ShadowHand", n, sim_device=dev)
+        tcfg["env"]["objectType"] = args.object_type
+        mk["cfg"] = {"task": tcfg}
     env = migym.make(seed=rank, task=args.task, num_envs=n, sim_device=dev, rl_device=dev, headless=True,
-                     multi_gpu=world > 1)
+                     multi_gpu=world > 1, **mk)
     na = env.num_actions
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
@@ -172,7 +180,8 @@ def main():
                        "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
                        "agents_per_env": env.num_agents, "agent_steps_per_s": value * env.num_agents,
                        "obs_gather": args.gather if gather is not None else None,
-                       "parallelism": f"env-sharded x{world}"},
+                       "parallelism": f"env-sharded x{world}",
+                       **({"object_type": args.object_type} if args.task == "ShadowHand" else {})},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms),
                          "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",

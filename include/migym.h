@@ -64,7 +64,7 @@ extern "C" {
 #define MG_MAX_HAND_DOFS 32
 
 enum { MG_JT_FREE = 0, MG_JT_FIXED = 1, MG_JT_HINGE = 2, MG_JT_SLIDE = 3 };
-enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4 };
+enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4, MG_GT_ELLIPSOID = 5 };
 enum { MG_OK = 0, MG_EINVAL = -1, MG_EDEVICE = -2, MG_ENOMEM = -3, MG_ECAPACITY = -4 };
 enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2, MG_TASK_SHADOW_HAND = 3 };
 #define MG_MAX_AGENTS 8
@@ -122,11 +122,12 @@ typedef struct mg_model {
   /* One free rigid body per env next to the articulation (the manipulated object), plus a
    * kinematic goal actor.  Root-state rows per env are then [articulation, object, goal] and
    * rigid-body rows [articulation bodies..., object, goal]. */
-  int32_t obj_type;                  /* 0 = none, MG_GT_BOX */
+  int32_t obj_type;                  /* 0 = none, MG_GT_BOX (block), MG_GT_ELLIPSOID (egg), MG_GT_CAPSULE (pen) */
   int32_t obj_pad;
   float obj_mass;
   float obj_inertia[3];              /* principal moments, object frame (COM at the origin) */
-  float obj_size[3];                 /* box half extents */
+  float obj_size[3];                 /* box half extents | ellipsoid semi-axes | capsule (radius, half length
+                                      * along the object's z, 0) */
   float obj_lin_damping;
   float obj_ang_damping;
   float obj_gravity;                 /* 1 = the object falls under sim gravity */

@@ -1,0 +1,307 @@
+// convex.hpp — narrowphase of articulation geoms against the egg (ellipsoid) object of ShadowHand's
+// objectType egg (shadow_hand.py:86-100; open_ai_assets/hand/egg.xml), fp64, one lane per candidate.
+// Same algorithm and constants as the oracle's cvx_* functions (oracle/oracle_physics.c):
+//
+//   * everything in the object frame (ellipsoid of semi-axes e centred at the origin);
+//   * shape A is a hand geom's core: a segment (sphere / capsule, radius added afterwards) or a box;
+//   * GJK distance on A - B: closest point of the simplex by Voronoi-region tests (Ericson 5.1.2,
+//     5.1.5, 5.1.6), stop on |v|^2 - v.w <= 1e-10 |v|^2 + 1e-24, a repeated support point, no progress
+//     or 64 iterations;
+//   * overlapping cores -> MPR (Minkowski portal refinement): a fixed five-point state (interior
+//     point, portal triangle, candidate), so nothing grows per lane the way an EPA polytope would;
+//     the penetration vector is the refined portal's point nearest the origin.
+//
+// The narrowphase runs in fp64 (the CDNA4 VALU's fp64 rate is ample for a few candidates per env):
+// GJK against a curved surface converges linearly, and an fp32 stop criterion leaves ~1e-3 of
+// direction error in the contact normal; in fp64 the normal is resolved to ~1e-5 and the kernel
+// follows the fp64 oracle.  The simplex lives in small fixed arrays that the unrolled loops index
+// with constants; the code runs only for the egg, behind a wave-uniform branch on the object type.
+#pragma once
+#include "device_math.hpp"
+
+namespace mg {
+
+struct D3 {
+  double x, y, z;
+};
+__device__ __forceinline__ D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 d3(V3 a) { return D3{a.x, a.y, a.z}; }
+__device__ __forceinline__ V3 f3(D3 a) { return v3((float)a.x, (float)a.y, (float)a.z); }
+__device__ __forceinline__ D3 operator+(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ D3 operator-(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ D3 operator*(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ D3 operator-(D3 a) { return d3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ D3 cross(D3 a, D3 b) {
+  return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+struct CvxShape {
+  int kind;      // 0 segment [p0, p1], 1 box (centre c, axes = columns of R, half extents h)
+  D3 p0, p1;
+  D3 c, h;
+  double R[3][3];
+};
+
+__device__ __forceinline__ D3 cvx_support(const CvxShape& A, D3 d) {
+  if (A.kind == 0) return dot(A.p0, d) >= dot(A.p1, d) ? A.p0 : A.p1;
+  D3 o = A.c;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const D3 col = d3(A.R[0][k], A.R[1][k], A.R[2][k]);
+    const double hk = k == 0 ? A.h.x : (k == 1 ? A.h.y : A.h.z);
+    o = o + col * (dot(col, d) >= 0.0 ? hk : -hk);
+  }
+  return o;
+}
+
+// support point of the ellipsoid with semi-axes e in direction d
+__device__ __forceinline__ D3 ell_support(D3 e, D3 d) {
+  const D3 q = d3(e.x * e.x * d.x, e.y * e.y * d.y, e.z * e.z * d.z);
+  const double n = sqrt(q.x * d.x + q.y * d.y + q.z * d.z);
+  if (n < 1e-30) return d3(0, 0, 0);
+  return q * (1.0 / n);
+}
+
+__device__ __forceinline__ void cvx_seg(D3 a, D3 b, double* lam) {
+  const D3 ab = b - a;
+  const double den = dot(ab, ab);
+  double t = den > 0.0 ? -dot(a, ab) / den : 0.0;
+  t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+  lam[0] = 1.0 - t;
+  lam[1] = t;
+}
+
+__device__ __forceinline__ void cvx_tri(D3 a, D3 b, D3 c, double* lam) {
+  const D3 ab = b - a, ac = c - a;
+  lam[0] = lam[1] = lam[2] = 0.0;
+  const double d1 = -dot(ab, a), d2 = -dot(ac, a);
+  if (d1 <= 0.0 && d2 <= 0.0) { lam[0] = 1.0; return; }
+  const double e3 = -dot(ab, b), d4 = -dot(ac, b);
+  if (e3 >= 0.0 && d4 <= e3) { lam[1] = 1.0; return; }
+  const double vc = d1 * d4 - e3 * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && e3 <= 0.0) { const double v = d1 / (d1 - e3); lam[0] = 1.0 - v; lam[1] = v; return; }
+  const double d5 = -dot(ab, c), d6 = -dot(ac, c);
+  if (d6 >= 0.0 && d5 <= d6) { lam[2] = 1.0; return; }
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) { const double w = d2 / (d2 - d6); lam[0] = 1.0 - w; lam[2] = w; return; }
+  const double va = e3 * d6 - d5 * d4;
+  if (va <= 0.0 && (d4 - e3) >= 0.0 && (d5 - d6) >= 0.0) {
+    const double w = (d4 - e3) / ((d4 - e3) + (d5 - d6));
+    lam[1] = 1.0 - w;
+    lam[2] = w;
+    return;
+  }
+  const double den = va + vb + vc;
+  if (!(den > 0.0)) { cvx_seg(a, b, lam); lam[2] = 0.0; return; }
+  const double v = vb / den, w = vc / den;
+  lam[0] = 1.0 - v - w;
+  lam[1] = v;
+  lam[2] = w;
+}
+
+// closest point of the simplex W[0..n-1] to the origin; keeps the supporting vertices in order,
+// their weights in lk; returns true if the origin is inside a (non-degenerate) tetrahedron
+__device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, double* lk) {
+  double lam[4] = {0.0, 0.0, 0.0, 0.0};
+  if (n == 1) {
+    lam[0] = 1.0;
+  } else if (n == 2) {
+    cvx_seg(W[0], W[1], lam);
+  } else if (n == 3) {
+    cvx_tri(W[0], W[1], W[2], lam);
+  } else {
+    constexpr int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};  // face + opposite
+    double best = 1e300;
+    bool any = false;
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      const D3 a = W[F[f][0]], b = W[F[f][1]], c = W[F[f][2]], d = W[F[f][3]];
+      const D3 ab = b - a, ac = c - a, ad = d - a;
+      const D3 nf = cross(ab, ac);
+      const double sp = -dot(nf, a), sd = dot(nf, ad);
+      const double sc = dot(ab, ab) + dot(ac, ac) + dot(ad, ad);
+      const bool degenerate = sd * sd <= 1e-12 * sc * sc * sc;
+      if (!(sp * sd < 0.0) && !degenerate) continue;
+      any = true;
+      double l3[3];
+      cvx_tri(a, b, c, l3);
+      const D3 q = a * l3[0] + b * l3[1] + c * l3[2];
+      const double dq = dot(q, q);
+      if (dq < best) {
+        best = dq;
+#pragma unroll
+        for (int i = 0; i < 4; i++) lam[i] = 0.0;
+        lam[F[f][0]] = l3[0];
+        lam[F[f][1]] = l3[1];
+        lam[F[f][2]] = l3[2];
+      }
+    }
+    if (!any) return true;
+  }
+  int m = 0;
+  v = d3(0, 0, 0);
+  D3 Wn[4], Pn[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i < n && lam[i] > 0.0) {
+      v = v + W[i] * lam[i];
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (j == m) { Wn[j] = W[i]; Pn[j] = P[i]; lk[j] = lam[i]; }
+      m++;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (j < m) { W[j] = Wn[j]; P[j] = Pn[j]; }
+  n = m;
+  return false;
+}
+
+// GJK distance between core A and the origin-centred ellipsoid e: true when separated (closest
+// points pa on A, pb on the ellipsoid, distance), false when the cores overlap
+__device__ __forceinline__ bool cvx_gjk(const CvxShape& A, D3 e, D3& pa, D3& pb, double& dist) {
+  D3 W[4], P[4];
+  D3 v = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
+  if (dot(v, v) < 1e-20) v = d3(0, 0, 1);
+  int n = 0;
+  double vv = dot(v, v);
+  double lam[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int it = 0; it < 64; it++) {
+    const D3 a = cvx_support(A, -v), b = ell_support(e, v), w = a - b;
+    if (n > 0 && vv - dot(v, w) <= 1e-10 * vv + 1e-24) break;
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const D3 dd = W[i] - w;
+      if (i < n && dot(dd, dd) <= 1e-24) dup = true;
+    }
+    if (dup) break;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i == n) { W[i] = w; P[i] = a; }
+    n++;
+    if (cvx_simplex(W, P, n, v, lam)) return false;
+    const double vn = dot(v, v);
+    if (vn <= 1e-20) return false;
+    const bool stall = it > 0 && vn >= vv * (1.0 - 1e-14);
+    vv = vn;
+    if (stall) break;
+  }
+  pa = d3(0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (i < n) pa = pa + P[i] * lam[i];
+  pb = pa - v;
+  dist = sqrt(vv);
+  return true;
+}
+
+constexpr double MPR_TOL = 1e-10;   // portal reached the boundary (m)
+constexpr double MPR_EPS = 1e-12;  // origin-side tests
+
+__device__ __forceinline__ D3 unit3(D3 a) {
+  const double l = sqrt(dot(a, a));
+  return l > 0.0 ? a * (1.0 / l) : a;
+}
+
+// MPR penetration for overlapping cores: the boundary point x of A - B (moving A by -x separates
+// them) and the A-side witness pa; false if the portal search degenerates
+__device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) {
+  D3 v0 = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
+  if (dot(v0, v0) < 1e-20) v0 = d3(1e-6, 0, 0);
+  D3 dir = unit3(-v0);
+  D3 a1 = cvx_support(A, dir), v1 = a1 - ell_support(e, -dir);
+  if (dot(v1, dir) <= 0.0) return false;
+  dir = cross(v0, v1);
+  if (dot(dir, dir) <= 1e-24) { x = v1; pa = a1; return true; }
+  dir = unit3(dir);
+  D3 a2 = cvx_support(A, dir), v2 = a2 - ell_support(e, -dir);
+  if (dot(v2, dir) <= 0.0) return false;
+  dir = unit3(cross(v1 - v0, v2 - v0));
+  if (dot(dir, v0) > 0.0) {
+    D3 t = v1; v1 = v2; v2 = t;
+    t = a1; a1 = a2; a2 = t;
+    dir = -dir;
+  }
+  D3 a3, v3p;
+  int it;
+  for (it = 0; it < 64; it++) {  // a portal the origin ray passes through
+    a3 = cvx_support(A, dir);
+    v3p = a3 - ell_support(e, -dir);
+    if (dot(v3p, dir) <= 0.0) return false;
+    if (dot(cross(v1, v3p), v0) < -MPR_EPS) {
+      v2 = v3p; a2 = a3;
+    } else if (dot(cross(v3p, v2), v0) < -MPR_EPS) {
+      v1 = v3p; a1 = a3;
+    } else {
+      break;
+    }
+    dir = unit3(cross(v1 - v0, v2 - v0));
+  }
+  if (it == 64) return false;
+  // expand: replace one portal vertex by v4 so that the portal keeps facing the origin ray
+  auto expand = [&](D3 v4, D3 a4) {
+    const D3 c = cross(v4, v0);
+    int k;
+    if (dot(v1, c) > 0.0) k = dot(v2, c) > 0.0 ? 1 : 3;
+    else k = dot(v3p, c) > 0.0 ? 2 : 1;
+    if (k == 1) { v1 = v4; a1 = a4; }
+    else if (k == 2) { v2 = v4; a2 = a4; }
+    else { v3p = v4; a3 = a4; }
+  };
+  auto reached = [&](D3 v4, D3 d) {
+    const double d4 = dot(v4, d);
+    const double mm = fmin(d4 - dot(v1, d), fmin(d4 - dot(v2, d), d4 - dot(v3p, d)));
+    return mm <= MPR_TOL;
+  };
+  for (it = 0; it < 64; it++) {  // refine until the portal encloses the origin
+    dir = unit3(cross(v2 - v1, v3p - v1));
+    if (dot(v1, dir) >= 0.0) break;
+    const D3 a4 = cvx_support(A, dir), v4 = a4 - ell_support(e, -dir);
+    if (dot(v4, dir) < 0.0 || reached(v4, dir)) return false;
+    expand(v4, a4);
+  }
+  if (it == 64) return false;
+  for (it = 0;; it++) {  // push the portal onto the boundary
+    dir = unit3(cross(v2 - v1, v3p - v1));
+    const D3 a4 = cvx_support(A, dir), v4 = a4 - ell_support(e, -dir);
+    if (reached(v4, dir) || it >= 64) break;
+    expand(v4, a4);
+  }
+  double lam[3];
+  cvx_tri(v1, v2, v3p, lam);
+  x = v1 * lam[0] + v2 * lam[1] + v3p * lam[2];
+  pa = a1 * lam[0] + a2 * lam[1] + a3 * lam[2];
+  return true;
+}
+
+// one contact between core A (+ radius rA) and the ellipsoid e (object frame): GJK when apart, MPR
+// when overlapping, the centre direction if MPR degenerates.  Normal from the object to A.
+__device__ __forceinline__ void cvx_contact(const CvxShape& A, double rA, D3 e, D3* pt, D3* nrm, double* d) {
+  D3 pa, pb, x;
+  double dist;
+  if (cvx_gjk(A, e, pa, pb, dist) && dist > 1e-9) {
+    *nrm = (pa - pb) * (1.0 / dist);
+    *pt = ((pa - *nrm * rA) + pb) * 0.5;
+    *d = dist - rA;
+    return;
+  }
+  if (cvx_mpr(A, e, x, pa)) {
+    const double l = sqrt(dot(x, x));
+    if (l > 1e-9) {
+      *nrm = x * (-1.0 / l);
+      *pt = (pa - x * 0.5) - *nrm * (rA * 0.5);
+      *d = -l - rA;
+      return;
+    }
+  }
+  const D3 ca = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
+  const double l = sqrt(dot(ca, ca));
+  *nrm = l > 1e-12 ? ca * (1.0 / l) : d3(0, 0, 1);
+  *pt = ca * 0.5;
+  *d = -rA;
+}
+
+}  // namespace mg

@@ -6,6 +6,7 @@
 //   quat_from_angle_axis / quat_conjugate   utils/torch_jit_utils.py:107-123
 //   scale / tensor_clamp / unscale          utils/torch_jit_utils.py:229-240
 //   randomize_rotation                      tasks/shadow_hand.py:803-806
+//   randomize_rotation_pen                  tasks/shadow_hand.py:810-813
 //   compute_hand_reward                     tasks/shadow_hand.py:746-800
 //   compute_full_state                      tasks/shadow_hand.py:528-584
 //   reset_target_pose / reset_idx           tasks/shadow_hand.py:586-668
@@ -143,6 +144,22 @@ __device__ __forceinline__ void h_randomize_rotation(float r0, float r1, float* 
   h_quat_from_angle_axis(r0 * pi, 0, qa);
   h_quat_from_angle_axis(r1 * pi, 1, qb);
   t_quat_mul(qa, qb, q);
+}
+
+// randomize_rotation_pen(rand0, rand1, max_angle = tensor(0.3), x, y, z) (shadow_hand.py:810-813); rand1 is
+// unused, as in the reference
+__device__ __forceinline__ void h_randomize_rotation_pen(float r0, float* q) {
+  const float pi = 3.14159265358979323846f;
+  float qa[4], qb[4];
+  h_quat_from_angle_axis((float)(0.5 * 3.14159265358979323846) + r0 * 0.3f, 0, qa);
+  h_quat_from_angle_axis(r0 * pi, 2, qb);
+  t_quat_mul(qa, qb, q);
+}
+
+// the object's reset orientation (shadow_hand.py:625-629): pen (ignore_z_rot) or generic
+__device__ __forceinline__ void h_object_reset_rotation(const mg_task_params& tp, float r0, float r1, float* q) {
+  if (tp.ignore_z_rot) h_randomize_rotation_pen(r0, q);
+  else h_randomize_rotation(r0, r1, q);
 }
 
 __device__ __forceinline__ float h_rand_pm1(float u) { return 2.0f * u + -1.0f; }

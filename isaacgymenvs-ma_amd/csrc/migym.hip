@@ -61,7 +61,7 @@ struct mg_sim {
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
-template <int T, int MN, int MC, int MG, int MP, bool OBJ, bool DR>
+template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
                                                      mg_state_views v, int n) {
   constexpr int E = kBlock / T;
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state
     for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 4 + k));
     float* ob = root + 13;
     for (int k = 0; k < 3; k++) ob[k] = tp.object_start[k] + tp.reset_position_noise * r[k];
-    mg::h_randomize_rotation(r[3], r[4], ob + 3);
+    mg::h_object_reset_rotation(tp, r[3], r[4], ob + 3);
     for (int k = 7; k < 13; k++) ob[k] = 0.0f;
     float* dof = v.dof_state + (size_t)2 * nd * e;
     for (int j = 0; j < nd; j++) {
@@ -558,12 +558,12 @@ __global__ void k_hand_finalize(mg_task_params tp, mg_task_buffers tb) {
 // The whole ShadowHand VecTask.step for one env, fused: pre_physics_step (masked goal / env resets,
 // PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
 // the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
-template <int T, int MN, int MC, int MG, int MP, bool DR>
+template <int T, int MN, int MC, int MG, int MP, int OT, bool DR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
                                                       mg_task_params tp, mg_state_views v, mg_task_buffers tb,
                                                       int n) {
   constexpr int E = kBlock / T;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, true>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::load_tile(&tile, m);
@@ -574,8 +574,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
-  mg::TeamLDS<T, MN, MC, true>& L = lds[team].v;
-  mg::Team<T, MN, MC, MG, MP, true> t;
+  mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
+  mg::Team<T, MN, MC, MG, MP, OT> t;
   t.init(&L, &tile, m, &p);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       float r[5];
       for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 4 + k));
       for (int k = 0; k < 3; k++) L.oroot[k] = tp.object_start[k] + tp.reset_position_noise * r[k];
-      mg::h_randomize_rotation(r[3], r[4], L.oroot + 3);
+      mg::h_object_reset_rotation(tp, r[3], r[4], L.oroot + 3);
       for (int k = 7; k < 13; k++) L.oroot[k] = 0.0f;
     } else {
       for (int k = 0; k < 13; k++) L.oroot[k] = root[13 + k];
@@ -885,11 +885,13 @@ __global__ __launch_bounds__(kBlock) void k_dr_noise(mg_dr_noise_args a) {
 
 // ------------------------------------------------------------------------------------------------ dispatch
 // Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
-// contacts MC, geoms MG, self pairs MP, OBJ = hand-task envs with a free object.  The smallest
+// contacts MC, geoms MG, self pairs MP, OBJ = the free object's type in hand-task envs (0: none; one
+// instance per object shape, so the block's kernel carries no egg / pen code).  The smallest
 // instance that fits the model is launched.
 #define MG_INSTANCES(X)                                                                                     \
   X(8, 4, 8, 4, 0, false) X(16, 9, 16, 16, 0, false) X(16, 16, 24, 24, 32, false) X(32, 24, 32, 24, 160, false) \
-  X(32, 32, 48, 48, 192, false) X(64, 40, 48, 48, 192, false) X(32, 25, 24, 24, 0, true)
+  X(32, 32, 48, 48, 192, false) X(64, 40, 48, 48, 192, false) X(32, 25, 24, 24, 0, MG_GT_BOX)               \
+  X(32, 25, 24, 24, 0, MG_GT_CAPSULE) X(32, 25, 24, 24, 0, MG_GT_ELLIPSOID)
 
 static int model_lanes(const mg_model& m) {
   const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs + (m.obj_type ? 6 : 0);
@@ -897,7 +899,7 @@ static int model_lanes(const mg_model& m) {
 }
 #define MG_FITS(T, MN, MC, MG, MP, OBJ)                                                                    \
   (m.num_nodes <= MN && max_contacts <= MC && model_lanes(m) <= T && (m.fixed_base || T >= 6) &&        \
-   m.num_geoms <= MG && m.num_pairs <= MP && (m.obj_type != 0) == OBJ)
+   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ))
 
 // team size the dispatcher picks for a model (0: none fits)
 static int team_size(const mg_model& m, int max_contacts) {
@@ -908,7 +910,7 @@ static int team_size(const mg_model& m, int max_contacts) {
   return 0;
 }
 
-template <template <int, int, int, int, int, bool> class F, typename... A>
+template <template <int, int, int, int, int, int> class F, typename... A>
 static int dispatch(const mg_model& m, int max_contacts, A... args) {
 #define MG_TRY(T, MN, MC, MG, MP, OBJ)             \
   if (MG_FITS(T, MN, MC, MG, MP, OBJ)) {           \
@@ -919,7 +921,7 @@ static int dispatch(const mg_model& m, int max_contacts, A... args) {
   return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
 }
 
-template <int T, int MN, int MC, int MG, int MP, bool OBJ>
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
 struct RunSimulate {
   static int run(hipStream_t s, const mg_sim* sim) {
     const int E = kBlock / T;
@@ -933,7 +935,7 @@ struct RunSimulate {
     return MG_OK;
   }
 };
-template <int T, int MN, int MC, int MG, int MP, bool OBJ>
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
 struct RunEnvStep {
   static int run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
     const int E = kBlock / T;
@@ -948,10 +950,10 @@ struct RunEnvStep {
       mg::h_fill_maps(&tpm);
       tp = &tpm;
       if (sim->views.env_props)
-        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                            sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
       else
-        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
                            sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
       hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, s, *tp, *tb);
     } else {

@@ -30,6 +30,7 @@
 // articulation lanes + the box's closed-form inverse inertia on the object lanes).
 #pragma once
 #include "../../include/migym.h"
+#include "convex.hpp"
 #include "device_math.hpp"
 
 #include <type_traits>
@@ -130,7 +131,7 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
 #endif
 
-template <int T, int MN, int MC, bool OBJ = false>
+template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + MG_PGS_PREFETCH - 1) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;
@@ -361,7 +362,7 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
 }
 
 // Per-lane context of one team.
-template <int T, int MN, int MC, int MG, int MP, bool OBJ = false>
+template <int T, int MN, int MC, int MG, int MP, int OBJ = 0>  // OBJ: the free object's type (0: none)
 struct Team {
   using L = TeamLDS<T, MN, MC, OBJ>;
   using MT = ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>;
@@ -978,6 +979,91 @@ struct Team {
     return true;
   }
 
+  // object-contact candidates of an articulation geom of type ty (oracle obj_candidates): block
+  // sphere/capsule 1, box 16 (vertex tests both ways); pen sphere/capsule 1 (segment-segment), box 3
+  // (closest point + the two ends); egg 1 (GJK / MPR)
+  __device__ int ocand_count(int ty) const {
+    const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
+    if (!round && ty != MG_GT_BOX) return 0;
+    constexpr int ot = OBJ;
+    if (ot == MG_GT_BOX) return round ? 1 : 16;
+    if (ot == MG_GT_CAPSULE) return round ? 1 : 3;
+    return 1;
+  }
+  // bounding radius of the object (broadphase cull)
+  __device__ float obj_radius() const {
+    const V3 e = osize();
+    constexpr int ot = OBJ;
+    if (ot == MG_GT_BOX) return sqrtf(dot(e, e));
+    if (ot == MG_GT_CAPSULE) return e.x + e.y;
+    return fmaxf(e.x, fmaxf(e.y, e.z));
+  }
+  // candidate q of geom g against the pen / egg (oracle geom_object_convex); false = no candidate
+  __device__ bool obj_candidate_convex(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
+    const V3 os = osize();
+    const int ty = mt->gtype[g];
+    const float* gs = mt->gf[g] + 12;
+    const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
+    if constexpr (OBJ == MG_GT_ELLIPSOID) {
+      CvxShape A;  // fp64 from here (convex.hpp)
+      float r = 0.0f;
+      if (round) {
+        const float hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
+        const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
+        A.kind = 0;
+        A.p0 = d3(mulT(oR, (c - ax) - op));
+        A.p1 = d3(mulT(oR, (c + ax) - op));
+        r = gs[0];
+      } else {
+        A.kind = 1;
+        A.c = d3(mulT(oR, c - op));
+        M3 Rt;
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) Rt.m[a][b] = oR.m[b][a];
+        const M3 Rl = mul(Rt, Rg);
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) A.R[a][b] = Rl.m[a][b];
+        A.h = d3(gs[0], gs[1], gs[2]);
+      }
+      D3 pl, nl;
+      double dd;
+      cvx_contact(A, r, d3(os), &pl, &nl, &dd);
+      *dist = (float)dd;
+      *pt = mul(oR, f3(pl)) + op;
+      *nrm = mul(oR, f3(nl));
+      return true;
+    }
+    // pen: capsule of radius os.x along the object's z, half length os.y
+    const float ro = os.x;
+    const V3 oz = v3(oR.m[0][2], oR.m[1][2], oR.m[2][2]) * os.y;
+    const V3 p0 = op - oz, p1 = op + oz;
+    if (round) {
+      const float hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f, r = gs[0];
+      const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
+      const V3 a0 = c - ax, a1 = c + ax;
+      float ss, tt;
+      closest_seg_seg_t(a0, a1, p0, p1, &ss, &tt);
+      const V3 pa = a0 + (a1 - a0) * ss, pb = p0 + (p1 - p0) * tt, dv = pa - pb;
+      const float dl = sqrtf(dot(dv, dv));
+      if (!(dl > 1e-9f)) return false;
+      *nrm = dv * (1.0f / dl);
+      *pt = ((pa - *nrm * r) + (pb + *nrm * ro)) * 0.5f;
+      *dist = dl - r - ro;
+      return true;
+    }
+    const V3 hg = v3(gs[0], gs[1], gs[2]);
+    const V3 P0 = mulT(Rg, p0 - c), u = mulT(Rg, p1 - p0);
+    const float ts = seg_box_t(P0, u, hg);
+    if ((q == 1 && ts < 0.01f) || (q == 2 && ts > 0.99f)) return false;
+    const float t = q == 0 ? ts : (q == 1 ? 0.0f : 1.0f);
+    const V3 P = P0 + u * t;
+    V3 nb, cb;
+    *dist = point_box(P, hg, &nb, &cb) - ro;
+    *pt = mul(Rg, ((P - nb * ro) + cb) * 0.5f) + c;
+    *nrm = mul(Rg, nb) * -1.0f;
+    return true;
+  }
+
   __device__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
     s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
     s->cn[slot][0] = n.x; s->cn[slot][1] = n.y; s->cn[slot][2] = n.z;
@@ -1050,19 +1136,31 @@ struct Team {
         }
       }
     }
-    if (OBJ && m->obj_type == MG_GT_BOX) {  // the object's corners on the ground: lane per corner
+    if constexpr (OBJ != 0) {  // the object on the ground: lane per corner (block), end sphere (pen), or
+                               // the egg's support point in -z
       int cnt = 0;
       V3 e = v3(0, 0, 0);
-      if (tl < 8) {
-        const V3 hb = osize();
+      float r = 0.0f;
+      constexpr int ot = OBJ;
+      const V3 hb = osize();
+      if (ot == MG_GT_BOX && tl < 8) {
         e = mul(oR, v3((tl & 1 ? 1.f : -1.f) * hb.x, (tl & 2 ? 1.f : -1.f) * hb.y, (tl & 4 ? 1.f : -1.f) * hb.z)) + op;
-        cnt = e.z < off ? 1 : 0;
+        cnt = 1;
+      } else if (ot == MG_GT_CAPSULE && tl < 2) {
+        e = mul(oR, v3(0.0f, 0.0f, (tl == 0 ? -1.f : 1.f) * hb.y)) + op;
+        r = hb.x;
+        cnt = 1;
+      } else if (ot == MG_GT_ELLIPSOID && tl == 0) {
+        e = mul(oR, f3(ell_support(d3(hb), d3(-oR.m[2][0], -oR.m[2][1], -oR.m[2][2])))) + op;
+        cnt = 1;
       }
+      const float d = e.z - r;
+      cnt = cnt && d < off ? 1 : 0;
       const int incl = team_incl_scan<T>(cnt);
       const int tot = __shfl(incl, tb + T - 1);
       if (cnt) {
         const int slot = base + incl - 1;
-        if (slot < cap) put_contact(slot, e, v3(0, 0, 1), e.z, OBJ_NODE, -2, -1, -1);
+        if (slot < cap) put_contact(slot, v3(e.x, e.y, e.z - r), v3(0, 0, 1), d, OBJ_NODE, -2, -1, -1);
       }
       base += tot;
     }
@@ -1105,11 +1203,11 @@ struct Team {
       }
       base += tot;
     }
-    if (OBJ && m->obj_type == MG_GT_BOX) {
+    if constexpr (OBJ != 0) {
       // articulation geoms vs the object: one lane per (geom, candidate) in geom order (the oracle's
       // emission order); a candidate whose geom's bounding sphere cannot come within the contact
       // offset of the object's is skipped (conservative: the same contacts)
-      const float ro = sqrtf(dot(osize(), osize()));
+      const float ro = obj_radius();
       // pass 1, lane per geom: bounding-sphere cull of the whole geom (its centre only: R . pos + x);
       // the survivors' candidates are then enumerated densely, so culled boxes cost no lanes
       unsigned long long live = 0ull;
@@ -1127,7 +1225,7 @@ struct Team {
         live |= ((b >> tb) & (T >= 64 ? ~0ull : ((1ull << T) - 1ull))) << g0;
       }
       int NC = 0;
-      for (unsigned long long mm = live; mm; mm &= mm - 1) NC += mt->gtype[__builtin_ctzll(mm)] == MG_GT_BOX ? 16 : 1;
+      for (unsigned long long mm = live; mm; mm &= mm - 1) NC += ocand_count(mt->gtype[__builtin_ctzll(mm)]);
       for (int f0 = 0; f0 < NC; f0 += T) {
         const int f = f0 + tl;
         int cnt = 0, g = 0;
@@ -1138,15 +1236,17 @@ struct Team {
           int q = f;
           for (unsigned long long mm = live; mm; mm &= mm - 1) {
             g = __builtin_ctzll(mm);
-            const int n = mt->gtype[g] == MG_GT_BOX ? 16 : 1;
+            const int n = ocand_count(mt->gtype[g]);
             if (q < n) break;
             q -= n;
           }
           V3 c;
           M3 Rg;
           geom_staged(g, &c, &Rg);
-          obj_candidate(g, q, c, Rg, &pt, &nrm, &d);
-          cnt = d < off ? 1 : 0;
+          bool ok;
+          if constexpr (OBJ == MG_GT_BOX) ok = obj_candidate(g, q, c, Rg, &pt, &nrm, &d);
+          else ok = obj_candidate_convex(g, q, c, Rg, &pt, &nrm, &d);
+          cnt = ok && d < off ? 1 : 0;
         }
         const int incl = team_incl_scan<T>(cnt);
         const int tot = __shfl(incl, tb + T - 1);

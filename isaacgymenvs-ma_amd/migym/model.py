@@ -48,9 +48,9 @@ MAX_TENDONS = 8
 COLLIDE_GROUND, COLLIDE_OBJECT = 1, 2
 
 JT_FREE, JT_FIXED, JT_HINGE, JT_SLIDE = 0, 1, 2, 3
-GT_PLANE, GT_SPHERE, GT_CAPSULE, GT_BOX, GT_CYLINDER = 0, 1, 2, 3, 4
+GT_PLANE, GT_SPHERE, GT_CAPSULE, GT_BOX, GT_CYLINDER, GT_ELLIPSOID = 0, 1, 2, 3, 4, 5
 _GEOM_TYPES = {"plane": GT_PLANE, "sphere": GT_SPHERE, "capsule": GT_CAPSULE, "box": GT_BOX,
-               "cylinder": GT_CYLINDER}
+               "cylinder": GT_CYLINDER, "ellipsoid": GT_ELLIPSOID}
 
 
 # ---------------------------------------------------------------------------------------------
@@ -248,6 +248,10 @@ def geom_mass_inertia(gtype, size, density):
         x, y, z = size
         m = density * 8 * x * y * z
         return m, np.diag([m * (y * y + z * z) / 3, m * (x * x + z * z) / 3, m * (x * x + y * y) / 3])
+    if gtype == GT_ELLIPSOID:
+        a, b, c = size
+        m = density * 4.0 / 3.0 * math.pi * a * b * c
+        return m, np.diag([m * (b * b + c * c) / 5, m * (a * a + c * c) / 5, m * (a * a + b * b) / 5])
     if gtype == GT_CYLINDER:
         r, hl = size[0], size[1]
         h = 2 * hl
@@ -841,3 +845,14 @@ ASSET_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
 def load_builtin(name) -> ModelSpec:
     """Load one of the shipped model tables (generated by tools/build_models.py)."""
     return ModelSpec.from_json(os.path.join(ASSET_DIR, name + ".json"))
+
+
+def hand_object(kind: str) -> Dict:
+    """The free object of ShadowHand's objectType (shadow_hand.py:86-100): block = cube_multicolor.urdf,
+    egg = open_ai_assets/hand/egg.xml (ellipsoid), pen = open_ai_assets/hand/pen.xml (capsule).  Shipped
+    as migym/assets/hand_objects.json (tools/build_models.py)."""
+    with open(os.path.join(ASSET_DIR, "hand_objects.json")) as f:
+        objs = json.load(f)
+    if kind not in objs:
+        raise ValueError(f"objectType must be one of {sorted(objs)}, got {kind!r}")
+    return dict(objs[kind])

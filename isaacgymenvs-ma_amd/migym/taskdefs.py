@@ -72,14 +72,24 @@ def agent_offsets(A: int, spacing: float):
     return out
 
 
+def hand_spec(object_type: str = "block") -> M.ModelSpec:
+    """The ShadowHand model table with the free object of ``objectType`` (shadow_hand.py:86-100, 229-232)."""
+    spec = M.load_builtin("shadow_hand")
+    spec.obj = M.hand_object(object_type)
+    return spec
+
+
 def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     """ShadowHand constants (shadow_hand.py:46-118, 220-330)."""
     env = cfg["env"]
     obs_type = env.get("observationType", "full_state")
     if obs_type not in HAND_OBS:
         raise ValueError(f"Unknown type of observations! observationType should be one of: {sorted(HAND_OBS)}")
-    if env.get("objectType", "block") != "block":
-        raise ValueError("objectType must be 'block' (egg/pen meshes are out of scope)")
+    object_type = env.get("objectType", "block")
+    if object_type not in ("block", "egg", "pen"):   # shadow_hand.py:86-87
+        raise ValueError(f"objectType must be one of block, egg, pen, got {object_type!r}")
+    if spec.obj is None or spec.obj["type"] != M.hand_object(object_type)["type"]:
+        raise ValueError(f"model's object does not match objectType {object_type!r} (use taskdefs.hand_spec)")
     tp = _abi.TaskParams()
     tp.task_id = _abi.MG_TASK_SHADOW_HAND
     tp.num_agents = 1
@@ -103,7 +113,7 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
         tp.fingertip_body[i] = b
     tp.max_consecutive_successes = int(env.get("maxConsecutiveSuccesses", 0))
     tp.use_relative_control = int(bool(env.get("useRelativeControl", False)))
-    tp.ignore_z_rot = 0
+    tp.ignore_z_rot = int(object_type == "pen")   # shadow_hand.py:89, 421; also selects randomize_rotation_pen
     tp.dof_speed_scale = float(env["dofSpeedScale"])
     tp.act_moving_average = float(env["actionsMovingAverage"])
     tp.dist_reward_scale = float(env["distRewardScale"])
@@ -123,7 +133,7 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     # hand at (0, 0, 0.5); object at hand + (0, -0.39, 0.10); goal = object - 0.04 z, drawn displaced
     tp.start_pos[:] = (0.0, 0.0, 0.5)
     tp.start_rot[:] = (0.0, 0.0, 0.0, 1.0)
-    tp.object_start[:] = (0.0, 0.0 + -0.39, 0.5 + 0.10)
+    tp.object_start[:] = (0.0, 0.0 + -0.39, 0.5 + (0.02 if object_type == "pen" else 0.10))  # :315-318
     tp.goal_displacement[:] = (-0.2, -0.06, 0.12)
     tp.goal_dz = -0.04
     # asymmetric actor-critic: states_buf (N, 211) = compute_full_state(asymm_obs=True) (shadow_hand.py:125-131)

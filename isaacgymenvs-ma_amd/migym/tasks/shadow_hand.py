@@ -1,7 +1,7 @@
 """ShadowHand in-hand cube reorientation on the MI355X path.
 
-Reference counterpart: tasks/shadow_hand.py (ShadowHand, full_state 211-d
-observations, 20 actions, 24 DOFs, block object).  pre_physics_step (masked goal /
+Reference counterpart: tasks/shadow_hand.py (ShadowHand, every observationType,
+20 actions, 24 DOFs, objectType block / egg / pen).  pre_physics_step (masked goal /
 env resets and PD targets, :670-698), the physics (PD drives, tendons, hand-cube
 contacts), compute_full_state (:528-584) and compute_hand_reward (:746-800) run in
 the fused ``mg_env_step`` kernel (csrc/hand_task.hpp, team_physics.hpp); the global
@@ -50,7 +50,7 @@ class ShadowHand(VecTask):
     # ---------------------------------------------------------------------------------- setup
     def create_sim(self):
         _, table, _, _, _, max_contacts = taskdefs.TASK_INFO["ShadowHand"]
-        spec = M.load_builtin(table)
+        spec = taskdefs.hand_spec(self.object_type)   # block / egg / pen object (shadow_hand.py:86-100)
         self.model_spec = spec
         self.num_dof = self.num_shadow_hand_dofs = spec.num_dofs
         self.num_shadow_hand_bodies = len(spec.bodies)

@@ -52,6 +52,9 @@ int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float
  * (node, px,py,pz, nx,ny,nz, depth, nodeB) records of 9 doubles */
 int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, double* out,
                  int32_t cap);
+/* egg narrowphase KAT hook (GJK + shrunk-core retry): kind 0 segment p0,p1 / kind 1 box c, R (row-major),
+ * h, plus radius, vs the origin-centred ellipsoid e; out = point(3), normal(3), distance */
+int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, const double* e, double* out);
 /* world poses of the gym rigid bodies (n_bodies x 13, velocity at body COM) */
 int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out);
 

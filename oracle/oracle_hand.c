@@ -66,6 +66,21 @@ void orc_randomize_rotation(float r0, float r1, float* q) {
   h_quat_mul(qa, qb, q);
 }
 
+/* randomize_rotation_pen(rand0, rand1, max_angle = tensor(0.3), x, y, z) (shadow_hand.py:810-813): rand1 is
+ * unused, as in the reference */
+static void randomize_rotation_pen(float r0, float* q) {
+  float qa[4], qb[4];
+  h_quat_from_angle_axis((float)(0.5 * 3.14159265358979323846) + r0 * 0.3f, 0, qa);
+  h_quat_from_angle_axis(r0 * PI_F, 2, qb);
+  h_quat_mul(qa, qb, q);
+}
+
+/* the object's reset orientation (shadow_hand.py:625-629): pen (ignore_z_rot) or generic */
+static void object_reset_rotation(const mg_task_params* tp, float r0, float r1, float* q) {
+  if (tp->ignore_z_rot) randomize_rotation_pen(r0, q);
+  else orc_randomize_rotation(r0, r1, q);
+}
+
 /* per-env part of compute_hand_reward; returns the updated successes etc. through pointers */
 static void hand_reward_one(const mg_task_params* tp, float max_episode_length, const float* opos, const float* orot,
                             const float* tpos, const float* trot, const float* act, int64_t reset_in,
@@ -198,7 +213,7 @@ int orc_hand_pre_physics(const mg_model* m, const mg_task_params* tp, const mg_s
       ob[0] = tp->object_start[0] + tp->reset_position_noise * r[0];
       ob[1] = tp->object_start[1] + tp->reset_position_noise * r[1];
       ob[2] = tp->object_start[2] + tp->reset_position_noise * r[2];
-      orc_randomize_rotation(r[3], r[4], ob + 3);
+      object_reset_rotation(tp, r[3], r[4], ob + 3);
       for (int k = 7; k < 13; k++) ob[k] = 0.0f;
       float* dof = v->dof_state + (size_t)2 * nd * e;
       for (int j = 0; j < nd; j++) {

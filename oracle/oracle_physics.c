@@ -39,6 +39,8 @@
 #define OBJ_NODE (-2) /* contact side on the free object */
 #define MAXC 64
 #define MAXR (3 * MAXC + 2 * MG_MAX_NODES)
+#define MPR_TOL 1e-10 /* portal reached the boundary (m) */
+#define MPR_EPS 1e-12 /* origin-side tests */
 
 typedef double v3[3];
 
@@ -635,6 +637,413 @@ static int geom_object(const mg_model* m, const kin* k, int g, double off, conta
   return n;
 }
 
+/* ---- convex narrowphase against the egg (ellipsoid) and the pen (capsule) objects ------------------
+ * (ShadowHand objectType egg / pen, shadow_hand.py:86-100: open_ai_assets/hand/egg.xml = ellipsoid
+ * 0.03 x 0.03 x 0.04, pen.xml = capsule r 0.008, half length 0.1).  Everything is evaluated in the
+ * object frame (object centred at the origin).  Hand-geom cores: a segment (sphere/capsule core, the
+ * radius is added afterwards) or a box.
+ *
+ * GJK distance (Gilbert-Johnson-Keerthi on the Minkowski difference A - B; closest point of the
+ * simplex by Voronoi-region tests; stop when |v|^2 - v.w <= 1e-10 |v|^2 + 1e-24, a repeated support
+ * point, no progress, or 64 iterations; fp64).  Overlapping cores (the simplex encloses the origin) go to
+ * MPR (below) for the penetration vector.  The HIP kernel
+ * (csrc/convex.hpp) runs the same algorithm in fp32. */
+typedef struct {
+  int kind;                    /* 0 segment [p0, p1], 1 box (c, R columns = axes, h) */
+  double p0[3], p1[3];
+  double c[3], R[3][3], h[3];
+} cvx_shape;
+
+static void cvx_support(const cvx_shape* A, const double* d, double* o) {
+  if (A->kind == 0) {
+    const double* s = dot3(A->p0, d) >= dot3(A->p1, d) ? A->p0 : A->p1;
+    for (int a = 0; a < 3; a++) o[a] = s[a];
+    return;
+  }
+  for (int a = 0; a < 3; a++) o[a] = A->c[a];
+  for (int k = 0; k < 3; k++) {
+    double dk = A->R[0][k] * d[0] + A->R[1][k] * d[1] + A->R[2][k] * d[2];
+    double s = dk >= 0 ? A->h[k] : -A->h[k];
+    for (int a = 0; a < 3; a++) o[a] += s * A->R[a][k];
+  }
+}
+
+/* support point of the ellipsoid x^2/e0^2 + y^2/e1^2 + z^2/e2^2 = 1 in direction d */
+static void ell_support(const double* e, const double* d, double* o) {
+  double q[3] = {e[0] * e[0] * d[0], e[1] * e[1] * d[1], e[2] * e[2] * d[2]};
+  double n = sqrt(q[0] * d[0] + q[1] * d[1] + q[2] * d[2]);
+  if (n < 1e-30) { o[0] = o[1] = o[2] = 0.0; return; }
+  for (int a = 0; a < 3; a++) o[a] = q[a] / n;
+}
+
+/* closest point of segment / triangle (Ericson, Real-Time Collision Detection 5.1.2 / 5.1.5) to the
+ * origin as barycentric weights */
+static void cvx_seg(const double* a, const double* b, double* lam) {
+  double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, den = dot3(ab, ab);
+  double t = den > 0 ? -dot3(a, ab) / den : 0.0;
+  t = t < 0 ? 0 : (t > 1 ? 1 : t);
+  lam[0] = 1 - t; lam[1] = t;
+}
+static void cvx_tri(const double* a, const double* b, const double* c, double* lam) {
+  double ab[3], ac[3];
+  for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; }
+  lam[0] = lam[1] = lam[2] = 0.0;
+  double d1 = -dot3(ab, a), d2 = -dot3(ac, a);
+  if (d1 <= 0 && d2 <= 0) { lam[0] = 1; return; }
+  double d3 = -dot3(ab, b), d4 = -dot3(ac, b);
+  if (d3 >= 0 && d4 <= d3) { lam[1] = 1; return; }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { double v = d1 / (d1 - d3); lam[0] = 1 - v; lam[1] = v; return; }
+  double d5 = -dot3(ab, c), d6 = -dot3(ac, c);
+  if (d6 >= 0 && d5 <= d6) { lam[2] = 1; return; }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); lam[0] = 1 - w; lam[2] = w; return; }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    lam[1] = 1 - w; lam[2] = w; return;
+  }
+  double den = va + vb + vc;
+  if (!(den > 0)) { double l2[2]; cvx_seg(a, b, l2); lam[0] = l2[0]; lam[1] = l2[1]; return; }
+  double v = vb / den, w = vc / den;
+  lam[0] = 1 - v - w; lam[1] = v; lam[2] = w;
+}
+
+/* closest point of the simplex W[0..n-1] to the origin; keeps the supporting vertices (W, P in
+ * place, order preserved), returns 1 if the origin lies inside a (non-degenerate) tetrahedron */
+static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double* lk) {
+  double lam[4] = {0, 0, 0, 0};
+  if (*n == 1) {
+    lam[0] = 1;
+  } else if (*n == 2) {
+    cvx_seg(W[0], W[1], lam);
+  } else if (*n == 3) {
+    cvx_tri(W[0], W[1], W[2], lam);
+  } else {
+    static const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}}; /* face + opposite */
+    double best = 1e300;
+    int any = 0;
+    for (int f = 0; f < 4; f++) {
+      const double *a = W[F[f][0]], *b = W[F[f][1]], *c = W[F[f][2]], *d = W[F[f][3]];
+      double ab[3], ac[3], ad[3], nf[3];
+      for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ad[k] = d[k] - a[k]; }
+      cross3(ab, ac, nf);
+      double sp = -dot3(nf, a), sd = dot3(nf, ad);
+      double sc = dot3(ab, ab) + dot3(ac, ac) + dot3(ad, ad);
+      int degenerate = sd * sd <= 1e-12 * sc * sc * sc;
+      if (!(sp * sd < 0) && !degenerate) continue;
+      any = 1;
+      double l3[3], q[3];
+      cvx_tri(a, b, c, l3);
+      for (int k = 0; k < 3; k++) q[k] = l3[0] * a[k] + l3[1] * b[k] + l3[2] * c[k];
+      double dq = dot3(q, q);
+      if (dq < best) {
+        best = dq;
+        lam[0] = lam[1] = lam[2] = lam[3] = 0;
+        lam[F[f][0]] = l3[0]; lam[F[f][1]] = l3[1]; lam[F[f][2]] = l3[2];
+      }
+    }
+    if (!any) return 1;
+  }
+  int m = 0;
+  v[0] = v[1] = v[2] = 0;
+  double Wn[4][3], Pn[4][3];
+  for (int i = 0; i < *n; i++) {
+    if (!(lam[i] > 0)) continue;
+    for (int k = 0; k < 3; k++) { v[k] += lam[i] * W[i][k]; Wn[m][k] = W[i][k]; Pn[m][k] = P[i][k]; }
+    lk[m++] = lam[i];
+  }
+  memcpy(W, Wn, sizeof(double) * 3 * m);
+  memcpy(P, Pn, sizeof(double) * 3 * m);
+  *n = m;
+  return 0;
+}
+
+/* GJK distance between core A and the ellipsoid e (origin-centred).  Returns 1 when separated, with
+ * the closest points pa (on A), pb (on the ellipsoid) and the distance; 0 when the cores overlap. */
+static int cvx_gjk(const cvx_shape* A, const double* e, double* pa, double* pb, double* dist) {
+  double W[4][3], P[4][3], v[3];
+  if (A->kind == 0) for (int a = 0; a < 3; a++) v[a] = 0.5 * (A->p0[a] + A->p1[a]);
+  else for (int a = 0; a < 3; a++) v[a] = A->c[a];
+  if (dot3(v, v) < 1e-20) { v[0] = 0; v[1] = 0; v[2] = 1; }
+  int n = 0;
+  double vv = dot3(v, v);
+  double lam[4] = {0, 0, 0, 0};
+  for (int it = 0; it < 64; it++) {
+    double nd[3] = {-v[0], -v[1], -v[2]}, a[3], b[3], w[3];
+    cvx_support(A, nd, a);
+    ell_support(e, v, b);
+    for (int k = 0; k < 3; k++) w[k] = a[k] - b[k];
+    if (n > 0 && vv - dot3(v, w) <= 1e-10 * vv + 1e-24) break;
+    int dup = 0;
+    for (int i = 0; i < n; i++) {
+      double dd[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
+      if (dot3(dd, dd) <= 1e-24) dup = 1;
+    }
+    if (dup) break;
+    for (int k = 0; k < 3; k++) { W[n][k] = w[k]; P[n][k] = a[k]; }
+    n++;
+    if (cvx_simplex(W, P, &n, v, lam)) return 0;
+    double vn = dot3(v, v);
+    if (vn <= 1e-20) return 0;
+    int stall = it > 0 && vn >= vv * (1.0 - 1e-14); /* v starts at the centre difference */
+    vv = vn;
+    if (stall) break;
+  }
+  /* closest points: the kept simplex's weights applied to its A-side support points */
+  for (int k = 0; k < 3; k++) {
+    pa[k] = 0;
+    for (int i = 0; i < n; i++) pa[k] += lam[i] * P[i][k];
+    pb[k] = pa[k] - v[k];
+  }
+  *dist = sqrt(vv);
+  return 1;
+}
+
+/* one contact between core A (+ radius rA) and the ellipsoid e, object frame: GJK, then the
+ * shrunk-core retry, then the centre-direction fallback (see above).  Normal from the object to A. */
+/* MPR penetration (Minkowski portal refinement, XenoCollide; fixed state: the interior point v0 and a
+ * portal triangle v1 v2 v3, each with its A-side support point) for cores known to overlap.  Returns
+ * 1 with the boundary point x of A - B nearest to where the refined portal meets the origin's side
+ * (penetration vector: moving A by -x separates the cores) and the A-side witness pa; 0 if the portal
+ * search degenerates. */
+static void mpr_support(const cvx_shape* A, const double* e, const double* d, double* w, double* a) {
+  double b[3], nd[3] = {-d[0], -d[1], -d[2]};
+  cvx_support(A, d, a);
+  ell_support(e, nd, b);
+  for (int k = 0; k < 3; k++) w[k] = a[k] - b[k];
+}
+static void v3sub(const double* a, const double* b, double* o) { for (int k = 0; k < 3; k++) o[k] = a[k] - b[k]; }
+static void v3unit(double* a) {
+  double l = sqrt(dot3(a, a));
+  if (l > 0) for (int k = 0; k < 3; k++) a[k] /= l;
+}
+static void v3cp(double* d, const double* s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
+static void mpr_portal_dir(double V[5][3], double* dir) {
+  double a[3], b[3];
+  v3sub(V[2], V[1], a);
+  v3sub(V[3], V[1], b);
+  cross3(a, b, dir);
+  v3unit(dir);
+}
+/* replace one portal vertex by v4 so that the portal keeps facing the origin ray */
+static void mpr_expand(double V[5][3], double Pa[5][3]) {
+  double c[3];
+  cross3(V[4], V[0], c);
+  int k;
+  if (dot3(V[1], c) > 0) k = dot3(V[2], c) > 0 ? 1 : 3;
+  else k = dot3(V[3], c) > 0 ? 2 : 1;
+  v3cp(V[k], V[4]);
+  v3cp(Pa[k], Pa[4]);
+}
+static int mpr_reached(double V[5][3], const double* dir) {
+  double d4 = dot3(V[4], dir);
+  double m = fmin(d4 - dot3(V[1], dir), fmin(d4 - dot3(V[2], dir), d4 - dot3(V[3], dir)));
+  return m <= MPR_TOL;
+}
+static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
+  double V[5][3], Pa[5][3], dir[3];
+  if (A->kind == 0) for (int a = 0; a < 3; a++) V[0][a] = 0.5 * (A->p0[a] + A->p1[a]);
+  else for (int a = 0; a < 3; a++) V[0][a] = A->c[a];
+  if (dot3(V[0], V[0]) < 1e-20) { V[0][0] = 1e-6; V[0][1] = 0; V[0][2] = 0; }
+  for (int k = 0; k < 3; k++) dir[k] = -V[0][k];
+  v3unit(dir);
+  mpr_support(A, e, dir, V[1], Pa[1]);
+  if (dot3(V[1], dir) <= 0) return 0;
+  cross3(V[0], V[1], dir);
+  if (dot3(dir, dir) <= 1e-24) { /* the origin lies on the segment v0 - v1 */
+    v3cp(x, V[1]);
+    v3cp(pa, Pa[1]);
+    return 1;
+  }
+  v3unit(dir);
+  mpr_support(A, e, dir, V[2], Pa[2]);
+  if (dot3(V[2], dir) <= 0) return 0;
+  double va[3], vb[3];
+  v3sub(V[1], V[0], va);
+  v3sub(V[2], V[0], vb);
+  cross3(va, vb, dir);
+  v3unit(dir);
+  if (dot3(dir, V[0]) > 0) {
+    double t[3];
+    v3cp(t, V[1]); v3cp(V[1], V[2]); v3cp(V[2], t);
+    v3cp(t, Pa[1]); v3cp(Pa[1], Pa[2]); v3cp(Pa[2], t);
+    for (int k = 0; k < 3; k++) dir[k] = -dir[k];
+  }
+  int it;
+  for (it = 0; it < 64; it++) { /* discover a portal the origin ray passes through */
+    mpr_support(A, e, dir, V[3], Pa[3]);
+    if (dot3(V[3], dir) <= 0) return 0;
+    double c[3];
+    cross3(V[1], V[3], c);
+    if (dot3(c, V[0]) < -MPR_EPS) {
+      v3cp(V[2], V[3]); v3cp(Pa[2], Pa[3]);
+    } else {
+      cross3(V[3], V[2], c);
+      if (dot3(c, V[0]) < -MPR_EPS) {
+        v3cp(V[1], V[3]); v3cp(Pa[1], Pa[3]);
+      } else {
+        break;
+      }
+    }
+    v3sub(V[1], V[0], va);
+    v3sub(V[2], V[0], vb);
+    cross3(va, vb, dir);
+    v3unit(dir);
+  }
+  if (it == 64) return 0;
+  for (it = 0; it < 64; it++) { /* refine until the portal encloses the origin */
+    mpr_portal_dir(V, dir);
+    if (dot3(V[1], dir) >= 0) break;
+    mpr_support(A, e, dir, V[4], Pa[4]);
+    if (dot3(V[4], dir) < 0 || mpr_reached(V, dir)) return 0;
+    mpr_expand(V, Pa);
+  }
+  if (it == 64) return 0;
+  for (it = 0;; it++) { /* push the portal onto the boundary */
+    mpr_portal_dir(V, dir);
+    mpr_support(A, e, dir, V[4], Pa[4]);
+    if (mpr_reached(V, dir) || it >= 64) break;
+    mpr_expand(V, Pa);
+  }
+  double lam[3];
+  cvx_tri(V[1], V[2], V[3], lam);
+  for (int k = 0; k < 3; k++) {
+    x[k] = lam[0] * V[1][k] + lam[1] * V[2][k] + lam[2] * V[3][k];
+    pa[k] = lam[0] * Pa[1][k] + lam[1] * Pa[2][k] + lam[2] * Pa[3][k];
+  }
+  return 1;
+}
+
+/* one contact between core A (+ radius rA) and the ellipsoid e, object frame: GJK when the cores are
+ * apart, MPR penetration when they overlap, the centre direction if MPR degenerates.  Normal from the
+ * object to A. */
+static void cvx_contact(const cvx_shape* A, double rA, const double* e, double* pt, double* nrm, double* d) {
+  double pa[3], pb[3], dist, x[3];
+  if (cvx_gjk(A, e, pa, pb, &dist) && dist > 1e-9) {
+    for (int a = 0; a < 3; a++) nrm[a] = (pa[a] - pb[a]) / dist;
+    for (int a = 0; a < 3; a++) pt[a] = 0.5 * ((pa[a] - nrm[a] * rA) + pb[a]);
+    *d = dist - rA;
+    return;
+  }
+  if (cvx_mpr(A, e, x, pa)) {
+    double l = sqrt(dot3(x, x));
+    if (l > 1e-9) {
+      for (int a = 0; a < 3; a++) {
+        nrm[a] = -x[a] / l;
+        pt[a] = pa[a] - 0.5 * x[a] - nrm[a] * rA * 0.5;
+      }
+      *d = -l - rA;
+      return;
+    }
+  }
+  double ca[3];
+  if (A->kind == 0) for (int a = 0; a < 3; a++) ca[a] = 0.5 * (A->p0[a] + A->p1[a]);
+  else for (int a = 0; a < 3; a++) ca[a] = A->c[a];
+  double l = sqrt(dot3(ca, ca));
+  if (l > 1e-12) for (int a = 0; a < 3; a++) nrm[a] = ca[a] / l;
+  else { nrm[0] = 0; nrm[1] = 0; nrm[2] = 1; }
+  for (int a = 0; a < 3; a++) pt[a] = 0.5 * ca[a];
+  *d = -rA;
+}
+
+/* number of object-contact candidates of an articulation geom (the HIP kernel enumerates the same) */
+static int obj_candidates(int otype, int gtype) {
+  const int round = gtype == MG_GT_SPHERE || gtype == MG_GT_CAPSULE;
+  if (!round && gtype != MG_GT_BOX) return 0;
+  if (otype == MG_GT_BOX) return round ? 1 : 16;
+  if (otype == MG_GT_CAPSULE) return round ? 1 : 3;
+  return 1; /* ellipsoid */
+}
+
+/* hand geom g (A) vs the egg / pen object (B); normal points from the object to the geom */
+static int geom_object_convex(const mg_model* m, const kin* k, int g, double off, contact* out, int n, int cap) {
+  const int nd = m->geom_node[g], ty = m->geom_type[g], ot = m->obj_type;
+  const double os[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
+  double c[3], R[3][3];
+  geom_world(m, k, g, c, R);
+  const int round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
+  if (!round && ty != MG_GT_BOX) return n;
+  double pw[3], nw[3];
+  if (ot == MG_GT_ELLIPSOID) {
+    cvx_shape A;
+    double r = 0.0;
+    if (round) {
+      double hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, aw[3], bw[3];
+      for (int a = 0; a < 3; a++) { aw[a] = c[a] - R[a][2] * hl; bw[a] = c[a] + R[a][2] * hl; }
+      A.kind = 0;
+      to_obj(k, aw, A.p0);
+      to_obj(k, bw, A.p1);
+      r = m->geom_size[g][0];
+    } else {
+      A.kind = 1;
+      to_obj(k, c, A.c);
+      double Rt[3][3];
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Rt[a][b] = k->oR[b][a];
+      matmul3(Rt, R, A.R);
+      for (int a = 0; a < 3; a++) A.h[a] = m->geom_size[g][a];
+    }
+    double pl[3], nl[3], d;
+    cvx_contact(&A, r, os, pl, nl, &d);
+    if (d < off) {
+      from_obj_pt(k, pl, pw);
+      from_obj_dir(k, nl, nw);
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+    return n;
+  }
+  /* pen: capsule of radius os[0] along the object's z, half length os[1] */
+  const double ro = os[0];
+  double p0[3], p1[3];
+  for (int a = 0; a < 3; a++) { p0[a] = k->op[a] - k->oR[a][2] * os[1]; p1[a] = k->op[a] + k->oR[a][2] * os[1]; }
+  if (round) {
+    double hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, r = m->geom_size[g][0], a0[3], a1[3];
+    for (int a = 0; a < 3; a++) { a0[a] = c[a] - R[a][2] * hl; a1[a] = c[a] + R[a][2] * hl; }
+    double s, t, pa[3], pb[3], dv[3];
+    closest_seg_seg(a0, a1, p0, p1, &s, &t);
+    for (int a = 0; a < 3; a++) {
+      pa[a] = a0[a] + s * (a1[a] - a0[a]);
+      pb[a] = p0[a] + t * (p1[a] - p0[a]);
+      dv[a] = pa[a] - pb[a];
+    }
+    double dist = sqrt(dot3(dv, dv)), d = dist - r - ro;
+    if (d < off && dist > 1e-9) {
+      for (int a = 0; a < 3; a++) {
+        nw[a] = dv[a] / dist;
+        pw[a] = 0.5 * ((pa[a] - nw[a] * r) + (pb[a] + nw[a] * ro));
+      }
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+    return n;
+  }
+  /* hand box vs the pen: the pen segment's closest point to the box, then its two ends (an end is
+   * skipped when the closest point is within 1 % of the segment from it) */
+  const double hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
+  double d0[3], P0[3], du[3], u[3];
+  for (int a = 0; a < 3; a++) { d0[a] = p0[a] - c[a]; du[a] = p1[a] - p0[a]; }
+  mattvec3(R, d0, P0);
+  mattvec3(R, du, u);
+  int inside;
+  const double ts = seg_box_t(P0, u, hg, &inside);
+  for (int q = 0; q < 3; q++) {
+    if ((q == 1 && ts < 0.01) || (q == 2 && ts > 0.99)) continue;
+    const double t = q == 0 ? ts : (q == 1 ? 0.0 : 1.0);
+    double P[3], nb[3], cb[3], pm[3];
+    for (int a = 0; a < 3; a++) P[a] = P0[a] + t * u[a];
+    const double d = point_box(P, hg, nb, cb) - ro;
+    if (d < off) {
+      for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - nb[a] * ro) + cb[a]);
+      matvec3(R, pm, pw);
+      for (int a = 0; a < 3; a++) pw[a] += c[a];
+      matvec3(R, nb, nw);
+      for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+  }
+  return n;
+}
+
 /* contact order (the HIP kernel emits the same list): ground contacts of the articulation's geoms
  * in geom order, the object's box corners on the ground, self-collision pairs in pair order, then
  * articulation geoms against the object in geom order */
@@ -672,6 +1081,18 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       from_obj_pt(k, l, e);
       n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
     }
+  } else if (m->obj_type == MG_GT_CAPSULE) { /* pen: its two end spheres */
+    for (int s = -1; s <= 1; s += 2) {
+      double l[3] = {0.0, 0.0, s * (double)m->obj_size[1]}, e[3];
+      from_obj_pt(k, l, e);
+      n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, m->obj_size[0], off);
+    }
+  } else if (m->obj_type == MG_GT_ELLIPSOID) { /* egg: its support point in -z */
+    const double es[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
+    double dl[3] = {-k->oR[2][0], -k->oR[2][1], -k->oR[2][2]}, sl[3], e[3];
+    ell_support(es, dl, sl);
+    from_obj_pt(k, sl, e);
+    n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
   }
   for (int pi = 0; pi < m->num_pairs; pi++) {
     int ga = m->pair[pi][0], gb = m->pair[pi][1];
@@ -692,9 +1113,11 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pt, nrm, d);
     }
   }
-  if (m->obj_type == MG_GT_BOX)
+  if (m->obj_type)
     for (int g = 0; g < m->num_geoms; g++)
-      if (m->geom_filter[g] & MG_COLLIDE_OBJECT) n = geom_object(m, k, g, off, out, n, cap);
+      if (m->geom_filter[g] & MG_COLLIDE_OBJECT)
+        n = m->obj_type == MG_GT_BOX ? geom_object(m, k, g, off, out, n, cap)
+                                     : geom_object_convex(m, k, g, off, out, n, cap);
   return n;
 }
 
@@ -1184,4 +1607,24 @@ int orc_rigid_body_states(const mg_model* m, const float* root13, const float* d
   load_state(m, root13, dof2, &s);
   body_states(m, &s, out);
   return m->num_bodies;
+}
+
+/* KAT hook: the egg narrowphase (cvx_contact) for core A against the origin-centred ellipsoid e.
+ * kind 0: shape = segment p0, p1 (6 doubles); kind 1: shape = box centre (3), axes R row-major (9),
+ * half extents (3).  out = contact point (3), normal from the ellipsoid to A (3), signed distance. */
+int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, const double* e, double* out) {
+  cvx_shape A;
+  memset(&A, 0, sizeof(A));
+  A.kind = kind;
+  if (kind == 0) {
+    for (int a = 0; a < 3; a++) { A.p0[a] = shape[a]; A.p1[a] = shape[3 + a]; }
+  } else {
+    for (int a = 0; a < 3; a++) {
+      A.c[a] = shape[a];
+      A.h[a] = shape[12 + a];
+      for (int b = 0; b < 3; b++) A.R[a][b] = shape[3 + 3 * a + b];
+    }
+  }
+  cvx_contact(&A, radius, e, out, out + 3, out + 6);
+  return MG_OK;
 }

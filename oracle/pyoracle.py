@@ -55,6 +55,7 @@ def lib():
         l.orc_hand_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
                                         C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32,
                                         C.c_int32]
+        l.orc_ellipsoid_contact.argtypes = [C.c_int32, P, C.c_double, P, P]
         l.orc_dr_apply.argtypes = [C.POINTER(_abi.DrApplyArgs)]
         l.orc_dr_noise.argtypes = [C.POINTER(_abi.DrNoiseArgs)]
         _lib = l
@@ -96,6 +97,15 @@ def contacts(model_np, sp, root13, dof2, cap=64):
     out = np.zeros(9 * cap)
     n = lib().orc_contacts(model_np.ctypes.data, C.byref(sp), p(f32(root13)), p(f32(dof2)), p(out), cap)
     return out[: 9 * n].reshape(n, 9)
+
+
+def ellipsoid_contact(kind, shape, radius, e):
+    """egg narrowphase (oracle cvx_contact): returns (point, normal, signed distance)"""
+    sh = np.ascontiguousarray(shape, dtype=np.float64).ravel()
+    ev = np.ascontiguousarray(e, dtype=np.float64)
+    out = np.zeros(7)
+    lib().orc_ellipsoid_contact(int(kind), p(sh), float(radius), p(ev), p(out))
+    return out[0:3], out[3:6], out[6]
 
 
 def rigid_body_states(model_np, root13, dof2, nbodies):

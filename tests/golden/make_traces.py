@@ -378,7 +378,7 @@ class FakeHandGym(FakeGym):
 
     def get_asset_rigid_body_count(self, a):
         # the hand MJCF has the articulation's bodies; the object and goal URDFs one body each
-        return len(self.spec["bodies"]) if str(a).endswith(".xml") else 1
+        return len(self.spec["bodies"]) if "shadow_hand" in str(a) else 1
 
     def get_asset_actuator_count(self, a):
         return len(self.spec["actuated"])
@@ -498,7 +498,7 @@ class _TorchRecorder:
 
 
 def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state", force_scale=0.0, asymmetric=False,
-                   force_prob_range=None):
+                   force_prob_range=None, object_type="block"):
     import importlib
     sys.path.insert(0, os.path.join(HERE, "..", "..", "isaacgymenvs-ma_amd"))
     from migym import model as M
@@ -519,6 +519,7 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state", force_scale=0.0, 
     cfg["env"]["observationType"] = obs_type
     cfg["env"]["forceScale"] = force_scale
     cfg["env"]["asymmetric_observations"] = asymmetric
+    cfg["env"]["objectType"] = object_type
     if force_prob_range is not None:
         cfg["env"]["forceProbRange"] = force_prob_range
     torch.manual_seed(0)
@@ -596,6 +597,7 @@ def run_shadowhand(N=32, T=8, ep_len=4, obs_type="full_state", force_scale=0.0, 
     res["init_force_prob"] = init_force_prob
     res["force_scale"] = torch.tensor(force_scale)
     res["object_mass"] = torch.tensor(0.070875)
+    res["object_type"] = np.array(object_type)
     return res
 
 
@@ -865,7 +867,7 @@ def main():
     # one task per process: vec_task keeps a process-global sim (vec_task.py:55-64)
     if which == "all":
         import subprocess
-        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces", "ant_dr"):
+        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces", "shadowhand_pen", "ant_dr"):
             subprocess.check_call([sys.executable, __file__, t])
         return
     if which == "ant":
@@ -881,6 +883,8 @@ def main():
     elif which == "shadowhand_forces":  # random object forces + asymmetric states (forceScale > 0)
         save("trace_shadowhand_forces.npz", run_shadowhand(N=32, T=8, ep_len=4, force_scale=2.0, asymmetric=True,
                                                                force_prob_range=[0.2, 0.8]))
+    elif which == "shadowhand_pen":  # objectType pen: randomize_rotation_pen resets, ignore_z_rot reward
+        save("trace_shadowhand_pen.npz", run_shadowhand(N=32, T=8, ep_len=4, object_type="pen"))
     elif which == "shadowhand_obs":  # the other observationType layouts, smaller traces
         for ot in ("full", "full_no_vel", "openai"):
             save(f"trace_shadowhand_{ot}.npz", run_shadowhand(N=16, T=4, ep_len=3, obs_type=ot))

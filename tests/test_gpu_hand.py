@@ -43,10 +43,15 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def setup(n=16):
+def setup(n=16, kind="block"):
     cfg = configs.task_config("ShadowHand", n)
-    spec = M.load_builtin("shadow_hand")
+    cfg["env"]["objectType"] = kind
+    spec = taskdefs.hand_spec(kind)
     return spec, taskdefs.sim_params(cfg, 24), taskdefs.task_params("ShadowHand", cfg, spec)
+
+
+# object drop below its reset pose that puts it on / just above the palm
+PALM_DZ = {"block": 0.07, "egg": 0.065, "pen": 0.012}
 
 
 class DevHandEnv:
@@ -138,8 +143,8 @@ def test_hand_task_layer_replays_reference_trace(lib, trace):
                                        rtol=1e-4, atol=1e-4)
 
 
-def hand_states(spec, tp, n, rng):
-    """Cube on / just above the palm with random orientation and twist, random hand pose and targets."""
+def hand_states(spec, tp, n, rng, dz=0.07, pen=False):
+    """Object on / just above the palm with random orientation and twist, random hand pose and targets."""
     h = O.HandHostEnv(tp, spec, n)
     lo = np.array([x.lower for x in spec.nodes[1:]])
     hi = np.array([x.upper for x in spec.nodes[1:]])
@@ -147,9 +152,17 @@ def hand_states(spec, tp, n, rng):
     h.dof[:, :, 1] = rng.normal(0, 0.5, (n, spec.num_dofs))
     h.targets[:] = lo + (hi - lo) * rng.uniform(0, 1, (n, spec.num_dofs))
     ob = h.root[:, 1]
-    ob[:, 0:3] = np.array(tp.object_start[:3]) + rng.normal(0, 0.01, (n, 3)) - np.array([0, 0, 0.07])
+    ob[:, 0:3] = np.array(tp.object_start[:3]) + rng.normal(0, 0.01, (n, 3)) - np.array([0, 0, dz])
     q = rng.normal(0, 1, (n, 4))
     ob[:, 3:7] = q / np.linalg.norm(q, axis=-1, keepdims=True)
+    if pen:   # lying across the palm as reset_idx places it (randomize_rotation_pen), 0-8 mm above rest,
+              # fingers near the zero pose (curled fingers would cut through a 0.2 m pen)
+        h.dof[:, :, 0] = np.clip(rng.normal(0, 0.05, (n, spec.num_dofs)), lo, hi)
+        r0 = rng.uniform(-1, 1, n)
+        ha, hz = 0.5 * (0.5 * np.pi + 0.02 * r0), 0.5 * np.pi * r0   # tilt within 0.02 rad
+        ob[:, 3:7] = np.stack([np.sin(ha) * np.cos(hz), -np.sin(ha) * np.sin(hz), np.cos(ha) * np.sin(hz),
+                               np.cos(ha) * np.cos(hz)], -1)
+        ob[:, 2] = tp.object_start[2] - dz + rng.uniform(0.0, 0.008, n)
     ob[:, 7:13] = rng.normal(0, 0.2, (n, 6))
     return h
 
@@ -162,11 +175,13 @@ def env_agreement(a, b, atol, rtol):
     return ok.mean()
 
 
-def test_hand_physics_step_matches_oracle(lib):
-    spec, sp, tp = setup()
+@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
+def test_hand_physics_step_matches_oracle(lib, kind):
+    """One simulate from random states; egg = GJK / MPR narrowphase, pen = capsule contacts."""
+    spec, sp, tp = setup(kind=kind)
     n = 256
     rng = np.random.default_rng(5)
-    h = hand_states(spec, tp, n, rng)
+    h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
     # applied object forces (LOCAL_SPACE) on half of the envs
     h.rb_forces[: n // 2, len(spec.bodies)] = rng.normal(0, 0.3, (n // 2, 3))
     e = DevHandEnv(h)
@@ -195,9 +210,11 @@ def test_hand_physics_step_matches_oracle(lib):
     assert max(ncon) >= 3
 
 
-def test_hand_fused_env_step_matches_oracle(lib):
-    """mg_env_step (the bench path) vs orc_hand_env_step over 3 control steps, device RNG resets."""
-    spec, sp, tp = setup()
+@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
+def test_hand_fused_env_step_matches_oracle(lib, kind):
+    """mg_env_step (the bench path) vs orc_hand_env_step over 3 control steps, device RNG resets (pen:
+    randomize_rotation_pen, ignore_z_rot success tolerance)."""
+    spec, sp, tp = setup(kind=kind)
     n = 192
     h = O.HandHostEnv(tp, spec, n)
     e = DevHandEnv(h)
@@ -361,4 +378,34 @@ def test_hand_make_asymmetric_with_forces():
     assert float(f[:, obj].abs().sum()) > 0 and float(f[:, :obj].abs().sum()) == 0.0
     p = env.random_force_prob
     assert float(p.min()) >= 0.1 - 1e-6 and float(p.max()) <= 0.5 + 1e-6
+    env.close()
+
+
+@pytest.mark.parametrize("kind", ["egg", "pen"])
+def test_hand_make_object_types(kind):
+    """make(..., objectType egg / pen) through the fused step: finite state, the object held near the hand,
+    pen resets with randomize_rotation_pen (axis near horizontal: |R e_z . e_z| = |cos(pi/2 + 0.3 r)| <= sin 0.3
+    at the reset, before contacts act)."""
+    import migym
+    n = 1024
+    cfg = configs.task_config("ShadowHand", n, sim_device=DEV)
+    cfg["env"]["objectType"] = kind
+    env = migym.make(seed=0, task="ShadowHand", num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                     cfg={"task": cfg})
+    assert env.model_spec.obj["type"] == (M.GT_ELLIPSOID if kind == "egg" else M.GT_CAPSULE)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    obs, rew, reset, extras = env.step(torch.zeros((n, 20), device=DEV))
+    obj = env.root_state_tensor.view(n, 3, 13)[:, 1]
+    if kind == "pen":   # every env reset on the first step
+        q = obj[:, 3:7]
+        zz = 1 - 2 * (q[:, 0] ** 2 + q[:, 1] ** 2)
+        assert float(zz.abs().mean()) <= float(np.sin(0.3))   # after one step of contact physics
+    for _ in range(20):
+        obs, rew, reset, extras = env.step(torch.rand((n, 20), device=DEV, generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    o = obs["obs"]
+    assert torch.isfinite(o).all() and torch.isfinite(rew).all()
+    obj = env.root_state_tensor.view(n, 3, 13)[:, 1]
+    assert torch.isfinite(obj).all() and float(obj[:, 7:13].abs().max()) < 100.0
+    assert float((obj[:, 2] > 0.2).float().mean()) > 0.8
     env.close()

@@ -169,11 +169,13 @@ def hand_trace_setup(d, n=16):
     forceScale / forceProbRange / asymmetric states with the fake gym's object mass."""
     cfg = configs.task_config("ShadowHand", n)
     cfg["env"]["observationType"] = str(d["obs_type"])
-    if "force_scale" in d:
+    if "force_scale" in d and float(d["force_scale"]) > 0:
         cfg["env"]["forceScale"] = float(d["force_scale"])
         cfg["env"]["forceProbRange"] = [0.2, 0.8]
         cfg["env"]["asymmetric_observations"] = d["states"].shape[-1] > 0
-    spec = M.load_builtin("shadow_hand")
+    if "object_type" in d:   # objectType pen: pen start pose, randomize_rotation_pen, ignore_z_rot
+        cfg["env"]["objectType"] = str(d["object_type"])
+    spec = taskdefs.hand_spec(cfg["env"].get("objectType", "block"))
     tp = taskdefs.task_params("ShadowHand", cfg, spec)
     tp.max_episode_length = int(d["episode_length"])
     if "object_mass" in d:
@@ -182,7 +184,7 @@ def hand_trace_setup(d, n=16):
 
 
 HAND_TRACES = ["trace_shadowhand.npz", "trace_shadowhand_full.npz", "trace_shadowhand_full_no_vel.npz",
-               "trace_shadowhand_openai.npz", "trace_shadowhand_forces.npz"]
+               "trace_shadowhand_openai.npz", "trace_shadowhand_forces.npz", "trace_shadowhand_pen.npz"]
 
 
 @pytest.mark.parametrize("trace", HAND_TRACES)

@@ -133,3 +133,132 @@ def test_tendon_couples_distal_joint():
     # reported force on FFJ0 = c0 f (last substep's state: within 2 %) - damping * qd
     np.testing.assert_allclose(h.dof_force[0, j0] + 0.1 * qd0, 0.00705 * f, rtol=2e-2)
     del q0, q1, qd1
+
+
+# ---------------------------------------------------------------------------------------------------
+# objectType egg / pen (shadow_hand.py:86-100): GJK / MPR narrowphase against the ellipsoid, capsule
+# contacts for the pen.  Brute-force references are dense surface samples (scipy KD-tree).
+
+def setup_object(kind, n=2):
+    cfg = configs.task_config("ShadowHand", n)
+    cfg["env"]["objectType"] = kind
+    spec = taskdefs.hand_spec(kind)
+    tp = taskdefs.task_params("ShadowHand", cfg, spec)
+    sp = taskdefs.sim_params(cfg, 24)
+    h = O.HandHostEnv(tp, spec, n)
+    return spec, tp, sp, M.pack_model(spec), h
+
+
+def _rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _ellipsoid_tree(e, nu=200):
+    from scipy.spatial import cKDTree
+    u, v = np.meshgrid(np.linspace(0, np.pi, nu), np.linspace(0, 2 * np.pi, 2 * nu))
+    s = np.stack([e[0] * np.sin(u) * np.cos(v), e[1] * np.sin(u) * np.sin(v), e[2] * np.cos(u)], -1)
+    return cKDTree(s.reshape(-1, 3))
+
+
+def test_egg_gjk_distance_matches_dense_samples():
+    e = np.array([0.03, 0.03, 0.04])
+    tree = _ellipsoid_tree(e)
+    rng = np.random.default_rng(0)
+    g = np.linspace(-1, 1, 21)
+    grid = np.stack(np.meshgrid(g, g, g), -1).reshape(-1, 3)
+    box_surface = grid[(np.abs(grid) == 1).any(1)]
+    seen = 0
+    for i in range(60):
+        if i % 2 == 0:   # capsule core (segment) of radius 0.004
+            p0 = rng.normal(size=3)
+            p0 *= rng.uniform(0.05, 0.08) / np.linalg.norm(p0)
+            p1 = p0 + rng.normal(0, 0.03, 3)
+            pts = p0 + np.linspace(0, 1, 1500)[:, None] * (p1 - p0)
+            pt, n, d = O.ellipsoid_contact(0, np.r_[p0, p1], 0.004, e)
+            r = 0.004
+        else:            # box
+            q = rng.normal(size=4)
+            R = _rot(q / np.linalg.norm(q))
+            hb = rng.uniform(0.005, 0.02, 3)
+            c = rng.normal(size=3)
+            c *= rng.uniform(0.055, 0.08) / np.linalg.norm(c)
+            pts = c + (box_surface * hb) @ R.T
+            pt, n, d = O.ellipsoid_contact(1, np.r_[c, R.ravel(), hb], 0.0, e)
+            r = 0.0
+        if (((pts / e) ** 2).sum(1) < 1).any():
+            continue
+        seen += 1
+        ref = tree.query(pts)[0].min() - r
+        # the samples' spacing bounds the reference error (~1e-4 m on the box faces)
+        assert abs(d - ref) < 1.5e-4, (i, d, ref)
+        assert abs(np.linalg.norm(n) - 1) < 1e-9
+        # the normal points from the egg towards the geom: the contact point moved along it leaves the egg
+        out = pt + n * (abs(d) + 1e-3)
+        assert ((out / e) ** 2).sum() > 1
+    assert seen >= 40
+
+
+def test_egg_mpr_penetration_is_a_separating_translation():
+    """Overlapping cores: moving the geom by the reported depth along the normal leaves it touching."""
+    e = np.array([0.03, 0.03, 0.04])
+    rng = np.random.default_rng(1)
+    checked = 0
+    for i in range(80):
+        q = rng.normal(size=4)
+        R = _rot(q / np.linalg.norm(q))
+        hb = rng.uniform(0.005, 0.02, 3)
+        c = rng.normal(size=3)
+        c *= rng.uniform(0.02, 0.045) / np.linalg.norm(c)
+        pt, n, d = O.ellipsoid_contact(1, np.r_[c, R.ravel(), hb], 0.0, e)
+        if d >= 0:
+            continue
+        checked += 1
+        _, _, d2 = O.ellipsoid_contact(1, np.r_[c - d * n, R.ravel(), hb], 0.0, e)
+        assert abs(d2) < 1e-5, (i, d, d2)
+    assert checked >= 30
+
+
+def _settle(kind, pos, quat, steps):
+    spec, tp, sp, mnp, h = setup_object(kind)
+    h.root[:, 1, 0:3] = pos
+    h.root[:, 1, 3:7] = quat
+    h.root[:, 1, 7:] = 0
+    for _ in range(steps):
+        h.simulate(mnp, sp)
+    return spec, sp, mnp, h
+
+
+def test_egg_and_pen_rest_on_the_ground():
+    """Away from the hand: the pen lies flat at its radius, the egg comes to rest touching the plane."""
+    s = np.sin(np.pi / 4)
+    _, sp, mnp, h = _settle("pen", (0.4, 0.4, 0.05), (s, 0, 0, s), 120)   # axis horizontal
+    obj = h.root[0, 1]
+    np.testing.assert_allclose(obj[2], 0.008, atol=5e-4)
+    assert np.abs(obj[7:13]).max() < 1e-2, obj
+    _, sp, mnp, h = _settle("egg", (0.4, 0.4, 0.06), (0, 0, 0, 1), 120)   # upright egg
+    obj = h.root[0, 1]
+    np.testing.assert_allclose(obj[2], 0.04, atol=5e-4)
+    assert np.abs(obj[7:10]).max() < 1e-2, obj
+    con = O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)
+    assert len(con) >= 1 and abs(con[-1][7]) < 5e-4
+
+
+def test_egg_and_pen_land_on_the_palm():
+    """Dropped from the reset pose: the pen comes to rest across the palm; the egg lands on the palm and
+    is held by hand contacts (a round object later rolls off the zero-pose hand, as a real egg would)."""
+    s = np.sin(np.pi / 4)
+    for kind, q, steps in (("pen", (s, 0, 0, s), 60), ("egg", (0, 0, 0, 1), 15)):
+        spec, tp, sp, mnp, h = setup_object(kind)
+        start = np.array(tp.object_start[:3])
+        _, sp, mnp, h = _settle(kind, start, q, steps)
+        obj = h.root[0, 1]
+        assert np.isfinite(obj).all()
+        assert 0.50 < obj[2] < 0.55, (kind, obj)
+        assert np.abs(obj[0:2] - start[:2]).max() < 0.02, (kind, obj)
+        con = O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)
+        assert sum(1 for c in con if c[8] == -2 and c[0] >= 0) >= 2, (kind, con)
+        if kind == "pen":
+            assert np.abs(obj[7:13]).max() < 0.05, obj

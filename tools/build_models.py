@@ -14,7 +14,13 @@ them from migym/assets/*.json.
              tendon limit_stiffness 30 / damping 0.1 on the four T_*J1c tendons, fingertip force
              sensors; the object keeps gym's default AssetOptions: angular_damping 0.5, gravity on).
             The forearm's convex collision mesh is replaced by its bounding box.
+  hand_objects.json  the free object of each ShadowHand objectType (shadow_hand.py:86-100):
+            block = urdf/objects/cube_multicolor.urdf, egg = mjcf/open_ai_assets/hand/egg.xml
+            (ellipsoid), pen = mjcf/open_ai_assets/hand/pen.xml (capsule along the body z); mass and
+            principal inertia from the geom at MJCF's default density 1000; the object body's own
+            MJCF pose is replaced by the actor pose (as the cube's URDF origin is).
 """
+import json
 import os
 import struct
 import sys
@@ -71,6 +77,21 @@ def shadow_hand():
     return hand
 
 
+def hand_objects(hand):
+    objs = {"block": hand.obj}
+    for kind in ("egg", "pen"):
+        root = ET.parse(os.path.join(REF, f"assets/mjcf/open_ai_assets/hand/{kind}.xml")).getroot()
+        body = next(b for b in root.iter("body") if b.get("name") == "object")
+        geom = body.find("geom")
+        gtype = M._GEOM_TYPES[geom.get("type")]
+        size = [float(x) for x in geom.get("size").split()]
+        size = (size + [0.0, 0.0])[:3]
+        mass, inertia = M.geom_mass_inertia(gtype, size, float(geom.get("density", "1000")))
+        objs[kind] = dict(type=gtype, size=size, mass=mass, inertia=[float(x) for x in np.diag(inertia)],
+                          lin_damping=0.0, ang_damping=0.5, gravity=1)
+    return objs
+
+
 def main():
     out = M.ASSET_DIR
     ant = M.load_mjcf(os.path.join(REF, "assets/mjcf/nv_ant.xml"), "ant")
@@ -83,6 +104,10 @@ def main():
     cp.to_json(os.path.join(out, "cartpole.json"))
     sh = shadow_hand()
     sh.to_json(os.path.join(out, "shadow_hand.json"))
+    objs = hand_objects(sh)
+    with open(os.path.join(out, "hand_objects.json"), "w") as f:
+        json.dump(objs, f, indent=1)
+    print("hand objects:", {k: (v["type"], v["size"], round(v["mass"], 5)) for k, v in objs.items()})
     for s in (ant, hum, cp, sh):
         print(f"{s.name}: nodes={len(s.nodes)} dofs={s.num_dofs} bodies={len(s.bodies)} geoms={len(s.geoms)} "
               f"pairs={len(s.pairs)} mass={s.total_mass():.4f} sensors={s.sensors}")
