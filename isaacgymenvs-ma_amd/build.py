@@ -6,6 +6,7 @@
 phase, read back by ``mg_debug_phase_cycles``) into migym/_lib/libmigym_timing.so; it is a
 profiling aid (tools/phase_timing.py), never the measured product.
 """
+import glob
 import os
 import subprocess
 import sys
@@ -13,8 +14,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "migym.hip")
 OUT = os.path.join(HERE, "migym", "_lib", "libmigym.so")
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("team_physics.hpp", "hand_task.hpp", "task.hpp", "device_math.hpp")] + [
-    os.path.join(HERE, "..", "include", "migym.h")]
+HEADERS = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hpp"))) + [os.path.join(HERE, "..", "include", "migym.h")]
 ARCH = os.environ.get("MIGYM_ARCH", "gfx950")
 
 

@@ -5,8 +5,11 @@
 //   * everything in the object frame (ellipsoid of semi-axes e centred at the origin);
 //   * shape A is a hand geom's core: a segment (sphere / capsule, radius added afterwards) or a box;
 //   * GJK distance on A - B: closest point of the simplex by Voronoi-region tests (Ericson 5.1.2,
-//     5.1.5, 5.1.6), stop on |v|^2 - v.w <= 1e-10 |v|^2 + 1e-24, a repeated support point, no progress
-//     or 64 iterations;
+//     5.1.5, 5.1.6), stop on |v|^2 - v.w <= 1e-8 |v|^2 + 1e-24, a repeated support point, no progress
+//     or 64 iterations; exit early once a separating plane is farther than the contact offset (such a
+//     candidate is no contact, so most broadphase survivors cost one or two support calls);
+//   * box cores are rounded by a 1 mm margin, so penetrations shallower than that (resting contacts)
+//     stay with GJK;
 //   * overlapping cores -> MPR (Minkowski portal refinement): a fixed five-point state (interior
 //     point, portal triangle, candidate), so nothing grows per lane the way an EPA polytope would;
 //     the penetration vector is the refined portal's point nearest the origin.
@@ -161,7 +164,7 @@ __device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, double*
 
 // GJK distance between core A and the origin-centred ellipsoid e: true when separated (closest
 // points pa on A, pb on the ellipsoid, distance), false when the cores overlap
-__device__ __forceinline__ bool cvx_gjk(const CvxShape& A, D3 e, D3& pa, D3& pb, double& dist) {
+__device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, double cut, D3& pa, D3& pb, double& dist) {
   D3 W[4], P[4];
   D3 v = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
   if (dot(v, v) < 1e-20) v = d3(0, 0, 1);
@@ -170,7 +173,12 @@ __device__ __forceinline__ bool cvx_gjk(const CvxShape& A, D3 e, D3& pa, D3& pb,
   double lam[4] = {0.0, 0.0, 0.0, 0.0};
   for (int it = 0; it < 64; it++) {
     const D3 a = cvx_support(A, -v), b = ell_support(e, v), w = a - b;
-    if (n > 0 && vv - dot(v, w) <= 1e-10 * vv + 1e-24) break;
+    const double vw = dot(v, w);
+    if (vw > 0.0 && vw * vw > vv * cut * cut) {  // separating plane farther than cut: no contact
+      dist = vw / sqrt(vv);
+      return 2;
+    }
+    if (n > 0 && vv - vw <= 1e-8 * vv + 1e-24) break;
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -182,9 +190,9 @@ __device__ __forceinline__ bool cvx_gjk(const CvxShape& A, D3 e, D3& pa, D3& pb,
     for (int i = 0; i < 4; i++)
       if (i == n) { W[i] = w; P[i] = a; }
     n++;
-    if (cvx_simplex(W, P, n, v, lam)) return false;
+    if (cvx_simplex(W, P, n, v, lam)) return 0;
     const double vn = dot(v, v);
-    if (vn <= 1e-20) return false;
+    if (vn <= 1e-20) return 0;
     const bool stall = it > 0 && vn >= vv * (1.0 - 1e-14);
     vv = vn;
     if (stall) break;
@@ -195,10 +203,11 @@ __device__ __forceinline__ bool cvx_gjk(const CvxShape& A, D3 e, D3& pa, D3& pb,
     if (i < n) pa = pa + P[i] * lam[i];
   pb = pa - v;
   dist = sqrt(vv);
-  return true;
+  return 1;
 }
 
-constexpr double MPR_TOL = 1e-10;   // portal reached the boundary (m)
+constexpr double MPR_TOL = 1e-7;   // portal reached the boundary (m)
+constexpr double CVX_MARGIN = 1e-3;  // rounding of box cores against the egg (m)
 constexpr double MPR_EPS = 1e-12;  // origin-side tests
 
 __device__ __forceinline__ D3 unit3(D3 a) {
@@ -279,11 +288,27 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
 
 // one contact between core A (+ radius rA) and the ellipsoid e (object frame): GJK when apart, MPR
 // when overlapping, the centre direction if MPR degenerates.  Normal from the object to A.
-__device__ __forceinline__ void cvx_contact(const CvxShape& A, double rA, D3 e, D3* pt, D3* nrm, double* d) {
+__device__ __forceinline__ void cvx_contact(CvxShape A, double rA, D3 e, double cut, D3* pt, D3* nrm,
+                                                      double* d) {
   D3 pa, pb, x;
   double dist;
-  if (cvx_gjk(A, e, pa, pb, dist) && dist > 1e-9) {
-    *nrm = (pa - pb) * (1.0 / dist);
+  if (A.kind == 1) {  // box cores rounded by CVX_MARGIN (see the oracle): resting contacts stay with GJK
+    const double mg = fmin(CVX_MARGIN, 0.5 * fmin(A.h.x, fmin(A.h.y, A.h.z)));
+    A.h = A.h - d3(mg, mg, mg);
+    rA += mg;
+  }
+  const int g = cvx_gjk(A, e, rA + cut, pa, pb, dist);
+  if (g == 2) {  // farther than rA + cut: only the (lower-bound) distance is meaningful
+    *d = dist - rA;
+    *nrm = d3(0, 0, 1);
+    *pt = d3(0, 0, 0);
+    return;
+  }
+  if (g && dist > 1e-9) {
+    // the egg's surface normal at its witness point (gradient of the implicit function): better
+    // conditioned than (pa - pb) / dist when the gap is small
+    const D3 gr = d3(pb.x / (e.x * e.x), pb.y / (e.y * e.y), pb.z / (e.z * e.z));
+    *nrm = gr * (1.0 / sqrt(dot(gr, gr)));
     *pt = ((pa - *nrm * rA) + pb) * 0.5;
     *d = dist - rA;
     return;

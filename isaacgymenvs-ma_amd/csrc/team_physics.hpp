@@ -1027,7 +1027,7 @@ struct Team {
       }
       D3 pl, nl;
       double dd;
-      cvx_contact(A, r, d3(os), &pl, &nl, &dd);
+      cvx_contact(A, r, d3(os), p->contact_offset, &pl, &nl, &dd);
       *dist = (float)dd;
       *pt = mul(oR, f3(pl)) + op;
       *nrm = mul(oR, f3(nl));

@@ -39,7 +39,8 @@
 #define OBJ_NODE (-2) /* contact side on the free object */
 #define MAXC 64
 #define MAXR (3 * MAXC + 2 * MG_MAX_NODES)
-#define MPR_TOL 1e-10 /* portal reached the boundary (m) */
+#define MPR_TOL 1e-7  /* portal reached the boundary (m) */
+#define CVX_MARGIN 1e-3 /* rounding of box cores against the egg (m) */
 #define MPR_EPS 1e-12 /* origin-side tests */
 
 typedef double v3[3];
@@ -644,8 +645,11 @@ static int geom_object(const mg_model* m, const kin* k, int g, double off, conta
  * radius is added afterwards) or a box.
  *
  * GJK distance (Gilbert-Johnson-Keerthi on the Minkowski difference A - B; closest point of the
- * simplex by Voronoi-region tests; stop when |v|^2 - v.w <= 1e-10 |v|^2 + 1e-24, a repeated support
- * point, no progress, or 64 iterations; fp64).  Overlapping cores (the simplex encloses the origin) go to
+ * simplex by Voronoi-region tests; stop when |v|^2 - v.w <= 1e-8 |v|^2 + 1e-24, a repeated support
+ * point, no progress, or 64 iterations; fp64; early exit once a separating plane is farther than the
+ * contact offset, since such a candidate is not a contact).  Box cores are rounded by a 1 mm margin
+ * (CVX_MARGIN: edges and corners of a hand box become 1 mm round; penetrations shallower than that
+ * stay with GJK).  Overlapping cores (the simplex encloses the origin) go to
  * MPR (below) for the penetration vector.  The HIP kernel
  * (csrc/convex.hpp) runs the same algorithm in fp32. */
 typedef struct {
@@ -761,7 +765,7 @@ static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double
 
 /* GJK distance between core A and the ellipsoid e (origin-centred).  Returns 1 when separated, with
  * the closest points pa (on A), pb (on the ellipsoid) and the distance; 0 when the cores overlap. */
-static int cvx_gjk(const cvx_shape* A, const double* e, double* pa, double* pb, double* dist) {
+static int cvx_gjk(const cvx_shape* A, const double* e, double cut, double* pa, double* pb, double* dist) {
   double W[4][3], P[4][3], v[3];
   if (A->kind == 0) for (int a = 0; a < 3; a++) v[a] = 0.5 * (A->p0[a] + A->p1[a]);
   else for (int a = 0; a < 3; a++) v[a] = A->c[a];
@@ -774,7 +778,12 @@ static int cvx_gjk(const cvx_shape* A, const double* e, double* pa, double* pb, 
     cvx_support(A, nd, a);
     ell_support(e, v, b);
     for (int k = 0; k < 3; k++) w[k] = a[k] - b[k];
-    if (n > 0 && vv - dot3(v, w) <= 1e-10 * vv + 1e-24) break;
+    const double vw = dot3(v, w);
+    if (vw > 0 && vw * vw > vv * cut * cut) { /* separating plane farther than cut: no contact */
+      *dist = vw / sqrt(vv);
+      return 2;
+    }
+    if (n > 0 && vv - vw <= 1e-8 * vv + 1e-24) break;
     int dup = 0;
     for (int i = 0; i < n; i++) {
       double dd[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
@@ -918,10 +927,31 @@ static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
 /* one contact between core A (+ radius rA) and the ellipsoid e, object frame: GJK when the cores are
  * apart, MPR penetration when they overlap, the centre direction if MPR degenerates.  Normal from the
  * object to A. */
-static void cvx_contact(const cvx_shape* A, double rA, const double* e, double* pt, double* nrm, double* d) {
+static void cvx_contact(const cvx_shape* A0, double rA, const double* e, double cut, double* pt, double* nrm,
+                        double* d) {
   double pa[3], pb[3], dist, x[3];
-  if (cvx_gjk(A, e, pa, pb, &dist) && dist > 1e-9) {
-    for (int a = 0; a < 3; a++) nrm[a] = (pa[a] - pb[a]) / dist;
+  /* a box core is rounded by a 1 mm margin (at most half its smallest half extent): GJK then resolves
+   * penetrations shallower than the margin (resting contacts), and MPR only runs for deeper ones */
+  cvx_shape As = *A0;
+  const cvx_shape* A = &As;
+  if (As.kind == 1) {
+    const double mg = fmin(CVX_MARGIN, 0.5 * fmin(As.h[0], fmin(As.h[1], As.h[2])));
+    for (int a = 0; a < 3; a++) As.h[a] -= mg;
+    rA += mg;
+  }
+  const int g = cvx_gjk(A, e, rA + cut, pa, pb, &dist);
+  if (g == 2) { /* farther than rA + cut: only the (lower-bound) distance is meaningful */
+    *d = dist - rA;
+    nrm[0] = nrm[1] = 0; nrm[2] = 1;
+    pt[0] = pt[1] = pt[2] = 0;
+    return;
+  }
+  if (g && dist > 1e-9) {
+    /* the normal is the egg's surface normal at its witness point (the gradient of the implicit
+     * function): better conditioned than (pa - pb) / dist when the gap is small */
+    double gr[3] = {pb[0] / (e[0] * e[0]), pb[1] / (e[1] * e[1]), pb[2] / (e[2] * e[2])};
+    double gl = sqrt(dot3(gr, gr));
+    for (int a = 0; a < 3; a++) nrm[a] = gr[a] / gl;
     for (int a = 0; a < 3; a++) pt[a] = 0.5 * ((pa[a] - nrm[a] * rA) + pb[a]);
     *d = dist - rA;
     return;
@@ -985,7 +1015,7 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, double off
       for (int a = 0; a < 3; a++) A.h[a] = m->geom_size[g][a];
     }
     double pl[3], nl[3], d;
-    cvx_contact(&A, r, os, pl, nl, &d);
+    cvx_contact(&A, r, os, off, pl, nl, &d);
     if (d < off) {
       from_obj_pt(k, pl, pw);
       from_obj_dir(k, nl, nw);
@@ -1625,6 +1655,6 @@ int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, cons
       for (int b = 0; b < 3; b++) A.R[a][b] = shape[3 + 3 * a + b];
     }
   }
-  cvx_contact(&A, radius, e, out, out + 3, out + 6);
+  cvx_contact(&A, radius, e, 1e300, out, out + 3, out + 6);
   return MG_OK;
 }

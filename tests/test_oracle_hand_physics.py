@@ -192,8 +192,12 @@ def test_egg_gjk_distance_matches_dense_samples():
             continue
         seen += 1
         ref = tree.query(pts)[0].min() - r
-        # the samples' spacing bounds the reference error (~1e-4 m on the box faces)
-        assert abs(d - ref) < 1.5e-4, (i, d, ref)
+        # the samples' spacing bounds the reference error (~1e-4 m on the box faces); box cores are
+        # rounded by 1 mm (CVX_MARGIN), which can only add up to (sqrt(3) - 1) mm at a corner
+        if r > 0:
+            assert abs(d - ref) < 1.5e-4, (i, d, ref)
+        else:
+            assert ref - 1.5e-4 < d < ref + 0.74e-3, (i, d, ref)
         assert abs(np.linalg.norm(n) - 1) < 1e-9
         # the normal points from the egg towards the geom: the contact point moved along it leaves the egg
         out = pt + n * (abs(d) + 1e-3)
@@ -217,7 +221,7 @@ def test_egg_mpr_penetration_is_a_separating_translation():
             continue
         checked += 1
         _, _, d2 = O.ellipsoid_contact(1, np.r_[c - d * n, R.ravel(), hb], 0.0, e)
-        assert abs(d2) < 1e-5, (i, d, d2)
+        assert abs(d2) < 1e-4 + 0.01 * abs(d), (i, d, d2)   # MPR: the portal point, not the exact minimum
     assert checked >= 30
 
 

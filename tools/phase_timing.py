@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--num-envs", type=int, default=65536)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--object-type", default="block", help="ShadowHand objectType")
     args = ap.parse_args()
     import ctypes as C
     import numpy as np
@@ -34,8 +35,14 @@ def main():
     import migym
     from migym import _abi
     lib = _abi.lib()
+    mk = {}
+    if args.task == "ShadowHand" and args.object_type != "block":
+        from migym import configs
+        tcfg = configs.task_config("ShadowHand", args.num_envs, sim_device="cuda:0")
+        tcfg["env"]["objectType"] = args.object_type
+        mk["cfg"] = {"task": tcfg}
     env = migym.make(seed=0, task=args.task, num_envs=args.num_envs, sim_device="cuda:0", rl_device="cuda:0",
-                     headless=True)
+                     headless=True, **mk)
     g = torch.Generator(device="cuda:0").manual_seed(0)
     acts = [torch.rand((env.num_actors, env.num_actions), device="cuda:0", generator=g) * 2 - 1 for _ in range(4)]
     for i in range(args.warmup):
