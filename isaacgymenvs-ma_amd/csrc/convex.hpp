@@ -24,17 +24,26 @@
 
 namespace mg {
 
+// the narrowphase scalar type: fp64 (an fp32 build, -DMG_CVX_REAL=float, is a host-harness experiment:
+// its GJK / MPR decisions near contact drift from the fp64 oracle)
+#ifndef MG_CVX_REAL
+#define MG_CVX_REAL double
+#endif
+typedef MG_CVX_REAL creal;
 struct D3 {
-  double x, y, z;
+  creal x, y, z;
 };
-__device__ __forceinline__ D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 d3(creal x, creal y, creal z) { return D3{x, y, z}; }
 __device__ __forceinline__ D3 d3(V3 a) { return D3{a.x, a.y, a.z}; }
+// GJK stop / no-progress thresholds: relative to |v|^2, within reach of the scalar's precision
+constexpr creal GJK_REL = sizeof(creal) == 4 ? (creal)1e-6 : (creal)1e-8;
+constexpr creal GJK_STALL = sizeof(creal) == 4 ? (creal)1e-7 : (creal)1e-14;
 __device__ __forceinline__ V3 f3(D3 a) { return v3((float)a.x, (float)a.y, (float)a.z); }
 __device__ __forceinline__ D3 operator+(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ D3 operator-(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ D3 operator*(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ D3 operator*(D3 a, creal s) { return d3(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ D3 operator-(D3 a) { return d3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ creal dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 __device__ __forceinline__ D3 cross(D3 a, D3 b) {
   return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -43,7 +52,7 @@ struct CvxShape {
   int kind;      // 0 segment [p0, p1], 1 box (centre c, axes = columns of R, half extents h)
   D3 p0, p1;
   D3 c, h;
-  double R[3][3];
+  creal R[3][3];
 };
 
 __device__ __forceinline__ D3 cvx_support(const CvxShape& A, D3 d) {
@@ -52,7 +61,7 @@ __device__ __forceinline__ D3 cvx_support(const CvxShape& A, D3 d) {
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const D3 col = d3(A.R[0][k], A.R[1][k], A.R[2][k]);
-    const double hk = k == 0 ? A.h.x : (k == 1 ? A.h.y : A.h.z);
+    const creal hk = k == 0 ? A.h.x : (k == 1 ? A.h.y : A.h.z);
     o = o + col * (dot(col, d) >= 0.0 ? hk : -hk);
   }
   return o;
@@ -61,43 +70,43 @@ __device__ __forceinline__ D3 cvx_support(const CvxShape& A, D3 d) {
 // support point of the ellipsoid with semi-axes e in direction d
 __device__ __forceinline__ D3 ell_support(D3 e, D3 d) {
   const D3 q = d3(e.x * e.x * d.x, e.y * e.y * d.y, e.z * e.z * d.z);
-  const double n = sqrt(q.x * d.x + q.y * d.y + q.z * d.z);
+  const creal n = sqrt(q.x * d.x + q.y * d.y + q.z * d.z);
   if (n < 1e-30) return d3(0, 0, 0);
   return q * (1.0 / n);
 }
 
-__device__ __forceinline__ void cvx_seg(D3 a, D3 b, double* lam) {
+__device__ __forceinline__ void cvx_seg(D3 a, D3 b, creal* lam) {
   const D3 ab = b - a;
-  const double den = dot(ab, ab);
-  double t = den > 0.0 ? -dot(a, ab) / den : 0.0;
+  const creal den = dot(ab, ab);
+  creal t = den > 0.0 ? -dot(a, ab) / den : 0.0;
   t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
   lam[0] = 1.0 - t;
   lam[1] = t;
 }
 
-__device__ __forceinline__ void cvx_tri(D3 a, D3 b, D3 c, double* lam) {
+__device__ __forceinline__ void cvx_tri(D3 a, D3 b, D3 c, creal* lam) {
   const D3 ab = b - a, ac = c - a;
   lam[0] = lam[1] = lam[2] = 0.0;
-  const double d1 = -dot(ab, a), d2 = -dot(ac, a);
+  const creal d1 = -dot(ab, a), d2 = -dot(ac, a);
   if (d1 <= 0.0 && d2 <= 0.0) { lam[0] = 1.0; return; }
-  const double e3 = -dot(ab, b), d4 = -dot(ac, b);
+  const creal e3 = -dot(ab, b), d4 = -dot(ac, b);
   if (e3 >= 0.0 && d4 <= e3) { lam[1] = 1.0; return; }
-  const double vc = d1 * d4 - e3 * d2;
-  if (vc <= 0.0 && d1 >= 0.0 && e3 <= 0.0) { const double v = d1 / (d1 - e3); lam[0] = 1.0 - v; lam[1] = v; return; }
-  const double d5 = -dot(ab, c), d6 = -dot(ac, c);
+  const creal vc = d1 * d4 - e3 * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && e3 <= 0.0) { const creal v = d1 / (d1 - e3); lam[0] = 1.0 - v; lam[1] = v; return; }
+  const creal d5 = -dot(ab, c), d6 = -dot(ac, c);
   if (d6 >= 0.0 && d5 <= d6) { lam[2] = 1.0; return; }
-  const double vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) { const double w = d2 / (d2 - d6); lam[0] = 1.0 - w; lam[2] = w; return; }
-  const double va = e3 * d6 - d5 * d4;
+  const creal vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) { const creal w = d2 / (d2 - d6); lam[0] = 1.0 - w; lam[2] = w; return; }
+  const creal va = e3 * d6 - d5 * d4;
   if (va <= 0.0 && (d4 - e3) >= 0.0 && (d5 - d6) >= 0.0) {
-    const double w = (d4 - e3) / ((d4 - e3) + (d5 - d6));
+    const creal w = (d4 - e3) / ((d4 - e3) + (d5 - d6));
     lam[1] = 1.0 - w;
     lam[2] = w;
     return;
   }
-  const double den = va + vb + vc;
+  const creal den = va + vb + vc;
   if (!(den > 0.0)) { cvx_seg(a, b, lam); lam[2] = 0.0; return; }
-  const double v = vb / den, w = vc / den;
+  const creal v = vb / den, w = vc / den;
   lam[0] = 1.0 - v - w;
   lam[1] = v;
   lam[2] = w;
@@ -105,8 +114,8 @@ __device__ __forceinline__ void cvx_tri(D3 a, D3 b, D3 c, double* lam) {
 
 // closest point of the simplex W[0..n-1] to the origin; keeps the supporting vertices in order,
 // their weights in lk; returns true if the origin is inside a (non-degenerate) tetrahedron
-__device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, double* lk) {
-  double lam[4] = {0.0, 0.0, 0.0, 0.0};
+__device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, creal* lk) {
+  creal lam[4] = {0.0, 0.0, 0.0, 0.0};
   if (n == 1) {
     lam[0] = 1.0;
   } else if (n == 2) {
@@ -115,22 +124,22 @@ __device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, double*
     cvx_tri(W[0], W[1], W[2], lam);
   } else {
     constexpr int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};  // face + opposite
-    double best = 1e300;
+    creal best = (creal)3.0e38;
     bool any = false;
 #pragma unroll
     for (int f = 0; f < 4; f++) {
       const D3 a = W[F[f][0]], b = W[F[f][1]], c = W[F[f][2]], d = W[F[f][3]];
       const D3 ab = b - a, ac = c - a, ad = d - a;
       const D3 nf = cross(ab, ac);
-      const double sp = -dot(nf, a), sd = dot(nf, ad);
-      const double sc = dot(ab, ab) + dot(ac, ac) + dot(ad, ad);
+      const creal sp = -dot(nf, a), sd = dot(nf, ad);
+      const creal sc = dot(ab, ab) + dot(ac, ac) + dot(ad, ad);
       const bool degenerate = sd * sd <= 1e-12 * sc * sc * sc;
       if (!(sp * sd < 0.0) && !degenerate) continue;
       any = true;
-      double l3[3];
+      creal l3[3];
       cvx_tri(a, b, c, l3);
       const D3 q = a * l3[0] + b * l3[1] + c * l3[2];
-      const double dq = dot(q, q);
+      const creal dq = dot(q, q);
       if (dq < best) {
         best = dq;
 #pragma unroll
@@ -164,21 +173,21 @@ __device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, double*
 
 // GJK distance between core A and the origin-centred ellipsoid e: true when separated (closest
 // points pa on A, pb on the ellipsoid, distance), false when the cores overlap
-__device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, double cut, D3& pa, D3& pb, double& dist) {
+__device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, creal cut, D3& pa, D3& pb, creal& dist) {
   D3 W[4], P[4];
   D3 v = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
   if (dot(v, v) < 1e-20) v = d3(0, 0, 1);
   int n = 0;
-  double vv = dot(v, v);
-  double lam[4] = {0.0, 0.0, 0.0, 0.0};
+  creal vv = dot(v, v);
+  creal lam[4] = {0.0, 0.0, 0.0, 0.0};
   for (int it = 0; it < 64; it++) {
     const D3 a = cvx_support(A, -v), b = ell_support(e, v), w = a - b;
-    const double vw = dot(v, w);
+    const creal vw = dot(v, w);
     if (vw > 0.0 && vw * vw > vv * cut * cut) {  // separating plane farther than cut: no contact
       dist = vw / sqrt(vv);
       return 2;
     }
-    if (n > 0 && vv - vw <= 1e-8 * vv + 1e-24) break;
+    if (n > 0 && vv - vw <= GJK_REL * vv + (creal)1e-24) break;
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -191,9 +200,9 @@ __device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, double cut, D3& 
       if (i == n) { W[i] = w; P[i] = a; }
     n++;
     if (cvx_simplex(W, P, n, v, lam)) return 0;
-    const double vn = dot(v, v);
+    const creal vn = dot(v, v);
     if (vn <= 1e-20) return 0;
-    const bool stall = it > 0 && vn >= vv * (1.0 - 1e-14);
+    const bool stall = it > 0 && vn >= vv * ((creal)1.0 - GJK_STALL);
     vv = vn;
     if (stall) break;
   }
@@ -206,12 +215,12 @@ __device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, double cut, D3& 
   return 1;
 }
 
-constexpr double MPR_TOL = 1e-7;   // portal reached the boundary (m)
-constexpr double CVX_MARGIN = 1e-3;  // rounding of box cores against the egg (m)
-constexpr double MPR_EPS = 1e-12;  // origin-side tests
+constexpr creal MPR_TOL = 1e-7;   // portal reached the boundary (m)
+constexpr creal CVX_MARGIN = 1e-3;  // rounding of box cores against the egg (m)
+constexpr creal MPR_EPS = 1e-12;  // origin-side tests
 
 __device__ __forceinline__ D3 unit3(D3 a) {
-  const double l = sqrt(dot(a, a));
+  const creal l = sqrt(dot(a, a));
   return l > 0.0 ? a * (1.0 / l) : a;
 }
 
@@ -261,8 +270,8 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
     else { v3p = v4; a3 = a4; }
   };
   auto reached = [&](D3 v4, D3 d) {
-    const double d4 = dot(v4, d);
-    const double mm = fmin(d4 - dot(v1, d), fmin(d4 - dot(v2, d), d4 - dot(v3p, d)));
+    const creal d4 = dot(v4, d);
+    const creal mm = fmin(d4 - dot(v1, d), fmin(d4 - dot(v2, d), d4 - dot(v3p, d)));
     return mm <= MPR_TOL;
   };
   for (it = 0; it < 64; it++) {  // refine until the portal encloses the origin
@@ -279,7 +288,7 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
     if (reached(v4, dir) || it >= 64) break;
     expand(v4, a4);
   }
-  double lam[3];
+  creal lam[3];
   cvx_tri(v1, v2, v3p, lam);
   x = v1 * lam[0] + v2 * lam[1] + v3p * lam[2];
   pa = a1 * lam[0] + a2 * lam[1] + a3 * lam[2];
@@ -288,12 +297,14 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
 
 // one contact between core A (+ radius rA) and the ellipsoid e (object frame): GJK when apart, MPR
 // when overlapping, the centre direction if MPR degenerates.  Normal from the object to A.
-__device__ __forceinline__ void cvx_contact(CvxShape A, double rA, D3 e, double cut, D3* pt, D3* nrm,
-                                                      double* d) {
+// a real call, not inlined: the fp64 GJK / MPR working set stays out of the register allocation of
+// the rest of the step kernel
+__device__ __attribute__((noinline)) void cvx_contact(CvxShape A, creal rA, D3 e, creal cut, D3* pt, D3* nrm,
+                                                      creal* d) {
   D3 pa, pb, x;
-  double dist;
+  creal dist;
   if (A.kind == 1) {  // box cores rounded by CVX_MARGIN (see the oracle): resting contacts stay with GJK
-    const double mg = fmin(CVX_MARGIN, 0.5 * fmin(A.h.x, fmin(A.h.y, A.h.z)));
+    const creal mg = fmin(CVX_MARGIN, 0.5 * fmin(A.h.x, fmin(A.h.y, A.h.z)));
     A.h = A.h - d3(mg, mg, mg);
     rA += mg;
   }
@@ -314,7 +325,7 @@ __device__ __forceinline__ void cvx_contact(CvxShape A, double rA, D3 e, double 
     return;
   }
   if (cvx_mpr(A, e, x, pa)) {
-    const double l = sqrt(dot(x, x));
+    const creal l = sqrt(dot(x, x));
     if (l > 1e-9) {
       *nrm = x * (-1.0 / l);
       *pt = (pa - x * 0.5) - *nrm * (rA * 0.5);
@@ -323,7 +334,7 @@ __device__ __forceinline__ void cvx_contact(CvxShape A, double rA, D3 e, double 
     }
   }
   const D3 ca = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
-  const double l = sqrt(dot(ca, ca));
+  const creal l = sqrt(dot(ca, ca));
   *nrm = l > 1e-12 ? ca * (1.0 / l) : d3(0, 0, 1);
   *pt = ca * 0.5;
   *d = -rA;
