@@ -297,9 +297,10 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
 
 // one contact between core A (+ radius rA) and the ellipsoid e (object frame): GJK when apart, MPR
 // when overlapping, the centre direction if MPR degenerates.  Normal from the object to A.
-// a real call, not inlined: the fp64 GJK / MPR working set stays out of the register allocation of
-// the rest of the step kernel
-__device__ __attribute__((noinline)) void cvx_contact(CvxShape A, creal rA, D3 e, creal cut, D3* pt, D3* nrm,
+// inlined: as a real call (noinline) the egg kernel ran ~25 % faster but produced order-dependent NaN
+// object states on the GPU after other kernels had run (reproduced, not explained; the host build of
+// this file is clean under MemorySanitizer), so the call stays inline
+__device__ __forceinline__ void cvx_contact(CvxShape A, creal rA, D3 e, creal cut, D3* pt, D3* nrm,
                                                       creal* d) {
   D3 pa, pb, x;
   creal dist;
