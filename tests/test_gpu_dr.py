@@ -142,12 +142,15 @@ def test_dr_physics_matches_oracle_ant(lib):
     assert agreement(h2.dof[..., 1], h.dof[..., 1], 2e-3, 2e-3) < 0.5
 
 
-def test_dr_physics_matches_oracle_hand(lib):
-    from test_gpu_hand import DevHandEnv, hand_states, setup
-    spec, sp, tp = setup()
+@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
+def test_dr_physics_matches_oracle_hand(lib, kind):
+    """env_props rows (masses, drives, friction, object mass / friction / scale) on the GPU vs the oracle;
+    the object's scale reaches every shape's size (box half extents, egg semi-axes, pen radius + length)."""
+    from test_gpu_hand import DevHandEnv, PALM_DZ, hand_states, setup
+    spec, sp, tp = setup(kind=kind)
     n = 192
     rng = np.random.default_rng(23)
-    h = hand_states(spec, tp, n, rng)
+    h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
     props = np.ascontiguousarray(random_props(spec, n, rng), np.float32)
     e = DevHandEnv(h)
     mnp = M.pack_model(spec)
