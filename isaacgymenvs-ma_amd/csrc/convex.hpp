@@ -151,31 +151,53 @@ __device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, creal* 
     }
     if (!any) return true;
   }
+  // compact in place (a kept vertex only moves down: slot m <= i), no second copy of the simplex
   int m = 0;
   v = d3(0, 0, 0);
-  D3 Wn[4], Pn[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     if (i < n && lam[i] > 0.0) {
       v = v + W[i] * lam[i];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (j == m) { Wn[j] = W[i]; Pn[j] = P[i]; lk[j] = lam[i]; }
+      for (int j = 0; j <= i; j++)
+        if (j == m) { W[j] = W[i]; P[j] = P[i]; lk[j] = lam[i]; }
       m++;
     }
   }
-#pragma unroll
-  for (int j = 0; j < 4; j++)
-    if (j < m) { W[j] = Wn[j]; P[j] = Pn[j]; }
   n = m;
   return false;
 }
 
 // GJK distance between core A and the origin-centred ellipsoid e: true when separated (closest
 // points pa on A, pb on the ellipsoid, distance), false when the cores overlap
+// the core's point nearest the egg's centre in the egg-scaled metric (x / e): the segment's exact
+// minimiser of |p(t) / e|^2, or the box centre; true when it lies inside the egg (the cores certainly
+// overlap: exact for a segment, sufficient for a box)
+__device__ __forceinline__ bool cvx_core_point(const CvxShape& A, D3 e, D3& sp) {
+  if (A.kind == 0) {
+    const D3 q0 = d3(A.p0.x / e.x, A.p0.y / e.y, A.p0.z / e.z);
+    const D3 du = A.p1 - A.p0, qu = d3(du.x / e.x, du.y / e.y, du.z / e.z);
+    const creal den = dot(qu, qu);
+    creal t = den > 0.0 ? -dot(q0, qu) / den : 0.0;
+    t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+    sp = A.p0 + du * t;
+  } else {
+    sp = A.c;
+  }
+  const creal x = sp.x / e.x, y = sp.y / e.y, z = sp.z / e.z;
+  return x * x + y * y + z * z < 1.0;
+}
+
 __device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, creal cut, D3& pa, D3& pb, creal& dist) {
   D3 W[4], P[4];
-  D3 v = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
+  D3 v;
+  if (A.kind == 0) {  // start from the segment point nearest the egg in its metric, towards the egg
+    D3 sp;
+    cvx_core_point(A, e, sp);
+    v = sp - ell_support(e, d3(sp.x / (e.x * e.x), sp.y / (e.y * e.y), sp.z / (e.z * e.z)));
+  } else {
+    v = A.c;
+  }
   if (dot(v, v) < 1e-20) v = d3(0, 0, 1);
   int n = 0;
   creal vv = dot(v, v);
@@ -309,7 +331,8 @@ __device__ __forceinline__ void cvx_contact(CvxShape A, creal rA, D3 e, creal cu
     A.h = A.h - d3(mg, mg, mg);
     rA += mg;
   }
-  const int g = cvx_gjk(A, e, rA + cut, pa, pb, dist);
+  D3 sp;
+  const int g = cvx_core_point(A, e, sp) ? 0 : cvx_gjk(A, e, rA + cut, pa, pb, dist);  // overlap: MPR
   if (g == 2) {  // farther than rA + cut: only the (lower-bound) distance is meaningful
     *d = dist - rA;
     *nrm = d3(0, 0, 1);

@@ -765,10 +765,35 @@ static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double
 
 /* GJK distance between core A and the ellipsoid e (origin-centred).  Returns 1 when separated, with
  * the closest points pa (on A), pb (on the ellipsoid) and the distance; 0 when the cores overlap. */
+/* the core's point nearest the egg's centre in the egg-scaled metric (x / e): the segment's exact
+ * minimiser of |p(t) / e|^2, or the box centre.  Returns 1 when that point lies inside the egg, i.e. the
+ * cores certainly overlap (exact for a segment; sufficient for a box). */
+static int cvx_core_point(const cvx_shape* A, const double* e, double* sp) {
+  if (A->kind == 0) {
+    double q0[3], qu[3];
+    for (int a = 0; a < 3; a++) { q0[a] = A->p0[a] / e[a]; qu[a] = (A->p1[a] - A->p0[a]) / e[a]; }
+    double den = dot3(qu, qu), t = den > 0 ? -dot3(q0, qu) / den : 0.0;
+    t = t < 0 ? 0 : (t > 1 ? 1 : t);
+    for (int a = 0; a < 3; a++) sp[a] = A->p0[a] + t * (A->p1[a] - A->p0[a]);
+  } else {
+    for (int a = 0; a < 3; a++) sp[a] = A->c[a];
+  }
+  double r2 = 0;
+  for (int a = 0; a < 3; a++) r2 += (sp[a] / e[a]) * (sp[a] / e[a]);
+  return r2 < 1.0;
+}
+
 static int cvx_gjk(const cvx_shape* A, const double* e, double cut, double* pa, double* pb, double* dist) {
   double W[4][3], P[4][3], v[3];
-  if (A->kind == 0) for (int a = 0; a < 3; a++) v[a] = 0.5 * (A->p0[a] + A->p1[a]);
-  else for (int a = 0; a < 3; a++) v[a] = A->c[a];
+  if (A->kind == 0) { /* start from the segment point nearest the egg in its metric, towards the egg */
+    double sp[3], gr[3], bs[3];
+    cvx_core_point(A, e, sp);
+    for (int a = 0; a < 3; a++) gr[a] = sp[a] / (e[a] * e[a]);
+    ell_support(e, gr, bs);
+    for (int a = 0; a < 3; a++) v[a] = sp[a] - bs[a];
+  } else {
+    for (int a = 0; a < 3; a++) v[a] = A->c[a];
+  }
   if (dot3(v, v) < 1e-20) { v[0] = 0; v[1] = 0; v[2] = 1; }
   int n = 0;
   double vv = dot3(v, v);
@@ -939,7 +964,8 @@ static void cvx_contact(const cvx_shape* A0, double rA, const double* e, double 
     for (int a = 0; a < 3; a++) As.h[a] -= mg;
     rA += mg;
   }
-  const int g = cvx_gjk(A, e, rA + cut, pa, pb, &dist);
+  double sp[3];
+  const int g = cvx_core_point(A, e, sp) ? 0 : cvx_gjk(A, e, rA + cut, pa, pb, &dist); /* overlap: MPR */
   if (g == 2) { /* farther than rA + cut: only the (lower-bound) distance is meaningful */
     *d = dist - rA;
     nrm[0] = nrm[1] = 0; nrm[2] = 1;
