@@ -114,7 +114,7 @@ __device__ __forceinline__ void cvx_tri(D3 a, D3 b, D3 c, creal* lam) {
 
 // closest point of the simplex W[0..n-1] to the origin; keeps the supporting vertices in order,
 // their weights in lk; returns true if the origin is inside a (non-degenerate) tetrahedron
-__device__ __forceinline__ bool cvx_simplex(D3* W, D3* P, int& n, D3& v, creal* lk) {
+__device__ __forceinline__ bool cvx_simplex(D3* W, V3* P, int& n, D3& v, creal* lk) {
   creal lam[4] = {0.0, 0.0, 0.0, 0.0};
   if (n == 1) {
     lam[0] = 1.0;
@@ -189,7 +189,8 @@ __device__ __forceinline__ bool cvx_core_point(const CvxShape& A, D3 e, D3& sp) 
 }
 
 __device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, creal cut, D3& pa, D3& pb, creal& dist) {
-  D3 W[4], P[4];
+  D3 W[4];
+  V3 P[4];  // A-side support points: only the final witness reads them, fp32 is enough (halves their registers)
   D3 v;
   if (A.kind == 0) {  // start from the segment point nearest the egg in its metric, towards the egg
     D3 sp;
@@ -219,7 +220,7 @@ __device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, creal cut, D3& p
     if (dup) break;
 #pragma unroll
     for (int i = 0; i < 4; i++)
-      if (i == n) { W[i] = w; P[i] = a; }
+      if (i == n) { W[i] = w; P[i] = f3(a); }
     n++;
     if (cvx_simplex(W, P, n, v, lam)) return 0;
     const creal vn = dot(v, v);
@@ -231,7 +232,7 @@ __device__ __forceinline__ int cvx_gjk(const CvxShape& A, D3 e, creal cut, D3& p
   pa = d3(0, 0, 0);
 #pragma unroll
   for (int i = 0; i < 4; i++)
-    if (i < n) pa = pa + P[i] * lam[i];
+    if (i < n) pa = pa + d3(P[i]) * lam[i];
   pb = pa - v;
   dist = sqrt(vv);
   return 1;
