@@ -253,24 +253,30 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
   D3 v0 = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
   if (dot(v0, v0) < 1e-20) v0 = d3(1e-6, 0, 0);
   D3 dir = unit3(-v0);
-  D3 a1 = cvx_support(A, dir), v1 = a1 - ell_support(e, -dir);
+  const D3 s1 = cvx_support(A, dir);
+  D3 v1 = s1 - ell_support(e, -dir);
+  V3 a1 = f3(s1);  // A-side points in fp32: only the final witness reads them
   if (dot(v1, dir) <= 0.0) return false;
   dir = cross(v0, v1);
-  if (dot(dir, dir) <= 1e-24) { x = v1; pa = a1; return true; }
+  if (dot(dir, dir) <= 1e-24) { x = v1; pa = d3(a1); return true; }
   dir = unit3(dir);
-  D3 a2 = cvx_support(A, dir), v2 = a2 - ell_support(e, -dir);
+  const D3 s2 = cvx_support(A, dir);
+  D3 v2 = s2 - ell_support(e, -dir);
+  V3 a2 = f3(s2);
   if (dot(v2, dir) <= 0.0) return false;
   dir = unit3(cross(v1 - v0, v2 - v0));
   if (dot(dir, v0) > 0.0) {
-    D3 t = v1; v1 = v2; v2 = t;
-    t = a1; a1 = a2; a2 = t;
+    const D3 t = v1; v1 = v2; v2 = t;
+    const V3 ta = a1; a1 = a2; a2 = ta;
     dir = -dir;
   }
-  D3 a3, v3p;
+  D3 v3p;
+  V3 a3;
   int it;
   for (it = 0; it < 64; it++) {  // a portal the origin ray passes through
-    a3 = cvx_support(A, dir);
-    v3p = a3 - ell_support(e, -dir);
+    const D3 s3 = cvx_support(A, dir);
+    v3p = s3 - ell_support(e, -dir);
+    a3 = f3(s3);
     if (dot(v3p, dir) <= 0.0) return false;
     if (dot(cross(v1, v3p), v0) < -MPR_EPS) {
       v2 = v3p; a2 = a3;
@@ -283,7 +289,7 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
   }
   if (it == 64) return false;
   // expand: replace one portal vertex by v4 so that the portal keeps facing the origin ray
-  auto expand = [&](D3 v4, D3 a4) {
+  auto expand = [&](D3 v4, V3 a4) {
     const D3 c = cross(v4, v0);
     int k;
     if (dot(v1, c) > 0.0) k = dot(v2, c) > 0.0 ? 1 : 3;
@@ -300,21 +306,21 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
   for (it = 0; it < 64; it++) {  // refine until the portal encloses the origin
     dir = unit3(cross(v2 - v1, v3p - v1));
     if (dot(v1, dir) >= 0.0) break;
-    const D3 a4 = cvx_support(A, dir), v4 = a4 - ell_support(e, -dir);
+    const D3 s4 = cvx_support(A, dir), v4 = s4 - ell_support(e, -dir);
     if (dot(v4, dir) < 0.0 || reached(v4, dir)) return false;
-    expand(v4, a4);
+    expand(v4, f3(s4));
   }
   if (it == 64) return false;
   for (it = 0;; it++) {  // push the portal onto the boundary
     dir = unit3(cross(v2 - v1, v3p - v1));
-    const D3 a4 = cvx_support(A, dir), v4 = a4 - ell_support(e, -dir);
+    const D3 s4 = cvx_support(A, dir), v4 = s4 - ell_support(e, -dir);
     if (reached(v4, dir) || it >= 64) break;
-    expand(v4, a4);
+    expand(v4, f3(s4));
   }
   creal lam[3];
   cvx_tri(v1, v2, v3p, lam);
   x = v1 * lam[0] + v2 * lam[1] + v3p * lam[2];
-  pa = a1 * lam[0] + a2 * lam[1] + a3 * lam[2];
+  pa = d3(a1) * lam[0] + d3(a2) * lam[1] + d3(a3) * lam[2];
   return true;
 }
 
