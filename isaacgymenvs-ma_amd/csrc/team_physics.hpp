@@ -135,7 +135,6 @@ template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + MG_PGS_PREFETCH - 1) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;
-  static constexpr int MRO = OBJ ? MR : 1;
   static constexpr int RB = (T >= 32 && !OBJ) ? MG_RB_WIDE : 6;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
@@ -187,8 +186,12 @@ struct TeamLDS {
       Row rows[MR];
     } sv;
   } u;
-  // free object (OBJ): Jacobian rows on its columns, staged root row, obs staging
-  float rwo[MRO][6];
+  // free object (OBJ): staged root row, obs staging.  The object part of a contact row, [(p - c) x d; d],
+  // is recomputed from the contact list where it is needed (the 2.9 KB per team saved lets 6 blocks
+  // share a CU: block 12.5 -> 13.8 M env-steps/s); the egg instance keeps the rows in LDS, whose code
+  // the compiler schedules better around the fp64 narrowphase (5.7 vs 3.6-3.9 M env-steps/s measured)
+  static constexpr int OROWS = OBJ == MG_GT_ELLIPSOID ? 3 * MC : 1;
+  float rwo[OROWS][6];
   float oroot[OBJ ? 13 : 1];
   float goal[OBJ ? 26 : 1];   // goal actor root row, goal_states row
   float obs[OBJ ? 212 : 1];
@@ -703,12 +706,28 @@ struct Team {
       nu *= k < 3 ? 1.0f / (1.0f + h * m->obj_ang_damping) : 1.0f / (1.0f + h * m->obj_lin_damping);
     }
   }
+  // object part of contact row r on the object's columns [w; v_com]: +-[(p - c_obj) x d; d] (d = the
+  // row's direction: normal or a tangent; sign + when the object is side A)
+  __device__ void obj_jrow(int r, V3* wo, V3* d) const {
+    const int c = r / 3, q = r - 3 * c;
+    const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
+    const V3 dir = ld3(q == 0 ? s->cn[c] : (q == 1 ? s->ct1[c] : s->ct2[c]));
+    *wo = cross(ld3(s->cp[c]) - op, dir) * so;
+    *d = dir * so;
+  }
   // object part of the response column Y_r = M^-1 J_r^T (object lanes)
   __device__ float obj_response(int r) const {
-    const float* J = s->rwo[r];
     const int k = tl - ob0;
-    if (k >= 3) return J[k] / omass();
-    const V3 y = obj_inv_inertia(v3(J[0], J[1], J[2]));
+    if constexpr (L::OROWS > 1) {
+      const float* J = s->rwo[r];
+      if (k >= 3) return J[k] / omass();
+      const V3 y = obj_inv_inertia(v3(J[0], J[1], J[2]));
+      return k == 0 ? y.x : k == 1 ? y.y : y.z;
+    }
+    V3 wo, d;
+    obj_jrow(r, &wo, &d);
+    if (k >= 3) return (k == 3 ? d.x : (k == 4 ? d.y : d.z)) / omass();
+    const V3 y = obj_inv_inertia(wo);
     return k == 0 ? y.x : k == 1 ? y.y : y.z;
   }
 
@@ -856,7 +875,14 @@ struct Team {
   }
   // J_r[tl] from the lane's code (object lanes: the stored object part)
   __device__ float jac_value(int r, int code) const {
-    if (OBJ && objl) return r >= 3 * ncr ? 0.0f : s->rwo[r][tl - ob0];
+    if (OBJ && objl) {
+      if constexpr (L::OROWS > 1) return r >= 3 * ncr ? 0.0f : s->rwo[r][tl - ob0];
+      if (r >= 3 * ncr) return 0.0f;
+      V3 wo, d;
+      obj_jrow(r, &wo, &d);
+      const int k = tl - ob0;
+      return k == 0 ? wo.x : k == 1 ? wo.y : k == 2 ? wo.z : k == 3 ? d.x : k == 4 ? d.y : d.z;
+    }
     if (code == 0) return 0.0f;
     if (r >= 3 * ncr) return code == 1 ? 1.0f : -1.0f;
     float w[6];
@@ -873,8 +899,19 @@ struct Team {
 #pragma unroll
     for (int q = 0; q < 3; q++) J[q] = 0.0f;
     if (OBJ && objl) {
-      if (r0 < 3 * ncr)
-        for (int q = 0; q < 3; q++) J[q] = s->rwo[r0 + q][tl - ob0];
+      if constexpr (L::OROWS > 1) {
+        if (r0 < 3 * ncr)
+          for (int q = 0; q < 3; q++) J[q] = s->rwo[r0 + q][tl - ob0];
+        return;
+      }
+      if (r0 < 3 * ncr) {
+        const int k = tl - ob0;
+        for (int q = 0; q < 3; q++) {
+          V3 wo, d;
+          obj_jrow(r0 + q, &wo, &d);
+          J[q] = k == 0 ? wo.x : k == 1 ? wo.y : k == 2 ? wo.z : k == 3 ? d.x : k == 4 ? d.y : d.z;
+        }
+      }
       return;
     }
     if (tl >= nv) return;
@@ -1307,7 +1344,7 @@ struct Team {
       s->u.sv.rows[3 * c].b = bn;
       s->u.sv.rows[3 * c + 1].b = 0.0f;
       s->u.sv.rows[3 * c + 2].b = 0.0f;
-      if (OBJ) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
+      if constexpr (L::OROWS > 1) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
         const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
         V3 dirs[3] = {n, t1, t2};
         for (int r = 0; r < 3; r++) {
