@@ -127,6 +127,9 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #ifndef MG_PGS_EARLY
 #define MG_PGS_EARLY 1  // issue a block's private J/Y loads one whole block ahead (compiler barrier)
 #endif
+#ifndef MG_PGS_JY2
+#define MG_PGS_JY2 0  // rows' (J, Y) private columns interleaved as float2
+#endif
 #ifndef MG_RB_WIDE
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
 #endif
@@ -1421,7 +1424,18 @@ struct Team {
         }
       }
     }
+#if MG_PGS_JY2
+    // (J, Y) of a row interleaved: one 8-byte private load per visit instead of two 4-byte ones
+    float2 JYcol[MR];
+#define MG_JSET(r, j, y) (JYcol[r] = make_float2((j), (y)))
+#define MG_JGET(r) (JYcol[r].x)
+#define MG_YGET(r) (JYcol[r].y)
+#else
     float Jcol[MR], Ycol[MR];
+#define MG_JSET(r, j, y) (Jcol[r] = (j), Ycol[r] = (y))
+#define MG_JGET(r) (Jcol[r])
+#define MG_YGET(r) (Ycol[r])
+#endif
     for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
       float jb[L::RB], yb[L::RB];
 #pragma unroll
@@ -1438,8 +1452,7 @@ struct Team {
           if (OBJ && objl) y = contact ? obj_response(r) : 0.0f;
           y = active ? y : 0.0f;
           const float J = jb[q];
-          Ycol[r] = y;
-          Jcol[r] = J;
+          MG_JSET(r, J, y);
           const float Wr = team_sum<T>(J * y, tb);
           if (tl == 0) {
             typename L::Row& rw = s->u.sv.rows[r];
@@ -1462,8 +1475,7 @@ struct Team {
     static_assert(MR % PF == 0, "row capacity must be a multiple of the PGS prefetch depth");
     const int prow = wave_rows == 0 ? 0 : ((wave_rows + PF - 1) / PF) * PF;
     for (int r = wave_rows; r < prow; r++) {
-      Ycol[r] = 0.0f;
-      Jcol[r] = 0.0f;
+      MG_JSET(r, 0.0f, 0.0f);
       if (tl == 0) s->u.sv.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};
     }
     __syncthreads();
@@ -1479,8 +1491,8 @@ struct Team {
     if (prow > 0) {
 #pragma unroll
       for (int k = 0; k < PF; k++) {
-        pJ[k] = Jcol[k];
-        pY[k] = Ycol[k];
+        pJ[k] = MG_JGET(k);
+        pY[k] = MG_YGET(k);
         pR[k] = s->u.sv.rows[k];
       }
     }
@@ -1494,8 +1506,8 @@ struct Team {
         float nJ[PF], nY[PF];
 #pragma unroll
         for (int k = 0; k < PF; k++) {
-          nJ[k] = Jcol[rn + k];
-          nY[k] = Ycol[rn + k];
+          nJ[k] = MG_JGET(rn + k);
+          nY[k] = MG_YGET(rn + k);
         }
         asm volatile("" ::: "memory");
 #endif
@@ -1516,14 +1528,17 @@ struct Team {
           pJ[k] = nJ[k];
           pY[k] = nY[k];
 #else
-          pJ[k] = Jcol[rn + k];
-          pY[k] = Ycol[rn + k];
+          pJ[k] = MG_JGET(rn + k);
+          pY[k] = MG_YGET(rn + k);
 #endif
           pR[k] = s->u.sv.rows[rn + k];
         }
       }
     }
     __syncthreads();
+#undef MG_JSET
+#undef MG_JGET
+#undef MG_YGET
     ph_mark(6);
     integrate();
     ph_mark(7);
