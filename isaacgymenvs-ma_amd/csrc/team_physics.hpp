@@ -40,7 +40,7 @@ namespace mg {
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
 // loaded once per launch, so every per-node / per-geom constant is an LDS read
 // (~64 cycles) instead of a dependent global load.  Rows padded to odd strides.
-template <int MN, int MG, int MP, int OC = 1>
+template <int MN, int MG, int MP, int OC = 1>  // OC: unused (kept in the instance signatures)
 struct ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
@@ -52,8 +52,7 @@ struct ModelTile {
   int nten;
   float gf[MG][17];   // 0-2 pos, 3-11 R, 12-14 size, 15 bounding radius
   int pairs[MP > 0 ? MP : 1][2];
-  unsigned short ocand[OC];  // object-collision candidates (geom << 4 | candidate), geom order
-  int nn, ng, np, noc;
+  int nn, ng, np;
 };
 
 template <int MN, int MG, int MP, int OC>
@@ -102,21 +101,11 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
     f[15] = ty == MG_GT_BOX ? sqrtf(sz[0] * sz[0] + sz[1] * sz[1] + sz[2] * sz[2])
                             : (ty == MG_GT_CAPSULE ? sz[0] + sz[1] : sz[0]);
   }
-  if (OC > 1 && tid == 0) {  // object candidates: spheres/capsules 1 (closest point), boxes 16 (vertex tests)
-    int n = 0;
-    for (int g = 0; g < ng; g++) {
-      if (!(m->geom_filter[g] & MG_COLLIDE_OBJECT)) continue;
-      const int ty = m->geom_type[g];
-      const int nc = (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) ? 1 : (ty == MG_GT_BOX ? 16 : 0);
-      for (int q = 0; q < nc && n < OC; q++) t->ocand[n++] = (unsigned short)((g << 4) | q);
-    }
-    t->noc = n;
-  }
   for (int q = tid; q < np; q += nt) {
     t->pairs[q][0] = m->pair[q][0];
     t->pairs[q][1] = m->pair[q][1];
   }
-  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; if (OC <= 1) t->noc = 0; }
+  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; }
 }
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
@@ -150,7 +139,16 @@ struct TeamLDS {
   float Iinv[36];
   int ncon, nrows;
   // contacts: point, frame (normal + tangent basis), gap, sides (nodes / geoms)
-  float cp[MC][3], cn[MC][3], ct1[MC][3], ct2[MC][3], cd[MC];
+  // (hand tasks: once the last substep's outputs have read the contacts, their storage is the
+  // observation staging row)
+  union {
+    struct {
+      float cp[MC][3], cn[MC][3], ct1[MC][3], ct2[MC][3];
+    };
+    float obs[OBJ ? 212 : 1];
+  };
+  float cd[MC];
+  static_assert(!OBJ || 12 * MC >= 212, "the hand's observation row must fit the contact storage");
   int cside[MC];  // packed int8 [node A, node B, geom A, geom B] (-1 none, -2 the free object)
   // joint-limit rows (after the 3 rows per contact): kind | node << 4
   int lmeta[2 * (MN - 1)];
@@ -197,7 +195,6 @@ struct TeamLDS {
   float rwo[OROWS][6];
   float oroot[OBJ ? 13 : 1];
   float goal[OBJ ? 26 : 1];   // goal actor root row, goal_states row
-  float obs[OBJ ? 212 : 1];
   float oforce[OBJ ? 4 : 1];  // external force on the object (apply_rigid_body_force_tensors), [3] = local
 };
 
