@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_VERSION 3
+#define MG_VERSION 4
 
 #define MG_MAX_NODES 40
 #define MG_MAX_BODIES 40
@@ -204,7 +204,9 @@ typedef struct mg_task_params {
    * of its agents are done (AND filter); obs rows append the other agents' torso positions
    * relative to self in cyclic-shift order.  num_agents = 1 for single-agent tasks. */
   int32_t num_agents;
-  int32_t pad_ma;
+  /* env.controlFrequencyInv: gym.simulate runs this many times per VecTask.step (vec_task.py:381-384)
+   * while pre_physics_step / post_physics_step run once; 0 is taken as 1 */
+  int32_t control_freq_inv;
   float agent_offset[8][3]; /* start-pose / target offset of each agent within its env */
   /* in-hand manipulation (MG_TASK_SHADOW_HAND; tasks/shadow_hand.py:40-118, ShadowHand.yaml) */
   int32_t num_fingertips;
@@ -272,7 +274,9 @@ typedef struct mg_task_buffers {
                              * (shadow_hand.py:587, 610, 642-643, 704-706) */
   uint64_t seed;            /* device RNG seed (counter-based, keyed by global env id) */
   uint64_t step_counter;    /* VecTask.control_steps: RNG counter */
-  int64_t env_offset;       /* global id of this shard's first env (multi-GPU) */
+  int64_t env_offset;       /* global id of this shard's first env (multi-GPU); the RNG key of local actor a
+                             * is the global actor id env_offset * num_agents + a, so a rollout does not
+                             * depend on how the envs are sharded */
   /* in-hand manipulation (tasks/shadow_hand.py:186-219); unused by the other tasks */
   float* prev_targets;      /* (N, nD) */
   float* goal_states;       /* (N, 13) */
@@ -423,6 +427,24 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
 
 /* Whole VecTask.step: actions -> actuation -> simulate -> post_physics. */
 int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream);
+
+/* Physics-bypass replay of mg_env_step (test infrastructure: pins the fused kernels' own task layer
+ * to the reference's fake-gym traces).  The kernel instance mg_env_step launches is
+ * run with its whole task layer (action clamp, actuation / PD targets, masked resets, observations,
+ * reward, running mean, write-back), but gym.simulate is replaced by the state given here, exactly
+ * as the traces' fake gym.simulate overwrites the sim state (tests/golden/make_traces.py). */
+typedef struct mg_replay {
+  const float* root_states;       /* (N*A*R, 13) post-simulate root rows; hand tasks (R = 3): the object
+                                   * row is taken (hand and goal actors are not simulated) */
+  const float* dof_state;         /* (N*A*nD, 2) */
+  const float* sensors;           /* (N*A*S, 6) or NULL (zeros) */
+  const float* dof_force;         /* (N*A*nD) or NULL (zeros) */
+  const float* rigid_body_states; /* hand tasks: (N, nB + 2, 13); the articulation rows are taken */
+  float* pre_root_states;         /* out or NULL: root rows after pre_physics_step (what simulate starts from) */
+  float* pre_dof_state;           /* out or NULL: DOF state after pre_physics_step */
+} mg_replay;
+int mg_env_step_replay(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
+                       void* stream);
 
 #ifdef __cplusplus
 }

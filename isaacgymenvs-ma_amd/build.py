@@ -1,31 +1,57 @@
 """Build the in-tree HIP library (gfx950) — called by __graft_entry__.build().
 
-    hipcc -O3 --offload-arch=gfx950 -shared -fPIC csrc/migym.hip -> migym/_lib/libmigym.so
+    hipcc -O3 --offload-arch=gfx950 -c csrc/migym.hip            (C ABI + the one-lane-per-env kernels)
+    hipcc -O3 --offload-arch=gfx950 -c csrc/inst.hip -DMG_INST=i  (team kernels, one capacity instance
+                                                                    per object, i < MG_NUM_INST)
+    hipcc -shared *.o -> migym/_lib/libmigym.so
 
+The objects compile in parallel (one process per translation unit, at most MIGYM_JOBS / os.cpu_count()).
 ``--timing`` builds the phase-timing variant (-DMG_PHASE_TIMING, s_memtime per solver
 phase, read back by ``mg_debug_phase_cycles``) into migym/_lib/libmigym_timing.so; it is a
 profiling aid (tools/phase_timing.py), never the measured product.
 """
 import glob
 import os
+import re
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "migym.hip")
+CSRC = os.path.join(HERE, "csrc")
+SRC = os.path.join(CSRC, "migym.hip")
+INST = os.path.join(CSRC, "inst.hip")
 OUT = os.path.join(HERE, "migym", "_lib", "libmigym.so")
-HEADERS = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hpp"))) + [os.path.join(HERE, "..", "include", "migym.h")]
+OUT_TIMING = os.path.join(HERE, "migym", "_lib", "libmigym_timing.so")
+HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.hpp"))) + [os.path.join(HERE, "..", "include", "migym.h")]
 ARCH = os.environ.get("MIGYM_ARCH", "gfx950")
 
 
-OUT_TIMING = os.path.join(HERE, "migym", "_lib", "libmigym_timing.so")
+def num_instances():
+    txt = open(os.path.join(CSRC, "dispatch.hpp")).read()
+    return int(re.search(r"#define MG_NUM_INST (\d+)", txt).group(1))
 
 
 def needs_build(out=OUT):
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in [SRC] + HEADERS)
+    return any(os.path.getmtime(p) > t for p in [SRC, INST, __file__] + HEADERS)
+
+
+def _run_parallel(cmds, verbose):
+    jobs = int(os.environ.get("MIGYM_JOBS", min(16, os.cpu_count() or 1)))
+    pending, running, failed = list(cmds), [], []
+    while pending or running:
+        while pending and len(running) < jobs:
+            c = pending.pop(0)
+            if verbose:
+                print(" ".join(c), file=sys.stderr)
+            running.append((c, subprocess.Popen(c)))
+        c, p = running.pop(0)
+        if p.wait() != 0:
+            failed.append(" ".join(c))
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
 
 
 def build(force=False, verbose=False, timing=False):
@@ -34,13 +60,19 @@ def build(force=False, verbose=False, timing=False):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wno-unused-result"]
+    flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]
     if timing:
-        cmd.append("-DMG_PHASE_TIMING")
-    cmd += ["-o", out + ".tmp", SRC]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+        flags.append("-DMG_PHASE_TIMING")
+    objdir = os.path.join(HERE, "build", "timing" if timing else "release")
+    os.makedirs(objdir, exist_ok=True)
+    objs, cmds = [], []
+    for i in range(-1, num_instances()):
+        o = os.path.join(objdir, "migym.o" if i < 0 else f"inst{i}.o")
+        src = SRC if i < 0 else INST
+        cmds.append([hipcc] + flags + ([] if i < 0 else [f"-DMG_INST={i}"]) + ["-c", "-o", o, src])
+        objs.append(o)
+    _run_parallel(cmds, verbose)
+    subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs)
     os.replace(out + ".tmp", out)
     return out
 

@@ -1,0 +1,68 @@
+// dispatch.hpp — the kernel instances (one per model capacity) and the host entry points each
+// instance translation unit exports.  migym.hip sees only these declarations; inst.hip compiles
+// one instance per translation unit (build.py runs them in parallel) from step_kernels.hpp.
+#pragma once
+#include "common.hpp"
+
+// Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
+// contacts MC, geoms MG, self pairs MP, OBJ = the free object's type in hand-task envs (0: none; one
+// instance per object shape, so the block's kernel carries no egg / pen code).  The smallest
+// instance that fits the model is launched.
+#define MG_INSTANCES(X)                                                                                     \
+  X(8, 4, 8, 4, 0, 0) X(16, 9, 16, 16, 0, 0) X(16, 16, 24, 24, 32, 0) X(32, 24, 32, 24, 160, 0)            \
+  X(32, 32, 48, 48, 192, 0) X(64, 40, 48, 48, 192, 0) X(32, 25, 24, 24, 0, MG_GT_BOX)                       \
+  X(32, 25, 24, 24, 0, MG_GT_CAPSULE) X(32, 25, 24, 24, 0, MG_GT_ELLIPSOID)
+#define MG_NUM_INST 9
+
+namespace mgi {
+struct InstDesc {
+  int T, MN, MC, MG, MP, OBJ;
+};
+#define MG_DESC(T, MN, MC, MG, MP, OBJ) InstDesc{T, MN, MC, MG, MP, OBJ},
+constexpr InstDesc kInst[] = {MG_INSTANCES(MG_DESC)};
+#undef MG_DESC
+static_assert(sizeof(kInst) / sizeof(kInst[0]) == MG_NUM_INST, "MG_NUM_INST must count MG_INSTANCES");
+
+// gym.simulate alone (k_simulate)
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
+struct RunSimulate {
+  static int run(hipStream_t s, const mg_sim* sim);
+};
+// the whole VecTask.step (k_env_step / k_hand_step); rp != nullptr: physics-bypass replay instance
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
+struct RunEnvStep {
+  static int run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb,
+                 const mg_replay* rp);
+};
+// phase-timing build: publish the per-wave accumulator buffer to instance I's code object
+template <int I>
+int phase_buf_publish(unsigned long long* buf);
+
+inline int model_lanes(const mg_model& m) {
+  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs + (m.obj_type ? 6 : 0);
+  return nv > m.num_sensors ? nv : m.num_sensors;
+}
+#define MG_FITS(T, MN, MC, MG, MP, OBJ)                                                              \
+  (m.num_nodes <= MN && max_contacts <= MC && model_lanes(m) <= T && (m.fixed_base || T >= 6) &&   \
+   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ))
+
+// team size the dispatcher picks for a model (0: none fits)
+inline int team_size(const mg_model& m, int max_contacts) {
+#define MG_T(T, MN, MC, MG, MP, OBJ) \
+  if (MG_FITS(T, MN, MC, MG, MP, OBJ)) return T;
+  MG_INSTANCES(MG_T)
+#undef MG_T
+  return 0;
+}
+
+template <template <int, int, int, int, int, int> class F, typename... A>
+int dispatch(const mg_model& m, int max_contacts, A... args) {
+#define MG_TRY(T, MN, MC, MG, MP, OBJ)             \
+  if (MG_FITS(T, MN, MC, MG, MP, OBJ)) {           \
+    return F<T, MN, MC, MG, MP, OBJ>::run(args...); \
+  }
+  MG_INSTANCES(MG_TRY)
+#undef MG_TRY
+  return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
+}
+}  // namespace mgi

@@ -8,115 +8,35 @@
 #include <string>
 #include <vector>
 
-#include "../../include/migym.h"
+#include "dispatch.hpp"
 #include "hand_task.hpp"
 #include "task.hpp"
-#include "team_physics.hpp"
 
 namespace {
 thread_local std::string g_err;
-
-int fail(int code, const std::string& msg) {
+}  // namespace
+int mgi::fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+using mgi::fail;
+using mgi::kBlock;
+namespace {
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MG_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
   return MG_OK;
 }
-constexpr int kBlock = 64;
 inline int grid_for(int n) { return (n + kBlock - 1) / kBlock; }
-}  // namespace
 
-#ifdef MG_PHASE_TIMING
-// per-wave accumulators (one row of 16 per block; plain read-modify-writes by the block's own wave,
-// so the profiling build adds no atomic traffic that would slow the solver's memory path)
-constexpr int kPhaseCap = 1 << 16;  // blocks tracked
-__device__ unsigned long long* g_phase_buf;
-#define MG_PHASE_FLUSH(t)                                                              \
-  if (g_phase_buf && blockIdx.x < kPhaseCap && threadIdx.x < 16) {                     \
-    unsigned int v_ = 0;                                                               \
-    for (int i_ = 0; i_ < 16; i_++)                                                    \
-      if ((int)threadIdx.x == i_) v_ = (t).ph[i_];                                     \
-    g_phase_buf[16 * (size_t)blockIdx.x + threadIdx.x] += v_;                          \
-  }
-#else
-#define MG_PHASE_FLUSH(t)
-#endif
-
-struct mg_sim {
-  mg_model host_model;
-  mg_model* d_model;
-  mg_sim_params params;
-  int32_t n;        // actors
-  int32_t device;
-  mg_state_views views;
-  bool bound;
-};
-
-#ifndef MG_EXP
-#define MG_EXP 0  // profiling experiments only (phase attribution): skip parts of the hand post-physics
-#endif
-// ------------------------------------------------------------------------------------------------ kernels
-// gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
-// rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
-template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
-                                                     mg_state_views v, int n) {
-  constexpr int E = kBlock / T;
-  constexpr int ROWS = OBJ ? 3 : 1;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
-  __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
-  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::load_tile(&tile, m);
-  __syncthreads();
-  const int team = threadIdx.x / T;
-  const int a = blockIdx.x * E + team;
-  const bool valid = a < n;
-  const int ac = valid ? a : n - 1;
-  const int nd = m->num_dofs, ns = m->num_sensors;
-  mg::Team<T, MN, MC, MG, MP, OBJ> t;
-  t.init(&lds[team].v, &tile, m, &p);
-  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
-    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
-    t.drn = &drt[team].node[0][0];
-    t.drg = drt[team].geom;
-    t.drt = &drt[team].ten[0][0];
-    t.dro = drt[team].obj;
-  }
-  if (OBJ && t.tl < 4) {  // applied force on the object row of rb_forces (apply_rigid_body_force_tensors)
-    const float* fr = v.rb_forces ? v.rb_forces + ((size_t)(m->num_bodies + 2) * ac + m->num_bodies) * 3 : nullptr;
-    lds[team].v.oforce[t.tl] = t.tl < 3 ? (fr ? fr[t.tl] : 0.0f) : (v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f);
-  }
-  __syncthreads();
-  float* root = v.root_states + (size_t)13 * ROWS * ac;
-  t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
-         OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
-  for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(lds[team].v.u.sv.st.sens, lds[team].v.u.sv.st.dforce);
-  t.stage_state();
-  __syncthreads();
-  if (valid) {
-    mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team].v;
-    if (!m->fixed_base)
-      for (int k = t.tl; k < 13; k += T) root[k] = L.u.sv.st.root[k];
-    if (OBJ)
-      for (int k = t.tl; k < 13; k += T) root[13 + k] = L.oroot[k];
-    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.u.sv.st.dof[k];
-    if (v.sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.u.sv.st.sens[k];
-    if (v.dof_force)
-      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.u.sv.st.dforce[k];
-    if (v.rigid_body_states) {
-      const int nb = m->num_bodies, nbe = nb + (OBJ ? 2 : 0);
-      float* rb = v.rigid_body_states + (size_t)13 * nbe * a;
-      for (int b = t.tl; b < nb; b += T) t.body_state(b, rb + 13 * b);
-      if (OBJ)
-        for (int k = t.tl; k < 26; k += T) rb[13 * nb + k] = k < 13 ? L.oroot[k] : root[26 + k - 13];
-    }
-  }
+// publish the phase-timing buffer to every instance's code object
+template <int... I>
+int publish_all(unsigned long long* buf, std::integer_sequence<int, I...>) {
+  int rc = MG_OK;
+  ((rc = rc ? rc : mgi::phase_buf_publish<I>(buf)), ...);
+  return rc;
 }
+}  // namespace
 
 __global__ __launch_bounds__(kBlock) void k_observations(mg_task_params tp, int n, const float* __restrict__ root,
                                                          const float* __restrict__ dof, const float* __restrict__ dforce,
@@ -167,7 +87,7 @@ __device__ __forceinline__ void post_physics_env(const mg_task_params& tp, const
   float prev = tb.prev_potentials ? tb.prev_potentials[a] : 0.0f;
   if (do_reset) {
     mg::reset_env(&tp, off, tb.noise ? tb.noise + (size_t)2 * nd * a : nullptr, tb.seed,
-                  (uint64_t)(tb.env_offset + a), tb.step_counter, root, dof, &pot, &prev);
+                  (uint64_t)(tb.env_offset * A + a), tb.step_counter, root, dof, &pot, &prev);
     progress = 0;
     reset = 0;
   }
@@ -219,180 +139,6 @@ __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_s
   post_physics_env(tp, v, tb, e, act, tb.reset[e]);
 }
 
-// The whole VecTask.step for one actor, fused: clamp -> actuation -> simulate -> post_physics.
-// One team of T lanes per actor; the team leader (tl == 0) runs the task layer on the LDS-staged
-// state, the team writes it back to HBM.  Multi-agent: the agents of an env are consecutive
-// teams of one wave, so the AND-filter is a ballot over team leaders and the others-block a
-// shuffle from the other agents' leaders.
-// amdgpu_waves_per_eu(2): the register budget that lets two waves share a SIMD (the team kernels
-// are latency-bound; occupancy is the lever — DESIGN.md §3)
-template <int T, int MN, int MC, int MG, int MP, bool DR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
-                                                     mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n) {
-  constexpr int E = kBlock / T;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP> tile;
-  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::load_tile(&tile, m);
-  __syncthreads();
-  const int team = threadIdx.x / T;
-  const int a = blockIdx.x * E + team;
-  const bool valid = a < n;
-  const int ac = valid ? a : n - 1;
-  const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
-  mg::TeamLDS<T, MN, MC>& L = lds[team].v;
-  mg::Team<T, MN, MC, MG, MP> t;
-  t.init(&L, &tile, m, &p);
-  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
-    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
-    t.drn = &drt[team].node[0][0];
-    t.drg = drt[team].geom;
-    t.drt = &drt[team].ten[0][0];
-    t.dro = drt[team].obj;
-  }
-  __syncthreads();
-  const int64_t reset_in = tb.reset[ac];
-  t.ph_start();
-  // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
-  t.load(v.root_states + (size_t)13 * ac, v.dof_state + (size_t)2 * nd * ac, nullptr);
-  if (t.node > 0) {
-    const int d = t.node - 1;
-    float tau;
-    if (tp.task_id == MG_TASK_CARTPOLE) {
-      tau = d == 0 ? mg::clampf(tb.actions[(size_t)na * ac], tp.clip_actions) * tp.power_scale : 0.0f;
-    } else {
-      const float act = d < na ? mg::clampf(tb.actions[(size_t)na * ac + d], tp.clip_actions) : 0.0f;
-      tau = act * tp.motor_effort[d] * tp.power_scale;
-    }
-    t.tau = tau;
-    if (valid && v.dof_actuation) const_cast<float*>(v.dof_actuation)[(size_t)nd * a + d] = tau;
-  }
-  t.ph_mark(14);
-  for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
-  t.stage_state();
-  __syncthreads();
-  t.ph_mark(8);
-
-  // ---------------- post_physics_step (ant.py:287-297) on the staged state
-  const int A = tp.num_agents > 1 ? tp.num_agents : 1;
-  const int k = a % A;
-  const float* off = tp.agent_offset[k];
-  const int lane = threadIdx.x & 63;
-  bool do_reset = reset_in != 0;
-  if (A > 1) {  // AND filter over the env's agents (franka_reach_MA.py:875-885)
-    const unsigned long long mk = __ballot(t.tl == 0 && valid && reset_in != 0);
-    bool all = true;
-    for (int j = 0; j < A; j++) all = all && ((mk >> ((team - k + j) * T)) & 1ull);
-    do_reset = all;
-  }
-  float pot = 0.0f, prev = 0.0f, up[3] = {0, 0, 0}, hd[3] = {0, 0, 0};
-  int64_t progress = tb.progress[ac] + 1;
-  int64_t reset = reset_in;
-  // self.actions: one lane per action column (na <= T, checked by mg_env_step)
-  const bool alane = t.tl < na;
-  const float act_l = alane ? mg::clampf(tb.actions[(size_t)na * ac + t.tl], tp.clip_actions) : 0.0f;
-  if (valid && alane && tb.actions_out) tb.actions_out[(size_t)na * a + t.tl] = act_l;
-  if (tb.potentials) { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
-  if (do_reset) {  // reset_idx: one lane per DOF draws its noise; the leader resets root and potentials
-    const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr;
-    for (int i = t.tl; i < nd; i += T)
-      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset + a), tb.step_counter, L.u.sv.st.dof);
-    if (t.tl == 0) mg::reset_root(&tp, off, L.u.sv.st.root, &pot, &prev);
-    progress = 0;
-    reset = 0;
-  }
-  __syncthreads();
-  // observations staged in the row storage (dead after outputs()), then stored coalesced
-  const int no = tp.num_obs;
-  float* ost = &L.u.sv.rows[0].b;
-  if (tp.task_id == MG_TASK_CARTPOLE) {
-    if (t.tl < 4) ost[t.tl] = L.u.sv.st.dof[t.tl];
-  } else {
-    if (t.tl == 0) mg::obs_head(&tp, off, L.u.sv.st.root, &pot, &prev, up, hd, ost);
-    const bool hum = tp.task_id == MG_TASK_HUMANOID;
-    for (int q = t.tl; q < nd; q += T) {
-      ost[12 + q] = mg::t_unscale(L.u.sv.st.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
-      ost[12 + nd + q] = L.u.sv.st.dof[2 * q + 1] * tp.dof_vel_scale;
-      if (hum) ost[12 + 2 * nd + q] = L.u.sv.st.dforce[q] * tp.contact_force_scale;
-    }
-    const int bs = 12 + (hum ? 3 : 2) * nd, nss = mg::t_sensors(&tp);
-    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.u.sv.st.sens[q] * tp.contact_force_scale;
-    if (alane) ost[bs + 6 * nss + t.tl] = act_l;
-  }
-  if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
-    const float px = L.u.sv.st.root[0], py = L.u.sv.st.root[1], pz = L.u.sv.st.root[2];
-    const int base = no - 3 * (A - 1);
-    for (int j = 1; j < A; j++) {
-      const int src = (team - k + (k + j) % A) * T;
-      const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
-      if (t.tl == 0) {
-        ost[base + 3 * (j - 1) + 0] = qx - px;
-        ost[base + 3 * (j - 1) + 1] = qy - py;
-        ost[base + 3 * (j - 1) + 2] = qz - pz;
-      }
-    }
-  }
-  __syncthreads();
-  // reward: per-action terms as team sums (DPP), the rest on the leader
-  float rew = 0.0f;
-  if (tp.task_id == MG_TASK_CARTPOLE) {
-    if (t.tl == 0) mg::reward_env(&tp, ost, &act_l, pot, prev, progress, &reset, &rew);
-  } else {
-    float ac2 = act_l * act_l, el = 0.0f, lim = 0.0f;
-    if (alane) {
-      if (tp.task_id == MG_TASK_ANT) {
-        el = fabsf(act_l * ost[12 + nd + t.tl]);
-        lim = ost[12 + t.tl] > 0.99f ? 1.0f : 0.0f;
-      } else {
-        const float ratio = tp.motor_effort[t.tl] / tp.max_motor_effort;
-        const float ab = fabsf(ost[12 + t.tl]);
-        const float scaled = tp.joints_at_limit_cost_scale * (ab - 0.98f) / 0.02f;
-        lim = (ab > 0.98f ? 1.0f : 0.0f) * scaled * ratio;
-        el = fabsf(act_l * ost[12 + nd + t.tl]) * ratio;
-      }
-    }
-    ac2 = mg::team_sum<T>(ac2, t.tb);
-    el = mg::team_sum<T>(el, t.tb);
-    lim = mg::team_sum<T>(lim, t.tb);
-    if (tp.task_id == MG_TASK_ANT) lim = lim * tp.joints_at_limit_cost_scale;
-    if (t.tl == 0) mg::reward_from_sums(&tp, ost, ac2, el, lim, pot, prev, progress, &reset, &rew);
-  }
-  if (t.tl == 0 && valid) {
-    const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
-    tb.rew[a] = rew;
-    tb.reset[a] = reset;
-    tb.progress[a] = progress;
-    tb.timeout[a] = (uint8_t)(((float)progress >= max_ep_m1) && (reset != 0));
-    if (tp.task_id != MG_TASK_CARTPOLE) {
-      tb.potentials[a] = pot;
-      tb.prev_potentials[a] = prev;
-      for (int c = 0; c < 3; c++) {
-        tb.up_vec[3 * (size_t)a + c] = up[c];
-        tb.heading_vec[3 * (size_t)a + c] = hd[c];
-      }
-    }
-  }
-  if (valid) {
-    float* o = tb.obs + (size_t)no * a;
-    for (int q = t.tl; q < no; q += T) {
-      o[q] = ost[q];
-      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(ost[q], tp.clip_obs);
-    }
-  }
-  __syncthreads();
-  if (valid) {  // state write-back (gym layouts), team-cooperative
-    if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
-      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
-    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.u.sv.st.dof[q];
-    if (v.sensors)
-      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.u.sv.st.sens[q];
-    if (v.dof_force)
-      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
-  }
-  t.ph_mark(9);
-  MG_PHASE_FLUSH(t)
-}
 
 // pre_physics_step of the locomotion tasks: effort = clamp(a) * gear * power_scale
 // (ant.py:281-285, humanoid.py:281-285; cartpole.py:159-163: DOF 0 only)
@@ -411,13 +157,6 @@ __global__ __launch_bounds__(kBlock) void k_pre_loco(mg_task_params tp, mg_state
   const_cast<float*>(v.dof_actuation)[t] = tau;
 }
 
-// ------------------------------------------------------------------------------------------------ hand tasks
-// index of DOF d in the actuated list (action column), -1 if not actuated
-__device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
-  for (int i = 0; i < tp.num_actions; i++)
-    if (tp.actuated_dof[i] == d) return i;
-  return -1;
-}
 
 // pre_physics_step of one env on one lane (physics-free path, shadow_hand.py:670-698)
 __global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
@@ -555,216 +294,6 @@ __global__ void k_hand_finalize(mg_task_params tp, mg_task_buffers tb) {
   tb.reduce_scratch[1] = 0;
 }
 
-// The whole ShadowHand VecTask.step for one env, fused: pre_physics_step (masked goal / env resets,
-// PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
-// the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
-template <int T, int MN, int MC, int MG, int MP, int OT, bool DR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
-                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb,
-                                                      int n) {
-  constexpr int E = kBlock / T;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
-  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::load_tile(&tile, m);
-  __syncthreads();
-  const int team = threadIdx.x / T;
-  const int e = blockIdx.x * E + team;
-  const bool valid = e < n;
-  const int ec = valid ? e : n - 1;
-  const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
-  const int nb = m->num_bodies, nbe = nb + 2;
-  mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
-  mg::Team<T, MN, MC, MG, MP, OT> t;
-  t.init(&L, &tile, m, &p);
-  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
-    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
-    t.drn = &drt[team].node[0][0];
-    t.drg = drt[team].geom;
-    t.drt = &drt[team].ten[0][0];
-    t.dro = drt[team].obj;
-  }
-  t.ph_start();
-  const uint64_t gid = (uint64_t)(tb.env_offset + ec);
-  const bool env_reset = tb.reset[ec] != 0, goal_reset = tb.reset_goal[ec] != 0;
-  float* root = v.root_states + (size_t)39 * ec;
-  // ---- pre_physics_step: goal / object resets staged in LDS by the team leader
-  if (t.tl == 0) {
-    float* gr = L.goal;
-    float* gs = L.goal + 13;
-    if (env_reset || goal_reset) {
-      const int c0 = env_reset ? 57 : 0;  // env reset: reset_idx's own reset_target_pose draw wins
-      mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, c0)),
-                       mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, c0 + 1)), gs, gr);
-      for (int k = 7; k < 13; k++) gs[k] = tb.goal_states[(size_t)13 * ec + k];
-    } else {
-      for (int k = 0; k < 13; k++) { gr[k] = root[26 + k]; gs[k] = tb.goal_states[(size_t)13 * ec + k]; }
-    }
-    // random object forces: reset_idx zeroes / redraws the probability, pre_physics_step decays / draws
-    float f[3] = {0.0f, 0.0f, 0.0f};
-    if (v.rb_forces || tb.random_force_prob) {
-      const float* fr = v.rb_forces ? v.rb_forces + ((size_t)nbe * ec + nb) * 3 : nullptr;
-      if (fr)
-        for (int k = 0; k < 3; k++) f[k] = fr[k];
-      if (valid) mg::h_object_force(tp, tb, ec, gid, env_reset, f);
-    }
-    for (int k = 0; k < 3; k++) L.oforce[k] = f[k];
-    L.oforce[3] = v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f;
-    if (env_reset) {
-      float r[5];
-      for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 4 + k));
-      for (int k = 0; k < 3; k++) L.oroot[k] = tp.object_start[k] + tp.reset_position_noise * r[k];
-      mg::h_object_reset_rotation(tp, r[3], r[4], L.oroot + 3);
-      for (int k = 7; k < 13; k++) L.oroot[k] = 0.0f;
-    } else {
-      for (int k = 0; k < 13; k++) L.oroot[k] = root[13 + k];
-    }
-  }
-  __syncthreads();
-  t.load(root, v.dof_state + (size_t)2 * nd * ec, nullptr, L.oroot, nullptr);
-  float prev = 0.0f;
-  if (t.node > 0) {  // DOF lanes: reset_idx's DOF draw, then actions -> PD targets
-    const int d = t.node - 1;
-    float cur;
-    if (env_reset) {
-      const float rp = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 9 + d));
-      const float rv = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 9 + nd + d));
-      const float dmax = tp.dof_upper[d] - tp.initial_dof_pos[d], dmin = tp.dof_lower[d] - tp.initial_dof_pos[d];
-      const float pos = tp.initial_dof_pos[d] + tp.reset_dof_pos_noise * (dmin + (dmax - dmin) * 0.5f * (rp + 1.0f));
-      t.qj = pos;
-      t.nu = 0.0f + tp.reset_dof_vel_noise * rv;
-      prev = pos;
-      cur = pos;
-    } else {
-      prev = tb.prev_targets[(size_t)nd * ec + d];
-      cur = v.dof_targets[(size_t)nd * ec + d];
-    }
-    const int ai = hand_action_of(tp, d);
-    if (ai >= 0) {
-      const float a = mg::clampf(tb.actions[(size_t)na * ec + ai], tp.clip_actions);
-      cur = mg::h_target(tp, d, a, prev);
-      prev = cur;
-    }
-    t.tgt = cur;
-  }
-  // ---- gym.simulate
-  t.ph_mark(14);
-  for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
-  t.stage_state();
-  __syncthreads();
-  t.ph_mark(8);
-  // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
-  const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
-  float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
-  // rigid-body states of the hand once (one lane per body) into the dead row storage: the fingertip
-  // observations and the rigid_body_states write-back both read them
-  float* bst = &L.u.sv.rows[0].b;
-#if !(MG_EXP & 1)
-  for (int b = t.tl; b < nb; b += T) t.body_state(b, bst + 13 * b);
-#endif
-  __syncthreads();
-#if !(MG_EXP & 2)
-  {
-    const float* gs = L.goal + 13;
-    float qdiff[4];
-    const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
-    mg::t_quat_mul(L.oroot + 3, gc, qdiff);
-    for (int k = t.tl; k < no; k += T) {
-      const int mk = tp.obs_map[k], seg = mk >> 8, i = mk & 255;   // column -> (segment, index)
-      float x;
-      if (seg == mg::HS_ACTIONS) {  // self.actions (clamped)
-        x = mg::clampf(tb.actions[(size_t)na * ec + i], tp.clip_actions);
-      } else if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {  // fingertip state from the post-step FK
-        int b, c;
-        mg::h_ft_ref(tp, seg, i, &b, &c);
-        x = bst[13 * b + c];
-      } else {
-        x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
-      }
-      L.obs[k] = x;
-    }
-  }
-#endif
-  __syncthreads();
-  int64_t ro = 0;
-  float fin = 0.0f;
-  if (!(MG_EXP & 4) && t.tl == 0) {
-    const float* gs = L.goal + 13;
-    float succ = env_reset ? 0.0f : tb.successes[ec], rew;
-    int64_t prog = progress_in + 1, go;
-    mg::h_reward(tp, L.oroot, L.oroot + 3, gs, gs + 3, L.obs + (no - na), 0, 0, &prog, &succ, &rew, &ro, &go);
-    if (valid) {
-      tb.rew[e] = rew;
-      tb.reset[e] = ro;
-      tb.reset_goal[e] = go;
-      tb.progress[e] = prog;
-      tb.successes[e] = succ;
-      tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
-      fin = succ * (float)ro;
-    } else {
-      ro = 0;
-    }
-  }
-  // partial sums of the global running mean: wave reduce, one atomic pair per wave
-  unsigned long long cr = (unsigned long long)ro, cf = (unsigned long long)fin;
-  for (int off = 32; off >= 1; off >>= 1) {
-    cr += __shfl_xor(cr, off);
-    cf += __shfl_xor(cf, off);
-  }
-  if (threadIdx.x == 0 && (cr | cf)) {
-    atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
-    atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
-  }
-  if (!(MG_EXP & 8) && valid) {  // write-back (gym layouts), team-cooperative
-    float* o = tb.obs + (size_t)no * e;
-    for (int k = t.tl; k < no; k += T) {
-      o[k] = L.obs[k];
-      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(L.obs[k], tp.clip_obs);
-    }
-    if (tb.actions_out)
-      for (int k = t.tl; k < na; k += T) tb.actions_out[(size_t)na * e + k] = L.obs[no - na + k];
-    for (int k = t.tl; k < 13; k += T) {
-      root[13 + k] = L.oroot[k];
-      root[26 + k] = L.goal[k];
-      tb.goal_states[(size_t)13 * e + k] = L.goal[13 + k];
-    }
-    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.u.sv.st.dof[k];
-    if (t.node > 0) {
-      const int d = t.node - 1;
-      const_cast<float*>(v.dof_targets)[(size_t)nd * e + d] = t.tgt;
-      tb.prev_targets[(size_t)nd * e + d] = prev;
-    }
-    if (v.sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.u.sv.st.sens[k];
-    if (v.dof_force)
-      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.u.sv.st.dforce[k];
-    for (int k = t.tl; k < 13 * nb; k += T) rbs[k] = bst[k];
-    for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
-    if (v.rb_forces && t.tl < 3) v.rb_forces[((size_t)nbe * e + nb) * 3 + t.tl] = L.oforce[t.tl];
-    if (tb.states) {  // asymmetric_observations: the full_state layout (compute_full_state(asymm_obs=True))
-      const float* gs = L.goal + 13;
-      float qdiff[4];
-      const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
-      mg::t_quat_mul(L.oroot + 3, gc, qdiff);
-      for (int k = t.tl; k < tp.num_states; k += T) {
-        const int mk = tp.state_map[k], seg = mk >> 8, i = mk & 255;
-        float x;
-        if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
-          int b, c;
-          mg::h_ft_ref(tp, seg, i, &b, &c);
-          x = bst[13 * b + c];
-        } else {
-          x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
-                              L.obs + (no - na));
-        }
-        tb.states[(size_t)tp.num_states * e + k] = x;
-      }
-    }
-  }
-  t.ph_mark(9);
-  MG_PHASE_FLUSH(t)
-}
 
 __global__ void k_set_indexed(float* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
                               int nidx, int row, int div) {
@@ -883,91 +412,6 @@ __global__ __launch_bounds__(kBlock) void k_dr_noise(mg_dr_noise_args a) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------ dispatch
-// Kernel instances by capacity: team size T (>= velocity columns, nodes and sensors), nodes MN,
-// contacts MC, geoms MG, self pairs MP, OBJ = the free object's type in hand-task envs (0: none; one
-// instance per object shape, so the block's kernel carries no egg / pen code).  The smallest
-// instance that fits the model is launched.
-#define MG_INSTANCES(X)                                                                                     \
-  X(8, 4, 8, 4, 0, false) X(16, 9, 16, 16, 0, false) X(16, 16, 24, 24, 32, false) X(32, 24, 32, 24, 160, false) \
-  X(32, 32, 48, 48, 192, false) X(64, 40, 48, 48, 192, false) X(32, 25, 24, 24, 0, MG_GT_BOX)               \
-  X(32, 25, 24, 24, 0, MG_GT_CAPSULE) X(32, 25, 24, 24, 0, MG_GT_ELLIPSOID)
-
-static int model_lanes(const mg_model& m) {
-  const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs + (m.obj_type ? 6 : 0);
-  return nv > m.num_sensors ? nv : m.num_sensors;
-}
-#define MG_FITS(T, MN, MC, MG, MP, OBJ)                                                                    \
-  (m.num_nodes <= MN && max_contacts <= MC && model_lanes(m) <= T && (m.fixed_base || T >= 6) &&        \
-   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ))
-
-// team size the dispatcher picks for a model (0: none fits)
-static int team_size(const mg_model& m, int max_contacts) {
-#define MG_T(T, MN, MC, MG, MP, OBJ) \
-  if (MG_FITS(T, MN, MC, MG, MP, OBJ)) return T;
-  MG_INSTANCES(MG_T)
-#undef MG_T
-  return 0;
-}
-
-template <template <int, int, int, int, int, int> class F, typename... A>
-static int dispatch(const mg_model& m, int max_contacts, A... args) {
-#define MG_TRY(T, MN, MC, MG, MP, OBJ)             \
-  if (MG_FITS(T, MN, MC, MG, MP, OBJ)) {           \
-    return F<T, MN, MC, MG, MP, OBJ>::run(args...); \
-  }
-  MG_INSTANCES(MG_TRY)
-#undef MG_TRY
-  return fail(MG_ECAPACITY, "model exceeds the largest kernel instance");
-}
-
-template <int T, int MN, int MC, int MG, int MP, int OBJ>
-struct RunSimulate {
-  static int run(hipStream_t s, const mg_sim* sim) {
-    const int E = kBlock / T;
-    // the domain-randomized instance reads each actor's env_props row (mg_dr_apply)
-    if (sim->views.env_props)
-      hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                         sim->d_model, sim->params, sim->views, sim->n);
-    else
-      hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                         sim->d_model, sim->params, sim->views, sim->n);
-    return MG_OK;
-  }
-};
-template <int T, int MN, int MC, int MG, int MP, int OBJ>
-struct RunEnvStep {
-  static int run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb) {
-    const int E = kBlock / T;
-    // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
-    if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
-      return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
-    // hand tasks stage the rigid-body states of the articulation in the same storage
-    if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(mg::TeamLDS<T, MN, MC, OBJ>::u.sv.rows))
-      return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
-    if constexpr (OBJ) {
-      mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
-      mg::h_fill_maps(&tpm);
-      tp = &tpm;
-      if (sim->views.env_props)
-        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
-      else
-        hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
-      hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, s, *tp, *tb);
-    } else {
-      if (sim->views.env_props)
-        hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
-      else
-        hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                           sim->d_model, sim->params, *tp, sim->views, *tb, sim->n);
-    }
-    return MG_OK;
-  }
-};
-
 // ------------------------------------------------------------------------------------------------ C ABI
 extern "C" {
 
@@ -988,12 +432,13 @@ size_t mg_dr_noise_args_sizeof(void) { return sizeof(mg_dr_noise_args); }
 // write-back, 13 constraint rows (count), 14 load + pre-physics, 15 substep entry.
 int mg_debug_phase_cycles(uint64_t* out16, int32_t reset) {
 #ifdef MG_PHASE_TIMING
+  constexpr int kPhaseCap = 1 << 16;  // blocks tracked (step_kernels.hpp)
   static unsigned long long* buf = nullptr;
   const size_t bytes = (size_t)kPhaseCap * 16 * sizeof(unsigned long long);
   if (!buf) {  // first call: allocate + zero the per-wave rows and publish them to the kernels
-    if (hipMalloc(&buf, bytes) != hipSuccess || hipMemset(buf, 0, bytes) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(g_phase_buf), &buf, sizeof(buf)) != hipSuccess)
+    if (hipMalloc(&buf, bytes) != hipSuccess || hipMemset(buf, 0, bytes) != hipSuccess)
       return fail(MG_EDEVICE, "mg_debug_phase_cycles: buffer setup failed");
+    if (int rc = publish_all(buf, std::make_integer_sequence<int, MG_NUM_INST>{})) return rc;
     if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
     if (out16) memset(out16, 0, 16 * sizeof(uint64_t));
     return MG_OK;
@@ -1062,7 +507,7 @@ int mg_sim_bind(mg_sim* sim, const mg_state_views* views) {
 
 int mg_sim_simulate(mg_sim* sim, void* stream) {
   if (!sim || !sim->bound) return fail(MG_EINVAL, "mg_sim_simulate: sim not bound");
-  int rc = dispatch<RunSimulate>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
+  int rc = mgi::dispatch<mgi::RunSimulate>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
                                  (const mg_sim*)sim);
   if (rc) return rc;
   return check_launch("mg_sim_simulate");
@@ -1189,6 +634,9 @@ static int hand_args_ok(const mg_task_params* tp, const mg_state_views& v, const
                                               "dof_force and the hand task buffers");
   if (tp->num_dofs <= 0 || tp->num_dofs > MG_MAX_HAND_DOFS || tp->num_actions > MG_MAX_HAND_DOFS)
     return fail(MG_EINVAL, std::string(who) + ": bad hand DOF / action count");
+  // obs_map / state_map hold 256 columns; the fused kernel's LDS row holds 212 (checked at launch)
+  if (tp->num_obs <= 0 || tp->num_obs > 256 || tp->num_states < 0 || tp->num_states > 256)
+    return fail(MG_EINVAL, std::string(who) + ": bad hand observation / state count");
   return MG_OK;
 }
 
@@ -1223,6 +671,7 @@ int mg_pre_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* 
 int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views, const mg_task_buffers* tb,
                     int32_t n, void* stream) {
   if (!tp || !tb) return fail(MG_EINVAL, "mg_post_physics: bad args");
+  if (tp->num_actions > 64) return fail(MG_EINVAL, "mg_post_physics: num_actions > 64");
   if (tp->num_agents > 1 && (64 % tp->num_agents != 0 || tp->num_agents > MG_MAX_AGENTS ||
                              (sim ? sim->n : n) % tp->num_agents != 0))
     return fail(MG_EINVAL, "mg_post_physics: num_agents must divide 64 and the actor count");
@@ -1248,7 +697,8 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
   return check_launch("mg_post_physics");
 }
 
-int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {
+static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
+                    void* stream) {
   if (!sim || !sim->bound || !tp || !tb || !tb->actions || !tb->obs || !tb->rew || !tb->reset || !tb->progress ||
       !tb->timeout)
     return fail(MG_EINVAL, "mg_env_step: bad arguments");
@@ -1265,21 +715,38 @@ int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb
       return fail(MG_EINVAL, "mg_env_step: locomotion task needs potential/up/heading buffers");
     if (tp->num_actions > sim->host_model.num_nodes && tp->task_id != MG_TASK_CARTPOLE)
       return fail(MG_EINVAL, "mg_env_step: more actions than DOFs");
-    if (tp->num_actions > team_size(sim->host_model, sim->params.max_contacts))
+    if (tp->num_actions > mgi::team_size(sim->host_model, sim->params.max_contacts))
       return fail(MG_EINVAL, "mg_env_step: more actions than lanes per actor");
   }
   if (tp->num_agents > 1) {
     // the agents of an env must be teams of one wave (ballot/shuffle exchange): A | 64/T
-    const int T = team_size(sim->host_model, sim->params.max_contacts);
+    const int T = mgi::team_size(sim->host_model, sim->params.max_contacts);
     if (T == 0 || tp->num_agents > MG_MAX_AGENTS || (64 / T) % tp->num_agents != 0 ||
         sim->n % tp->num_agents != 0)
       return fail(MG_EINVAL, "mg_env_step: num_agents must divide the envs per wave (64 / team size) "
                              "and the actor count");
   }
-  int rc = dispatch<RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream, (const mg_sim*)sim,
-                                tp, tb);
+  if (tp->num_actions > 64 || tp->num_obs > 256 || tp->num_states > 256)
+    return fail(MG_EINVAL, "mg_env_step: num_actions > 64, num_obs > 256 or num_states > 256");
+  int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
+                                          (const mg_sim*)sim, tp, tb, rp);
   if (rc) return rc;
-  return check_launch("mg_env_step");
+  if (hand)  // consecutive_successes running mean from the step's partial sums
+    hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
+  return check_launch(rp ? "mg_env_step_replay" : "mg_env_step");
 }
+
+int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {
+  return env_step(sim, tp, tb, nullptr, stream);
+}
+
+int mg_env_step_replay(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
+                       void* stream) {
+  if (!rp || !rp->dof_state) return fail(MG_EINVAL, "mg_env_step_replay: bad replay state");
+  if (sim && sim->host_model.obj_type && (!rp->root_states || !rp->rigid_body_states))
+    return fail(MG_EINVAL, "mg_env_step_replay: hand tasks need root and rigid-body states");
+  return env_step(sim, tp, tb, rp, stream);
+}
+
 
 }  // extern "C"

@@ -1,0 +1,592 @@
+// step_kernels.hpp — the team kernels of the hot path (one team of T lanes per actor):
+//   k_simulate   gym.simulate alone
+//   k_env_step   the whole VecTask.step of the locomotion tasks (Ant, Humanoid, Cartpole, MA-Ant)
+//   k_hand_step  the whole VecTask.step of ShadowHand
+// plus the host launchers RunSimulate / RunEnvStep (dispatch.hpp).  Included only by inst.hip, which
+// instantiates one capacity instance per translation unit.
+#pragma once
+#include "dispatch.hpp"
+#include "hand_task.hpp"
+#include "task.hpp"
+#include "team_physics.hpp"
+
+namespace mgi {
+#ifdef MG_PHASE_TIMING
+// per-wave accumulators (one row of 16 per block; plain read-modify-writes by the block's own wave,
+// so the profiling build adds no atomic traffic that would slow the solver's memory path)
+constexpr int kPhaseCap = 1 << 16;  // blocks tracked
+// one copy per instance translation unit (each is its own code object): phase_buf_publish<I> sets it
+static __device__ unsigned long long* g_phase_buf;
+#define MG_PHASE_FLUSH(t)                                                              \
+  if (g_phase_buf && blockIdx.x < kPhaseCap && threadIdx.x < 16) {                     \
+    unsigned int v_ = 0;                                                               \
+    for (int i_ = 0; i_ < 16; i_++)                                                    \
+      if ((int)threadIdx.x == i_) v_ = (t).ph[i_];                                     \
+    g_phase_buf[16 * (size_t)blockIdx.x + threadIdx.x] += v_;                          \
+  }
+#else
+#define MG_PHASE_FLUSH(t)
+#endif
+
+#ifndef MG_EXP
+#define MG_EXP 0  // profiling experiments only (phase attribution): skip parts of the hand post-physics
+#endif
+// ------------------------------------------------------------------------------------------------ kernels
+// gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
+// rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
+template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
+                                                     mg_state_views v, int n) {
+  constexpr int E = kBlock / T;
+  constexpr int ROWS = OBJ ? 3 : 1;
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
+  __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  mg::load_tile(&tile, m);
+  __syncthreads();
+  const int team = threadIdx.x / T;
+  const int a = blockIdx.x * E + team;
+  const bool valid = a < n;
+  const int ac = valid ? a : n - 1;
+  const int nd = m->num_dofs, ns = m->num_sensors;
+  mg::Team<T, MN, MC, MG, MP, OBJ> t;
+  t.init(&lds[team].v, &tile, m, &p);
+  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
+    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
+    t.drn = &drt[team].node[0][0];
+    t.drg = drt[team].geom;
+    t.drt = &drt[team].ten[0][0];
+    t.dro = drt[team].obj;
+  }
+  if (OBJ && t.tl < 4) {  // applied force on the object row of rb_forces (apply_rigid_body_force_tensors)
+    const float* fr = v.rb_forces ? v.rb_forces + ((size_t)(m->num_bodies + 2) * ac + m->num_bodies) * 3 : nullptr;
+    lds[team].v.oforce[t.tl] = t.tl < 3 ? (fr ? fr[t.tl] : 0.0f) : (v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f);
+  }
+  __syncthreads();
+  float* root = v.root_states + (size_t)13 * ROWS * ac;
+  t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
+         OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
+  for (int st = 0; st < p.substeps; st++) t.substep();
+  t.outputs(lds[team].v.u.sv.st.sens, lds[team].v.u.sv.st.dforce);
+  t.stage_state();
+  __syncthreads();
+  if (valid) {
+    mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team].v;
+    if (!m->fixed_base)
+      for (int k = t.tl; k < 13; k += T) root[k] = L.u.sv.st.root[k];
+    if (OBJ)
+      for (int k = t.tl; k < 13; k += T) root[13 + k] = L.oroot[k];
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.u.sv.st.dof[k];
+    if (v.sensors)
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.u.sv.st.sens[k];
+    if (v.dof_force)
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.u.sv.st.dforce[k];
+    if (v.rigid_body_states) {
+      const int nb = m->num_bodies, nbe = nb + (OBJ ? 2 : 0);
+      float* rb = v.rigid_body_states + (size_t)13 * nbe * a;
+      for (int b = t.tl; b < nb; b += T) t.body_state(b, rb + 13 * b);
+      if (OBJ)
+        for (int k = t.tl; k < 26; k += T) rb[13 * nb + k] = k < 13 ? L.oroot[k] : root[26 + k - 13];
+    }
+  }
+}
+
+// The whole VecTask.step for one actor, fused: clamp -> actuation -> simulate -> post_physics.
+// One team of T lanes per actor; the team leader (tl == 0) runs the task layer on the LDS-staged
+// state, the team writes it back to HBM.  Multi-agent: the agents of an env are consecutive
+// teams of one wave, so the AND-filter is a ballot over team leaders and the others-block a
+// shuffle from the other agents' leaders.
+// amdgpu_waves_per_eu(2): the register budget that lets two waves share a SIMD (the team kernels
+// are latency-bound; occupancy is the lever — DESIGN.md §3)
+// RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
+// post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
+template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
+                                                     mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n,
+                                                     mg_replay rp) {
+  constexpr int E = kBlock / T;
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  mg::load_tile(&tile, m);
+  __syncthreads();
+  const int team = threadIdx.x / T;
+  const int a = blockIdx.x * E + team;
+  const bool valid = a < n;
+  const int ac = valid ? a : n - 1;
+  const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
+  mg::TeamLDS<T, MN, MC>& L = lds[team].v;
+  mg::Team<T, MN, MC, MG, MP> t;
+  t.init(&L, &tile, m, &p);
+  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
+    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
+    t.drn = &drt[team].node[0][0];
+    t.drg = drt[team].geom;
+    t.drt = &drt[team].ten[0][0];
+    t.dro = drt[team].obj;
+  }
+  __syncthreads();
+  const int64_t reset_in = tb.reset[ac];
+  t.ph_start();
+  // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
+  t.load(v.root_states + (size_t)13 * ac, v.dof_state + (size_t)2 * nd * ac, nullptr);
+  if (t.node > 0) {
+    const int d = t.node - 1;
+    float tau;
+    if (tp.task_id == MG_TASK_CARTPOLE) {
+      tau = d == 0 ? mg::clampf(tb.actions[(size_t)na * ac], tp.clip_actions) * tp.power_scale : 0.0f;
+    } else {
+      const float act = d < na ? mg::clampf(tb.actions[(size_t)na * ac + d], tp.clip_actions) : 0.0f;
+      tau = act * tp.motor_effort[d] * tp.power_scale;
+    }
+    t.tau = tau;
+    if (valid && v.dof_actuation) const_cast<float*>(v.dof_actuation)[(size_t)nd * a + d] = tau;
+  }
+  t.ph_mark(14);
+  if constexpr (RP) {  // gym.simulate replaced by the injected post-simulate state
+    const float* rr = rp.root_states ? rp.root_states : v.root_states;
+    for (int q = t.tl; q < 13; q += T) L.u.sv.st.root[q] = rr[(size_t)13 * ac + q];
+    for (int q = t.tl; q < 2 * nd; q += T) L.u.sv.st.dof[q] = rp.dof_state[(size_t)2 * nd * ac + q];
+    for (int q = t.tl; q < 6 * ns; q += T) L.u.sv.st.sens[q] = rp.sensors ? rp.sensors[(size_t)6 * ns * ac + q] : 0.0f;
+    for (int q = t.tl; q < nd; q += T) L.u.sv.st.dforce[q] = rp.dof_force ? rp.dof_force[(size_t)nd * ac + q] : 0.0f;
+  } else {
+    // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
+    const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
+    for (int st = 0; st < nsub; st++) t.substep();
+    t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
+    t.stage_state();
+  }
+  __syncthreads();
+  t.ph_mark(8);
+
+  // ---------------- post_physics_step (ant.py:287-297) on the staged state
+  const int A = tp.num_agents > 1 ? tp.num_agents : 1;
+  const int k = a % A;
+  const float* off = tp.agent_offset[k];
+  const int lane = threadIdx.x & 63;
+  bool do_reset = reset_in != 0;
+  if (A > 1) {  // AND filter over the env's agents (franka_reach_MA.py:875-885)
+    const unsigned long long mk = __ballot(t.tl == 0 && valid && reset_in != 0);
+    bool all = true;
+    for (int j = 0; j < A; j++) all = all && ((mk >> ((team - k + j) * T)) & 1ull);
+    do_reset = all;
+  }
+  float pot = 0.0f, prev = 0.0f, up[3] = {0, 0, 0}, hd[3] = {0, 0, 0};
+  int64_t progress = tb.progress[ac] + 1;
+  int64_t reset = reset_in;
+  // self.actions: one lane per action column (na <= T, checked by mg_env_step)
+  const bool alane = t.tl < na;
+  const float act_l = alane ? mg::clampf(tb.actions[(size_t)na * ac + t.tl], tp.clip_actions) : 0.0f;
+  if (valid && alane && tb.actions_out) tb.actions_out[(size_t)na * a + t.tl] = act_l;
+  if (tb.potentials) { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
+  if (do_reset) {  // reset_idx: one lane per DOF draws its noise; the leader resets root and potentials
+    const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr;
+    for (int i = t.tl; i < nd; i += T)
+      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset * A + a), tb.step_counter, L.u.sv.st.dof);
+    if (t.tl == 0) mg::reset_root(&tp, off, L.u.sv.st.root, &pot, &prev);
+    progress = 0;
+    reset = 0;
+  }
+  __syncthreads();
+  // observations staged in the row storage (dead after outputs()), then stored coalesced
+  const int no = tp.num_obs;
+  float* ost = &L.u.sv.rows[0].b;
+  if (tp.task_id == MG_TASK_CARTPOLE) {
+    if (t.tl < 4) ost[t.tl] = L.u.sv.st.dof[t.tl];
+  } else {
+    if (t.tl == 0) mg::obs_head(&tp, off, L.u.sv.st.root, &pot, &prev, up, hd, ost);
+    const bool hum = tp.task_id == MG_TASK_HUMANOID;
+    for (int q = t.tl; q < nd; q += T) {
+      ost[12 + q] = mg::t_unscale(L.u.sv.st.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
+      ost[12 + nd + q] = L.u.sv.st.dof[2 * q + 1] * tp.dof_vel_scale;
+      if (hum) ost[12 + 2 * nd + q] = L.u.sv.st.dforce[q] * tp.contact_force_scale;
+    }
+    const int bs = 12 + (hum ? 3 : 2) * nd, nss = mg::t_sensors(&tp);
+    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.u.sv.st.sens[q] * tp.contact_force_scale;
+    if (alane) ost[bs + 6 * nss + t.tl] = act_l;
+  }
+  if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
+    const float px = L.u.sv.st.root[0], py = L.u.sv.st.root[1], pz = L.u.sv.st.root[2];
+    const int base = no - 3 * (A - 1);
+    for (int j = 1; j < A; j++) {
+      const int src = (team - k + (k + j) % A) * T;
+      const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
+      if (t.tl == 0) {
+        ost[base + 3 * (j - 1) + 0] = qx - px;
+        ost[base + 3 * (j - 1) + 1] = qy - py;
+        ost[base + 3 * (j - 1) + 2] = qz - pz;
+      }
+    }
+  }
+  __syncthreads();
+  // reward: per-action terms as team sums (DPP), the rest on the leader
+  float rew = 0.0f;
+  if (tp.task_id == MG_TASK_CARTPOLE) {
+    if (t.tl == 0) mg::reward_env(&tp, ost, &act_l, pot, prev, progress, &reset, &rew);
+  } else {
+    float ac2 = act_l * act_l, el = 0.0f, lim = 0.0f;
+    if (alane) {
+      if (tp.task_id == MG_TASK_ANT) {
+        el = fabsf(act_l * ost[12 + nd + t.tl]);
+        lim = ost[12 + t.tl] > 0.99f ? 1.0f : 0.0f;
+      } else {
+        const float ratio = tp.motor_effort[t.tl] / tp.max_motor_effort;
+        const float ab = fabsf(ost[12 + t.tl]);
+        const float scaled = tp.joints_at_limit_cost_scale * (ab - 0.98f) / 0.02f;
+        lim = (ab > 0.98f ? 1.0f : 0.0f) * scaled * ratio;
+        el = fabsf(act_l * ost[12 + nd + t.tl]) * ratio;
+      }
+    }
+    ac2 = mg::team_sum<T>(ac2, t.tb);
+    el = mg::team_sum<T>(el, t.tb);
+    lim = mg::team_sum<T>(lim, t.tb);
+    if (tp.task_id == MG_TASK_ANT) lim = lim * tp.joints_at_limit_cost_scale;
+    if (t.tl == 0) mg::reward_from_sums(&tp, ost, ac2, el, lim, pot, prev, progress, &reset, &rew);
+  }
+  if (t.tl == 0 && valid) {
+    const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
+    tb.rew[a] = rew;
+    tb.reset[a] = reset;
+    tb.progress[a] = progress;
+    tb.timeout[a] = (uint8_t)(((float)progress >= max_ep_m1) && (reset != 0));
+    if (tp.task_id != MG_TASK_CARTPOLE) {
+      tb.potentials[a] = pot;
+      tb.prev_potentials[a] = prev;
+      for (int c = 0; c < 3; c++) {
+        tb.up_vec[3 * (size_t)a + c] = up[c];
+        tb.heading_vec[3 * (size_t)a + c] = hd[c];
+      }
+    }
+  }
+  if (valid) {
+    float* o = tb.obs + (size_t)no * a;
+    for (int q = t.tl; q < no; q += T) {
+      o[q] = ost[q];
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(ost[q], tp.clip_obs);
+    }
+  }
+  __syncthreads();
+  if (valid) {  // state write-back (gym layouts), team-cooperative
+    if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
+      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
+    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.u.sv.st.dof[q];
+    if (v.sensors)
+      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.u.sv.st.sens[q];
+    if (v.dof_force)
+      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
+  }
+  t.ph_mark(9);
+  MG_PHASE_FLUSH(t)
+}
+
+// ------------------------------------------------------------------------------------------------ hand tasks
+// index of DOF d in the actuated list (action column), -1 if not actuated
+__device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
+  for (int i = 0; i < tp.num_actions; i++)
+    if (tp.actuated_dof[i] == d) return i;
+  return -1;
+}
+
+// The whole ShadowHand VecTask.step for one env, fused: pre_physics_step (masked goal / env resets,
+// PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
+// the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
+// RP: physics-bypass replay instance (mg_env_step_replay), as k_env_step's.
+template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
+                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                      int n, mg_replay rp) {
+  constexpr int E = kBlock / T;
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  mg::load_tile(&tile, m);
+  __syncthreads();
+  const int team = threadIdx.x / T;
+  const int e = blockIdx.x * E + team;
+  const bool valid = e < n;
+  const int ec = valid ? e : n - 1;
+  const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
+  const int nb = m->num_bodies, nbe = nb + 2;
+  mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
+  mg::Team<T, MN, MC, MG, MP, OT> t;
+  t.init(&L, &tile, m, &p);
+  if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
+    mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
+    t.drn = &drt[team].node[0][0];
+    t.drg = drt[team].geom;
+    t.drt = &drt[team].ten[0][0];
+    t.dro = drt[team].obj;
+  }
+  t.ph_start();
+  const uint64_t gid = (uint64_t)(tb.env_offset + ec);
+  const bool env_reset = tb.reset[ec] != 0, goal_reset = tb.reset_goal[ec] != 0;
+  float* root = v.root_states + (size_t)39 * ec;
+  // ---- pre_physics_step: goal / object resets staged in LDS by the team leader
+  if (t.tl == 0) {
+    float* gr = L.goal;
+    float* gs = L.goal + 13;
+    if (env_reset || goal_reset) {
+      const int c0 = env_reset ? 57 : 0;  // env reset: reset_idx's own reset_target_pose draw wins
+      mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, c0)),
+                       mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, c0 + 1)), gs, gr);
+      for (int k = 7; k < 13; k++) gs[k] = tb.goal_states[(size_t)13 * ec + k];
+    } else {
+      for (int k = 0; k < 13; k++) { gr[k] = root[26 + k]; gs[k] = tb.goal_states[(size_t)13 * ec + k]; }
+    }
+    // random object forces: reset_idx zeroes / redraws the probability, pre_physics_step decays / draws
+    float f[3] = {0.0f, 0.0f, 0.0f};
+    if (v.rb_forces || tb.random_force_prob) {
+      const float* fr = v.rb_forces ? v.rb_forces + ((size_t)nbe * ec + nb) * 3 : nullptr;
+      if (fr)
+        for (int k = 0; k < 3; k++) f[k] = fr[k];
+      if (valid) mg::h_object_force(tp, tb, ec, gid, env_reset, f);
+    }
+    for (int k = 0; k < 3; k++) L.oforce[k] = f[k];
+    L.oforce[3] = v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f;
+    if (env_reset) {
+      float r[5];
+      for (int k = 0; k < 5; k++) r[k] = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 4 + k));
+      for (int k = 0; k < 3; k++) L.oroot[k] = tp.object_start[k] + tp.reset_position_noise * r[k];
+      mg::h_object_reset_rotation(tp, r[3], r[4], L.oroot + 3);
+      for (int k = 7; k < 13; k++) L.oroot[k] = 0.0f;
+    } else {
+      for (int k = 0; k < 13; k++) L.oroot[k] = root[13 + k];
+    }
+  }
+  __syncthreads();
+  t.load(root, v.dof_state + (size_t)2 * nd * ec, nullptr, L.oroot, nullptr);
+  float prev = 0.0f;
+  if (t.node > 0) {  // DOF lanes: reset_idx's DOF draw, then actions -> PD targets
+    const int d = t.node - 1;
+    float cur;
+    if (env_reset) {
+      const float rp = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 9 + d));
+      const float rv = mg::h_rand_pm1(mg::h_uniform(tb, ec, gid, 9 + nd + d));
+      const float dmax = tp.dof_upper[d] - tp.initial_dof_pos[d], dmin = tp.dof_lower[d] - tp.initial_dof_pos[d];
+      const float pos = tp.initial_dof_pos[d] + tp.reset_dof_pos_noise * (dmin + (dmax - dmin) * 0.5f * (rp + 1.0f));
+      t.qj = pos;
+      t.nu = 0.0f + tp.reset_dof_vel_noise * rv;
+      prev = pos;
+      cur = pos;
+    } else {
+      prev = tb.prev_targets[(size_t)nd * ec + d];
+      cur = v.dof_targets[(size_t)nd * ec + d];
+    }
+    const int ai = hand_action_of(tp, d);
+    if (ai >= 0) {
+      const float a = mg::clampf(tb.actions[(size_t)na * ec + ai], tp.clip_actions);
+      cur = mg::h_target(tp, d, a, prev);
+      prev = cur;
+    }
+    t.tgt = cur;
+  }
+  // ---- gym.simulate
+  t.ph_mark(14);
+  if constexpr (RP) {  // replaced by the injected post-simulate state; the pre-physics state goes out
+    if (valid && rp.pre_root_states) {
+      float* pr = rp.pre_root_states + (size_t)39 * e;
+      for (int k = t.tl; k < 13; k += T) { pr[k] = root[k]; pr[13 + k] = L.oroot[k]; pr[26 + k] = L.goal[k]; }
+    }
+    if (valid && rp.pre_dof_state && t.node > 0) {
+      rp.pre_dof_state[(size_t)2 * nd * e + 2 * (t.node - 1)] = t.qj;
+      rp.pre_dof_state[(size_t)2 * nd * e + 2 * (t.node - 1) + 1] = t.nu;
+    }
+    __syncthreads();
+    for (int k = t.tl; k < 13; k += T) L.oroot[k] = rp.root_states[(size_t)39 * ec + 13 + k];
+    for (int k = t.tl; k < 2 * nd; k += T) L.u.sv.st.dof[k] = rp.dof_state[(size_t)2 * nd * ec + k];
+    for (int k = t.tl; k < 6 * ns; k += T) L.u.sv.st.sens[k] = rp.sensors ? rp.sensors[(size_t)6 * ns * ec + k] : 0.0f;
+    for (int k = t.tl; k < nd; k += T) L.u.sv.st.dforce[k] = rp.dof_force ? rp.dof_force[(size_t)nd * ec + k] : 0.0f;
+  } else {
+    // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
+    const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
+    for (int st = 0; st < nsub; st++) t.substep();
+    t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
+    t.stage_state();
+  }
+  __syncthreads();
+  t.ph_mark(8);
+  // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
+  const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
+  float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
+  // rigid-body states of the hand once (one lane per body) into the dead row storage: the fingertip
+  // observations and the rigid_body_states write-back both read them
+  float* bst = &L.u.sv.rows[0].b;
+#if !(MG_EXP & 1)
+  if constexpr (RP) {
+    for (int k = t.tl; k < 13 * nb; k += T) bst[k] = rp.rigid_body_states[(size_t)13 * nbe * ec + k];
+  } else {
+    for (int b = t.tl; b < nb; b += T) t.body_state(b, bst + 13 * b);
+  }
+#endif
+  __syncthreads();
+#if !(MG_EXP & 2)
+  {
+    const float* gs = L.goal + 13;
+    float qdiff[4];
+    const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
+    mg::t_quat_mul(L.oroot + 3, gc, qdiff);
+    for (int k = t.tl; k < no; k += T) {
+      const int mk = tp.obs_map[k], seg = mk >> 8, i = mk & 255;   // column -> (segment, index)
+      float x;
+      if (seg == mg::HS_ACTIONS) {  // self.actions (clamped)
+        x = mg::clampf(tb.actions[(size_t)na * ec + i], tp.clip_actions);
+      } else if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {  // fingertip state from the post-step FK
+        int b, c;
+        mg::h_ft_ref(tp, seg, i, &b, &c);
+        x = bst[13 * b + c];
+      } else {
+        x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
+      }
+      L.obs[k] = x;
+    }
+  }
+#endif
+  __syncthreads();
+  int64_t ro = 0;
+  float fin = 0.0f;
+  if (!(MG_EXP & 4) && t.tl == 0) {
+    const float* gs = L.goal + 13;
+    float succ = env_reset ? 0.0f : tb.successes[ec], rew;
+    int64_t prog = progress_in + 1, go;
+    mg::h_reward(tp, L.oroot, L.oroot + 3, gs, gs + 3, L.obs + (no - na), 0, 0, &prog, &succ, &rew, &ro, &go);
+    if (valid) {
+      tb.rew[e] = rew;
+      tb.reset[e] = ro;
+      tb.reset_goal[e] = go;
+      tb.progress[e] = prog;
+      tb.successes[e] = succ;
+      tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
+      fin = succ * (float)ro;
+    } else {
+      ro = 0;
+    }
+  }
+  // partial sums of the global running mean: wave reduce, one atomic pair per wave
+  unsigned long long cr = (unsigned long long)ro, cf = (unsigned long long)fin;
+  for (int off = 32; off >= 1; off >>= 1) {
+    cr += __shfl_xor(cr, off);
+    cf += __shfl_xor(cf, off);
+  }
+  if (threadIdx.x == 0 && (cr | cf)) {
+    atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
+    atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
+  }
+  if (!(MG_EXP & 8) && valid) {  // write-back (gym layouts), team-cooperative
+    float* o = tb.obs + (size_t)no * e;
+    for (int k = t.tl; k < no; k += T) {
+      o[k] = L.obs[k];
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(L.obs[k], tp.clip_obs);
+    }
+    if (tb.actions_out)
+      for (int k = t.tl; k < na; k += T) tb.actions_out[(size_t)na * e + k] = L.obs[no - na + k];
+    for (int k = t.tl; k < 13; k += T) {
+      root[13 + k] = L.oroot[k];
+      root[26 + k] = L.goal[k];
+      tb.goal_states[(size_t)13 * e + k] = L.goal[13 + k];
+    }
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.u.sv.st.dof[k];
+    if (t.node > 0) {
+      const int d = t.node - 1;
+      const_cast<float*>(v.dof_targets)[(size_t)nd * e + d] = t.tgt;
+      tb.prev_targets[(size_t)nd * e + d] = prev;
+    }
+    if (v.sensors)
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.u.sv.st.sens[k];
+    if (v.dof_force)
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.u.sv.st.dforce[k];
+    for (int k = t.tl; k < 13 * nb; k += T) rbs[k] = bst[k];
+    for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
+    if (v.rb_forces && t.tl < 3) v.rb_forces[((size_t)nbe * e + nb) * 3 + t.tl] = L.oforce[t.tl];
+    if (tb.states) {  // asymmetric_observations: the full_state layout (compute_full_state(asymm_obs=True))
+      const float* gs = L.goal + 13;
+      float qdiff[4];
+      const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
+      mg::t_quat_mul(L.oroot + 3, gc, qdiff);
+      for (int k = t.tl; k < tp.num_states; k += T) {
+        const int mk = tp.state_map[k], seg = mk >> 8, i = mk & 255;
+        float x;
+        if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
+          int b, c;
+          mg::h_ft_ref(tp, seg, i, &b, &c);
+          x = bst[13 * b + c];
+        } else {
+          x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
+                              L.obs + (no - na));
+        }
+        tb.states[(size_t)tp.num_states * e + k] = x;
+      }
+    }
+  }
+  t.ph_mark(9);
+  MG_PHASE_FLUSH(t)
+}
+
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
+int RunSimulate<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim) {
+  const int E = kBlock / T;
+  // the domain-randomized instance reads each actor's env_props row (mg_dr_apply)
+  if (sim->views.env_props)
+    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                       sim->d_model, sim->params, sim->views, sim->n);
+  else
+    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
+                       sim->d_model, sim->params, sim->views, sim->n);
+  return MG_OK;
+}
+
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
+int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp,
+                                             const mg_task_buffers* tb, const mg_replay* rp) {
+  const int E = kBlock / T;
+  const dim3 grid((sim->n + E - 1) / E), block(kBlock);
+  using TL = mg::TeamLDS<T, MN, MC, OBJ>;
+  // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
+  if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(TL::u.sv.rows))
+    return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
+  // hand tasks stage the rigid-body states of the articulation in the same storage, the observation
+  // row in the contact storage
+  if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(TL::u.sv.rows))
+    return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
+  if (OBJ && (size_t)tp->num_obs > sizeof(TL::obs) / sizeof(float))
+    return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the hand kernel's staging area");
+  if (rp && sim->views.env_props)
+    return fail(MG_EINVAL, "mg_env_step_replay: no replay instance with domain randomization");
+  const mg_replay r = rp ? *rp : mg_replay{};
+  if constexpr (OBJ != 0) {
+    mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
+    mg::h_fill_maps(&tpm);
+    if (rp)
+      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>), grid, block, 0, s, sim->d_model,
+                         sim->params, tpm, sim->views, *tb, sim->n, r);
+    else if (sim->views.env_props)
+      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>), grid, block, 0, s, sim->d_model,
+                         sim->params, tpm, sim->views, *tb, sim->n, r);
+    else
+      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>), grid, block, 0, s, sim->d_model,
+                         sim->params, tpm, sim->views, *tb, sim->n, r);
+  } else {
+    if (rp)
+      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, false, true>), grid, block, 0, s, sim->d_model, sim->params,
+                         *tp, sim->views, *tb, sim->n, r);
+    else if (sim->views.env_props)
+      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, true, false>), grid, block, 0, s, sim->d_model, sim->params,
+                         *tp, sim->views, *tb, sim->n, r);
+    else
+      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, false, false>), grid, block, 0, s, sim->d_model, sim->params,
+                         *tp, sim->views, *tb, sim->n, r);
+  }
+  return MG_OK;
+}
+
+template <int I>
+int phase_buf_publish(unsigned long long* buf) {
+#ifdef MG_PHASE_TIMING
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_buf), &buf, sizeof(buf)) != hipSuccess)
+    return fail(MG_EDEVICE, "mg_debug_phase_cycles: buffer publish failed");
+  return MG_OK;
+#else
+  (void)buf;
+  return fail(MG_EINVAL, "mg_debug_phase_cycles: library built without MG_PHASE_TIMING");
+#endif
+}
+}  // namespace mgi

@@ -83,7 +83,7 @@ class TaskParams(C.Structure):
                 ("reset_dist", C.c_float), ("target", C.c_float * 3), ("start_pos", C.c_float * 3),
                 ("start_rot", C.c_float * 4), ("motor_effort", C.c_float * 64), ("dof_lower", C.c_float * 64),
                 ("dof_upper", C.c_float * 64), ("initial_dof_pos", C.c_float * 64),
-                ("num_agents", C.c_int32), ("pad_ma", C.c_int32), ("agent_offset", (C.c_float * 3) * 8),
+                ("num_agents", C.c_int32), ("control_freq_inv", C.c_int32), ("agent_offset", (C.c_float * 3) * 8),
                 # in-hand manipulation (MG_TASK_SHADOW_HAND)
                 ("num_fingertips", C.c_int32), ("fingertip_body", C.c_int32 * 8),
                 ("actuated_dof", C.c_int32 * MG_MAX_HAND_DOFS), ("max_consecutive_successes", C.c_int32),
@@ -112,6 +112,13 @@ class TaskBuffers(C.Structure):
                 ("prev_targets", C.c_void_p), ("goal_states", C.c_void_p), ("reset_goal", C.c_void_p),
                 ("successes", C.c_void_p), ("consecutive_successes", C.c_void_p), ("reduce_scratch", C.c_void_p),
                 ("states", C.c_void_p), ("random_force_prob", C.c_void_p)]
+
+
+class Replay(C.Structure):
+    """mg_replay: the post-simulate state mg_env_step_replay injects in place of gym.simulate (tests)."""
+    _fields_ = [("root_states", C.c_void_p), ("dof_state", C.c_void_p), ("sensors", C.c_void_p),
+                ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p), ("pre_root_states", C.c_void_p),
+                ("pre_dof_state", C.c_void_p)]
 
 
 def model_bytes(spec) -> np.ndarray:
@@ -150,6 +157,8 @@ EXPORTS = {
     "mg_pre_physics": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(StateViews),
                                  C.POINTER(TaskBuffers), C.c_int32, C.c_void_p]),
     "mg_env_step": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p]),
+    "mg_env_step_replay": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.POINTER(Replay),
+                                     C.c_void_p]),
     "mg_dr_desc_sizeof": (C.c_size_t, []),
     "mg_dr_apply_args_sizeof": (C.c_size_t, []),
     "mg_dr_noise_args_sizeof": (C.c_size_t, []),

@@ -93,6 +93,7 @@ def hand_task_params(cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     tp = _abi.TaskParams()
     tp.task_id = _abi.MG_TASK_SHADOW_HAND
     tp.num_agents = 1
+    tp.control_freq_inv = max(1, int(env.get("controlFrequencyInv", 1)))   # vec_task.py:381-384
     tp.obs_type, tp.num_obs = HAND_OBS[obs_type]
     tp.num_actions = len(spec.actuators)
     tp.dt = float(cfg["sim"]["dt"])
@@ -162,6 +163,7 @@ def task_params(task: str, cfg: dict, spec: M.ModelSpec) -> _abi.TaskParams:
     tp = _abi.TaskParams()
     tp.task_id = task_id
     tp.num_agents = 1
+    tp.control_freq_inv = max(1, int(env.get("controlFrequencyInv", 1)))   # vec_task.py:381-384
     if task == "MAAnt":
         # build-defined multi-agent Ant (SURVEY.md §8(a) A-MA): A ants on a square grid,
         # obs = Ant obs + the other agents' torso positions relative to self (3 (A-1))

@@ -237,10 +237,11 @@ class VecTask(DomainRandomizationMixin, Env):
         tb.actions = a.data_ptr()
         tb.noise = _abi.ptr(self._noise)
         stream = self._stream()
-        for k in range(self.control_freq_inv):
-            tb.step_counter = self.control_steps
-            _abi.check(self._lib.mg_env_step(self.sim, _abi.C.byref(self.task_params), _abi.C.byref(tb), stream),
-                       self._lib)
+        # one launch: pre_physics_step, gym.simulate x controlFrequencyInv (task_params.control_freq_inv),
+        # post_physics_step (vec_task.py:376-396)
+        tb.step_counter = self.control_steps
+        _abi.check(self._lib.mg_env_step(self.sim, _abi.C.byref(self.task_params), _abi.C.byref(tb), stream),
+                   self._lib)
         self.control_steps += 1
         self.frame_count += self.control_freq_inv
         if dr:

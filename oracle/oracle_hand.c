@@ -346,6 +346,8 @@ int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_
 int orc_hand_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp,
                       const mg_state_views* v, const mg_task_buffers* tb, int32_t n, int32_t threads) {
   orc_hand_pre_physics(m, tp, v, tb, n);
-  orc_simulate_views(m, p, n, v, threads);
+  /* gym.simulate x controlFrequencyInv (vec_task.py:381-384) */
+  for (int k = 0; k < (tp->control_freq_inv > 1 ? tp->control_freq_inv : 1); k++)
+    orc_simulate_views(m, p, n, v, threads);
   return orc_hand_post_physics(m, tp, v, tb, n);
 }

@@ -259,7 +259,8 @@ static void reset_one(const mg_task_params* tp, int e, const mg_state_views* v, 
   float u[128];
   for (int k = 0; k < 2 * nd; k++)
     u[k] = tb->noise ? tb->noise[(size_t)2 * nd * e + k]
-                     : orc_uniform(tb->seed, (uint64_t)(tb->env_offset + e), tb->step_counter, (uint32_t)k);
+                     : orc_uniform(tb->seed, (uint64_t)(tb->env_offset * (tp->num_agents > 1 ? tp->num_agents : 1) + e),
+                                   tb->step_counter, (uint32_t)k);
   float* dof = v->dof_state + 2 * nd * e;
   if (tp->task_id == MG_TASK_CARTPOLE) {
     for (int i = 0; i < nd; i++) {
@@ -346,6 +347,8 @@ int orc_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params
                                                                     : a * tp->motor_effort[i] * tp->power_scale;
       }
   }
-  orc_simulate(m, p, n, v->root_states, v->dof_state, eff, v->sensors, v->dof_force, threads);
+  /* gym.simulate x controlFrequencyInv (vec_task.py:381-384) */
+  for (int k = 0; k < (tp->control_freq_inv > 1 ? tp->control_freq_inv : 1); k++)
+    orc_simulate(m, p, n, v->root_states, v->dof_state, eff, v->sensors, v->dof_force, threads);
   return orc_post_physics(tp, v, tb, n);
 }
