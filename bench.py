@@ -7,7 +7,7 @@
 One "step" = one VecTask.step of every env on every rank (controlFrequencyInv=1,
 2 physics substeps), random U(-1,1) actions generated on device before the timed
 region, inputs resident in HBM.  Envs are independent, so ranks shard them
-(weak scaling: --num-envs per GPU, no data-path collective).  Rank 0 prints ONE
+(weak scaling: --num-envs per GPU; the only collective is the obs/rew/reset gather to rank 0, timed).  Rank 0 prints ONE
 JSON line.  See DESIGN.md §Measurement for the roofline accounting.
 """
 import argparse
@@ -29,36 +29,58 @@ ALGO_BYTES = {"Ant": 673, "Humanoid": 1161, "Cartpole": 89, "MAAnt": 4 * 709,
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md (spec)
 
 
-def cpu_baseline(task, seconds=12.0, n=4096):
-    """CPU oracle (fp32 task layer + fp64 physics restatement), OpenMP over envs, bounded sample."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(task, seconds=10.0, n=65536):
+    """The oracle's fp32 restatement of the same step (oracle/build/liboracle_f32.so: fp32 physics, fp32 task
+    layer, OpenMP over envs), timed on this box's host cores at the workload's own env count on a bounded
+    sample of steps: once with every thread this process may use (OMP_NUM_THREADS, the box's CPU share for
+    one GPU; nproc and the CPU model are reported beside it) and once on 1 core.  The reference's
+    pipeline=cpu PhysX path cannot run anywhere here (no isaacgym), so this is a port, not the reference."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     from migym import configs, model as M, taskdefs
-    cores = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+    nproc = os.cpu_count() or 1
+    threads = max(1, min(nproc, int(os.environ.get("OMP_NUM_THREADS", str(nproc)))))
     cfg = configs.task_config(task, n)
     base = "Ant" if task == "MAAnt" else task
-    spec = M.load_builtin(taskdefs.TASK_INFO[base][1])
     A = int(cfg["env"].get("numAgents", 1)) if task == "MAAnt" else 1
+    spec = taskdefs.hand_spec("block") if task == "ShadowHand" else M.load_builtin(taskdefs.TASK_INFO[base][1])
     sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[base][5], A)
     tp = taskdefs.task_params(task, cfg, spec)
     mnp = M.pack_model(spec)
-    if task == "ShadowHand":
-        n = min(n, 1024)
-    h = O.HandHostEnv(tp, spec, n) if task == "ShadowHand" else O.HostEnv(tp, spec, n * A)
-    rng = np.random.default_rng(0)
-    acts = rng.uniform(-1, 1, (8,) + h.actions.shape).astype(np.float32)
-    h.actions[:] = acts[0]
-    h.env_step(mnp, sp, tp, 0, 0, cores)  # warm-up (first step resets every env)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds and steps < 5000:
-        h.actions[:] = acts[steps % 8]
-        h.env_step(mnp, sp, tp, 0, steps + 1, cores)
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{task} {n} envs x {steps} steps ({dt:.1f} s), oracle/ CPU restatement "
-                      f"(fp64 physics, fp32 task layer), not PhysX"}
+
+    def leg(nthreads, n_envs, secs):
+        h = O.HandHostEnv(tp, spec, n_envs) if task == "ShadowHand" else O.HostEnv(tp, spec, n_envs * A)
+        rng = np.random.default_rng(0)
+        acts = rng.uniform(-1, 1, (4,) + h.actions.shape).astype(np.float32)
+        h.actions[:] = acts[0]
+        h.env_step(mnp, sp, tp, 0, 0, nthreads, fp32=True)   # warm-up (the first step resets every env)
+        steps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs and steps < 5000:
+            h.actions[:] = acts[steps % 4]
+            h.env_step(mnp, sp, tp, 0, steps + 1, nthreads, fp32=True)
+            steps += 1
+        dt = time.perf_counter() - t0
+        return n_envs * steps / dt, f"{task} {n_envs} envs x {steps} steps ({dt:.1f} s)"
+
+    v, smp = leg(threads, n, seconds)
+    v1, smp1 = leg(1, min(n, 8192), seconds)
+    return {"value": v, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{smp}, {threads} OpenMP threads; oracle/ fp32 CPU restatement of the same step "
+                      f"(liboracle_f32.so), not PhysX",
+            "nproc": nproc, "cpu_model": _cpu_model(),
+            "single_core": {"value": v1, "unit": "env-steps/s", "cores": 1, "sample": smp1}}
 
 
 def pmc_traffic(task, n, kern_ms):
@@ -66,7 +88,14 @@ def pmc_traffic(task, n, kern_ms):
     passes of the same bench command (tools/gpu_prof.sh -> tools/pmc_summary.py --json): FETCH_SIZE x2
     (gfx950 correction) + WRITE_SIZE per launch, expressed over this run's launch time like `achieved`.
     None when no pass was recorded for this workload."""
-    path = os.path.join(ROOT, "profiles", "r01", f"pmc_{task}_{n}.json")
+    path = None
+    for rnd in ("r02", "r01"):   # the newest round's passes of this workload
+        cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{task}_{n}.json")
+        if os.path.exists(cand):
+            path = cand
+            break
+    if path is None:
+        return {"traffic": None}
     try:
         with open(path) as f:
             b = json.load(f)["traffic_bytes_per_launch"]
@@ -94,10 +123,12 @@ def main():
     ap.add_argument("--task", default="Ant")
     ap.add_argument("--num-envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gather", nargs="?", const="all", default=None, choices=["all", "root"],
-                    help="concatenate obs/rew/reset of every rank each step: 'all' = one RCCL all-gather, "
-                         "'root' = point-to-point sends to rank 0 (migym.dist.OutputGather)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--gather", default=None, choices=["all", "root", "none"],
+                    help="concatenate obs/rew/reset of every rank each step, inside the timed region "
+                         "(migym.dist.PackedGather: rows packed by the kernel, double-buffered, overlapped with "
+                         "the next step): 'root' = point-to-point sends to rank 0 (default when --gpus > 1), "
+                         "'all' = one RCCL all-gather, 'none' = no gather")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--object-type", default="block", choices=["block", "egg", "pen"],
                     help="ShadowHand objectType (shadow_hand.py:86-100)")
@@ -131,20 +162,19 @@ def main():
     na = env.num_actions
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
+    gather_mode = args.gather or ("root" if world > 1 else "none")
     gather = None
-    if args.gather and world > 1 and args.backend == "nccl":
-        from migym.dist import OutputGather
-        gather = OutputGather(env.num_actors, env.num_obs, dev, mode=args.gather)
-
-    def step(a):
-        obs, rew, reset, _ = env.step(a)
-        if gather is not None:
-            gather(obs["obs"], rew, reset)
+    if gather_mode != "none" and world > 1:
+        from migym.dist import PackedGather
+        gather = PackedGather(env.num_actors, env.num_obs, dev, mode=gather_mode)
+        env.attach_output_gather(gather)
 
     for i in range(args.warmup):
-        step(pool[i % 8])
+        env.step(pool[i % 8])
+    if gather is not None:
+        gather.drain()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    # HIP events around each fused launch, on the stream it is launched on (VecTask.launch_events)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
@@ -152,13 +182,15 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        starts[i].record(stream)
-        step(pool[i % 8])
-        ends[i].record(stream)
+        env.launch_events = (starts[i], ends[i])
+        env.step(pool[i % 8])
+    if gather is not None:
+        gather.drain()   # the last step's rows have reached the root
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    env.launch_events = None
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
@@ -179,7 +211,9 @@ def main():
                                    f"PGS x{env.sim_params.pos_iters}",
                        "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
                        "agents_per_env": env.num_agents, "agent_steps_per_s": value * env.num_agents,
-                       "obs_gather": args.gather if gather is not None else None,
+                       "obs_gather": (f"{gather_mode}: kernel-packed [obs|rew|reset] rows, double-buffered, "
+                                      f"overlapped with the next step, inside the timed region")
+                                     if gather is not None else None,
                        "parallelism": f"env-sharded x{world}",
                        **({"object_type": args.object_type} if args.task == "ShadowHand" else {})},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
@@ -190,7 +224,7 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n)
             except Exception as ex:  # noqa: BLE001
                 out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)

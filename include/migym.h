@@ -286,6 +286,14 @@ typedef struct mg_task_buffers {
   uint64_t* reduce_scratch; /* (2) device scratch: sum(resets), sum(successes * resets) */
   float* states;            /* (N, num_states) states_buf, may be NULL */
   float* random_force_prob; /* (N) per-env force probability, redrawn on reset; may be NULL */
+  /* multi-GPU output path: when set, the step also writes each actor's row
+   * [clamped obs (nO) | rew | reset] into this (N*A, nO + 2) f32 buffer, the message the obs gather
+   * sends (migym/dist.py); the caller double-buffers it so the gather of step k overlaps step k+1 */
+  float* out_pack;
+  /* ShadowHand: 1 = leave this step's running-mean partial sums in reduce_scratch (the caller
+   * all-reduces them over the ranks, then calls mg_hand_finalize); 0 = apply them in the step */
+  int32_t defer_finalize;
+  int32_t pad_tb;
 } mg_task_buffers;
 
 typedef struct mg_sim mg_sim;
@@ -424,6 +432,11 @@ int mg_pre_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* 
  * as the post-physics state (physics-free replay, parity tests). */
 int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views* views,
                     const mg_task_buffers* tb, int32_t n, void* stream);
+
+/* ShadowHand: apply the consecutive_successes running mean (shadow_hand.py:795-798) from the partial
+ * sums in tb->reduce_scratch and clear them.  Only needed with tb->defer_finalize (multi-GPU: the caller
+ * all-reduces reduce_scratch over the ranks first, so every rank holds the whole-node mean). */
+int mg_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb, void* stream);
 
 /* Whole VecTask.step: actions -> actuation -> simulate -> post_physics. */
 int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream);

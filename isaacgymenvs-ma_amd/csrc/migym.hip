@@ -124,6 +124,12 @@ __device__ __forceinline__ void post_physics_env(const mg_task_params& tp, const
   }
   if (tb.obs_clamped)
     for (int i = 0; i < no; i++) tb.obs_clamped[(size_t)no * a + i] = mg::clampf(o[i], tp.clip_obs);
+  if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset]
+    float* pk = tb.out_pack + (size_t)(no + 2) * a;
+    for (int i = 0; i < no; i++) pk[i] = mg::clampf(o[i], tp.clip_obs);
+    pk[no] = rew;
+    pk[no + 1] = (float)reset;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_post_physics(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
@@ -271,6 +277,12 @@ __global__ __launch_bounds__(kBlock) void k_hand_post(mg_task_params tp, mg_stat
     tb.successes[e] = succ;
     tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
     fin = succ * (float)ro;
+    if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset]
+      float* pk = tb.out_pack + (size_t)(no + 2) * e;
+      for (int k = 0; k < no; k++) pk[k] = mg::clampf(o[k], tp.clip_obs);
+      pk[no] = rew;
+      pk[no + 1] = (float)ro;
+    }
   }
   // partial sums of compute_hand_reward's global reduction (integer-valued: exact in any order)
   unsigned long long cr = (unsigned long long)ro, cf = (unsigned long long)fin;
@@ -690,7 +702,8 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
     if (rc) return rc;
     hipLaunchKernelGGL(k_hand_post, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n,
                        tp->num_dofs);
-    hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
+    if (!tb->defer_finalize)
+      hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
     return check_launch("mg_post_physics");
   }
   hipLaunchKernelGGL(k_post_physics, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, v, *tb, n);
@@ -731,13 +744,20 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
                                           (const mg_sim*)sim, tp, tb, rp);
   if (rc) return rc;
-  if (hand)  // consecutive_successes running mean from the step's partial sums
+  if (hand && !tb->defer_finalize)  // consecutive_successes running mean from the step's partial sums
     hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
   return check_launch(rp ? "mg_env_step_replay" : "mg_env_step");
 }
 
 int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {
   return env_step(sim, tp, tb, nullptr, stream);
+}
+
+int mg_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {
+  if (!tp || !tb || !tb->reduce_scratch || !tb->consecutive_successes)
+    return fail(MG_EINVAL, "mg_hand_finalize: needs reduce_scratch and consecutive_successes");
+  hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
+  return check_launch("mg_hand_finalize");
 }
 
 int mg_env_step_replay(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,

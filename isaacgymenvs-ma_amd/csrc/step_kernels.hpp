@@ -264,6 +264,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       o[q] = ost[q];
       if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(ost[q], tp.clip_obs);
     }
+    if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset] (migym/dist.py)
+      float* pk = tb.out_pack + (size_t)(no + 2) * a;
+      for (int q = t.tl; q < no; q += T) pk[q] = mg::clampf(ost[q], tp.clip_obs);
+      if (t.tl == 0) { pk[no] = rew; pk[no + 1] = (float)reset; }
+    }
   }
   __syncthreads();
   if (valid) {  // state write-back (gym layouts), team-cooperative
@@ -457,6 +462,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       tb.successes[e] = succ;
       tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
       fin = succ * (float)ro;
+      if (tb.out_pack) {
+        tb.out_pack[(size_t)(no + 2) * e + no] = rew;
+        tb.out_pack[(size_t)(no + 2) * e + no + 1] = (float)ro;
+      }
     } else {
       ro = 0;
     }
@@ -476,6 +485,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     for (int k = t.tl; k < no; k += T) {
       o[k] = L.obs[k];
       if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(L.obs[k], tp.clip_obs);
+    }
+    if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset] (migym/dist.py)
+      float* pk = tb.out_pack + (size_t)(no + 2) * e;
+      for (int k = t.tl; k < no; k += T) pk[k] = mg::clampf(L.obs[k], tp.clip_obs);
     }
     if (tb.actions_out)
       for (int k = t.tl; k < na; k += T) tb.actions_out[(size_t)na * e + k] = L.obs[no - na + k];

@@ -111,7 +111,8 @@ class TaskBuffers(C.Structure):
                 ("env_offset", C.c_int64),
                 ("prev_targets", C.c_void_p), ("goal_states", C.c_void_p), ("reset_goal", C.c_void_p),
                 ("successes", C.c_void_p), ("consecutive_successes", C.c_void_p), ("reduce_scratch", C.c_void_p),
-                ("states", C.c_void_p), ("random_force_prob", C.c_void_p)]
+                ("states", C.c_void_p), ("random_force_prob", C.c_void_p), ("out_pack", C.c_void_p),
+                ("defer_finalize", C.c_int32), ("pad_tb", C.c_int32)]
 
 
 class Replay(C.Structure):
@@ -157,6 +158,7 @@ EXPORTS = {
     "mg_pre_physics": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(StateViews),
                                  C.POINTER(TaskBuffers), C.c_int32, C.c_void_p]),
     "mg_env_step": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p]),
+    "mg_hand_finalize": (C.c_int, [C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p]),
     "mg_env_step_replay": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.POINTER(Replay),
                                      C.c_void_p]),
     "mg_dr_desc_sizeof": (C.c_size_t, []),

@@ -124,6 +124,8 @@ class VecTask(DomainRandomizationMixin, Env):
         self.seed = int(config.get("seed", 0) or 0)
         self.env_offset = int(config.get("env_offset", 0))
         self._lib = _abi.lib()
+        self._gather = None
+        self.launch_events = None
         self.create_sim()
         self.allocate_buffers()
         self.obs_dict = {}
@@ -236,12 +238,22 @@ class VecTask(DomainRandomizationMixin, Env):
         tb = self._tb
         tb.actions = a.data_ptr()
         tb.noise = _abi.ptr(self._noise)
+        g = self._gather
+        tb.out_pack = _abi.ptr(g.next_pack()) if g is not None else None
         stream = self._stream()
         # one launch: pre_physics_step, gym.simulate x controlFrequencyInv (task_params.control_freq_inv),
         # post_physics_step (vec_task.py:376-396)
         tb.step_counter = self.control_steps
+        ev = self.launch_events   # optional (start, end) torch.cuda.Event pair around the launch (bench.py)
+        if ev is not None:
+            ev[0].record(torch.cuda.current_stream(self.device))
         _abi.check(self._lib.mg_env_step(self.sim, _abi.C.byref(self.task_params), _abi.C.byref(tb), stream),
                    self._lib)
+        if ev is not None:
+            ev[1].record(torch.cuda.current_stream(self.device))
+        self.post_launch()
+        if g is not None:
+            g.issue()   # gather of this step's rows, overlapped with the next step (migym/dist.py)
         self.control_steps += 1
         self.frame_count += self.control_freq_inv
         if dr:
@@ -263,6 +275,17 @@ class VecTask(DomainRandomizationMixin, Env):
             self.apply_randomizations(self.randomization_params, reset_mask=mask, increment=pending_increment)
         elif pending_increment:
             self.randomize_buf_actors += 1
+
+    def post_launch(self):
+        """Device work that follows the fused launch in stream order (ShadowHand: the cross-rank
+        running-mean reduction)."""
+
+    def attach_output_gather(self, gather):
+        """Route every step's [clamped obs | rew | reset] rows into ``gather`` (migym.dist.PackedGather):
+        the kernel writes them into the gather's message slot and the gather overlaps the next step."""
+        if gather is not None and (gather.rows != self.num_actors or gather.nobs != self.num_obs):
+            raise ValueError("gather shape does not match (num_actors, num_obs)")
+        self._gather = gather
 
     def post_step_extras(self):
         """Task-specific extras (e.g. Ant's true_objective); cheap device views only."""

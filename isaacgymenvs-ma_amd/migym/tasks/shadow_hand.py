@@ -130,6 +130,19 @@ class ShadowHand(VecTask):
         self.random_force_prob = torch.exp((torch.log(lo) - torch.log(hi)) * torch.rand(N, device=dev) + torch.log(hi))
         tb.random_force_prob = _abi.ptr(self.random_force_prob)
         tb.states = _abi.ptr(self.states_buf) if self.num_states > 0 else None
+        # multi-GPU: the running mean over the envs of all ranks; the step leaves its
+        # partial sums, post_launch all-reduces them (16 bytes) and applies shadow_hand.py:795-798.
+        # env.globalConsecutiveSuccesses: False keeps the reference's per-rank statistic.
+        self._global_cons = bool(self.cfg["env"].get("globalConsecutiveSuccesses", True)) and \
+            torch.distributed.is_available() and torch.distributed.is_initialized() and \
+            torch.distributed.get_world_size() > 1
+        tb.defer_finalize = 1 if self._global_cons else 0
+
+    def post_launch(self):
+        if self._global_cons:
+            torch.distributed.all_reduce(self._reduce)
+            _abi.check(self._lib.mg_hand_finalize(_abi.C.byref(self.task_params), _abi.C.byref(self._tb),
+                                                  self._stream()), self._lib)
 
     def post_step_extras(self):
         self.extras["consecutive_successes"] = self.consecutive_successes.mean()

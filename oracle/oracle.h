@@ -79,6 +79,7 @@ int orc_hand_pre_physics(const mg_model* m, const mg_task_params* tp, const mg_s
                          const mg_task_buffers* tb, int32_t n);
 int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_state_views* v,
                           const mg_task_buffers* tb, int32_t n);
+int orc_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb);
 int orc_hand_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp,
                       const mg_state_views* v, const mg_task_buffers* tb, int32_t n, int32_t threads);
 

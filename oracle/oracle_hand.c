@@ -339,7 +339,20 @@ int orc_hand_post_physics(const mg_model* m, const mg_task_params* tp, const mg_
         tb->obs_clamped[(size_t)no * e + i] = x;
       }
   }
+  if (tb->defer_finalize) {  /* partial sums for a cross-rank all-reduce (mg_hand_finalize) */
+    tb->reduce_scratch[0] += (uint64_t)nres;
+    tb->reduce_scratch[1] += (uint64_t)fin;
+    return 0;
+  }
   tb->consecutive_successes[0] = hand_cons_update(tp, nres, fin, tb->consecutive_successes[0]);
+  return 0;
+}
+
+int orc_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb) {
+  tb->consecutive_successes[0] =
+      hand_cons_update(tp, (int64_t)tb->reduce_scratch[0], (float)tb->reduce_scratch[1], tb->consecutive_successes[0]);
+  tb->reduce_scratch[0] = 0;
+  tb->reduce_scratch[1] = 0;
   return 0;
 }
 

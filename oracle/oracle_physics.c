@@ -28,6 +28,19 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Scalar type of the physics restatement: fp64 for the checker (default).  -DORC_FP32 builds the
+ * fp32 variant that bench.py times as the CPU baseline (liboracle_f32.so), with the float libm. */
+#ifdef ORC_FP32
+typedef float real;
+#define sqrt sqrtf
+#define fabs fabsf
+#define fmin fminf
+#define sin sinf
+#define cos cosf
+#else
+typedef double real;
+#endif
+
 #include "oracle.h"
 
 #ifdef _OPENMP
@@ -43,91 +56,91 @@
 #define CVX_MARGIN 1e-3 /* rounding of box cores against the egg (m) */
 #define MPR_EPS 1e-12 /* origin-side tests */
 
-typedef double v3[3];
+typedef real v3[3];
 
 /* ---------------------------------------------------------------- small math */
-static void cross3(const double* a, const double* b, double* o) {
-  double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+static void cross3(const real* a, const real* b, real* o) {
+  real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
 }
-static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-static void quat_to_mat(const double* q, double R[3][3]) {
-  double x = q[0], y = q[1], z = q[2], w = q[3];
+static real dot3(const real* a, const real* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void quat_to_mat(const real* q, real R[3][3]) {
+  real x = q[0], y = q[1], z = q[2], w = q[3];
   R[0][0] = 1 - 2 * (y * y + z * z); R[0][1] = 2 * (x * y - z * w); R[0][2] = 2 * (x * z + y * w);
   R[1][0] = 2 * (x * y + z * w); R[1][1] = 1 - 2 * (x * x + z * z); R[1][2] = 2 * (y * z - x * w);
   R[2][0] = 2 * (x * z - y * w); R[2][1] = 2 * (y * z + x * w); R[2][2] = 1 - 2 * (x * x + y * y);
 }
-static void mat_to_quat(double R[3][3], double* q) {
-  double tr = R[0][0] + R[1][1] + R[2][2];
+static void mat_to_quat(real R[3][3], real* q) {
+  real tr = R[0][0] + R[1][1] + R[2][2];
   if (tr > 0) {
-    double s = sqrt(tr + 1.0) * 2;
+    real s = sqrt(tr + 1.0) * 2;
     q[3] = 0.25 * s; q[0] = (R[2][1] - R[1][2]) / s; q[1] = (R[0][2] - R[2][0]) / s; q[2] = (R[1][0] - R[0][1]) / s;
   } else if (R[0][0] > R[1][1] && R[0][0] > R[2][2]) {
-    double s = sqrt(1.0 + R[0][0] - R[1][1] - R[2][2]) * 2;
+    real s = sqrt(1.0 + R[0][0] - R[1][1] - R[2][2]) * 2;
     q[3] = (R[2][1] - R[1][2]) / s; q[0] = 0.25 * s; q[1] = (R[0][1] + R[1][0]) / s; q[2] = (R[0][2] + R[2][0]) / s;
   } else if (R[1][1] > R[2][2]) {
-    double s = sqrt(1.0 + R[1][1] - R[0][0] - R[2][2]) * 2;
+    real s = sqrt(1.0 + R[1][1] - R[0][0] - R[2][2]) * 2;
     q[3] = (R[0][2] - R[2][0]) / s; q[0] = (R[0][1] + R[1][0]) / s; q[1] = 0.25 * s; q[2] = (R[1][2] + R[2][1]) / s;
   } else {
-    double s = sqrt(1.0 + R[2][2] - R[0][0] - R[1][1]) * 2;
+    real s = sqrt(1.0 + R[2][2] - R[0][0] - R[1][1]) * 2;
     q[3] = (R[1][0] - R[0][1]) / s; q[0] = (R[0][2] + R[2][0]) / s; q[1] = (R[1][2] + R[2][1]) / s; q[2] = 0.25 * s;
   }
 }
-static void matmul3(double A[3][3], double B[3][3], double C[3][3]) {
-  double T[3][3];
+static void matmul3(real A[3][3], real B[3][3], real C[3][3]) {
+  real T[3][3];
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) T[i][j] = A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j];
   memcpy(C, T, sizeof(T));
 }
-static void matvec3(double A[3][3], const double* v, double* o) {
-  double x = A[0][0] * v[0] + A[0][1] * v[1] + A[0][2] * v[2];
-  double y = A[1][0] * v[0] + A[1][1] * v[1] + A[1][2] * v[2];
-  double z = A[2][0] * v[0] + A[2][1] * v[1] + A[2][2] * v[2];
+static void matvec3(real A[3][3], const real* v, real* o) {
+  real x = A[0][0] * v[0] + A[0][1] * v[1] + A[0][2] * v[2];
+  real y = A[1][0] * v[0] + A[1][1] * v[1] + A[1][2] * v[2];
+  real z = A[2][0] * v[0] + A[2][1] * v[1] + A[2][2] * v[2];
   o[0] = x; o[1] = y; o[2] = z;
 }
-static void mattvec3(double A[3][3], const double* v, double* o) {
-  double x = A[0][0] * v[0] + A[1][0] * v[1] + A[2][0] * v[2];
-  double y = A[0][1] * v[0] + A[1][1] * v[1] + A[2][1] * v[2];
-  double z = A[0][2] * v[0] + A[1][2] * v[1] + A[2][2] * v[2];
+static void mattvec3(real A[3][3], const real* v, real* o) {
+  real x = A[0][0] * v[0] + A[1][0] * v[1] + A[2][0] * v[2];
+  real y = A[0][1] * v[0] + A[1][1] * v[1] + A[2][1] * v[2];
+  real z = A[0][2] * v[0] + A[1][2] * v[1] + A[2][2] * v[2];
   o[0] = x; o[1] = y; o[2] = z;
 }
-static void axis_angle_mat(const double* a, double ang, double R[3][3]) {
-  double c = cos(ang), s = sin(ang), t = 1 - c, x = a[0], y = a[1], z = a[2];
+static void axis_angle_mat(const real* a, real ang, real R[3][3]) {
+  real c = cos(ang), s = sin(ang), t = 1 - c, x = a[0], y = a[1], z = a[2];
   R[0][0] = t * x * x + c; R[0][1] = t * x * y - s * z; R[0][2] = t * x * z + s * y;
   R[1][0] = t * x * y + s * z; R[1][1] = t * y * y + c; R[1][2] = t * y * z - s * x;
   R[2][0] = t * x * z - s * y; R[2][1] = t * y * z + s * x; R[2][2] = t * z * z + c;
 }
-static void quat_mul_d(const double* a, const double* b, double* o) {
-  double x = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
-  double y = a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0];
-  double z = a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3];
-  double w = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+static void quat_mul_d(const real* a, const real* b, real* o) {
+  real x = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+  real y = a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0];
+  real z = a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3];
+  real w = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
   o[0] = x; o[1] = y; o[2] = z; o[3] = w;
 }
 
 /* spatial algebra (6-vectors: angular first) */
-static void crm(const double* v, const double* m, double* o) { /* v x m (motion) */
-  double a[3], b[3], c[3];
+static void crm(const real* v, const real* m, real* o) { /* v x m (motion) */
+  real a[3], b[3], c[3];
   cross3(v, m, a);
   cross3(v, m + 3, b);
   cross3(v + 3, m, c);
   o[0] = a[0]; o[1] = a[1]; o[2] = a[2];
   o[3] = b[0] + c[0]; o[4] = b[1] + c[1]; o[5] = b[2] + c[2];
 }
-static void crf(const double* v, const double* f, double* o) { /* v x* f (force) */
-  double a[3], b[3], c[3];
+static void crf(const real* v, const real* f, real* o) { /* v x* f (force) */
+  real a[3], b[3], c[3];
   cross3(v, f, a);
   cross3(v + 3, f + 3, b);
   cross3(v, f + 3, c);
   o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2];
   o[3] = c[0]; o[4] = c[1]; o[5] = c[2];
 }
-static double dot6(const double* a, const double* b) {
+static real dot6(const real* a, const real* b) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
 }
-static void mat6vec(double I[6][6], const double* v, double* o) {
+static void mat6vec(real I[6][6], const real* v, real* o) {
   for (int i = 0; i < 6; i++) {
-    double s = 0;
+    real s = 0;
     for (int j = 0; j < 6; j++) s += I[i][j] * v[j];
     o[i] = s;
   }
@@ -135,31 +148,31 @@ static void mat6vec(double I[6][6], const double* v, double* o) {
 
 /* ---------------------------------------------------------------- per-actor state */
 typedef struct {
-  double p[3], q[4];     /* root pose */
-  double nu0[6];         /* root spatial velocity at root origin [w; v_o] */
-  double qj[MAXN], qd[MAXN];
-  double op[3], oq[4];   /* free object pose (COM = origin) */
-  double ow[3], ov[3];   /* object angular / COM linear velocity (world) */
-  double of[3];          /* applied force on the object COM (apply_rigid_body_force_tensors) */
+  real p[3], q[4];     /* root pose */
+  real nu0[6];         /* root spatial velocity at root origin [w; v_o] */
+  real qj[MAXN], qd[MAXN];
+  real op[3], oq[4];   /* free object pose (COM = origin) */
+  real ow[3], ov[3];   /* object angular / COM linear velocity (world) */
+  real of[3];          /* applied force on the object COM (apply_rigid_body_force_tensors) */
   int of_local;          /* LOCAL_SPACE: of is in the object frame at the start of each substep */
-  const double* gmu;     /* DR: friction per geom, [num_geoms] = the object's; NULL = sim friction */
+  const real* gmu;     /* DR: friction per geom, [num_geoms] = the object's; NULL = sim friction */
   const float* tgt;      /* PD targets (nD) or NULL */
   int sat[MAXN];         /* drive saturated in the last substep */
-  double ttend[MAXN];    /* tendon generalized force of the last substep */
+  real ttend[MAXN];    /* tendon generalized force of the last substep */
 } astate;
 
 typedef struct {
-  double R[MAXN][3][3], x[MAXN][3];
-  double S[MAXN][6];
-  double I[MAXN][6][6];
-  double V[MAXN][6];
-  double o[3];
-  double oR[3][3], op[3]; /* free object pose */
+  real R[MAXN][3][3], x[MAXN][3];
+  real S[MAXN][6];
+  real I[MAXN][6][6];
+  real V[MAXN][6];
+  real o[3];
+  real oR[3][3], op[3]; /* free object pose */
 } kin;
 
 typedef struct {
   int nodeA, nodeB, geomA, geomB;
-  double p[3], n[3], d;
+  real p[3], n[3], d;
 } contact;
 
 static int nv_of(const mg_model* m) { return (m->fixed_base ? 0 : 6) + m->num_dofs; }
@@ -168,17 +181,17 @@ static int dof_col(const mg_model* m, int node) { return (m->fixed_base ? 0 : 6)
 
 static void load_state(const mg_model* m, const float* root, const float* dof, astate* s) {
   for (int k = 0; k < 3; k++) s->p[k] = root[k];
-  double nq = 0;
+  real nq = 0;
   for (int k = 0; k < 4; k++) { s->q[k] = root[3 + k]; nq += s->q[k] * s->q[k]; }
   nq = sqrt(nq);
   for (int k = 0; k < 4; k++) s->q[k] /= nq;
   memset(s->nu0, 0, sizeof(s->nu0));
   if (!m->fixed_base) {
-    double R[3][3], cw[3], wxc[3];
+    real R[3][3], cw[3], wxc[3];
     quat_to_mat(s->q, R);
-    double c[3] = {m->body_com[0][0], m->body_com[0][1], m->body_com[0][2]};
+    real c[3] = {m->body_com[0][0], m->body_com[0][1], m->body_com[0][2]};
     matvec3(R, c, cw);
-    double w[3] = {root[10], root[11], root[12]};
+    real w[3] = {root[10], root[11], root[12]};
     cross3(w, cw, wxc);
     for (int k = 0; k < 3; k++) { s->nu0[k] = w[k]; s->nu0[3 + k] = root[7 + k] - wxc[k]; }
   }
@@ -187,9 +200,9 @@ static void load_state(const mg_model* m, const float* root, const float* dof, a
 
 static void store_state(const mg_model* m, const astate* s, float* root, float* dof) {
   if (!m->fixed_base) {
-    double R[3][3], cw[3], wxc[3];
+    real R[3][3], cw[3], wxc[3];
     quat_to_mat(s->q, R);
-    double c[3] = {m->body_com[0][0], m->body_com[0][1], m->body_com[0][2]};
+    real c[3] = {m->body_com[0][0], m->body_com[0][1], m->body_com[0][2]};
     matvec3(R, c, cw);
     cross3(s->nu0, cw, wxc);
     for (int k = 0; k < 3; k++) {
@@ -210,20 +223,20 @@ static void forward_kinematics(const mg_model* m, const astate* s, kin* k) {
   for (int c = 0; c < 3; c++) { k->x[0][c] = s->p[c]; k->o[c] = s->p[c]; }
   for (int i = 1; i < m->num_nodes; i++) {
     int par = m->parent[i];
-    double r0[4] = {m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]};
-    double R0[3][3], Rp0[3][3], tp[3];
+    real r0[4] = {m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]};
+    real R0[3][3], Rp0[3][3], tp[3];
     quat_to_mat(r0, R0);
     matmul3(k->R[par], R0, Rp0);
-    double t[3] = {m->t[i][0], m->t[i][1], m->t[i][2]};
+    real t[3] = {m->t[i][0], m->t[i][1], m->t[i][2]};
     matvec3(k->R[par], t, tp);
-    double ax[3] = {m->axis[i][0], m->axis[i][1], m->axis[i][2]};
+    real ax[3] = {m->axis[i][0], m->axis[i][1], m->axis[i][2]};
     if (m->jtype[i] == MG_JT_HINGE) {
-      double Rj[3][3];
+      real Rj[3][3];
       axis_angle_mat(ax, s->qj[i], Rj);
       matmul3(Rp0, Rj, k->R[i]);
       for (int c = 0; c < 3; c++) k->x[i][c] = k->x[par][c] + tp[c];
     } else {
-      double sw[3];
+      real sw[3];
       memcpy(k->R[i], Rp0, sizeof(Rp0));
       matvec3(Rp0, ax, sw);
       for (int c = 0; c < 3; c++) k->x[i][c] = k->x[par][c] + tp[c] + sw[c] * s->qj[i];
@@ -231,7 +244,7 @@ static void forward_kinematics(const mg_model* m, const astate* s, kin* k) {
   }
   /* motion subspaces at o */
   for (int i = 1; i < m->num_nodes; i++) {
-    double ax[3] = {m->axis[i][0], m->axis[i][1], m->axis[i][2]}, sw[3], r[3], rxs[3];
+    real ax[3] = {m->axis[i][0], m->axis[i][1], m->axis[i][2]}, sw[3], r[3], rxs[3];
     matvec3(k->R[i], ax, sw);
     if (m->jtype[i] == MG_JT_HINGE) {
       for (int c = 0; c < 3; c++) r[c] = k->x[i][c] - k->o[c];
@@ -243,19 +256,19 @@ static void forward_kinematics(const mg_model* m, const astate* s, kin* k) {
   }
   /* spatial inertias at o */
   for (int i = 0; i < m->num_nodes; i++) {
-    double mass = m->mass[i];
-    double cl[3] = {m->com[i][0], m->com[i][1], m->com[i][2]}, cw[3], c[3];
+    real mass = m->mass[i];
+    real cl[3] = {m->com[i][0], m->com[i][1], m->com[i][2]}, cw[3], c[3];
     matvec3(k->R[i], cl, cw);
     for (int a = 0; a < 3; a++) c[a] = k->x[i][a] + cw[a] - k->o[a];
     const float* in = m->inertia[i];
-    double Il[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
-    double T[3][3], Iw[3][3], Rt[3][3];
+    real Il[3][3] = {{in[0], in[3], in[4]}, {in[3], in[1], in[5]}, {in[4], in[5], in[2]}};
+    real T[3][3], Iw[3][3], Rt[3][3];
     matmul3(k->R[i], Il, T);
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) Rt[a][b] = k->R[i][b][a];
     matmul3(T, Rt, Iw);
-    double cc = dot3(c, c);
-    double cx[3][3] = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
+    real cc = dot3(c, c);
+    real cx[3][3] = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) {
         k->I[i][a][b] = Iw[a][b] + mass * ((a == b ? cc : 0.0) - c[a] * c[b]);
@@ -279,17 +292,17 @@ static void forward_kinematics(const mg_model* m, const astate* s, kin* k) {
  * damping, unless the explicit estimate kp (tgt - q) - b qd exceeds the effort limit: then a constant
  * +-limit force and no implicit terms (PhysX clamps the drive force, shadow_hand.py:241-242). */
 typedef struct {
-  double k, b, ref, tadd;
+  real k, b, ref, tadd;
   int sat;
 } dofterm;
 
 static dofterm dof_term(const mg_model* m, const astate* s, int i) {
   dofterm t = {m->stiffness[i], m->damping[i], 0.0, 0.0, 0};
-  double kp = m->drive_kp[i];
+  real kp = m->drive_kp[i];
   if (kp > 0.0) {
-    double tgt = s->tgt ? s->tgt[i - 1] : 0.0;
-    double fe = kp * (tgt - s->qj[i]) - m->damping[i] * s->qd[i];
-    double F = m->effort_limit[i];
+    real tgt = s->tgt ? s->tgt[i - 1] : 0.0;
+    real fe = kp * (tgt - s->qj[i]) - m->damping[i] * s->qd[i];
+    real F = m->effort_limit[i];
     if (fabs(fe) > F) {
       t.k = 0.0; t.b = 0.0; t.tadd = fe > 0 ? F : -F; t.sat = 1;
     } else {
@@ -300,44 +313,44 @@ static dofterm dof_term(const mg_model* m, const astate* s, int i) {
 }
 
 /* fixed tendons: length L = sum c q, force f = -ks (L - clamp(L, lo, hi)) - kd dL/dt (explicit) */
-static void tendon_forces(const mg_model* m, const astate* s, double* tau /* per node */) {
+static void tendon_forces(const mg_model* m, const astate* s, real* tau /* per node */) {
   for (int i = 0; i < m->num_nodes; i++) tau[i] = 0.0;
   for (int t = 0; t < m->num_tendons; t++) {
     int n0 = m->tendon_dof[t][0] + 1, n1 = m->tendon_dof[t][1] + 1;
-    double c0 = m->tendon_coef[t][0], c1 = m->tendon_coef[t][1];
-    double L = c0 * s->qj[n0] + c1 * s->qj[n1];
-    double Ld = c0 * s->qd[n0] + c1 * s->qd[n1];
-    double lo = m->tendon_range[t][0], hi = m->tendon_range[t][1];
-    double cl = L < lo ? lo : (L > hi ? hi : L);
-    double f = -m->tendon_limit_stiffness[t] * (L - cl) - m->tendon_damping[t] * Ld;
+    real c0 = m->tendon_coef[t][0], c1 = m->tendon_coef[t][1];
+    real L = c0 * s->qj[n0] + c1 * s->qj[n1];
+    real Ld = c0 * s->qd[n0] + c1 * s->qd[n1];
+    real lo = m->tendon_range[t][0], hi = m->tendon_range[t][1];
+    real cl = L < lo ? lo : (L > hi ? hi : L);
+    real f = -m->tendon_limit_stiffness[t] * (L - cl) - m->tendon_damping[t] * Ld;
     tau[n0] += c0 * f;
     tau[n1] += c1 * f;
   }
 }
 
 /* joint-space inertia (CRBA) incl. implicit diagonal, h = substep */
-static void mass_matrix(const mg_model* m, const kin* k, double h, double* M, const double* diag, int ld) {
+static void mass_matrix(const mg_model* m, const kin* k, real h, real* M, const real* diag, int ld) {
   int nv = ld, nn = m->num_nodes;
-  double Ic[MAXN][6][6];
-  memcpy(Ic, k->I, sizeof(double) * 36 * nn);
+  real Ic[MAXN][6][6];
+  memcpy(Ic, k->I, sizeof(real) * 36 * nn);
   for (int i = nn - 1; i >= 1; i--) {
     int p = m->parent[i];
     for (int a = 0; a < 6; a++)
       for (int b = 0; b < 6; b++) Ic[p][a][b] += Ic[i][a][b];
   }
-  memset(M, 0, sizeof(double) * nv * nv);
+  memset(M, 0, sizeof(real) * nv * nv);
   if (!m->fixed_base)
     for (int a = 0; a < 6; a++)
       for (int b = 0; b < 6; b++) M[a * nv + b] = Ic[0][a][b];
   for (int i = 1; i < nn; i++) {
-    double F[6];
+    real F[6];
     mat6vec(Ic[i], k->S[i], F);
     int ci = dof_col(m, i);
     M[ci * nv + ci] = dot6(k->S[i], F) + (diag ? diag[i] : m->armature[i] + h * m->damping[i] + h * h * m->stiffness[i]);
     int j = m->parent[i];
     while (j > 0) {
       int cj = dof_col(m, j);
-      double v = dot6(k->S[j], F);
+      real v = dot6(k->S[j], F);
       M[ci * nv + cj] = v;
       M[cj * nv + ci] = v;
       j = m->parent[j];
@@ -348,78 +361,78 @@ static void mass_matrix(const mg_model* m, const kin* k, double h, double* M, co
 }
 
 /* bias forces C(q,v) incl. gravity (RNEA with qdd = 0) */
-static void bias_forces(const mg_model* m, const kin* k, const astate* s, const double* g, double* C) {
+static void bias_forces(const mg_model* m, const kin* k, const astate* s, const real* g, real* C) {
   int nn = m->num_nodes, nv = nv_of(m); /* C has at least nv entries */
-  double A[MAXN][6], f[MAXN][6];
+  real A[MAXN][6], f[MAXN][6];
   for (int c = 0; c < 6; c++) A[0][c] = 0;
   for (int i = 1; i < nn; i++) {
-    double sq[6], t[6];
+    real sq[6], t[6];
     for (int c = 0; c < 6; c++) sq[c] = k->S[i][c] * s->qd[i];
     crm(k->V[i], sq, t);
     for (int c = 0; c < 6; c++) A[i][c] = A[m->parent[i]][c] + t[c];
   }
   for (int i = 0; i < nn; i++) {
-    double IA[6], IV[6], vIV[6];
-    mat6vec((double(*)[6])k->I[i], A[i], IA);
-    mat6vec((double(*)[6])k->I[i], k->V[i], IV);
+    real IA[6], IV[6], vIV[6];
+    mat6vec((real(*)[6])k->I[i], A[i], IA);
+    mat6vec((real(*)[6])k->I[i], k->V[i], IV);
     crf(k->V[i], IV, vIV);
     /* gravity: force m g at COM; moment about o = c x m g */
-    double mass = m->mass[i];
-    double cl[3] = {m->com[i][0], m->com[i][1], m->com[i][2]}, cw[3], c[3], mg[3], n[3];
-    matvec3((double(*)[3])k->R[i], cl, cw);
+    real mass = m->mass[i];
+    real cl[3] = {m->com[i][0], m->com[i][1], m->com[i][2]}, cw[3], c[3], mg[3], n[3];
+    matvec3((real(*)[3])k->R[i], cl, cw);
     for (int a = 0; a < 3; a++) { c[a] = k->x[i][a] + cw[a] - k->o[a]; mg[a] = mass * g[a]; }
     cross3(c, mg, n);
     for (int a = 0; a < 3; a++) { f[i][a] = IA[a] + vIV[a] - n[a]; f[i][3 + a] = IA[3 + a] + vIV[3 + a] - mg[a]; }
   }
   for (int i = nn - 1; i >= 1; i--)
     for (int c = 0; c < 6; c++) f[m->parent[i]][c] += f[i][c];
-  memset(C, 0, sizeof(double) * nv);
+  memset(C, 0, sizeof(real) * nv);
   if (!m->fixed_base)
     for (int c = 0; c < 6; c++) C[c] = f[0][c];
   for (int i = 1; i < nn; i++) C[dof_col(m, i)] = dot6(k->S[i], f[i]);
 }
 
-static int cholesky(double* A, int n) {
+static int cholesky(real* A, int n) {
   for (int j = 0; j < n; j++) {
-    double s = A[j * n + j];
+    real s = A[j * n + j];
     for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
     if (s <= 0) return -1;
-    double d = sqrt(s);
+    real d = sqrt(s);
     A[j * n + j] = d;
     for (int i = j + 1; i < n; i++) {
-      double t = A[i * n + j];
+      real t = A[i * n + j];
       for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
       A[i * n + j] = t / d;
     }
   }
   return 0;
 }
-static void chol_solve(const double* L, int n, double* b) {
+static void chol_solve(const real* L, int n, real* b) {
   for (int i = 0; i < n; i++) {
-    double s = b[i];
+    real s = b[i];
     for (int k = 0; k < i; k++) s -= L[i * n + k] * b[k];
     b[i] = s / L[i * n + i];
   }
   for (int i = n - 1; i >= 0; i--) {
-    double s = b[i];
+    real s = b[i];
     for (int k = i + 1; k < n; k++) s -= L[k * n + i] * b[k];
     b[i] = s / L[i * n + i];
   }
 }
 
 /* ---------------------------------------------------------------- collision */
-static void geom_world(const mg_model* m, const kin* k, int g, double* c, double R[3][3]) {
+static void geom_world(const mg_model* m, const kin* k, int g, real* c, real R[3][3]) {
   int nd = m->geom_node[g];
-  double pl[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]}, pw[3];
-  matvec3((double(*)[3])k->R[nd], pl, pw);
+  real pl[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]}, pw[3];
+  matvec3((real(*)[3])k->R[nd], pl, pw);
   for (int a = 0; a < 3; a++) c[a] = k->x[nd][a] + pw[a];
-  double gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]}, Rg[3][3];
+  real gq[4] = {m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]}, Rg[3][3];
   quat_to_mat(gq, Rg);
-  matmul3((double(*)[3])k->R[nd], Rg, R);
+  matmul3((real(*)[3])k->R[nd], Rg, R);
 }
 
-static int push_contact(contact* out, int n, int cap, int nodeA, int gA, int nodeB, int gB, const double* p,
-                        const double* nrm, double d) {
+static int push_contact(contact* out, int n, int cap, int nodeA, int gA, int nodeB, int gB, const real* p,
+                        const real* nrm, real d) {
   if (n >= cap) return n;
   contact* c = &out[n];
   c->nodeA = nodeA; c->geomA = gA; c->nodeB = nodeB; c->geomB = gB;
@@ -429,29 +442,29 @@ static int push_contact(contact* out, int n, int cap, int nodeA, int gA, int nod
 }
 
 /* sphere (center c, radius r) vs ground plane z = 0 */
-static int sphere_plane(contact* out, int n, int cap, int node, int g, const double* c, double r, double off) {
-  double d = c[2] - r;
+static int sphere_plane(contact* out, int n, int cap, int node, int g, const real* c, real r, real off) {
+  real d = c[2] - r;
   if (d < off) {
-    double p[3] = {c[0], c[1], c[2] - r}, nz[3] = {0, 0, 1};
+    real p[3] = {c[0], c[1], c[2] - r}, nz[3] = {0, 0, 1};
     n = push_contact(out, n, cap, node, g, -1, -1, p, nz, d);
   }
   return n;
 }
 
-static void closest_seg_seg(const double* p1, const double* q1, const double* p2, const double* q2, double* s_out,
-                            double* t_out) {
-  double d1[3], d2[3], r[3];
+static void closest_seg_seg(const real* p1, const real* q1, const real* p2, const real* q2, real* s_out,
+                            real* t_out) {
+  real d1[3], d2[3], r[3];
   for (int a = 0; a < 3; a++) { d1[a] = q1[a] - p1[a]; d2[a] = q2[a] - p2[a]; r[a] = p1[a] - p2[a]; }
-  double a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
-  double s, t;
-  double eps = 1e-12;
+  real a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+  real s, t;
+  real eps = 1e-12;
   if (a <= eps && e <= eps) { s = t = 0; }
   else if (a <= eps) { s = 0; t = f / e; t = t < 0 ? 0 : (t > 1 ? 1 : t); }
   else {
-    double c = dot3(d1, r);
+    real c = dot3(d1, r);
     if (e <= eps) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
     else {
-      double b = dot3(d1, d2), den = a * e - b * b;
+      real b = dot3(d1, d2), den = a * e - b * b;
       s = den > eps ? (b * f - c * e) / den : 0.0;
       s = s < 0 ? 0 : (s > 1 ? 1 : s);
       t = (b * s + f) / e;
@@ -463,8 +476,8 @@ static void closest_seg_seg(const double* p1, const double* q1, const double* p2
 }
 
 /* segment (or point) endpoints + radius for sphere/capsule geoms */
-static int geom_segment(const mg_model* m, const kin* k, int g, double* a, double* b, double* r) {
-  double c[3], R[3][3];
+static int geom_segment(const mg_model* m, const kin* k, int g, real* a, real* b, real* r) {
+  real c[3], R[3][3];
   geom_world(m, k, g, c, R);
   int ty = m->geom_type[g];
   if (ty == MG_GT_SPHERE) {
@@ -473,7 +486,7 @@ static int geom_segment(const mg_model* m, const kin* k, int g, double* a, doubl
     return 1;
   }
   if (ty == MG_GT_CAPSULE) {
-    double hl = m->geom_size[g][1];
+    real hl = m->geom_size[g][1];
     for (int i = 0; i < 3; i++) { a[i] = c[i] - R[i][2] * hl; b[i] = c[i] + R[i][2] * hl; }
     *r = m->geom_size[g][0];
     return 1;
@@ -486,27 +499,27 @@ static int geom_segment(const mg_model* m, const kin* k, int g, double* a, doubl
 /* signed distance of point pl (box frame) to a box of half extents hb: outside -> distance to the
  * closest point cb, normal away from the box; inside -> minus the smallest face depth (ties: x, y, z
  * order), normal = that face's outward normal, cb = the projection onto that face */
-static double point_box(const double* pl, const double* hb, double* nb, double* cb) {
-  double q[3];
+static real point_box(const real* pl, const real* hb, real* nb, real* cb) {
+  real q[3];
   int out = 0;
   for (int a = 0; a < 3; a++) {
     q[a] = pl[a] < -hb[a] ? -hb[a] : (pl[a] > hb[a] ? hb[a] : pl[a]);
     if (q[a] != pl[a]) out = 1;
   }
   if (out) {
-    double d[3] = {pl[0] - q[0], pl[1] - q[1], pl[2] - q[2]};
-    double l = sqrt(dot3(d, d));
+    real d[3] = {pl[0] - q[0], pl[1] - q[1], pl[2] - q[2]};
+    real l = sqrt(dot3(d, d));
     for (int a = 0; a < 3; a++) { nb[a] = d[a] / l; cb[a] = q[a]; }
     return l;
   }
   int kmin = 0;
-  double dmin = hb[0] - fabs(pl[0]);
+  real dmin = hb[0] - fabs(pl[0]);
   for (int a = 1; a < 3; a++) {
-    double dd = hb[a] - fabs(pl[a]);
+    real dd = hb[a] - fabs(pl[a]);
     if (dd < dmin) { dmin = dd; kmin = a; }
   }
   for (int a = 0; a < 3; a++) { nb[a] = 0.0; cb[a] = pl[a]; }
-  double sg = pl[kmin] < 0 ? -1.0 : 1.0;
+  real sg = pl[kmin] < 0 ? -1.0 : 1.0;
   nb[kmin] = sg;
   cb[kmin] = sg * hb[kmin];
   return -dmin;
@@ -516,15 +529,15 @@ static double point_box(const double* pl, const double* hb, double* nb, double* 
  * max(|a_k + t u_k| - h_k, 0)^2 is convex piecewise quadratic; it is minimised exactly on each
  * interval between the (sorted) slab crossings.  If the segment passes through the box
  * (Liang-Barsky), returns the middle of the inside portion and *inside = 1. */
-static double seg_box_t(const double* a, const double* u, const double* hb, int* inside) {
-  double t0 = 0.0, t1 = 1.0;
+static real seg_box_t(const real* a, const real* u, const real* hb, int* inside) {
+  real t0 = 0.0, t1 = 1.0;
   int hit = 1;
   for (int k = 0; k < 3 && hit; k++) {
     if (fabs(u[k]) < 1e-12) {
       if (a[k] < -hb[k] || a[k] > hb[k]) hit = 0;
     } else {
-      double ta = (-hb[k] - a[k]) / u[k], tb = (hb[k] - a[k]) / u[k];
-      if (ta > tb) { double x = ta; ta = tb; tb = x; }
+      real ta = (-hb[k] - a[k]) / u[k], tb = (hb[k] - a[k]) / u[k];
+      if (ta > tb) { real x = ta; ta = tb; tb = x; }
       if (ta > t0) t0 = ta;
       if (tb < t1) t1 = tb;
       if (t0 > t1) hit = 0;
@@ -532,32 +545,32 @@ static double seg_box_t(const double* a, const double* u, const double* hb, int*
   }
   if (hit) { *inside = 1; return 0.5 * (t0 + t1); }
   *inside = 0;
-  double bp[8];
+  real bp[8];
   int nb = 0;
   bp[nb++] = 0.0;
   for (int k = 0; k < 3; k++) {
     if (fabs(u[k]) < 1e-12) continue;
     for (int sgn = -1; sgn <= 1; sgn += 2) {
-      double t = (sgn * hb[k] - a[k]) / u[k];
+      real t = (sgn * hb[k] - a[k]) / u[k];
       if (t > 0.0 && t < 1.0) bp[nb++] = t;
     }
   }
   bp[nb++] = 1.0;
   for (int i = 1; i < nb; i++) /* insertion sort */
-    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { double x = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = x; }
-  double best_t = 0.0, best_f = 1e300;
+    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { real x = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = x; }
+  real best_t = 0.0, best_f = 1e300;
   for (int i = 0; i + 1 < nb; i++) {
-    double lo = bp[i], hi = bp[i + 1], mid = 0.5 * (lo + hi), num = 0.0, den = 0.0;
+    real lo = bp[i], hi = bp[i + 1], mid = 0.5 * (lo + hi), num = 0.0, den = 0.0;
     for (int k = 0; k < 3; k++) {
-      double x = a[k] + mid * u[k];
+      real x = a[k] + mid * u[k];
       if (x > hb[k]) { num += (a[k] - hb[k]) * u[k]; den += u[k] * u[k]; }
       else if (x < -hb[k]) { num += (a[k] + hb[k]) * u[k]; den += u[k] * u[k]; }
     }
-    double t = den > 0.0 ? -num / den : lo;
+    real t = den > 0.0 ? -num / den : lo;
     t = t < lo ? lo : (t > hi ? hi : t);
-    double f = 0.0;
+    real f = 0.0;
     for (int k = 0; k < 3; k++) {
-      double x = fabs(a[k] + t * u[k]) - hb[k];
+      real x = fabs(a[k] + t * u[k]) - hb[k];
       if (x > 0) f += x * x;
     }
     if (f < best_f) { best_f = f; best_t = t; }
@@ -565,35 +578,35 @@ static double seg_box_t(const double* a, const double* u, const double* hb, int*
   return best_t;
 }
 
-static void to_obj(const kin* k, const double* pw, double* pl) {
-  double d[3] = {pw[0] - k->op[0], pw[1] - k->op[1], pw[2] - k->op[2]};
-  mattvec3((double(*)[3])k->oR, d, pl);
+static void to_obj(const kin* k, const real* pw, real* pl) {
+  real d[3] = {pw[0] - k->op[0], pw[1] - k->op[1], pw[2] - k->op[2]};
+  mattvec3((real(*)[3])k->oR, d, pl);
 }
-static void from_obj_dir(const kin* k, const double* dl, double* dw) { matvec3((double(*)[3])k->oR, dl, dw); }
-static void from_obj_pt(const kin* k, const double* pl, double* pw) {
-  matvec3((double(*)[3])k->oR, pl, pw);
+static void from_obj_dir(const kin* k, const real* dl, real* dw) { matvec3((real(*)[3])k->oR, dl, dw); }
+static void from_obj_pt(const kin* k, const real* pl, real* pw) {
+  matvec3((real(*)[3])k->oR, pl, pw);
   for (int a = 0; a < 3; a++) pw[a] += k->op[a];
 }
 
 /* hand geom g (A) vs the object box (B); normal points from the object to the geom */
-static int geom_object(const mg_model* m, const kin* k, int g, double off, contact* out, int n, int cap) {
-  const double hb[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
+static int geom_object(const mg_model* m, const kin* k, int g, real off, contact* out, int n, int cap) {
+  const real hb[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
   int nd = m->geom_node[g], ty = m->geom_type[g];
-  double c[3], R[3][3];
+  real c[3], R[3][3];
   geom_world(m, k, g, c, R);
   if (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) {
-    double r = m->geom_size[g][0], hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0;
-    double aw[3], bw[3], al[3], bl[3], u[3];
+    real r = m->geom_size[g][0], hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0;
+    real aw[3], bw[3], al[3], bl[3], u[3];
     for (int a = 0; a < 3; a++) { aw[a] = c[a] - R[a][2] * hl; bw[a] = c[a] + R[a][2] * hl; }
     to_obj(k, aw, al);
     to_obj(k, bw, bl);
     for (int a = 0; a < 3; a++) u[a] = bl[a] - al[a];
     int inside;
-    double t = seg_box_t(al, u, hb, &inside), P[3], nb[3], cb[3];
+    real t = seg_box_t(al, u, hb, &inside), P[3], nb[3], cb[3];
     for (int a = 0; a < 3; a++) P[a] = al[a] + t * u[a];
-    double sd = point_box(P, hb, nb, cb), d = sd - r;
+    real sd = point_box(P, hb, nb, cb), d = sd - r;
     if (d < off) {
-      double pm[3], pw[3], nw[3];
+      real pm[3], pw[3], nw[3];
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - r * nb[a]) + cb[a]);
       from_obj_pt(k, pm, pw);
       from_obj_dir(k, nb, nw);
@@ -602,16 +615,16 @@ static int geom_object(const mg_model* m, const kin* k, int g, double off, conta
     return n;
   }
   if (ty != MG_GT_BOX) return n;
-  const double hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
+  const real hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
   /* the geom's vertices against the object */
   for (int v = 0; v < 8; v++) {
-    double l[3] = {(v & 1 ? 1 : -1) * hg[0], (v & 2 ? 1 : -1) * hg[1], (v & 4 ? 1 : -1) * hg[2]}, w[3], pl[3];
+    real l[3] = {(v & 1 ? 1 : -1) * hg[0], (v & 2 ? 1 : -1) * hg[1], (v & 4 ? 1 : -1) * hg[2]}, w[3], pl[3];
     matvec3(R, l, w);
     for (int a = 0; a < 3; a++) w[a] += c[a];
     to_obj(k, w, pl);
-    double nb[3], cb[3], d = point_box(pl, hb, nb, cb);
+    real nb[3], cb[3], d = point_box(pl, hb, nb, cb);
     if (d < off) {
-      double pm[3], pw[3], nw[3];
+      real pm[3], pw[3], nw[3];
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
       from_obj_pt(k, pm, pw);
       from_obj_dir(k, nb, nw);
@@ -620,13 +633,13 @@ static int geom_object(const mg_model* m, const kin* k, int g, double off, conta
   }
   /* the object's vertices against the geom box (normal flipped: geom -> object is -n) */
   for (int v = 0; v < 8; v++) {
-    double l[3] = {(v & 1 ? 1 : -1) * hb[0], (v & 2 ? 1 : -1) * hb[1], (v & 4 ? 1 : -1) * hb[2]}, w[3], d3[3], pl[3];
+    real l[3] = {(v & 1 ? 1 : -1) * hb[0], (v & 2 ? 1 : -1) * hb[1], (v & 4 ? 1 : -1) * hb[2]}, w[3], d3[3], pl[3];
     from_obj_pt(k, l, w);
     for (int a = 0; a < 3; a++) d3[a] = w[a] - c[a];
     mattvec3(R, d3, pl);
-    double nb[3], cb[3], d = point_box(pl, hg, nb, cb);
+    real nb[3], cb[3], d = point_box(pl, hg, nb, cb);
     if (d < off) {
-      double pm[3], pw[3], nw[3];
+      real pm[3], pw[3], nw[3];
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
       matvec3(R, pm, pw);
       for (int a = 0; a < 3; a++) pw[a] += c[a];
@@ -654,69 +667,69 @@ static int geom_object(const mg_model* m, const kin* k, int g, double off, conta
  * (csrc/convex.hpp) runs the same algorithm in fp32. */
 typedef struct {
   int kind;                    /* 0 segment [p0, p1], 1 box (c, R columns = axes, h) */
-  double p0[3], p1[3];
-  double c[3], R[3][3], h[3];
+  real p0[3], p1[3];
+  real c[3], R[3][3], h[3];
 } cvx_shape;
 
-static void cvx_support(const cvx_shape* A, const double* d, double* o) {
+static void cvx_support(const cvx_shape* A, const real* d, real* o) {
   if (A->kind == 0) {
-    const double* s = dot3(A->p0, d) >= dot3(A->p1, d) ? A->p0 : A->p1;
+    const real* s = dot3(A->p0, d) >= dot3(A->p1, d) ? A->p0 : A->p1;
     for (int a = 0; a < 3; a++) o[a] = s[a];
     return;
   }
   for (int a = 0; a < 3; a++) o[a] = A->c[a];
   for (int k = 0; k < 3; k++) {
-    double dk = A->R[0][k] * d[0] + A->R[1][k] * d[1] + A->R[2][k] * d[2];
-    double s = dk >= 0 ? A->h[k] : -A->h[k];
+    real dk = A->R[0][k] * d[0] + A->R[1][k] * d[1] + A->R[2][k] * d[2];
+    real s = dk >= 0 ? A->h[k] : -A->h[k];
     for (int a = 0; a < 3; a++) o[a] += s * A->R[a][k];
   }
 }
 
 /* support point of the ellipsoid x^2/e0^2 + y^2/e1^2 + z^2/e2^2 = 1 in direction d */
-static void ell_support(const double* e, const double* d, double* o) {
-  double q[3] = {e[0] * e[0] * d[0], e[1] * e[1] * d[1], e[2] * e[2] * d[2]};
-  double n = sqrt(q[0] * d[0] + q[1] * d[1] + q[2] * d[2]);
+static void ell_support(const real* e, const real* d, real* o) {
+  real q[3] = {e[0] * e[0] * d[0], e[1] * e[1] * d[1], e[2] * e[2] * d[2]};
+  real n = sqrt(q[0] * d[0] + q[1] * d[1] + q[2] * d[2]);
   if (n < 1e-30) { o[0] = o[1] = o[2] = 0.0; return; }
   for (int a = 0; a < 3; a++) o[a] = q[a] / n;
 }
 
 /* closest point of segment / triangle (Ericson, Real-Time Collision Detection 5.1.2 / 5.1.5) to the
  * origin as barycentric weights */
-static void cvx_seg(const double* a, const double* b, double* lam) {
-  double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, den = dot3(ab, ab);
-  double t = den > 0 ? -dot3(a, ab) / den : 0.0;
+static void cvx_seg(const real* a, const real* b, real* lam) {
+  real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, den = dot3(ab, ab);
+  real t = den > 0 ? -dot3(a, ab) / den : 0.0;
   t = t < 0 ? 0 : (t > 1 ? 1 : t);
   lam[0] = 1 - t; lam[1] = t;
 }
-static void cvx_tri(const double* a, const double* b, const double* c, double* lam) {
-  double ab[3], ac[3];
+static void cvx_tri(const real* a, const real* b, const real* c, real* lam) {
+  real ab[3], ac[3];
   for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; }
   lam[0] = lam[1] = lam[2] = 0.0;
-  double d1 = -dot3(ab, a), d2 = -dot3(ac, a);
+  real d1 = -dot3(ab, a), d2 = -dot3(ac, a);
   if (d1 <= 0 && d2 <= 0) { lam[0] = 1; return; }
-  double d3 = -dot3(ab, b), d4 = -dot3(ac, b);
+  real d3 = -dot3(ab, b), d4 = -dot3(ac, b);
   if (d3 >= 0 && d4 <= d3) { lam[1] = 1; return; }
-  double vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) { double v = d1 / (d1 - d3); lam[0] = 1 - v; lam[1] = v; return; }
-  double d5 = -dot3(ab, c), d6 = -dot3(ac, c);
+  real vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { real v = d1 / (d1 - d3); lam[0] = 1 - v; lam[1] = v; return; }
+  real d5 = -dot3(ab, c), d6 = -dot3(ac, c);
   if (d6 >= 0 && d5 <= d6) { lam[2] = 1; return; }
-  double vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); lam[0] = 1 - w; lam[2] = w; return; }
-  double va = d3 * d6 - d5 * d4;
+  real vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { real w = d2 / (d2 - d6); lam[0] = 1 - w; lam[2] = w; return; }
+  real va = d3 * d6 - d5 * d4;
   if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    real w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
     lam[1] = 1 - w; lam[2] = w; return;
   }
-  double den = va + vb + vc;
-  if (!(den > 0)) { double l2[2]; cvx_seg(a, b, l2); lam[0] = l2[0]; lam[1] = l2[1]; return; }
-  double v = vb / den, w = vc / den;
+  real den = va + vb + vc;
+  if (!(den > 0)) { real l2[2]; cvx_seg(a, b, l2); lam[0] = l2[0]; lam[1] = l2[1]; return; }
+  real v = vb / den, w = vc / den;
   lam[0] = 1 - v - w; lam[1] = v; lam[2] = w;
 }
 
 /* closest point of the simplex W[0..n-1] to the origin; keeps the supporting vertices (W, P in
  * place, order preserved), returns 1 if the origin lies inside a (non-degenerate) tetrahedron */
-static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double* lk) {
-  double lam[4] = {0, 0, 0, 0};
+static int cvx_simplex(real W[4][3], real P[4][3], int* n, real* v, real* lk) {
+  real lam[4] = {0, 0, 0, 0};
   if (*n == 1) {
     lam[0] = 1;
   } else if (*n == 2) {
@@ -725,22 +738,22 @@ static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double
     cvx_tri(W[0], W[1], W[2], lam);
   } else {
     static const int F[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}}; /* face + opposite */
-    double best = 1e300;
+    real best = 1e300;
     int any = 0;
     for (int f = 0; f < 4; f++) {
-      const double *a = W[F[f][0]], *b = W[F[f][1]], *c = W[F[f][2]], *d = W[F[f][3]];
-      double ab[3], ac[3], ad[3], nf[3];
+      const real *a = W[F[f][0]], *b = W[F[f][1]], *c = W[F[f][2]], *d = W[F[f][3]];
+      real ab[3], ac[3], ad[3], nf[3];
       for (int k = 0; k < 3; k++) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ad[k] = d[k] - a[k]; }
       cross3(ab, ac, nf);
-      double sp = -dot3(nf, a), sd = dot3(nf, ad);
-      double sc = dot3(ab, ab) + dot3(ac, ac) + dot3(ad, ad);
+      real sp = -dot3(nf, a), sd = dot3(nf, ad);
+      real sc = dot3(ab, ab) + dot3(ac, ac) + dot3(ad, ad);
       int degenerate = sd * sd <= 1e-12 * sc * sc * sc;
       if (!(sp * sd < 0) && !degenerate) continue;
       any = 1;
-      double l3[3], q[3];
+      real l3[3], q[3];
       cvx_tri(a, b, c, l3);
       for (int k = 0; k < 3; k++) q[k] = l3[0] * a[k] + l3[1] * b[k] + l3[2] * c[k];
-      double dq = dot3(q, q);
+      real dq = dot3(q, q);
       if (dq < best) {
         best = dq;
         lam[0] = lam[1] = lam[2] = lam[3] = 0;
@@ -751,14 +764,14 @@ static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double
   }
   int m = 0;
   v[0] = v[1] = v[2] = 0;
-  double Wn[4][3], Pn[4][3];
+  real Wn[4][3], Pn[4][3];
   for (int i = 0; i < *n; i++) {
     if (!(lam[i] > 0)) continue;
     for (int k = 0; k < 3; k++) { v[k] += lam[i] * W[i][k]; Wn[m][k] = W[i][k]; Pn[m][k] = P[i][k]; }
     lk[m++] = lam[i];
   }
-  memcpy(W, Wn, sizeof(double) * 3 * m);
-  memcpy(P, Pn, sizeof(double) * 3 * m);
+  memcpy(W, Wn, sizeof(real) * 3 * m);
+  memcpy(P, Pn, sizeof(real) * 3 * m);
   *n = m;
   return 0;
 }
@@ -768,25 +781,25 @@ static int cvx_simplex(double W[4][3], double P[4][3], int* n, double* v, double
 /* the core's point nearest the egg's centre in the egg-scaled metric (x / e): the segment's exact
  * minimiser of |p(t) / e|^2, or the box centre.  Returns 1 when that point lies inside the egg, i.e. the
  * cores certainly overlap (exact for a segment; sufficient for a box). */
-static int cvx_core_point(const cvx_shape* A, const double* e, double* sp) {
+static int cvx_core_point(const cvx_shape* A, const real* e, real* sp) {
   if (A->kind == 0) {
-    double q0[3], qu[3];
+    real q0[3], qu[3];
     for (int a = 0; a < 3; a++) { q0[a] = A->p0[a] / e[a]; qu[a] = (A->p1[a] - A->p0[a]) / e[a]; }
-    double den = dot3(qu, qu), t = den > 0 ? -dot3(q0, qu) / den : 0.0;
+    real den = dot3(qu, qu), t = den > 0 ? -dot3(q0, qu) / den : 0.0;
     t = t < 0 ? 0 : (t > 1 ? 1 : t);
     for (int a = 0; a < 3; a++) sp[a] = A->p0[a] + t * (A->p1[a] - A->p0[a]);
   } else {
     for (int a = 0; a < 3; a++) sp[a] = A->c[a];
   }
-  double r2 = 0;
+  real r2 = 0;
   for (int a = 0; a < 3; a++) r2 += (sp[a] / e[a]) * (sp[a] / e[a]);
   return r2 < 1.0;
 }
 
-static int cvx_gjk(const cvx_shape* A, const double* e, double cut, double* pa, double* pb, double* dist) {
-  double W[4][3], P[4][3], v[3];
+static int cvx_gjk(const cvx_shape* A, const real* e, real cut, real* pa, real* pb, real* dist) {
+  real W[4][3], P[4][3], v[3];
   if (A->kind == 0) { /* start from the segment point nearest the egg in its metric, towards the egg */
-    double sp[3], gr[3], bs[3];
+    real sp[3], gr[3], bs[3];
     cvx_core_point(A, e, sp);
     for (int a = 0; a < 3; a++) gr[a] = sp[a] / (e[a] * e[a]);
     ell_support(e, gr, bs);
@@ -796,14 +809,14 @@ static int cvx_gjk(const cvx_shape* A, const double* e, double cut, double* pa, 
   }
   if (dot3(v, v) < 1e-20) { v[0] = 0; v[1] = 0; v[2] = 1; }
   int n = 0;
-  double vv = dot3(v, v);
-  double lam[4] = {0, 0, 0, 0};
+  real vv = dot3(v, v);
+  real lam[4] = {0, 0, 0, 0};
   for (int it = 0; it < 64; it++) {
-    double nd[3] = {-v[0], -v[1], -v[2]}, a[3], b[3], w[3];
+    real nd[3] = {-v[0], -v[1], -v[2]}, a[3], b[3], w[3];
     cvx_support(A, nd, a);
     ell_support(e, v, b);
     for (int k = 0; k < 3; k++) w[k] = a[k] - b[k];
-    const double vw = dot3(v, w);
+    const real vw = dot3(v, w);
     if (vw > 0 && vw * vw > vv * cut * cut) { /* separating plane farther than cut: no contact */
       *dist = vw / sqrt(vv);
       return 2;
@@ -811,14 +824,14 @@ static int cvx_gjk(const cvx_shape* A, const double* e, double cut, double* pa, 
     if (n > 0 && vv - vw <= 1e-8 * vv + 1e-24) break;
     int dup = 0;
     for (int i = 0; i < n; i++) {
-      double dd[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
+      real dd[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
       if (dot3(dd, dd) <= 1e-24) dup = 1;
     }
     if (dup) break;
     for (int k = 0; k < 3; k++) { W[n][k] = w[k]; P[n][k] = a[k]; }
     n++;
     if (cvx_simplex(W, P, &n, v, lam)) return 0;
-    double vn = dot3(v, v);
+    real vn = dot3(v, v);
     if (vn <= 1e-20) return 0;
     int stall = it > 0 && vn >= vv * (1.0 - 1e-14); /* v starts at the centre difference */
     vv = vn;
@@ -841,28 +854,28 @@ static int cvx_gjk(const cvx_shape* A, const double* e, double cut, double* pa, 
  * 1 with the boundary point x of A - B nearest to where the refined portal meets the origin's side
  * (penetration vector: moving A by -x separates the cores) and the A-side witness pa; 0 if the portal
  * search degenerates. */
-static void mpr_support(const cvx_shape* A, const double* e, const double* d, double* w, double* a) {
-  double b[3], nd[3] = {-d[0], -d[1], -d[2]};
+static void mpr_support(const cvx_shape* A, const real* e, const real* d, real* w, real* a) {
+  real b[3], nd[3] = {-d[0], -d[1], -d[2]};
   cvx_support(A, d, a);
   ell_support(e, nd, b);
   for (int k = 0; k < 3; k++) w[k] = a[k] - b[k];
 }
-static void v3sub(const double* a, const double* b, double* o) { for (int k = 0; k < 3; k++) o[k] = a[k] - b[k]; }
-static void v3unit(double* a) {
-  double l = sqrt(dot3(a, a));
+static void v3sub(const real* a, const real* b, real* o) { for (int k = 0; k < 3; k++) o[k] = a[k] - b[k]; }
+static void v3unit(real* a) {
+  real l = sqrt(dot3(a, a));
   if (l > 0) for (int k = 0; k < 3; k++) a[k] /= l;
 }
-static void v3cp(double* d, const double* s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
-static void mpr_portal_dir(double V[5][3], double* dir) {
-  double a[3], b[3];
+static void v3cp(real* d, const real* s) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
+static void mpr_portal_dir(real V[5][3], real* dir) {
+  real a[3], b[3];
   v3sub(V[2], V[1], a);
   v3sub(V[3], V[1], b);
   cross3(a, b, dir);
   v3unit(dir);
 }
 /* replace one portal vertex by v4 so that the portal keeps facing the origin ray */
-static void mpr_expand(double V[5][3], double Pa[5][3]) {
-  double c[3];
+static void mpr_expand(real V[5][3], real Pa[5][3]) {
+  real c[3];
   cross3(V[4], V[0], c);
   int k;
   if (dot3(V[1], c) > 0) k = dot3(V[2], c) > 0 ? 1 : 3;
@@ -870,13 +883,13 @@ static void mpr_expand(double V[5][3], double Pa[5][3]) {
   v3cp(V[k], V[4]);
   v3cp(Pa[k], Pa[4]);
 }
-static int mpr_reached(double V[5][3], const double* dir) {
-  double d4 = dot3(V[4], dir);
-  double m = fmin(d4 - dot3(V[1], dir), fmin(d4 - dot3(V[2], dir), d4 - dot3(V[3], dir)));
+static int mpr_reached(real V[5][3], const real* dir) {
+  real d4 = dot3(V[4], dir);
+  real m = fmin(d4 - dot3(V[1], dir), fmin(d4 - dot3(V[2], dir), d4 - dot3(V[3], dir)));
   return m <= MPR_TOL;
 }
-static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
-  double V[5][3], Pa[5][3], dir[3];
+static int cvx_mpr(const cvx_shape* A, const real* e, real* x, real* pa) {
+  real V[5][3], Pa[5][3], dir[3];
   if (A->kind == 0) for (int a = 0; a < 3; a++) V[0][a] = 0.5 * (A->p0[a] + A->p1[a]);
   else for (int a = 0; a < 3; a++) V[0][a] = A->c[a];
   if (dot3(V[0], V[0]) < 1e-20) { V[0][0] = 1e-6; V[0][1] = 0; V[0][2] = 0; }
@@ -893,13 +906,13 @@ static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
   v3unit(dir);
   mpr_support(A, e, dir, V[2], Pa[2]);
   if (dot3(V[2], dir) <= 0) return 0;
-  double va[3], vb[3];
+  real va[3], vb[3];
   v3sub(V[1], V[0], va);
   v3sub(V[2], V[0], vb);
   cross3(va, vb, dir);
   v3unit(dir);
   if (dot3(dir, V[0]) > 0) {
-    double t[3];
+    real t[3];
     v3cp(t, V[1]); v3cp(V[1], V[2]); v3cp(V[2], t);
     v3cp(t, Pa[1]); v3cp(Pa[1], Pa[2]); v3cp(Pa[2], t);
     for (int k = 0; k < 3; k++) dir[k] = -dir[k];
@@ -908,7 +921,7 @@ static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
   for (it = 0; it < 64; it++) { /* discover a portal the origin ray passes through */
     mpr_support(A, e, dir, V[3], Pa[3]);
     if (dot3(V[3], dir) <= 0) return 0;
-    double c[3];
+    real c[3];
     cross3(V[1], V[3], c);
     if (dot3(c, V[0]) < -MPR_EPS) {
       v3cp(V[2], V[3]); v3cp(Pa[2], Pa[3]);
@@ -940,7 +953,7 @@ static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
     if (mpr_reached(V, dir) || it >= 64) break;
     mpr_expand(V, Pa);
   }
-  double lam[3];
+  real lam[3];
   cvx_tri(V[1], V[2], V[3], lam);
   for (int k = 0; k < 3; k++) {
     x[k] = lam[0] * V[1][k] + lam[1] * V[2][k] + lam[2] * V[3][k];
@@ -952,19 +965,19 @@ static int cvx_mpr(const cvx_shape* A, const double* e, double* x, double* pa) {
 /* one contact between core A (+ radius rA) and the ellipsoid e, object frame: GJK when the cores are
  * apart, MPR penetration when they overlap, the centre direction if MPR degenerates.  Normal from the
  * object to A. */
-static void cvx_contact(const cvx_shape* A0, double rA, const double* e, double cut, double* pt, double* nrm,
-                        double* d) {
-  double pa[3], pb[3], dist, x[3];
+static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, real* pt, real* nrm,
+                        real* d) {
+  real pa[3], pb[3], dist, x[3];
   /* a box core is rounded by a 1 mm margin (at most half its smallest half extent): GJK then resolves
    * penetrations shallower than the margin (resting contacts), and MPR only runs for deeper ones */
   cvx_shape As = *A0;
   const cvx_shape* A = &As;
   if (As.kind == 1) {
-    const double mg = fmin(CVX_MARGIN, 0.5 * fmin(As.h[0], fmin(As.h[1], As.h[2])));
+    const real mg = fmin(CVX_MARGIN, 0.5 * fmin(As.h[0], fmin(As.h[1], As.h[2])));
     for (int a = 0; a < 3; a++) As.h[a] -= mg;
     rA += mg;
   }
-  double sp[3];
+  real sp[3];
   const int g = cvx_core_point(A, e, sp) ? 0 : cvx_gjk(A, e, rA + cut, pa, pb, &dist); /* overlap: MPR */
   if (g == 2) { /* farther than rA + cut: only the (lower-bound) distance is meaningful */
     *d = dist - rA;
@@ -975,15 +988,15 @@ static void cvx_contact(const cvx_shape* A0, double rA, const double* e, double 
   if (g && dist > 1e-9) {
     /* the normal is the egg's surface normal at its witness point (the gradient of the implicit
      * function): better conditioned than (pa - pb) / dist when the gap is small */
-    double gr[3] = {pb[0] / (e[0] * e[0]), pb[1] / (e[1] * e[1]), pb[2] / (e[2] * e[2])};
-    double gl = sqrt(dot3(gr, gr));
+    real gr[3] = {pb[0] / (e[0] * e[0]), pb[1] / (e[1] * e[1]), pb[2] / (e[2] * e[2])};
+    real gl = sqrt(dot3(gr, gr));
     for (int a = 0; a < 3; a++) nrm[a] = gr[a] / gl;
     for (int a = 0; a < 3; a++) pt[a] = 0.5 * ((pa[a] - nrm[a] * rA) + pb[a]);
     *d = dist - rA;
     return;
   }
   if (cvx_mpr(A, e, x, pa)) {
-    double l = sqrt(dot3(x, x));
+    real l = sqrt(dot3(x, x));
     if (l > 1e-9) {
       for (int a = 0; a < 3; a++) {
         nrm[a] = -x[a] / l;
@@ -993,10 +1006,10 @@ static void cvx_contact(const cvx_shape* A0, double rA, const double* e, double 
       return;
     }
   }
-  double ca[3];
+  real ca[3];
   if (A->kind == 0) for (int a = 0; a < 3; a++) ca[a] = 0.5 * (A->p0[a] + A->p1[a]);
   else for (int a = 0; a < 3; a++) ca[a] = A->c[a];
-  double l = sqrt(dot3(ca, ca));
+  real l = sqrt(dot3(ca, ca));
   if (l > 1e-12) for (int a = 0; a < 3; a++) nrm[a] = ca[a] / l;
   else { nrm[0] = 0; nrm[1] = 0; nrm[2] = 1; }
   for (int a = 0; a < 3; a++) pt[a] = 0.5 * ca[a];
@@ -1013,19 +1026,19 @@ static int obj_candidates(int otype, int gtype) {
 }
 
 /* hand geom g (A) vs the egg / pen object (B); normal points from the object to the geom */
-static int geom_object_convex(const mg_model* m, const kin* k, int g, double off, contact* out, int n, int cap) {
+static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, contact* out, int n, int cap) {
   const int nd = m->geom_node[g], ty = m->geom_type[g], ot = m->obj_type;
-  const double os[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
-  double c[3], R[3][3];
+  const real os[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
+  real c[3], R[3][3];
   geom_world(m, k, g, c, R);
   const int round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
   if (!round && ty != MG_GT_BOX) return n;
-  double pw[3], nw[3];
+  real pw[3], nw[3];
   if (ot == MG_GT_ELLIPSOID) {
     cvx_shape A;
-    double r = 0.0;
+    real r = 0.0;
     if (round) {
-      double hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, aw[3], bw[3];
+      real hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, aw[3], bw[3];
       for (int a = 0; a < 3; a++) { aw[a] = c[a] - R[a][2] * hl; bw[a] = c[a] + R[a][2] * hl; }
       A.kind = 0;
       to_obj(k, aw, A.p0);
@@ -1034,13 +1047,13 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, double off
     } else {
       A.kind = 1;
       to_obj(k, c, A.c);
-      double Rt[3][3];
+      real Rt[3][3];
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) Rt[a][b] = k->oR[b][a];
       matmul3(Rt, R, A.R);
       for (int a = 0; a < 3; a++) A.h[a] = m->geom_size[g][a];
     }
-    double pl[3], nl[3], d;
+    real pl[3], nl[3], d;
     cvx_contact(&A, r, os, off, pl, nl, &d);
     if (d < off) {
       from_obj_pt(k, pl, pw);
@@ -1050,20 +1063,20 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, double off
     return n;
   }
   /* pen: capsule of radius os[0] along the object's z, half length os[1] */
-  const double ro = os[0];
-  double p0[3], p1[3];
+  const real ro = os[0];
+  real p0[3], p1[3];
   for (int a = 0; a < 3; a++) { p0[a] = k->op[a] - k->oR[a][2] * os[1]; p1[a] = k->op[a] + k->oR[a][2] * os[1]; }
   if (round) {
-    double hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, r = m->geom_size[g][0], a0[3], a1[3];
+    real hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, r = m->geom_size[g][0], a0[3], a1[3];
     for (int a = 0; a < 3; a++) { a0[a] = c[a] - R[a][2] * hl; a1[a] = c[a] + R[a][2] * hl; }
-    double s, t, pa[3], pb[3], dv[3];
+    real s, t, pa[3], pb[3], dv[3];
     closest_seg_seg(a0, a1, p0, p1, &s, &t);
     for (int a = 0; a < 3; a++) {
       pa[a] = a0[a] + s * (a1[a] - a0[a]);
       pb[a] = p0[a] + t * (p1[a] - p0[a]);
       dv[a] = pa[a] - pb[a];
     }
-    double dist = sqrt(dot3(dv, dv)), d = dist - r - ro;
+    real dist = sqrt(dot3(dv, dv)), d = dist - r - ro;
     if (d < off && dist > 1e-9) {
       for (int a = 0; a < 3; a++) {
         nw[a] = dv[a] / dist;
@@ -1075,19 +1088,19 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, double off
   }
   /* hand box vs the pen: the pen segment's closest point to the box, then its two ends (an end is
    * skipped when the closest point is within 1 % of the segment from it) */
-  const double hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
-  double d0[3], P0[3], du[3], u[3];
+  const real hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
+  real d0[3], P0[3], du[3], u[3];
   for (int a = 0; a < 3; a++) { d0[a] = p0[a] - c[a]; du[a] = p1[a] - p0[a]; }
   mattvec3(R, d0, P0);
   mattvec3(R, du, u);
   int inside;
-  const double ts = seg_box_t(P0, u, hg, &inside);
+  const real ts = seg_box_t(P0, u, hg, &inside);
   for (int q = 0; q < 3; q++) {
     if ((q == 1 && ts < 0.01) || (q == 2 && ts > 0.99)) continue;
-    const double t = q == 0 ? ts : (q == 1 ? 0.0 : 1.0);
-    double P[3], nb[3], cb[3], pm[3];
+    const real t = q == 0 ? ts : (q == 1 ? 0.0 : 1.0);
+    real P[3], nb[3], cb[3], pm[3];
     for (int a = 0; a < 3; a++) P[a] = P0[a] + t * u[a];
-    const double d = point_box(P, hg, nb, cb) - ro;
+    const real d = point_box(P, hg, nb, cb) - ro;
     if (d < off) {
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - nb[a] * ro) + cb[a]);
       matvec3(R, pm, pw);
@@ -1105,25 +1118,25 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, double off
  * articulation geoms against the object in geom order */
 static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, contact* out, int cap) {
   int n = 0;
-  double off = p->contact_offset;
+  real off = p->contact_offset;
   for (int g = 0; g < m->num_geoms; g++) {
     if (!(m->geom_filter[g] & MG_COLLIDE_GROUND)) continue;
     int nd = m->geom_node[g], ty = m->geom_type[g];
-    double c[3], R[3][3];
+    real c[3], R[3][3];
     geom_world(m, k, g, c, R);
     if (ty == MG_GT_SPHERE) {
       n = sphere_plane(out, n, cap, nd, g, c, m->geom_size[g][0], off);
     } else if (ty == MG_GT_CAPSULE) {
-      double hl = m->geom_size[g][1], r = m->geom_size[g][0], e[3];
+      real hl = m->geom_size[g][1], r = m->geom_size[g][0], e[3];
       for (int s = -1; s <= 1; s += 2) {
         for (int a = 0; a < 3; a++) e[a] = c[a] + s * R[a][2] * hl;
         n = sphere_plane(out, n, cap, nd, g, e, r, off);
       }
     } else if (ty == MG_GT_BOX) {
       for (int corner = 0; corner < 8; corner++) {
-        double l[3] = {(corner & 1 ? 1 : -1) * m->geom_size[g][0], (corner & 2 ? 1 : -1) * m->geom_size[g][1],
+        real l[3] = {(corner & 1 ? 1 : -1) * m->geom_size[g][0], (corner & 2 ? 1 : -1) * m->geom_size[g][1],
                        (corner & 4 ? 1 : -1) * m->geom_size[g][2]};
-        double w[3], e[3];
+        real w[3], e[3];
         matvec3(R, l, w);
         for (int a = 0; a < 3; a++) e[a] = c[a] + w[a];
         n = sphere_plane(out, n, cap, nd, g, e, 0.0, off);
@@ -1132,39 +1145,39 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
   }
   if (m->obj_type == MG_GT_BOX) {
     for (int corner = 0; corner < 8; corner++) {
-      double l[3] = {(corner & 1 ? 1 : -1) * m->obj_size[0], (corner & 2 ? 1 : -1) * m->obj_size[1],
+      real l[3] = {(corner & 1 ? 1 : -1) * m->obj_size[0], (corner & 2 ? 1 : -1) * m->obj_size[1],
                      (corner & 4 ? 1 : -1) * m->obj_size[2]}, e[3];
       from_obj_pt(k, l, e);
       n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
     }
   } else if (m->obj_type == MG_GT_CAPSULE) { /* pen: its two end spheres */
     for (int s = -1; s <= 1; s += 2) {
-      double l[3] = {0.0, 0.0, s * (double)m->obj_size[1]}, e[3];
+      real l[3] = {0.0, 0.0, s * (real)m->obj_size[1]}, e[3];
       from_obj_pt(k, l, e);
       n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, m->obj_size[0], off);
     }
   } else if (m->obj_type == MG_GT_ELLIPSOID) { /* egg: its support point in -z */
-    const double es[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
-    double dl[3] = {-k->oR[2][0], -k->oR[2][1], -k->oR[2][2]}, sl[3], e[3];
+    const real es[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
+    real dl[3] = {-k->oR[2][0], -k->oR[2][1], -k->oR[2][2]}, sl[3], e[3];
     ell_support(es, dl, sl);
     from_obj_pt(k, sl, e);
     n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
   }
   for (int pi = 0; pi < m->num_pairs; pi++) {
     int ga = m->pair[pi][0], gb = m->pair[pi][1];
-    double a0[3], a1[3], b0[3], b1[3], ra, rb;
+    real a0[3], a1[3], b0[3], b1[3], ra, rb;
     if (!geom_segment(m, k, ga, a0, a1, &ra) || !geom_segment(m, k, gb, b0, b1, &rb)) continue;
-    double s, t, pa[3], pb[3], dv[3];
+    real s, t, pa[3], pb[3], dv[3];
     closest_seg_seg(a0, a1, b0, b1, &s, &t);
     for (int a = 0; a < 3; a++) {
       pa[a] = a0[a] + s * (a1[a] - a0[a]);
       pb[a] = b0[a] + t * (b1[a] - b0[a]);
       dv[a] = pa[a] - pb[a];
     }
-    double dist = sqrt(dot3(dv, dv));
-    double d = dist - ra - rb;
+    real dist = sqrt(dot3(dv, dv));
+    real d = dist - ra - rb;
     if (d < off && dist > 1e-9) {
-      double nrm[3] = {dv[0] / dist, dv[1] / dist, dv[2] / dist}, pt[3];
+      real nrm[3] = {dv[0] / dist, dv[1] / dist, dv[2] / dist}, pt[3];
       for (int a = 0; a < 3; a++) pt[a] = 0.5 * (pa[a] - ra * nrm[a] + pb[a] + rb * nrm[a]);
       n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pt, nrm, d);
     }
@@ -1177,30 +1190,30 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
   return n;
 }
 
-static void tangent_basis(const double* n, double* t1, double* t2) {
-  double a[3] = {0, 0, 0};
+static void tangent_basis(const real* n, real* t1, real* t2) {
+  real a[3] = {0, 0, 0};
   if (fabs(n[0]) < 0.57735) a[0] = 1; else a[1] = 1;
   cross3(a, n, t1);
-  double l = sqrt(dot3(t1, t1));
+  real l = sqrt(dot3(t1, t1));
   for (int i = 0; i < 3; i++) t1[i] /= l;
   cross3(n, t1, t2);
 }
 
 /* generalized Jacobian row of a unit force `dir` at point p on nodeA (minus on nodeB); a side
  * equal to OBJ_NODE acts on the free object's columns [w; v_com] (after the articulation's) */
-static void jac_row(const mg_model* m, const kin* k, int nodeA, int nodeB, const double* p, const double* dir,
-                    double* J) {
+static void jac_row(const mg_model* m, const kin* k, int nodeA, int nodeB, const real* p, const real* dir,
+                    real* J) {
   int nv = nv_of(m), nvt = nvt_of(m);
-  memset(J, 0, sizeof(double) * nvt);
-  double r[3], w[6];
+  memset(J, 0, sizeof(real) * nvt);
+  real r[3], w[6];
   for (int a = 0; a < 3; a++) r[a] = p[a] - k->o[a];
   cross3(r, dir, w);
   w[3] = dir[0]; w[4] = dir[1]; w[5] = dir[2];
   for (int side = 0; side < 2; side++) {
     int node = side == 0 ? nodeA : nodeB;
-    double sg = side == 0 ? 1.0 : -1.0;
+    real sg = side == 0 ? 1.0 : -1.0;
     if (node == OBJ_NODE) {
-      double ro[3], rxd[3];
+      real ro[3], rxd[3];
       for (int a = 0; a < 3; a++) ro[a] = p[a] - k->op[a];
       cross3(ro, dir, rxd);
       for (int a = 0; a < 3; a++) { J[nv + a] += sg * rxd[a]; J[nv + 3 + a] += sg * dir[a]; }
@@ -1215,25 +1228,25 @@ static void jac_row(const mg_model* m, const kin* k, int nodeA, int nodeB, const
 
 /* ---------------------------------------------------------------- one substep */
 typedef struct {
-  double h;
+  real h;
   contact con[MAXC];
   int ncon;
-  double lam[MAXR];
+  real lam[MAXR];
   int nrows;
   int row_kind[MAXR]; /* 0 normal, 1 friction, 2 limit-lower, 3 limit-upper */
   int row_ref[MAXR];  /* contact index or node */
 } substep_out;
 
-static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const double* tau_act, substep_out* so) {
+static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const real* tau_act, substep_out* so) {
   int nv = nv_of(m), nvt = nvt_of(m), nn = m->num_nodes;
-  double h = p->dt / p->substeps;
+  real h = p->dt / p->substeps;
   so->h = h;
   kin k;
   forward_kinematics(m, s, &k);
-  static __thread double M[MAXV * MAXV];
-  double C[MAXV], diag[MAXN], tadd[MAXN], kk[MAXN], bb[MAXN], ref[MAXN];
-  double ga = m->gravity_off ? 0.0 : 1.0;
-  double g[3] = {ga * p->gravity[0], ga * p->gravity[1], ga * p->gravity[2]};
+  static __thread real M[MAXV * MAXV];
+  real C[MAXV], diag[MAXN], tadd[MAXN], kk[MAXN], bb[MAXN], ref[MAXN];
+  real ga = m->gravity_off ? 0.0 : 1.0;
+  real g[3] = {ga * p->gravity[0], ga * p->gravity[1], ga * p->gravity[2]};
   tendon_forces(m, s, s->ttend);
   for (int i = 1; i < nn; i++) {
     dofterm t = dof_term(m, s, i);
@@ -1242,18 +1255,18 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   }
   mass_matrix(m, &k, h, M, diag, nvt);
   bias_forces(m, &k, s, g, C);
-  double nu[MAXV], rhs[MAXV];
+  real nu[MAXV], rhs[MAXV];
   for (int c = 0; c < 6 && !m->fixed_base; c++) nu[c] = s->nu0[c];
   for (int i = 1; i < nn; i++) nu[dof_col(m, i)] = s->qd[i];
   for (int c = 0; c < nv; c++) rhs[c] = -C[c];
   for (int i = 1; i < nn; i++) {
     int ci = dof_col(m, i);
-    double t = tau_act ? tau_act[i - 1] : 0.0;
+    real t = tau_act ? tau_act[i - 1] : 0.0;
     rhs[ci] += t + tadd[i] + s->ttend[i] - bb[i] * s->qd[i] - kk[i] * (s->qj[i] - ref[i] + h * s->qd[i]);
   }
   if (m->obj_type) {
     /* object block: diag(I_world, m 1); bias = [w x I w; -m g] */
-    double Iw[3][3], Rt[3][3], T[3][3], Il[3][3] = {{m->obj_inertia[0], 0, 0}, {0, m->obj_inertia[1], 0},
+    real Iw[3][3], Rt[3][3], T[3][3], Il[3][3] = {{m->obj_inertia[0], 0, 0}, {0, m->obj_inertia[1], 0},
                                                       {0, 0, m->obj_inertia[2]}};
     matmul3(k.oR, Il, T);
     for (int a = 0; a < 3; a++)
@@ -1263,7 +1276,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       for (int b = 0; b < 3; b++) M[(nv + a) * nvt + nv + b] = Iw[a][b];
       M[(nv + 3 + a) * nvt + nv + 3 + a] = m->obj_mass;
     }
-    double Iwv[3], gyro[3];
+    real Iwv[3], gyro[3];
     matvec3(Iw, s->ow, Iwv);
     cross3(s->ow, Iwv, gyro);
     for (int a = 0; a < 3; a++) {
@@ -1272,7 +1285,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       rhs[nv + a] = -gyro[a];
       rhs[nv + 3 + a] = m->obj_mass * m->obj_gravity * p->gravity[a];
     }
-    double fw[3];
+    real fw[3];
     if (s->of_local) matvec3(k.oR, s->of, fw);
     else for (int a = 0; a < 3; a++) fw[a] = s->of[a];
     for (int a = 0; a < 3; a++) rhs[nv + 3 + a] += fw[a];
@@ -1281,23 +1294,23 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   chol_solve(M, nvt, rhs);
   for (int c = 0; c < nvt; c++) nu[c] += h * rhs[c];
   if (m->obj_type) { /* velocity damping of the free body (gym AssetOptions angular/linear_damping) */
-    double fa = 1.0 / (1.0 + h * m->obj_ang_damping), fl = 1.0 / (1.0 + h * m->obj_lin_damping);
+    real fa = 1.0 / (1.0 + h * m->obj_ang_damping), fl = 1.0 / (1.0 + h * m->obj_lin_damping);
     for (int a = 0; a < 3; a++) { nu[nv + a] *= fa; nu[nv + 3 + a] *= fl; }
   }
 
   /* constraint rows */
   int cap = p->max_contacts < MAXC ? p->max_contacts : MAXC;
   so->ncon = collide(m, p, &k, so->con, cap);
-  static __thread double J[MAXR][MAXV], Y[MAXR][MAXV];
-  double b[MAXR], W[MAXR];
+  static __thread real J[MAXR][MAXV], Y[MAXR][MAXV];
+  real b[MAXR], W[MAXR];
   int nr = 0;
   for (int c = 0; c < so->ncon; c++) {
     contact* ct = &so->con[c];
-    double t1[3], t2[3];
+    real t1[3], t2[3];
     tangent_basis(ct->n, t1, t2);
-    double deff = ct->d - p->rest_offset;
-    double bn = deff >= 0 ? -deff / h : fmin(-p->baumgarte * deff / h, p->max_depen_vel);
-    const double* dirs[3] = {ct->n, t1, t2};
+    real deff = ct->d - p->rest_offset;
+    real bn = deff >= 0 ? -deff / h : fmin(-p->baumgarte * deff / h, p->max_depen_vel);
+    const real* dirs[3] = {ct->n, t1, t2};
     for (int r = 0; r < 3; r++) {
       jac_row(m, &k, ct->nodeA, ct->nodeB, ct->p, dirs[r], J[nr]);
       b[nr] = r == 0 ? bn : 0.0;
@@ -1308,11 +1321,11 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   }
   for (int i = 1; i < nn; i++) {
     if (!m->limited[i]) continue;
-    double dl = s->qj[i] - m->lower[i], du = m->upper[i] - s->qj[i];
+    real dl = s->qj[i] - m->lower[i], du = m->upper[i] - s->qj[i];
     for (int side = 0; side < 2; side++) {
-      double d = side == 0 ? dl : du;
+      real d = side == 0 ? dl : du;
       if (d >= p->limit_margin) continue;
-      memset(J[nr], 0, sizeof(double) * nvt);
+      memset(J[nr], 0, sizeof(real) * nvt);
       J[nr][dof_col(m, i)] = side == 0 ? 1.0 : -1.0;
       b[nr] = d >= 0 ? -d / h : fmin(-p->baumgarte * d / h, p->max_depen_vel);
       so->row_kind[nr] = 2 + side;
@@ -1324,7 +1337,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   for (int r = 0; r < nr; r++) {
     for (int c = 0; c < nvt; c++) Y[r][c] = J[r][c];
     chol_solve(M, nvt, Y[r]);
-    double w = 0;
+    real w = 0;
     for (int c = 0; c < nvt; c++) w += J[r][c] * Y[r][c];
     W[r] = w;
     so->lam[r] = 0;
@@ -1332,46 +1345,46 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   for (int it = 0; it < p->pos_iters; it++) {
     for (int r = 0; r < nr; r++) {
       if (W[r] <= 1e-12) continue;
-      double v = 0;
+      real v = 0;
       for (int c = 0; c < nvt; c++) v += J[r][c] * nu[c];
-      double lnew = so->lam[r] + (b[r] - v) / W[r];
+      real lnew = so->lam[r] + (b[r] - v) / W[r];
       if (so->row_kind[r] == 1) {
-        double mu = p->friction;
+        real mu = p->friction;
         if (s->gmu) { /* DR: mean of the two shapes' friction (ground plane: sim friction) */
           const contact* ct = &so->con[so->row_ref[r]];
           const int g2[2] = {ct->geomA, ct->geomB};
-          double sum = 0.0;
+          real sum = 0.0;
           for (int k = 0; k < 2; k++)
             sum += g2[k] >= 0 ? s->gmu[g2[k]] : (g2[k] == -2 ? s->gmu[m->num_geoms] : p->friction);
           mu = 0.5 * sum;
         }
-        double lim = mu * so->lam[3 * so->row_ref[r]];  /* normal row of this contact */
+        real lim = mu * so->lam[3 * so->row_ref[r]];  /* normal row of this contact */
         lnew = lnew < -lim ? -lim : (lnew > lim ? lim : lnew);
       } else if (lnew < 0) {
         lnew = 0;
       }
-      double dl = lnew - so->lam[r];
+      real dl = lnew - so->lam[r];
       so->lam[r] = lnew;
       for (int c = 0; c < nvt; c++) nu[c] += Y[r][c] * dl;
     }
   }
   /* integrate */
   if (!m->fixed_base) {
-    double w[3] = {nu[0], nu[1], nu[2]}, vo[3] = {nu[3], nu[4], nu[5]};
-    double pn[3];
+    real w[3] = {nu[0], nu[1], nu[2]}, vo[3] = {nu[3], nu[4], nu[5]};
+    real pn[3];
     for (int a = 0; a < 3; a++) pn[a] = s->p[a] + h * vo[a];
-    double wn = sqrt(dot3(w, w)), dq[4];
+    real wn = sqrt(dot3(w, w)), dq[4];
     if (wn * h > 1e-12) {
-      double ha = 0.5 * wn * h, sn = sin(ha) / wn;
+      real ha = 0.5 * wn * h, sn = sin(ha) / wn;
       dq[0] = w[0] * sn; dq[1] = w[1] * sn; dq[2] = w[2] * sn; dq[3] = cos(ha);
     } else {
       dq[0] = 0.5 * h * w[0]; dq[1] = 0.5 * h * w[1]; dq[2] = 0.5 * h * w[2]; dq[3] = 1.0;
     }
-    double qn[4];
+    real qn[4];
     quat_mul_d(dq, s->q, qn);
-    double l = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+    real l = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
     for (int a = 0; a < 4; a++) s->q[a] = qn[a] / l;
-    double dp[3] = {pn[0] - s->p[0], pn[1] - s->p[1], pn[2] - s->p[2]}, wxdp[3];
+    real dp[3] = {pn[0] - s->p[0], pn[1] - s->p[1], pn[2] - s->p[2]}, wxdp[3];
     cross3(w, dp, wxdp);
     for (int a = 0; a < 3; a++) { s->p[a] = pn[a]; s->nu0[a] = w[a]; s->nu0[3 + a] = vo[a] + wxdp[a]; }
   }
@@ -1380,16 +1393,16 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     s->qj[i] += h * s->qd[i];
   }
   if (m->obj_type) {
-    double w[3] = {nu[nv], nu[nv + 1], nu[nv + 2]}, dq[4], qn[4];
-    double wn = sqrt(dot3(w, w));
+    real w[3] = {nu[nv], nu[nv + 1], nu[nv + 2]}, dq[4], qn[4];
+    real wn = sqrt(dot3(w, w));
     if (wn * h > 1e-12) {
-      double ha = 0.5 * wn * h, sn = sin(ha) / wn;
+      real ha = 0.5 * wn * h, sn = sin(ha) / wn;
       dq[0] = w[0] * sn; dq[1] = w[1] * sn; dq[2] = w[2] * sn; dq[3] = cos(ha);
     } else {
       dq[0] = 0.5 * h * w[0]; dq[1] = 0.5 * h * w[1]; dq[2] = 0.5 * h * w[2]; dq[3] = 1.0;
     }
     quat_mul_d(dq, s->oq, qn);
-    double l = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+    real l = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
     for (int a = 0; a < 4; a++) s->oq[a] = qn[a] / l;
     for (int a = 0; a < 3; a++) {
       s->ow[a] = w[a];
@@ -1400,37 +1413,37 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
 }
 
 /* sensor wrench and dof force from the last substep's impulses */
-static void sensor_outputs(const mg_model* m, const astate* s, const substep_out* so, const double* tau_act,
+static void sensor_outputs(const mg_model* m, const astate* s, const substep_out* so, const real* tau_act,
                            float* sensors, float* dof_force) {
   if (sensors && m->num_sensors > 0) {
     kin k;
     forward_kinematics(m, s, &k);  /* post-step pose for the body frame */
     for (int si = 0; si < m->num_sensors; si++) {
       int body = m->sensor_body[si], nd = m->body_node[body];
-      double Rb[3][3], bq[4] = {m->body_quat[body][0], m->body_quat[body][1], m->body_quat[body][2],
+      real Rb[3][3], bq[4] = {m->body_quat[body][0], m->body_quat[body][1], m->body_quat[body][2],
                                  m->body_quat[body][3]}, Rl[3][3];
       quat_to_mat(bq, Rl);
       matmul3(k.R[nd], Rl, Rb);
-      double bp[3] = {m->body_pos[body][0], m->body_pos[body][1], m->body_pos[body][2]}, bw[3], xb[3];
+      real bp[3] = {m->body_pos[body][0], m->body_pos[body][1], m->body_pos[body][2]}, bw[3], xb[3];
       matvec3(k.R[nd], bp, bw);
       for (int a = 0; a < 3; a++) xb[a] = k.x[nd][a] + bw[a];
-      double F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
+      real F[3] = {0, 0, 0}, T[3] = {0, 0, 0};
       for (int c = 0; c < so->ncon; c++) {
         const contact* ct = &so->con[c];
-        double sg = 0;
+        real sg = 0;
         if (ct->geomA >= 0 && m->geom_body[ct->geomA] == body) sg = 1;
         else if (ct->geomB >= 0 && m->geom_body[ct->geomB] == body) sg = -1;
         if (sg == 0) continue;
-        double t1[3], t2[3];
+        real t1[3], t2[3];
         tangent_basis(ct->n, t1, t2);
-        double f[3], r[3], rf[3];
+        real f[3], r[3], rf[3];
         for (int a = 0; a < 3; a++)
           f[a] = sg * (so->lam[3 * c] * ct->n[a] + so->lam[3 * c + 1] * t1[a] + so->lam[3 * c + 2] * t2[a]) / so->h;
         for (int a = 0; a < 3; a++) r[a] = ct->p[a] - xb[a];
         cross3(r, f, rf);
         for (int a = 0; a < 3; a++) { F[a] += f[a]; T[a] += rf[a]; }
       }
-      double Fl[3], Tl[3];
+      real Fl[3], Tl[3];
       mattvec3(Rb, F, Fl);
       mattvec3(Rb, T, Tl);
       for (int a = 0; a < 3; a++) { sensors[6 * si + a] = (float)Fl[a]; sensors[6 * si + 3 + a] = (float)Tl[a]; }
@@ -1440,9 +1453,9 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
     /* drive / passive force at the post-step state (saturated drives report +-effort), tendon force
      * of the last substep, plus the joint-limit impulses / h */
     for (int i = 1; i < m->num_nodes; i++) {
-      double t = (tau_act ? tau_act[i - 1] : 0.0) + s->ttend[i];
+      real t = (tau_act ? tau_act[i - 1] : 0.0) + s->ttend[i];
       if (m->drive_kp[i] > 0.0) {
-        double tgt = s->tgt ? s->tgt[i - 1] : 0.0;
+        real tgt = s->tgt ? s->tgt[i - 1] : 0.0;
         t += s->sat[i] ? (m->drive_kp[i] * (tgt - s->qj[i]) - m->damping[i] * s->qd[i] > 0 ? m->effort_limit[i]
                                                                                                  : -m->effort_limit[i])
                        : m->drive_kp[i] * (tgt - s->qj[i]) - m->damping[i] * s->qd[i];
@@ -1460,7 +1473,7 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
 }
 
 static void load_object(astate* s, const float* row) {
-  double nq = 0;
+  real nq = 0;
   for (int a = 0; a < 3; a++) { s->op[a] = row[a]; s->ov[a] = row[7 + a]; s->ow[a] = row[10 + a]; }
   for (int a = 0; a < 4; a++) { s->oq[a] = row[3 + a]; nq += s->oq[a] * s->oq[a]; }
   nq = sqrt(nq);
@@ -1481,15 +1494,15 @@ static void body_states(const mg_model* m, const astate* s, float* out) {
   forward_kinematics(m, s, &k);
   for (int b = 0; b < m->num_bodies; b++) {
     int nd = m->body_node[b];
-    double bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]}, Rl[3][3],
+    real bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]}, Rl[3][3],
            Rb[3][3];
     quat_to_mat(bq, Rl);
     matmul3(k.R[nd], Rl, Rb);
-    double bp[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]}, bw[3], xb[3], q[4];
+    real bp[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]}, bw[3], xb[3], q[4];
     matvec3(k.R[nd], bp, bw);
     for (int a = 0; a < 3; a++) xb[a] = k.x[nd][a] + bw[a];
     mat_to_quat(Rb, q);
-    double cl[3] = {m->body_com[b][0], m->body_com[b][1], m->body_com[b][2]}, cw[3], r[3], wxr[3];
+    real cl[3] = {m->body_com[b][0], m->body_com[b][1], m->body_com[b][2]}, cw[3], r[3], wxr[3];
     matvec3(Rb, cl, cw);
     for (int a = 0; a < 3; a++) r[a] = xb[a] + cw[a] - k.o[a];
     cross3(k.V[nd], r, wxr);
@@ -1506,14 +1519,14 @@ static void body_states(const mg_model* m, const astate* s, float* out) {
 /* one env: root rows [articulation, (object, goal)], dof rows, PD targets, sensors, dof forces,
  * rigid-body rows [articulation bodies, (object, goal)] */
 /* domain randomization: the model with one env_props row applied (include/migym.h layout) */
-static void apply_env_props(const mg_model* m, const float* row, mg_model* mm, double* gmu) {
+static void apply_env_props(const mg_model* m, const float* row, mg_model* mm, real* gmu) {
   *mm = *m;
   const int nn = m->num_nodes, ng = m->num_geoms, nt = m->num_tendons;
   for (int i = 0; i < nn; i++) {
     const float* r = row + 8 * i;
-    const double sc = m->mass[i] > 0.0f ? (double)r[0] / (double)m->mass[i] : 1.0;
+    const real sc = m->mass[i] > 0.0f ? (real)r[0] / (real)m->mass[i] : 1.0;
     mm->mass[i] = r[0];
-    for (int k = 0; k < 6; k++) mm->inertia[i][k] = (float)((double)m->inertia[i][k] * sc);
+    for (int k = 0; k < 6; k++) mm->inertia[i][k] = (float)((real)m->inertia[i][k] * sc);
     mm->armature[i] = r[1]; mm->damping[i] = r[2]; mm->stiffness[i] = r[3];
     mm->lower[i] = r[4]; mm->upper[i] = r[5]; mm->drive_kp[i] = r[6]; mm->effort_limit[i] = r[7];
   }
@@ -1524,11 +1537,11 @@ static void apply_env_props(const mg_model* m, const float* row, mg_model* mm, d
   const float* o = t + 2 * nt;
   gmu[ng] = o[1];
   if (m->obj_type) {
-    const double sc = (double)o[2], fm = (double)o[0] / (double)m->obj_mass;
+    const real sc = (real)o[2], fm = (real)o[0] / (real)m->obj_mass;
     mm->obj_mass = o[0];
     for (int a = 0; a < 3; a++) {
-      mm->obj_size[a] = (float)((double)m->obj_size[a] * sc);
-      mm->obj_inertia[a] = (float)((double)m->obj_inertia[a] * fm * sc * sc);
+      mm->obj_size[a] = (float)((real)m->obj_size[a] * sc);
+      mm->obj_inertia[a] = (float)((real)m->obj_inertia[a] * fm * sc * sc);
     }
   }
 }
@@ -1539,7 +1552,7 @@ static void simulate_env(const mg_model* m0, const mg_sim_params* p, float* root
   astate s;
   memset(&s, 0, sizeof(s));
   mg_model* mdr = NULL;
-  double gmu[MG_MAX_GEOMS + 1];
+  real gmu[MG_MAX_GEOMS + 1];
   const mg_model* m = m0;
   if (props) {
     mdr = (mg_model*)malloc(sizeof(mg_model));
@@ -1553,7 +1566,7 @@ static void simulate_env(const mg_model* m0, const mg_sim_params* p, float* root
   if (oforce)
     for (int a = 0; a < 3; a++) s.of[a] = oforce[a];
   s.of_local = oforce_local;
-  double tau[MAXN];
+  real tau[MAXN];
   for (int i = 0; i < m->num_dofs; i++) tau[i] = act ? act[i] : 0.0;
   substep_out* so = (substep_out*)malloc(sizeof(substep_out));
   memset(so, 0, sizeof(*so));
@@ -1606,8 +1619,9 @@ int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* ro
   return orc_simulate_views(m, p, n, &v, threads);
 }
 
+#ifndef ORC_FP32 /* fp64 inspection hooks of the checker (KATs); not in the fp32 timing build */
 int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
-                    double* M_out) {
+                    real* M_out) {
   astate s;
   kin k;
   load_state(m, root13, dof2, &s);
@@ -1617,13 +1631,13 @@ int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root
 }
 
 int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
-                          const float* tau, double* qacc_out) {
+                          const float* tau, real* qacc_out) {
   astate s;
   kin k;
   load_state(m, root13, dof2, &s);
   forward_kinematics(m, &s, &k);
   int nv = nv_of(m);
-  double h = p->dt / p->substeps, M[MAXV * MAXV], C[MAXV], g[3] = {p->gravity[0], p->gravity[1], p->gravity[2]};
+  real h = p->dt / p->substeps, M[MAXV * MAXV], C[MAXV], g[3] = {p->gravity[0], p->gravity[1], p->gravity[2]};
   mass_matrix(m, &k, h, M, 0, nv);
   bias_forces(m, &k, &s, g, C);
   if (cholesky(M, nv) != 0) return -1;
@@ -1635,7 +1649,7 @@ int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float
   return nv;
 }
 
-int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, double* out,
+int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, real* out,
                  int32_t cap) {
   astate s;
   kin k;
@@ -1647,7 +1661,7 @@ int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13,
   int c = cap < MAXC ? cap : MAXC;
   int nc = collide(m, p, &k, con, c);
   for (int i = 0; i < nc; i++) {
-    double* o = out + 9 * i;
+    real* o = out + 9 * i;
     o[0] = con[i].nodeA;
     o[1] = con[i].p[0]; o[2] = con[i].p[1]; o[3] = con[i].p[2];
     o[4] = con[i].n[0]; o[5] = con[i].n[1]; o[6] = con[i].n[2];
@@ -1657,6 +1671,8 @@ int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13,
   return nc;
 }
 
+#endif
+
 int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out) {
   astate s;
   memset(&s, 0, sizeof(s));
@@ -1665,10 +1681,11 @@ int orc_rigid_body_states(const mg_model* m, const float* root13, const float* d
   return m->num_bodies;
 }
 
+#ifndef ORC_FP32
 /* KAT hook: the egg narrowphase (cvx_contact) for core A against the origin-centred ellipsoid e.
  * kind 0: shape = segment p0, p1 (6 doubles); kind 1: shape = box centre (3), axes R row-major (9),
  * half extents (3).  out = contact point (3), normal from the ellipsoid to A (3), signed distance. */
-int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, const double* e, double* out) {
+int orc_ellipsoid_contact(int32_t kind, const real* shape, real radius, const real* e, real* out) {
   cvx_shape A;
   memset(&A, 0, sizeof(A));
   A.kind = kind;
@@ -1684,3 +1701,4 @@ int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, cons
   cvx_contact(&A, radius, e, 1e300, out, out + 3, out + 6);
   return MG_OK;
 }
+#endif

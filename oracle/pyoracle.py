@@ -17,7 +17,9 @@ LIB = os.path.join(HERE, "build", "liboracle.so")
 sys.path.insert(0, os.path.join(HERE, "..", "isaacgymenvs-ma_amd"))
 from migym import _abi  # noqa: E402  (struct mirrors only)
 
+LIB_F32 = os.path.join(HERE, "build", "liboracle_f32.so")
 _lib = None
+_lib32 = None
 
 
 def build():
@@ -55,11 +57,27 @@ def lib():
         l.orc_hand_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
                                         C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32,
                                         C.c_int32]
+        l.orc_hand_finalize.argtypes = [C.POINTER(_abi.TaskParams), C.POINTER(_abi.TaskBuffers)]
         l.orc_ellipsoid_contact.argtypes = [C.c_int32, P, C.c_double, P, P]
         l.orc_dr_apply.argtypes = [C.POINTER(_abi.DrApplyArgs)]
         l.orc_dr_noise.argtypes = [C.POINTER(_abi.DrNoiseArgs)]
         _lib = l
     return _lib
+
+
+def lib_f32():
+    """The fp32 physics build (bench.py's timed CPU baseline; the tests' checker is lib())."""
+    global _lib32
+    if _lib32 is None:
+        if not os.path.exists(LIB_F32):
+            build()
+        l = C.CDLL(LIB_F32)
+        P = C.c_void_p
+        l.orc_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
+                                   C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32, C.c_int32]
+        l.orc_hand_env_step.argtypes = l.orc_env_step.argtypes
+        _lib32 = l
+    return _lib32
 
 
 def f32(a):
@@ -206,9 +224,10 @@ class HostEnv:
         v, b = self.views(), self.buffers(seed, step, env_offset)
         lib().orc_post_physics(C.byref(tp), C.byref(v), C.byref(b), self.n)
 
-    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0):
+    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0, fp32=False):
         v, b = self.views(), self.buffers(seed, step, env_offset)
-        lib().orc_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v), C.byref(b), self.n, threads)
+        (lib_f32() if fp32 else lib()).orc_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v),
+                                                     C.byref(b), self.n, threads)
 
 
 class HandHostEnv:
@@ -253,6 +272,9 @@ class HandHostEnv:
         self.rb_forces = np.zeros((n, nb, 3), np.float32)
         self.force_prob = None
         self.states = None
+        # running-mean partial sums left for a cross-rank all-reduce (defer_finalize)
+        self.scratch = np.zeros(2, np.uint64)
+        self.defer_finalize = 0
 
     def views(self):
         v = _abi.StateViews()
@@ -272,7 +294,13 @@ class HandHostEnv:
         b.seed, b.step_counter, b.env_offset = seed, step, env_offset
         b.prev_targets, b.goal_states, b.reset_goal = p(self.prev_targets), p(self.goal_states), p(self.reset_goal)
         b.successes, b.consecutive_successes = p(self.successes), p(self.cons)
+        b.reduce_scratch, b.defer_finalize = p(self.scratch), self.defer_finalize
         return b
+
+    def finalize(self, tp):
+        """mg_hand_finalize: the running mean from the (all-reduced) partial sums in ``scratch``."""
+        b = self.buffers()
+        lib().orc_hand_finalize(C.byref(tp), C.byref(b))
 
     def pre_physics(self, model_np, tp, seed=0, step=0, env_offset=0):
         v, b = self.views(), self.buffers(seed, step, env_offset)
@@ -286,7 +314,7 @@ class HandHostEnv:
         v = self.views()
         lib().orc_simulate_views(model_np.ctypes.data, C.byref(sp), self.n, C.byref(v), threads)
 
-    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0):
+    def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0, fp32=False):
         v, b = self.views(), self.buffers(seed, step, env_offset)
-        lib().orc_hand_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v), C.byref(b), self.n,
-                                threads)
+        (lib_f32() if fp32 else lib()).orc_hand_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp),
+                                                          C.byref(v), C.byref(b), self.n, threads)

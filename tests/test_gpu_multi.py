@@ -1,0 +1,130 @@
+"""GPU side of the multi-GPU output path and of controlFrequencyInv.
+
+  * out_pack: the fused kernels write each row [clamped obs | rew | reset] of the gather's message
+    exactly equal to the buffers they write for the single-GPU caller (Ant, MA-Ant, ShadowHand);
+  * defer_finalize + mg_hand_finalize: the deferred running mean equals the in-step one bit for bit;
+  * controlFrequencyInv = 2: one launch runs simulate twice between one pre- and one post_physics_step,
+    held to the oracle running orc_simulate twice (vec_task.py:381-384), over 3 control steps.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import migym
+import pyoracle as O
+from migym import _abi, configs, model as M, taskdefs
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def lib():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    return _abi.lib()
+
+
+class _Pack:
+    """Single-rank stand-in for PackedGather: one slot, no collective."""
+
+    def __init__(self, rows, nobs):
+        self.rows, self.nobs = rows, nobs
+        self.buf = torch.full((rows, nobs + 2), float("nan"), device=DEV)
+
+    def next_pack(self):
+        return self.buf
+
+    def issue(self):
+        pass
+
+
+@pytest.mark.parametrize("task", ["Ant", "MAAnt", "ShadowHand", "Cartpole"])
+def test_out_pack_rows_equal_step_outputs(task):
+    env = migym.make(seed=0, task=task, num_envs=256, sim_device=DEV, rl_device=DEV, headless=True)
+    pk = _Pack(env.num_actors, env.num_obs)
+    env.attach_output_gather(pk)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    for _ in range(4):
+        a = torch.rand((env.num_actors, env.num_actions), device=DEV, generator=g) * 2.4 - 1.2
+        obs, rew, reset, _ = env.step(a)
+        torch.cuda.synchronize()
+        b = pk.buf
+        assert torch.equal(b[:, : env.num_obs], obs["obs"])
+        assert torch.equal(b[:, env.num_obs], rew)
+        assert torch.equal(b[:, env.num_obs + 1], reset.float())
+    env.close()
+
+
+def test_deferred_running_mean_equals_in_step(lib):
+    """Two identical ShadowHand envs; one defers the running mean (multi-GPU path) and finalizes after the
+    step: consecutive_successes is bit-identical every step."""
+    envs = []
+    for defer in (0, 1):
+        cfg = configs.task_config("ShadowHand", 512, sim_device=DEV)
+        cfg["env"]["episodeLength"] = 4
+        e = migym.make(seed=0, task="ShadowHand", num_envs=512, sim_device=DEV, rl_device=DEV, headless=True,
+                       cfg={"task": cfg})
+        e._tb.defer_finalize = defer
+        envs.append(e)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    for _ in range(10):
+        a = torch.rand((512, 20), device=DEV, generator=g) * 2 - 1
+        envs[0].step(a)
+        envs[1].step(a)
+        _abi.check(lib.mg_hand_finalize(C.byref(envs[1].task_params), C.byref(envs[1]._tb),
+                                        torch.cuda.current_stream().cuda_stream), lib)
+        torch.cuda.synchronize()
+        assert torch.equal(envs[0].consecutive_successes, envs[1].consecutive_successes)
+        assert int(envs[1]._reduce.abs().sum()) == 0
+    assert float(envs[0].consecutive_successes) != 0.0
+    for e in envs:
+        e.close()
+
+
+@pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128)])
+def test_control_freq_inv_runs_simulate_twice(lib, task, n):
+    cfg = configs.task_config(task, 16)
+    cfg["env"]["controlFrequencyInv"] = 2
+    spec = M.load_builtin(taskdefs.TASK_INFO[task][1])
+    sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[task][5])
+    tp = taskdefs.task_params(task, cfg, spec)
+    assert tp.control_freq_inv == 2
+    h = O.HostEnv(tp, spec, n)
+    T = lambda x, dt=torch.float32: torch.as_tensor(np.ascontiguousarray(x)).to(DEV, dt)  # noqa: E731
+    dev = {k: T(getattr(h, k)) for k in ("root", "dof", "act_eff", "sensors", "dof_force", "actions",
+                                          "actions_out", "obs", "obs_clamped", "rew", "potentials",
+                                          "prev_potentials", "up", "heading")}
+    reset, prog = T(h.reset, torch.int64), T(h.progress, torch.int64)
+    timeout = torch.zeros(n, dtype=torch.bool, device=DEV)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state, v.dof_actuation = (dev[k].data_ptr() for k in ("root", "dof", "act_eff"))
+    v.sensors, v.dof_force = dev["sensors"].data_ptr(), dev["dof_force"].data_ptr()
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(v)), lib)
+    rng = np.random.default_rng(4)
+    try:
+        for t in range(3):
+            a = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+            h.actions[:] = a
+            dev["actions"].copy_(T(a))
+            h.env_step(mnp, sp, tp, seed=2, step=t, threads=8)
+            b = _abi.TaskBuffers()
+            b.actions, b.actions_out = dev["actions"].data_ptr(), dev["actions_out"].data_ptr()
+            b.obs, b.obs_clamped, b.rew = dev["obs"].data_ptr(), dev["obs_clamped"].data_ptr(), dev["rew"].data_ptr()
+            b.reset, b.progress, b.timeout = reset.data_ptr(), prog.data_ptr(), timeout.data_ptr()
+            b.potentials, b.prev_potentials = dev["potentials"].data_ptr(), dev["prev_potentials"].data_ptr()
+            b.up_vec, b.heading_vec = dev["up"].data_ptr(), dev["heading"].data_ptr()
+            b.seed, b.step_counter = 2, t
+            _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(b), torch.cuda.current_stream().cuda_stream), lib)
+        torch.cuda.synchronize()
+    finally:
+        lib.mg_sim_destroy(sim)
+    np.testing.assert_array_equal(reset.cpu().numpy(), h.reset)
+    np.testing.assert_array_equal(prog.cpu().numpy(), h.progress)
+    og = dev["obs"].cpu().numpy()
+    bad = np.abs(og - h.obs) > (2e-2 + 2e-2 * np.abs(h.obs))
+    assert bad.mean() < 1e-3, (bad.sum(), np.argwhere(bad)[:10])

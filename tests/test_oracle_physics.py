@@ -221,3 +221,22 @@ def test_dropped_ant_comes_to_rest_on_the_plane():
         R = M.qmat(rb[b, 3:7].astype(np.float64))
         fz += (R @ sens[0, 6 * s:6 * s + 3])[2]
     assert abs(fz - spec.total_mass() * 9.81) < 0.15 * spec.total_mass() * 9.81
+
+
+def test_fp32_restatement_tracks_fp64_checker():
+    """liboracle_f32.so (bench.py's timed CPU baseline) computes the same step as the fp64 checker:
+    5 Ant control steps from the reset state agree to fp32 rounding (obs within 2e-3)."""
+    from migym import configs
+    cfg = configs.task_config("Ant", 256)
+    spec = M.load_builtin("ant")
+    sp, tp = taskdefs.sim_params(cfg, 16), taskdefs.task_params("Ant", cfg, spec)
+    mnp = M.pack_model(spec)
+    obs = []
+    for fp32 in (False, True):
+        h = O.HostEnv(tp, spec, 256)
+        rng = np.random.default_rng(0)
+        for t in range(5):
+            h.actions[:] = rng.uniform(-1, 1, h.actions.shape)
+            h.env_step(mnp, sp, tp, 0, t, 4, fp32=fp32)
+        obs.append(h.obs.copy())
+    np.testing.assert_allclose(obs[1], obs[0], atol=2e-3, rtol=2e-3)
