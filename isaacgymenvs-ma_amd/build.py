@@ -54,16 +54,21 @@ def _run_parallel(cmds, verbose):
         raise subprocess.CalledProcessError(1, failed[0])
 
 
-def build(force=False, verbose=False, timing=False):
+def build(force=False, verbose=False, timing=False, variant=None, defines=()):
+    """variant: build an A/B variant with extra -D defines into migym/_lib/var/<variant>.so (selected at
+    run time through MIGYM_LIB, tools/gpu_variants.sh)."""
     out = OUT_TIMING if timing else OUT
-    if not force and not needs_build(out):
+    if variant:
+        out = os.path.join(HERE, "migym", "_lib", "var", variant + ".so")
+    if not force and not variant and not needs_build(out):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]
     if timing:
         flags.append("-DMG_PHASE_TIMING")
-    objdir = os.path.join(HERE, "build", "timing" if timing else "release")
+    flags += ["-D" + d for d in defines]
+    objdir = os.path.join(HERE, "build", ("var_" + variant) if variant else ("timing" if timing else "release"))
     os.makedirs(objdir, exist_ok=True)
     objs, cmds = [], []
     for i in range(-1, num_instances()):
@@ -78,4 +83,11 @@ def build(force=False, verbose=False, timing=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, timing="--timing" in sys.argv))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--timing", action="store_true")
+    ap.add_argument("--variant", default=None)
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True, timing=a.timing, variant=a.variant, defines=a.defines))

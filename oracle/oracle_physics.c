@@ -710,14 +710,23 @@ static void cvx_tri(const real* a, const real* b, const real* c, real* lam) {
   real d3 = -dot3(ab, b), d4 = -dot3(ac, b);
   if (d3 >= 0 && d4 <= d3) { lam[1] = 1; return; }
   real vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) { real v = d1 / (d1 - d3); lam[0] = 1 - v; lam[1] = v; return; }
+  /* the three edge cases divide by a length that is 0 only for coincident vertices (a == b, a == c, b == c,
+   * e.g. an MPR portal whose support points repeat): then the vertex itself is the answer (no 0 / 0) */
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    real v = (d1 - d3) > 0 ? d1 / (d1 - d3) : 0;
+    lam[0] = 1 - v; lam[1] = v; return;
+  }
   real d5 = -dot3(ab, c), d6 = -dot3(ac, c);
   if (d6 >= 0 && d5 <= d6) { lam[2] = 1; return; }
   real vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) { real w = d2 / (d2 - d6); lam[0] = 1 - w; lam[2] = w; return; }
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    real w = (d2 - d6) > 0 ? d2 / (d2 - d6) : 0;
+    lam[0] = 1 - w; lam[2] = w; return;
+  }
   real va = d3 * d6 - d5 * d4;
   if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    real w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    real den2 = (d4 - d3) + (d5 - d6);
+    real w = den2 > 0 ? (d4 - d3) / den2 : 0;
     lam[1] = 1 - w; lam[2] = w; return;
   }
   real den = va + vb + vc;
@@ -965,6 +974,11 @@ static int cvx_mpr(const cvx_shape* A, const real* e, real* x, real* pa) {
 /* one contact between core A (+ radius rA) and the ellipsoid e, object frame: GJK when the cores are
  * apart, MPR penetration when they overlap, the centre direction if MPR degenerates.  Normal from the
  * object to A. */
+static int cvx_finite(const real* p, const real* n, real d) {
+  return isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]) && isfinite(n[0]) && isfinite(n[1]) && isfinite(n[2]) &&
+         isfinite(d);
+}
+
 static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, real* pt, real* nrm,
                         real* d) {
   real pa[3], pb[3], dist, x[3];
@@ -989,13 +1003,12 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
     /* the normal is the egg's surface normal at its witness point (the gradient of the implicit
      * function): better conditioned than (pa - pb) / dist when the gap is small */
     real gr[3] = {pb[0] / (e[0] * e[0]), pb[1] / (e[1] * e[1]), pb[2] / (e[2] * e[2])};
-    real gl = sqrt(dot3(gr, gr));
-    for (int a = 0; a < 3; a++) nrm[a] = gr[a] / gl;
+    real gl2 = dot3(gr, gr);
+    for (int a = 0; a < 3; a++) nrm[a] = gl2 > 1e-30 ? gr[a] / sqrt(gl2) : (pa[a] - pb[a]) / dist;
     for (int a = 0; a < 3; a++) pt[a] = 0.5 * ((pa[a] - nrm[a] * rA) + pb[a]);
     *d = dist - rA;
-    return;
-  }
-  if (cvx_mpr(A, e, x, pa)) {
+    if (cvx_finite(pt, nrm, *d)) return;
+  } else if (cvx_mpr(A, e, x, pa)) {
     real l = sqrt(dot3(x, x));
     if (l > 1e-9) {
       for (int a = 0; a < 3; a++) {
@@ -1003,9 +1016,10 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
         pt[a] = pa[a] - 0.5 * x[a] - nrm[a] * rA * 0.5;
       }
       *d = -l - rA;
-      return;
+      if (cvx_finite(pt, nrm, *d)) return;
     }
   }
+  /* MPR degenerate, or a non-finite result of a degenerate simplex: the centre direction */
   real ca[3];
   if (A->kind == 0) for (int a = 0; a < 3; a++) ca[a] = 0.5 * (A->p0[a] + A->p1[a]);
   else for (int a = 0; a < 3; a++) ca[a] = A->c[a];

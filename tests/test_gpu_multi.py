@@ -128,3 +128,56 @@ def test_control_freq_inv_runs_simulate_twice(lib, task, n):
     og = dev["obs"].cpu().numpy()
     bad = np.abs(og - h.obs) > (2e-2 + 2e-2 * np.abs(h.obs))
     assert bad.mean() < 1e-3, (bad.sum(), np.argwhere(bad)[:10])
+
+
+@pytest.mark.parametrize("task", ["Ant", "MAAnt", "ShadowHand"])
+def test_non_finite_state_flags_reset(task):
+    """NaN guard: a NaN injected into one env's state gives that env reset = 1 (all its
+    agents under MA), reward 0 and a zero observation row; the next step's reset restores a finite state;
+    the other envs are untouched."""
+    n = 64
+    env = migym.make(seed=0, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True)
+    A = env.num_agents
+    g = torch.Generator(device=DEV).manual_seed(0)
+    act = lambda: torch.rand((env.num_actors, env.num_actions), device=DEV, generator=g) * 2 - 1  # noqa: E731
+    for _ in range(3):
+        env.step(act())
+    e = 5
+    if task == "ShadowHand":
+        env.root_state_tensor[3 * e + 1, 3] = float("nan")     # the object's orientation
+    else:
+        env.root_states[e * A + (A - 1), 2] = float("nan")     # the last agent's torso height
+    obs, rew, reset, _ = env.step(act())
+    torch.cuda.synchronize()
+    rows = torch.arange(e * A, (e + 1) * A, device=DEV)
+    assert bool((reset[rows] == 1).all())
+    assert bool((obs["obs"][rows] == 0).all()) and bool((rew[rows] == 0).all())
+    others = torch.ones(env.num_actors, dtype=torch.bool, device=DEV)
+    others[rows] = False
+    assert bool(torch.isfinite(obs["obs"][others]).all())
+    for _ in range(2):   # ShadowHand resets in pre_physics (1 step), the locomotion tasks in post_physics
+        obs, rew, reset, _ = env.step(act())
+    torch.cuda.synchronize()
+    state = env.root_state_tensor if task == "ShadowHand" else env.root_states
+    assert bool(torch.isfinite(state).all()) and bool(torch.isfinite(obs["obs"]).all())
+    env.close()
+
+
+def test_egg_rollout_stays_finite_after_other_kernels():
+    """The egg narrowphase (GJK / MPR, convex.hpp) over a rollout that starts after other tasks' kernels
+    have run on the device: every object state stays finite (the round-1 NaN came from cvx_tri's 0 / 0 on
+    coincident vertices, guarded now)."""
+    ant = migym.make(seed=0, task="Ant", num_envs=4096, sim_device=DEV, rl_device=DEV, headless=True)
+    for _ in range(5):
+        ant.step(torch.rand((4096, 8), device=DEV) * 2 - 1)
+    ant.close()
+    cfg = configs.task_config("ShadowHand", 4096, sim_device=DEV)
+    cfg["env"]["objectType"] = "egg"
+    env = migym.make(seed=0, task="ShadowHand", num_envs=4096, sim_device=DEV, rl_device=DEV, headless=True,
+                     cfg={"task": cfg})
+    g = torch.Generator(device=DEV).manual_seed(3)
+    for _ in range(40):
+        env.step(torch.rand((4096, 20), device=DEV, generator=g) * 2 - 1)
+        torch.cuda.synchronize()
+        assert bool(torch.isfinite(env.root_state_tensor).all()), "non-finite object state"
+    env.close()
