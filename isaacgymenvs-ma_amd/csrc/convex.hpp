@@ -30,10 +30,10 @@ namespace mg {
 #define MG_CVX_REAL double
 #endif
 typedef MG_CVX_REAL creal;
-// cvx_contact is a real call: the caller keeps its own registers around one narrowphase call site
-// instead of inlining the fp64 GJK / MPR into the team kernel (measured: egg 6.86 -> 7.04 M env-steps/s)
+// cvx_contact_v is inlined into the team kernel.  A real call (-DMG_CVX_INLINE='__attribute__((noinline))',
+// A/B only) is not safe in these kernels: see the note at cvx_contact_v.
 #ifndef MG_CVX_INLINE
-#define MG_CVX_INLINE __attribute__((noinline))
+#define MG_CVX_INLINE __forceinline__
 #endif
 struct D3 {
   creal x, y, z;
@@ -343,14 +343,16 @@ __device__ __forceinline__ bool cvx_finite(D3 p, D3 n, creal d) {
          isfinite(d);
 }
 
+// the narrowphase result: contact point, normal from the object to A, signed distance
+struct CvxHit {
+  D3 pt, nrm;
+  creal d;
+};
+
 // one contact between core A (+ radius rA) and the ellipsoid e (object frame): GJK when apart, MPR
 // when overlapping, the centre direction if MPR degenerates.  Normal from the object to A.
-// NaN history: a noinline build once produced NaN object states.  The cause was cvx_tri's edge cases
-// dividing 0 / 0 when two simplex / portal vertices coincide (reachable through repeated support
-// points; whether it is hit depends on rounding, so on FMA contraction and on inlining): those
-// divisions are guarded now, and any non-finite result falls back to the centre direction below.
-__device__ MG_CVX_INLINE void cvx_contact(CvxShape A, creal rA, D3 e, creal cut, D3* pt, D3* nrm,
-                                                      creal* d) {
+__device__ __forceinline__ CvxHit cvx_contact_body(CvxShape A, creal rA, D3 e, creal cut) {
+  CvxHit o;
   D3 pa, pb, x;
   creal dist;
   if (A.kind == 1) {  // box cores rounded by CVX_MARGIN (see the oracle): resting contacts stay with GJK
@@ -361,35 +363,72 @@ __device__ MG_CVX_INLINE void cvx_contact(CvxShape A, creal rA, D3 e, creal cut,
   D3 sp;
   const int g = cvx_core_point(A, e, sp) ? 0 : cvx_gjk(A, e, rA + cut, pa, pb, dist);  // overlap: MPR
   if (g == 2) {  // farther than rA + cut: only the (lower-bound) distance is meaningful
-    *d = dist - rA;
-    *nrm = d3(0, 0, 1);
-    *pt = d3(0, 0, 0);
-    return;
+    o.d = dist - rA;
+    o.nrm = d3(0, 0, 1);
+    o.pt = d3(0, 0, 0);
+    return o;
   }
   if (g && dist > 1e-9) {
     // the egg's surface normal at its witness point (gradient of the implicit function): better
     // conditioned than (pa - pb) / dist when the gap is small
     const D3 gr = d3(pb.x / (e.x * e.x), pb.y / (e.y * e.y), pb.z / (e.z * e.z));
     const creal gl = dot(gr, gr);
-    *nrm = gl > 1e-30 ? gr * (1.0 / sqrt(gl)) : (pa - pb) * (1.0 / dist);
-    *pt = ((pa - *nrm * rA) + pb) * 0.5;
-    *d = dist - rA;
-    if (cvx_finite(*pt, *nrm, *d)) return;
+    o.nrm = gl > 1e-30 ? gr * (1.0 / sqrt(gl)) : (pa - pb) * (1.0 / dist);
+    o.pt = ((pa - o.nrm * rA) + pb) * 0.5;
+    o.d = dist - rA;
+    if (cvx_finite(o.pt, o.nrm, o.d)) return o;
   } else if (cvx_mpr(A, e, x, pa)) {
     const creal l = sqrt(dot(x, x));
     if (l > 1e-9) {
-      *nrm = x * (-1.0 / l);
-      *pt = (pa - x * 0.5) - *nrm * (rA * 0.5);
-      *d = -l - rA;
-      if (cvx_finite(*pt, *nrm, *d)) return;
+      o.nrm = x * (-1.0 / l);
+      o.pt = (pa - x * 0.5) - o.nrm * (rA * 0.5);
+      o.d = -l - rA;
+      if (cvx_finite(o.pt, o.nrm, o.d)) return o;
     }
   }
   // MPR degenerate, or a non-finite result of a degenerate simplex: the centre direction
   const D3 ca = A.kind == 0 ? (A.p0 + A.p1) * 0.5 : A.c;
   const creal l = sqrt(dot(ca, ca));
-  *nrm = l > 1e-12 ? ca * (1.0 / l) : d3(0, 0, 1);
-  *pt = ca * 0.5;
-  *d = -rA;
+  o.nrm = l > 1e-12 ? ca * (1.0 / l) : d3(0, 0, 1);
+  o.pt = ca * 0.5;
+  o.d = -rA;
+  return o;
+}
+
+// The narrowphase entry: the core as five 3-vectors (segment: p0, p1; box: centre, half extents, the three
+// axis columns), the result by value.
+// Why it is inlined (NaN / wrong-state history of the egg kernels):
+//   * as a real call taking the shape by value (an aggregate past the register budget, passed through
+//     the caller's stack) and writing its outputs through generic pointers into the caller's private
+//     frame, its results changed with unrelated edits to the calling kernel: round 1 saw order-dependent
+//     NaN object states; in round 2, replacing the model-tile prologue (no change to any code the egg
+//     path runs) turned k_simulate's egg step nondeterministic and wrong in 84 % of envs
+//     (tools/egg_diag.py: run-to-run differences of metres, identical source of the narrowphase);
+//   * this pointer-free signature as a real call did not finish a 256-env step within a 120 s limit;
+//   * inlined, every variant is deterministic and follows the oracle to 2e-7 m.
+// Every one of the kernels carries ~350 spilled VGPRs and a 2.2 KB private frame, and the callee's
+// 48-byte frame sits above it; the failures are consistent with the call's frame or return address being
+// clobbered, which no source-level defect of the narrowphase explains.  cvx_tri's 0 / 0 on coincident
+// vertices is a separate, real edge case, guarded in both the kernel and the oracle.
+__device__ MG_CVX_INLINE CvxHit cvx_contact_v(int kind, D3 a0, D3 a1, D3 a2, D3 a3, D3 a4, creal rA, D3 e,
+                                              creal cut) {
+  CvxShape A;
+  A.kind = kind;
+  if (kind == 0) {
+    A.p0 = a0;
+    A.p1 = a1;
+  } else {
+    A.c = a0;
+    A.h = a1;
+    const D3 col[3] = {a2, a3, a4};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      A.R[0][k] = col[k].x;
+      A.R[1][k] = col[k].y;
+      A.R[2][k] = col[k].z;
+    }
+  }
+  return cvx_contact_body(A, rA, e, cut);
 }
 
 }  // namespace mg

@@ -42,7 +42,7 @@ __device__ __forceinline__ M3 mul(const M3& A, const M3& B) {
     for (int j = 0; j < 3; j++) C.m[i][j] = A.m[i][0] * B.m[0][j] + A.m[i][1] * B.m[1][j] + A.m[i][2] * B.m[2][j];
   return C;
 }
-__device__ __forceinline__ M3 quat_to_mat(float x, float y, float z, float w) {
+__host__ __device__ __forceinline__ M3 quat_to_mat(float x, float y, float z, float w) {
   M3 R;
   R.m[0][0] = 1 - 2 * (y * y + z * z); R.m[0][1] = 2 * (x * y - z * w); R.m[0][2] = 2 * (x * z + y * w);
   R.m[1][0] = 2 * (x * y + z * w); R.m[1][1] = 1 - 2 * (x * x + z * z); R.m[1][2] = 2 * (y * z - x * w);

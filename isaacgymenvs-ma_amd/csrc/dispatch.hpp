@@ -23,6 +23,11 @@ constexpr InstDesc kInst[] = {MG_INSTANCES(MG_DESC)};
 #undef MG_DESC
 static_assert(sizeof(kInst) / sizeof(kInst[0]) == MG_NUM_INST, "MG_NUM_INST must count MG_INSTANCES");
 
+// the model tile image of an instance, built on the host and uploaded to sim->d_tile (mg_sim_create)
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
+struct BuildTile {
+  static int run(mg_sim* sim);
+};
 // gym.simulate alone (k_simulate)
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 struct RunSimulate {

@@ -502,6 +502,17 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
     delete s;
     return fail(MG_EDEVICE, "mg_sim_create: model upload failed");
   }
+  // the LDS model tile of the instance that will run this model, prebuilt once on the host; a model no
+  // instance fits is still created (its launches report MG_ECAPACITY)
+  s->d_tile = nullptr;
+  if (mgi::team_size(s->host_model, s->params.max_contacts) > 0) {
+    const int rc = mgi::dispatch<mgi::BuildTile>(s->host_model, s->params.max_contacts, s);
+    if (rc) {
+      (void)hipFree(s->d_model);
+      delete s;
+      return rc;
+    }
+  }
   *out = s;
   return MG_OK;
 }
@@ -582,6 +593,7 @@ int mg_dr_noise(const mg_dr_noise_args* a, void* stream) {
 int mg_sim_destroy(mg_sim* sim) {
   if (!sim) return MG_OK;
   (void)hipFree(sim->d_model);
+  if (sim->d_tile) (void)hipFree(sim->d_tile);
   delete sim;
   return MG_OK;
 }

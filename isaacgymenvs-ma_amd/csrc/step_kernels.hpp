@@ -5,6 +5,8 @@
 // plus the host launchers RunSimulate / RunEnvStep (dispatch.hpp).  Included only by inst.hip, which
 // instantiates one capacity instance per translation unit.
 #pragma once
+#include <new>
+
 #include "dispatch.hpp"
 #include "hand_task.hpp"
 #include "task.hpp"
@@ -14,36 +16,76 @@ namespace mgi {
 #ifdef MG_PHASE_TIMING
 // per-wave accumulators (one row of 16 per block; plain read-modify-writes by the block's own wave,
 // so the profiling build adds no atomic traffic that would slow the solver's memory path)
-constexpr int kPhaseCap = 1 << 16;  // blocks tracked
+constexpr int kPhaseCap = 1 << 16;  // waves tracked
 // one copy per instance translation unit (each is its own code object): phase_buf_publish<I> sets it
 static __device__ unsigned long long* g_phase_buf;
-#define MG_PHASE_FLUSH(t)                                                              \
-  if (g_phase_buf && blockIdx.x < kPhaseCap && threadIdx.x < 16) {                     \
-    unsigned int v_ = 0;                                                               \
-    for (int i_ = 0; i_ < 16; i_++)                                                    \
-      if ((int)threadIdx.x == i_) v_ = (t).ph[i_];                                     \
-    g_phase_buf[16 * (size_t)blockIdx.x + threadIdx.x] += v_;                          \
+#define MG_PHASE_FLUSH(t, W)                                                           \
+  {                                                                                    \
+    const unsigned gw_ = blockIdx.x * (W) + threadIdx.x / 64, l_ = threadIdx.x & 63;    \
+    if (g_phase_buf && gw_ < kPhaseCap && l_ < 16) {                                   \
+      unsigned int v_ = 0;                                                             \
+      for (int i_ = 0; i_ < 16; i_++)                                                  \
+        if ((int)l_ == i_) v_ = (t).ph[i_];                                            \
+      g_phase_buf[16 * (size_t)gw_ + l_] += v_;                                        \
+    }                                                                                  \
   }
 #else
-#define MG_PHASE_FLUSH(t)
+#define MG_PHASE_FLUSH(t, W)
 #endif
 
 #ifndef MG_EXP
 #define MG_EXP 0  // profiling experiments only (phase attribution): skip parts of the hand post-physics
 #endif
+// ------------------------------------------------------------------------------------------------ launch shape
+// Waves per block W.  A block's W waves share one LDS model tile (each team's own LDS is per wave), so a
+// larger W leaves more of the CU's 160 KB LDS for resident waves; a smaller W lets the CU refill sooner
+// when a wave finishes (a block's slots free only when its slowest wave is done).  W is the smallest
+// of 1, 2, 4, 8 that reaches the most resident waves per CU (at most 8: the 256-register budget).
+template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
+struct Shape {
+  static constexpr int E1 = 64 / T;  // teams (actors) per wave
+  static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP>);
+  static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T>) +
+                                        (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
+  static constexpr int per_cu(int w) {
+    const size_t blk = (kTile + w * kWave + 511) / 512 * 512;
+    const int b = (int)((160 * 1024) / blk);
+    return b * w < 8 ? b * w : 8;
+  }
+  static constexpr int pick() {
+    int best = 1;
+    for (int w = 2; w <= 8; w *= 2)
+      if (per_cu(w) > per_cu(best)) best = w;
+    return best;
+  }
+#ifdef MG_WAVES
+  static constexpr int W = MG_WAVES;  // A/B builds (tools/gpu_variants.sh)
+#else
+  static constexpr int W = pick();
+#endif
+  static constexpr int kThreads = 64 * W;
+  static constexpr int E = E1 * W;  // teams per block
+  static_assert(per_cu(W) >= 1, "one block must fit the CU's LDS");
+};
+
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(const mg_model* __restrict__ m, mg_sim_params p,
-                                                     mg_state_views v, int n) {
-  constexpr int E = kBlock / T;
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(
+    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_state_views v, int n) {
+  using SH = Shape<T, MN, MC, MG, MP, OBJ, DR>;
+  constexpr int E = SH::E, W = SH::W;
   constexpr int ROWS = OBJ ? 3 : 1;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::load_tile(&tile, m);
-  __syncthreads();
+  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
+  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
+#else
+  mg::copy_tile(&tile, static_cast<const typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT*>(timg));
+#endif
+  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   const int team = threadIdx.x / T;
   const int a = blockIdx.x * E + team;
   const bool valid = a < n;
@@ -62,14 +104,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const float* fr = v.rb_forces ? v.rb_forces + ((size_t)(m->num_bodies + 2) * ac + m->num_bodies) * 3 : nullptr;
     lds[team].v.oforce[t.tl] = t.tl < 3 ? (fr ? fr[t.tl] : 0.0f) : (v.rb_force_space == MG_LOCAL_SPACE ? 1.0f : 0.0f);
   }
-  __syncthreads();
+  mg::wsync();
   float* root = v.root_states + (size_t)13 * ROWS * ac;
   t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
          OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
   t.outputs(lds[team].v.u.sv.st.sens, lds[team].v.u.sv.st.dforce);
   t.stage_state();
-  __syncthreads();
+  mg::wsync();
   if (valid) {
     mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team].v;
     if (!m->fixed_base)
@@ -101,16 +143,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
 // RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
 // post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(const mg_model* __restrict__ m, mg_sim_params p,
-                                                     mg_task_params tp, mg_state_views v, mg_task_buffers tb, int n,
-                                                     mg_replay rp) {
-  constexpr int E = kBlock / T;
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(
+    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
+    mg_task_buffers tb, int n, mg_replay rp) {
+  using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
+  constexpr int E = SH::E, W = SH::W;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::load_tile(&tile, m);
-  __syncthreads();
+  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
+  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
+#else
+  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
+#endif
+  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   const int team = threadIdx.x / T;
+  const int wt = (threadIdx.x & 63) / T;  // team index within the wave (ballot / shuffle positions)
   const int a = blockIdx.x * E + team;
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
@@ -125,7 +173,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     t.drt = &drt[team].ten[0][0];
     t.dro = drt[team].obj;
   }
-  __syncthreads();
+  mg::wsync();
   const int64_t reset_in = tb.reset[ac];
   t.ph_start();
   // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
@@ -156,19 +204,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
     t.stage_state();
   }
-  __syncthreads();
+  mg::wsync();
   t.ph_mark(8);
 
   // ---------------- post_physics_step (ant.py:287-297) on the staged state
   const int A = tp.num_agents > 1 ? tp.num_agents : 1;
   const int k = a % A;
   const float* off = tp.agent_offset[k];
-  const int lane = threadIdx.x & 63;
   bool do_reset = reset_in != 0;
   if (A > 1) {  // AND filter over the env's agents (franka_reach_MA.py:875-885)
     const unsigned long long mk = __ballot(t.tl == 0 && valid && reset_in != 0);
     bool all = true;
-    for (int j = 0; j < A; j++) all = all && ((mk >> ((team - k + j) * T)) & 1ull);
+    for (int j = 0; j < A; j++) all = all && ((mk >> ((wt - k + j) * T)) & 1ull);
     do_reset = all;
   }
   float pot = 0.0f, prev = 0.0f, up[3] = {0, 0, 0}, hd[3] = {0, 0, 0};
@@ -187,7 +234,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     progress = 0;
     reset = 0;
   }
-  __syncthreads();
+  mg::wsync();
   // NaN guard: an actor whose state is not finite after the step gets reset = 1 (every agent
   // of its env under MA layouts, so the AND filter resets the env in the next step), reward 0 and a zero
   // observation row: no NaN reaches the policy, and the next step's masked reset_idx restores it
@@ -196,7 +243,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   for (int q = t.tl; q < 2 * nd; q += T) nf = nf || !isfinite(L.u.sv.st.dof[q]);
   const unsigned long long nfm = __ballot(nf);
   bool bad = false;
-  for (int j = 0; j < A; j++) bad = bad || ((nfm >> ((team - k + j) * T)) & mg::team_bits<T>()) != 0ull;
+  for (int j = 0; j < A; j++) bad = bad || ((nfm >> ((wt - k + j) * T)) & mg::team_bits<T>()) != 0ull;
   // observations staged in the row storage (dead after outputs()), then stored coalesced
   const int no = tp.num_obs;
   float* ost = &L.u.sv.rows[0].b;
@@ -218,7 +265,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const float px = L.u.sv.st.root[0], py = L.u.sv.st.root[1], pz = L.u.sv.st.root[2];
     const int base = no - 3 * (A - 1);
     for (int j = 1; j < A; j++) {
-      const int src = (team - k + (k + j) % A) * T;
+      const int src = (wt - k + (k + j) % A) * T;
       const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
       if (t.tl == 0) {
         ost[base + 3 * (j - 1) + 0] = qx - px;
@@ -227,7 +274,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       }
     }
   }
-  __syncthreads();
+  mg::wsync();
   // reward: per-action terms as team sums (DPP), the rest on the leader
   float rew = 0.0f;
   if (tp.task_id == MG_TASK_CARTPOLE) {
@@ -284,7 +331,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       if (t.tl == 0) { pk[no] = rew; pk[no + 1] = (float)reset; }
     }
   }
-  __syncthreads();
+  mg::wsync();
   if (valid) {  // state write-back (gym layouts), team-cooperative
     if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
       for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
@@ -295,7 +342,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
   t.ph_mark(9);
-  MG_PHASE_FLUSH(t)
+  MG_PHASE_FLUSH(t, W)
 }
 
 // ------------------------------------------------------------------------------------------------ hand tasks
@@ -311,15 +358,20 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
 // RP: physics-bypass replay instance (mg_env_step_replay), as k_env_step's.
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(const mg_model* __restrict__ m, mg_sim_params p,
-                                                      mg_task_params tp, mg_state_views v, mg_task_buffers tb,
-                                                      int n, mg_replay rp) {
-  constexpr int E = kBlock / T;
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(
+    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
+    mg_task_buffers tb, int n, mg_replay rp) {
+  using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
+  constexpr int E = SH::E, W = SH::W;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::load_tile(&tile, m);
-  __syncthreads();
+  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
+  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
+#else
+  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, 16 * MG>*>(timg));
+#endif
+  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   const int team = threadIdx.x / T;
   const int e = blockIdx.x * E + team;
   const bool valid = e < n;
@@ -372,7 +424,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       for (int k = 0; k < 13; k++) L.oroot[k] = root[13 + k];
     }
   }
-  __syncthreads();
+  mg::wsync();
   t.load(root, v.dof_state + (size_t)2 * nd * ec, nullptr, L.oroot, nullptr);
   float prev = 0.0f;
   if (t.node > 0) {  // DOF lanes: reset_idx's DOF draw, then actions -> PD targets
@@ -410,7 +462,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       rp.pre_dof_state[(size_t)2 * nd * e + 2 * (t.node - 1)] = t.qj;
       rp.pre_dof_state[(size_t)2 * nd * e + 2 * (t.node - 1) + 1] = t.nu;
     }
-    __syncthreads();
+    mg::wsync();
     for (int k = t.tl; k < 13; k += T) L.oroot[k] = rp.root_states[(size_t)39 * ec + 13 + k];
     for (int k = t.tl; k < 2 * nd; k += T) L.u.sv.st.dof[k] = rp.dof_state[(size_t)2 * nd * ec + k];
     for (int k = t.tl; k < 6 * ns; k += T) L.u.sv.st.sens[k] = rp.sensors ? rp.sensors[(size_t)6 * ns * ec + k] : 0.0f;
@@ -422,7 +474,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
     t.stage_state();
   }
-  __syncthreads();
+  mg::wsync();
   t.ph_mark(8);
   // NaN guard: a non-finite hand / object state after the step -> reset = 1 (the next
   // step's pre_physics reset_idx restores the env), reward 0, zero observation row
@@ -443,7 +495,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     for (int b = t.tl; b < nb; b += T) t.body_state(b, bst + 13 * b);
   }
 #endif
-  __syncthreads();
+  mg::wsync();
 #if !(MG_EXP & 2)
   {
     const float* gs = L.goal + 13;
@@ -466,7 +518,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
   }
 #endif
-  __syncthreads();
+  mg::wsync();
   int64_t ro = 0;
   float fin = 0.0f;
   if (!(MG_EXP & 4) && t.tl == 0) {
@@ -500,7 +552,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     cr += __shfl_xor(cr, off);
     cf += __shfl_xor(cf, off);
   }
-  if (threadIdx.x == 0 && (cr | cf)) {
+  if ((threadIdx.x & 63) == 0 && (cr | cf)) {
     atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
     atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
   }
@@ -556,62 +608,87 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
   }
   t.ph_mark(9);
-  MG_PHASE_FLUSH(t)
+  MG_PHASE_FLUSH(t, W)
+}
+
+// launch helper: grid of ceil(n / teams-per-block) blocks of the instance's shape
+template <class SH, class K, class... A>
+static void launch(K kern, hipStream_t s, int n, A... args) {
+  hipLaunchKernelGGL(kern, dim3((n + SH::E - 1) / SH::E), dim3(SH::kThreads), 0, s, args...);
+}
+
+template <int T, int MN, int MC, int MG, int MP, int OBJ>
+int BuildTile<T, MN, MC, MG, MP, OBJ>::run(mg_sim* sim) {
+  using MT = mg::ModelTile<MN, MG, MP>;
+  MT* img = new (std::nothrow) MT();
+  if (!img) return fail(MG_ENOMEM, "mg_sim_create: out of host memory (model tile)");
+  mg::build_tile(img, &sim->host_model);
+  int rc = MG_OK;
+  if (hipMalloc(&sim->d_tile, sizeof(MT)) != hipSuccess) {
+    sim->d_tile = nullptr;
+    rc = fail(MG_ENOMEM, "mg_sim_create: hipMalloc(model tile) failed");
+  } else if (hipMemcpy(sim->d_tile, img, sizeof(MT), hipMemcpyHostToDevice) != hipSuccess) {
+    rc = fail(MG_EDEVICE, "mg_sim_create: model tile upload failed");
+  }
+  delete img;
+  return rc;
 }
 
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int RunSimulate<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim) {
-  const int E = kBlock / T;
+  if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_sim_simulate: no model tile (model exceeds every kernel instance)");
   // the domain-randomized instance reads each actor's env_props row (mg_dr_apply)
   if (sim->views.env_props)
-    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, true>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                       sim->d_model, sim->params, sim->views, sim->n);
+    launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_simulate<T, MN, MC, MG, MP, OBJ, true>, s, sim->n, sim->d_model,
+                                                 (const void*)sim->d_tile, sim->params, sim->views, sim->n);
   else
-    hipLaunchKernelGGL((k_simulate<T, MN, MC, MG, MP, OBJ, false>), dim3((sim->n + E - 1) / E), dim3(kBlock), 0, s,
-                       sim->d_model, sim->params, sim->views, sim->n);
+    launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_simulate<T, MN, MC, MG, MP, OBJ, false>, s, sim->n, sim->d_model,
+                                                  (const void*)sim->d_tile, sim->params, sim->views, sim->n);
   return MG_OK;
 }
 
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp,
                                              const mg_task_buffers* tb, const mg_replay* rp) {
-  const int E = kBlock / T;
-  const dim3 grid((sim->n + E - 1) / E), block(kBlock);
   using TL = mg::TeamLDS<T, MN, MC, OBJ>;
+  if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_env_step: no model tile (model exceeds every kernel instance)");
   // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
   if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(TL::u.sv.rows))
     return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
   // hand tasks stage the rigid-body states of the articulation in the same storage, the observation
-  // row in the contact storage
+  // row in the contact storage; the observation / states column maps hold 256 entries
   if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(TL::u.sv.rows))
     return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
-  if (OBJ && (size_t)tp->num_obs > sizeof(TL::obs) / sizeof(float))
+  if (OBJ && (tp->num_obs < 0 || (size_t)tp->num_obs > sizeof(TL::obs) / sizeof(float)))
     return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the hand kernel's staging area");
+  if (OBJ && (tp->num_states < 0 || tp->num_states > (int)(sizeof(tp->state_map) / sizeof(tp->state_map[0]))))
+    return fail(MG_ECAPACITY, "mg_env_step: num_states exceeds the hand kernel's states map");
   if (rp && sim->views.env_props)
     return fail(MG_EINVAL, "mg_env_step_replay: no replay instance with domain randomization");
   const mg_replay r = rp ? *rp : mg_replay{};
+  const void* ti = sim->d_tile;
   if constexpr (OBJ != 0) {
     mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
     mg::h_fill_maps(&tpm);
     if (rp)
-      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>), grid, block, 0, s, sim->d_model,
-                         sim->params, tpm, sim->views, *tb, sim->n, r);
+      launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>, s, sim->n,
+                                                    sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>), grid, block, 0, s, sim->d_model,
-                         sim->params, tpm, sim->views, *tb, sim->n, r);
+      launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>, s, sim->n,
+                                                   sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else
-      hipLaunchKernelGGL((k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>), grid, block, 0, s, sim->d_model,
-                         sim->params, tpm, sim->views, *tb, sim->n, r);
+      launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>, s, sim->n,
+                                                    sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
   } else {
     if (rp)
-      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, false, true>), grid, block, 0, s, sim->d_model, sim->params,
-                         *tp, sim->views, *tb, sim->n, r);
+      launch<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim->n, sim->d_model,
+                                                  ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, true, false>), grid, block, 0, s, sim->d_model, sim->params,
-                         *tp, sim->views, *tb, sim->n, r);
+      launch<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim->n, sim->d_model,
+                                                 ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else
-      hipLaunchKernelGGL((k_env_step<T, MN, MC, MG, MP, false, false>), grid, block, 0, s, sim->d_model, sim->params,
-                         *tp, sim->views, *tb, sim->n, r);
+      launch<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim->n, sim->d_model,
+                                                  ti, sim->params, *tp, sim->views, *tb, sim->n, r);
   }
   return MG_OK;
 }

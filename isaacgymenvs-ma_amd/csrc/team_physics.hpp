@@ -19,8 +19,8 @@
 //   test-force ABA solve whose output lands distributed — lane j keeps
 //   Y_r[j] in a register (Ycol[r]); PGS row updates are then a team dot
 //   product (butterfly shuffles) plus one FMA per lane.
-// All lanes of a wave run every phase (teams never diverge on barriers);
-// the block is one wave, so __syncthreads() is a cheap wave barrier.
+// All lanes of a wave run every phase (teams never diverge on barriers); a team's
+// phases synchronise its wave (wsync), never the block: a block is W waves sharing one model tile.
 //
 // Hand tasks (OBJ = true, SURVEY.md §8(a) A4-A8 for ShadowHand): PD position drives
 // (implicit toward the target, +-effort when saturated), fixed tendons (explicit soft
@@ -38,10 +38,11 @@
 namespace mg {
 
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
-// loaded once per launch, so every per-node / per-geom constant is an LDS read
-// (~64 cycles) instead of a dependent global load.  Rows padded to odd strides.
+// every per-node / per-geom constant is an LDS read (~64 cycles) instead of a dependent global load.
+// Rows padded to odd strides.  The image is built once on the host (build_tile, at mg_sim_create) and
+// each block copies it with 16-byte loads; the W waves of a block share one copy.
 template <int MN, int MG, int MP, int OC = 1>  // OC: unused (kept in the instance signatures)
-struct ModelTile {
+struct alignas(16) ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
   float nf[MN][33];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
@@ -55,10 +56,10 @@ struct ModelTile {
   int nn, ng, np;
 };
 
+// host: the finished tile image of model m (child masks, rest rotations as matrices, geom frames)
 template <int MN, int MG, int MP, int OC>
-__device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const int nn = m->num_nodes, ng = m->num_geoms < MG ? m->num_geoms : MG;
+__host__ __device__ void build_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m, int tid = 0, int nt = 1) {
+  const int nn = m->num_nodes < MN ? m->num_nodes : MN, ng = m->num_geoms < MG ? m->num_geoms : MG;
   const int np = m->num_pairs < MP ? m->num_pairs : MP;
   for (int i = tid; i < nn; i += nt) {
     t->parent[i] = m->parent[i];
@@ -69,7 +70,7 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
       if (m->parent[k] == i) ch |= 1ull << k;
     t->children[i] = ch;
     float* f = t->nf[i];
-    M3 R0 = quat_to_mat(m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]);
+    const M3 R0 = quat_to_mat(m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]);
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) f[3 * a + b] = R0.m[a][b];
     for (int k = 0; k < 3; k++) { f[9 + k] = m->t[i][k]; f[12 + k] = m->axis[i][k]; f[15 + k] = m->com[i][k]; }
@@ -92,7 +93,7 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
     t->gbody[g] = m->geom_body[g];
     t->gfil[g] = m->geom_filter[g];
     float* f = t->gf[g];
-    M3 Rg = quat_to_mat(m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]);
+    const M3 Rg = quat_to_mat(m->geom_quat[g][0], m->geom_quat[g][1], m->geom_quat[g][2], m->geom_quat[g][3]);
     for (int k = 0; k < 3; k++) { f[k] = m->geom_pos[g][k]; f[12 + k] = m->geom_size[g][k]; }
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) f[3 + 3 * a + b] = Rg.m[a][b];
@@ -106,6 +107,28 @@ __device__ void load_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m) {
     t->pairs[q][1] = m->pair[q][1];
   }
   if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; }
+}
+
+// device: the block copies the prebuilt image (global) into its LDS tile, 16 bytes per lane and load
+template <class MT>
+__device__ __forceinline__ void copy_tile(MT* t, const MT* img) {
+  static_assert(sizeof(MT) % 16 == 0, "the tile is copied in 16-byte pieces");
+  const uint4* src = reinterpret_cast<const uint4*>(img);
+  uint4* dst = reinterpret_cast<uint4*>(t);
+  for (int i = threadIdx.x; i < (int)(sizeof(MT) / 16); i += blockDim.x) dst[i] = src[i];
+}
+
+// Teams never span a wave, so the team phases synchronise their own wave only (rocPRIM's wave_barrier:
+// a wave's LDS operations complete in order; the wavefront-scope fences keep the compiler from moving
+// LDS accesses across the point).  No s_barrier: the other waves of the block run on independently.
+__device__ __forceinline__ void wsync() {
+#ifdef MG_WSYNC_BLOCK  // A/B: the block barrier (one-wave blocks only)
+  __syncthreads();
+  return;
+#endif
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
@@ -380,7 +403,7 @@ struct Team {
   const MT* mt;
   const mg_model* m;
   const mg_sim_params* p;
-  int tl, tb;          // team lane, first lane of the team (absolute)
+  int tl, tb;          // team lane, first lane of the team within its wave
   bool freeb;
   int nn, nv, ncol0;   // nodes, velocity columns, first joint column
   int node;            // node owned by this lane (-1: none)
@@ -456,7 +479,7 @@ struct Team {
     p = pp;
     drn = drg = drt = dro = nullptr;
     tl = threadIdx.x % T;
-    tb = threadIdx.x - tl;
+    tb = (threadIdx.x & 63) - tl;  // first lane of the team within its wave
     freeb = !m->fixed_base;
     nn = m->num_nodes;
     ncol0 = freeb ? 6 : 0;
@@ -505,7 +528,7 @@ struct Team {
         for (int k = 0; k < 6; k++) s->V[0][k] = 0.0f;
     }
     if (freeb && tl < 6) s->V[0][tl] = nu;
-    __syncthreads();
+    wsync();
     if (node == 0) {
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) R.m[a][b] = s->R[0][3 * a + b];
@@ -546,7 +569,7 @@ struct Team {
         s->S[node][0] = S.a.x; s->S[node][1] = S.a.y; s->S[node][2] = S.a.z;
         s->S[node][3] = S.l.x; s->S[node][4] = S.l.y; s->S[node][5] = S.l.z;
       }
-      __syncthreads();
+      wsync();
     }
   }
 
@@ -615,7 +638,7 @@ struct Team {
         s->U[node][3] = U.l.x; s->U[node][4] = U.l.y; s->U[node][5] = U.l.z;
         s->Dinv[node] = Dinv;
       }
-      __syncthreads();
+      wsync();
       if (node >= 0 && depth == lev - 1) {
         unsigned long long ch = mt->children[node];
         while (ch) {
@@ -637,7 +660,7 @@ struct Team {
         for (int k = 0; k < 6; k++) s->u.sv.ts.aba.acc[0][k] = 0.0f;
       }
     }
-    __syncthreads();
+    wsync();
     if (freeb && tl < 6) {
       // column tl of IA0^-1 from the Cholesky factor (6 lanes in parallel); a0 = -IA0^-1 pA0
       const SV e = sv(v3(tl == 0 ? 1.f : 0.f, tl == 1 ? 1.f : 0.f, tl == 2 ? 1.f : 0.f),
@@ -651,7 +674,7 @@ struct Team {
       }
       s->u.sv.ts.aba.acc[0][tl] = a;
     }
-    __syncthreads();
+    wsync();
     float qdd = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
@@ -661,7 +684,7 @@ struct Team {
         s->u.sv.ts.aba.acc[node][0] = a.a.x; s->u.sv.ts.aba.acc[node][1] = a.a.y; s->u.sv.ts.aba.acc[node][2] = a.a.z;
         s->u.sv.ts.aba.acc[node][3] = a.l.x; s->u.sv.ts.aba.acc[node][4] = a.l.y; s->u.sv.ts.aba.acc[node][5] = a.l.z;
       }
-      __syncthreads();
+      wsync();
     }
     // nu* = nu + h * acc
     if (tl < nv) {
@@ -747,7 +770,7 @@ struct Team {
   __device__ void test_solve(int r0, int nrows_, const float* Wv, float* y) {
     auto& ts = s->u.sv.ts.ts;
     for (int i = tl; i < L::RB * MN; i += T) (&ts.ut[0][0])[i] = 0.0f;
-    __syncthreads();
+    wsync();
     if (tl < L::RB) {
       const int r = r0 + tl;
       SV proot = szero();
@@ -811,7 +834,7 @@ struct Team {
       pr[0] = proot.a.x; pr[1] = proot.a.y; pr[2] = proot.a.z;
       pr[3] = proot.l.x; pr[4] = proot.l.y; pr[5] = proot.l.z;
     }
-    __syncthreads();
+    wsync();
     ph_mark(10);
     // base_q = ut_j - U_j.a0 (joint lanes) or a0[tl] (root lanes), both as ut + Wv.p0 (see aba())
     // rem_q starts at base_q and loses C_ji y_i as the ancestors' values arrive
@@ -836,7 +859,7 @@ struct Team {
         const bool deeper = node > 0 && depth > lev;
         const int an = deeper ? __builtin_ctzll(path) : 1;
         if (deeper) path &= path - 1;
-        const int src = deeper ? tb + ncol0 + an - 1 : (int)threadIdx.x;
+        const int src = deeper ? tb + ncol0 + an - 1 : (int)(threadIdx.x & 63);
         const float C = deeper ? dot(U, sv(ld3(s->S[an]), ld3(s->S[an] + 3))) : 0.0f;
 #pragma unroll
         for (int q = 0; q < L::RB; q++) {
@@ -1048,32 +1071,33 @@ struct Team {
     const float* gs = mt->gf[g] + 12;
     const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
     if constexpr (OBJ == MG_GT_ELLIPSOID) {
-      CvxShape A;  // fp64 from here (convex.hpp)
+      // fp64 from here (convex.hpp); the core crosses the call as five 3-vectors (cvx_contact_v)
+      int kind;
+      D3 a0, a1, a2 = d3(0, 0, 0), a3 = d3(0, 0, 0), a4 = d3(0, 0, 0);
       float r = 0.0f;
       if (round) {
         const float hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
         const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
-        A.kind = 0;
-        A.p0 = d3(mulT(oR, (c - ax) - op));
-        A.p1 = d3(mulT(oR, (c + ax) - op));
+        kind = 0;
+        a0 = d3(mulT(oR, (c - ax) - op));
+        a1 = d3(mulT(oR, (c + ax) - op));
         r = gs[0];
       } else {
-        A.kind = 1;
-        A.c = d3(mulT(oR, c - op));
+        kind = 1;
+        a0 = d3(mulT(oR, c - op));
         M3 Rt;
         for (int a = 0; a < 3; a++)
           for (int b = 0; b < 3; b++) Rt.m[a][b] = oR.m[b][a];
-        const M3 Rl = mul(Rt, Rg);
-        for (int a = 0; a < 3; a++)
-          for (int b = 0; b < 3; b++) A.R[a][b] = Rl.m[a][b];
-        A.h = d3(gs[0], gs[1], gs[2]);
+        const M3 Rl = mul(Rt, Rg);  // box axes in the object frame (columns)
+        a1 = d3(gs[0], gs[1], gs[2]);
+        a2 = d3(Rl.m[0][0], Rl.m[1][0], Rl.m[2][0]);
+        a3 = d3(Rl.m[0][1], Rl.m[1][1], Rl.m[2][1]);
+        a4 = d3(Rl.m[0][2], Rl.m[1][2], Rl.m[2][2]);
       }
-      D3 pl, nl;
-      double dd;
-      cvx_contact(A, r, d3(os), p->contact_offset, &pl, &nl, &dd);
-      *dist = (float)dd;
-      *pt = mul(oR, f3(pl)) + op;
-      *nrm = mul(oR, f3(nl));
+      const CvxHit hit = cvx_contact_v(kind, a0, a1, a2, a3, a4, r, d3(os), p->contact_offset);
+      *dist = (float)hit.d;
+      *pt = mul(oR, f3(hit.pt)) + op;
+      *nrm = mul(oR, f3(hit.nrm));
       return true;
     }
     // pen: capsule of radius os.x along the object's z, half length os.y
@@ -1129,7 +1153,7 @@ struct Team {
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) w[3 + 3 * a + b] = Rg.m[a][b];
     }
-    __syncthreads();
+    wsync();
     // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
     // pass 1 counts, a team scan places them, pass 2 recomputes and writes (no private arrays).
     for (int g0 = 0; g0 < G; g0 += T) {
@@ -1301,7 +1325,7 @@ struct Team {
       }
     }
     if (tl == 0) s->ncon = base < cap ? base : cap;
-    __syncthreads();
+    wsync();
   }
 
   static __device__ void closest_seg_seg_t(V3 p1, V3 q1, V3 p2, V3 q2, float* s_out, float* t_out) {
@@ -1385,7 +1409,7 @@ struct Team {
       li++;
     }
     if (tl == 0) s->nrows = 3 * ncon + tot;
-    __syncthreads();
+    wsync();
   }
 
   // ---------------------------------------------------------------- one substep
@@ -1481,7 +1505,7 @@ struct Team {
       MG_JSET(r, 0.0f, 0.0f);
       if (tl == 0) s->u.sv.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};
     }
-    __syncthreads();
+    wsync();
     ph_mark(5);
     // PGS sweeps: per visit one team dot product (DPP), a branch-free clamp (med3), one multiply-add
     // per lane.  A visit's data (private J/Y, LDS row record) do not depend on the sweep's chain; they
@@ -1538,7 +1562,7 @@ struct Team {
         }
       }
     }
-    __syncthreads();
+    wsync();
 #undef MG_JSET
 #undef MG_JGET
 #undef MG_YGET

@@ -9,6 +9,7 @@
     the contact offset may differ; the bar is per-env agreement on >= 97 % of envs with the
     tolerances of tests/test_gpu_parity.py (positions 2e-4, velocities 2e-3 + 2e-3 |v|).
 """
+import copy
 import ctypes as C
 import os
 
@@ -185,6 +186,7 @@ def test_hand_physics_step_matches_oracle(lib, kind):
     # applied object forces (LOCAL_SPACE) on half of the envs
     h.rb_forces[: n // 2, len(spec.bodies)] = rng.normal(0, 0.3, (n // 2, 3))
     e = DevHandEnv(h)
+    h0 = copy.deepcopy(h)
     mnp = M.pack_model(spec)
     h.simulate(mnp, sp, threads=8)
     sim = C.c_void_p()
@@ -192,8 +194,16 @@ def test_hand_physics_step_matches_oracle(lib, kind):
     _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
     _abi.check(lib.mg_sim_simulate(sim, stream()), lib)
     torch.cuda.synchronize()
-    lib.mg_sim_destroy(sim)
     rg, dg = np_(e.root), np_(e.dof)
+    # the same step again from the same states must be bit-identical (the egg kernels once changed with
+    # unrelated edits to the calling kernel: convex.hpp, cvx_contact_v)
+    e2 = DevHandEnv(h0)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(e2.views())), lib)
+    _abi.check(lib.mg_sim_simulate(sim, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    np.testing.assert_array_equal(np_(e2.root), rg)
+    np.testing.assert_array_equal(np_(e2.dof), dg)
     assert np.isfinite(rg).all() and np.isfinite(dg).all()
     np.testing.assert_array_equal(rg[:, 0], h.root[:, 0])       # fixed hand root untouched
     np.testing.assert_array_equal(rg[:, 2], h.root[:, 2])       # goal actor untouched
