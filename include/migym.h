@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_VERSION 4
+#define MG_VERSION 5
 
 #define MG_MAX_NODES 40
 #define MG_MAX_BODIES 40
@@ -437,6 +437,17 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
  * sums in tb->reduce_scratch and clear them.  Only needed with tb->defer_finalize (multi-GPU: the caller
  * all-reduces reduce_scratch over the ranks first, so every rank holds the whole-node mean). */
 int mg_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb, void* stream);
+
+/* reset_idx(env_ids) applied immediately (ant.py:252-279, humanoid.py:251-278, cartpole.py:122-136,
+ * shadow_hand.py:586-668): for the n ids in `ids` (int32 device array; locomotion / MA: actor rows of
+ * reset_buf, ShadowHand: envs), write the reset DOF state (noise), root row, potentials (locomotion) or
+ * goal, object pose, hand DOFs and PD targets (ShadowHand), and clear progress / reset / successes --
+ * the state a caller reads right after the reference's reset_idx.  Noise: the counter RNG on its own
+ * stream (seed, global env id, tb->step_counter | 2^62), or tb->noise rows indexed like the step's.
+ * The fused step keeps applying reset_buf's masked resets itself; this entry serves callers that reset
+ * outside the step (evaluation, curricula). */
+int mg_reset_idx(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const int32_t* ids, int32_t n,
+                 void* stream);
 
 /* Whole VecTask.step: actions -> actuation -> simulate -> post_physics. */
 int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream);

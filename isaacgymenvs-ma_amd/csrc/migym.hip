@@ -164,21 +164,15 @@ __global__ __launch_bounds__(kBlock) void k_pre_loco(mg_task_params tp, mg_state
 }
 
 
-// pre_physics_step of one env on one lane (physics-free path, shadow_hand.py:670-698)
-__global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
-                                                     int n, int nd) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const uint64_t gid = (uint64_t)(tb.env_offset + e);
+// reset_idx of one ShadowHand env on one lane (shadow_hand.py:586-668): goal (reset_target_pose), object
+// pose, hand DOFs and PD targets, counters
+__device__ void hand_reset_env(const mg_task_params& tp, const mg_state_views& v, const mg_task_buffers& tb, int e,
+                               int nd, uint64_t gid) {
   float* root = v.root_states + (size_t)39 * e;
   float* gs = tb.goal_states + (size_t)13 * e;
-  const bool goal_reset = tb.reset_goal[e] != 0, env_reset = tb.reset[e] != 0;
-  if (goal_reset)
-    mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 0)), mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 1)),
-                     gs, root + 26);
   float* tgt = const_cast<float*>(v.dof_targets) + (size_t)nd * e;
   float* prev = tb.prev_targets + (size_t)nd * e;
-  if (env_reset) {
+  {
     mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 57)),
                      mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 58)), gs, root + 26);
     float r[5];
@@ -202,6 +196,60 @@ __global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state
     tb.reset[e] = 0;
     tb.successes[e] = 0.0f;
   }
+}
+
+// reset_idx(ids) of the locomotion tasks, one lane per listed actor (ant.py:252-279): DOF noise, root row
+// and potentials from task.hpp's reset_dof / reset_root (the fused step's own reset code), counters cleared
+__global__ __launch_bounds__(kBlock) void k_reset_idx(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                      const int32_t* ids, int n, int n_actors) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int a = ids[t];
+  if (a < 0 || a >= n_actors) return;
+  if (tp.task_id == MG_TASK_SHADOW_HAND) {
+    const uint64_t gid = (uint64_t)(tb.env_offset + a);
+    hand_reset_env(tp, v, tb, a, tp.num_dofs, gid);
+    tb.reset_goal[a] = 0;
+    // random object forces: reset_idx zeroes the force and redraws the env's probability (shadow_hand.py:641-643)
+    if (tb.random_force_prob) {
+      const float lhi = logf(tp.force_prob_hi);
+      tb.random_force_prob[a] = expf((logf(tp.force_prob_lo) - lhi) * mg::h_uniform(tb, a, gid, mg::HN_FORCE_PROB) + lhi);
+    }
+    if (v.rb_forces)
+      for (int k = 0; k < 3; k++) v.rb_forces[((size_t)tp.rb_per_env * a + tp.rb_per_env - 2) * 3 + k] = 0.0f;
+    return;
+  }
+  const int A = tp.num_agents > 1 ? tp.num_agents : 1;
+  const int nd = mg::t_dofs(&tp);
+  const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * a : nullptr;
+  float* dof = v.dof_state + (size_t)2 * nd * a;
+  for (int i = 0; i < nd; i++)
+    mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset * A + a), tb.step_counter, dof);
+  float pot = 0.0f, prev = 0.0f;
+  mg::reset_root(&tp, tp.agent_offset[a % A], v.root_states + (size_t)13 * a, &pot, &prev);
+  if (tp.task_id != MG_TASK_CARTPOLE && tb.potentials) {
+    tb.potentials[a] = pot;
+    tb.prev_potentials[a] = prev;
+  }
+  tb.progress[a] = 0;
+  tb.reset[a] = 0;
+}
+
+// pre_physics_step of one env on one lane (physics-free path, shadow_hand.py:670-698)
+__global__ __launch_bounds__(kBlock) void k_hand_pre(mg_task_params tp, mg_state_views v, mg_task_buffers tb,
+                                                     int n, int nd) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint64_t gid = (uint64_t)(tb.env_offset + e);
+  float* root = v.root_states + (size_t)39 * e;
+  float* gs = tb.goal_states + (size_t)13 * e;
+  const bool goal_reset = tb.reset_goal[e] != 0, env_reset = tb.reset[e] != 0;
+  if (goal_reset)
+    mg::h_reset_goal(tp, mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 0)), mg::h_rand_pm1(mg::h_uniform(tb, e, gid, 1)),
+                     gs, root + 26);
+  float* tgt = const_cast<float*>(v.dof_targets) + (size_t)nd * e;
+  float* prev = tb.prev_targets + (size_t)nd * e;
+  if (env_reset) hand_reset_env(tp, v, tb, e, nd, gid);
   if (goal_reset || env_reset) tb.reset_goal[e] = 0;
   const int na = tp.num_actions;
   for (int i = 0; i < na; i++) {
@@ -763,6 +811,26 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
 
 int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {
   return env_step(sim, tp, tb, nullptr, stream);
+}
+
+int mg_reset_idx(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const int32_t* ids, int32_t n,
+                 void* stream) {
+  if (!sim || !sim->bound || !tp || !tb || n < 0 || (n > 0 && !ids) || !tb->reset || !tb->progress)
+    return fail(MG_EINVAL, "mg_reset_idx: bad arguments");
+  if (n == 0) return MG_OK;
+  const bool hand = tp->task_id == MG_TASK_SHADOW_HAND;
+  if (hand) {
+    int rc = hand_args_ok(tp, sim->views, tb, "mg_reset_idx");
+    if (rc) return rc;
+  } else if (tp->task_id != MG_TASK_CARTPOLE && (!tb->potentials || !tb->prev_potentials)) {
+    return fail(MG_EINVAL, "mg_reset_idx: locomotion task needs potential buffers");
+  }
+  if (tp->num_agents > MG_MAX_AGENTS) return fail(MG_EINVAL, "mg_reset_idx: num_agents > MG_MAX_AGENTS");
+  mg_task_buffers t = *tb;
+  t.step_counter = tb->step_counter | (1ull << 62);  // the manual-reset stream of the counter RNG
+  hipLaunchKernelGGL(k_reset_idx, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, *tp, sim->views, t, ids,
+                     n, sim->n);
+  return check_launch("mg_reset_idx");
 }
 
 int mg_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb, void* stream) {

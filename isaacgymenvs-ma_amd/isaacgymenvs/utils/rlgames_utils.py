@@ -1,1 +1,2 @@
-from migym.utils.rlgames_utils import RLGPUEnv, get_rlgames_env_creator  # noqa: F401
+from migym.utils.rlgames_utils import (ComplexObsRLGPUEnv, RLGPUEnv, env_configurations,  # noqa: F401
+                                     get_rlgames_env_creator, register_env_creator)

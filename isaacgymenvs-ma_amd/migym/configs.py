@@ -220,7 +220,9 @@ TASKS["ShadowHand"] = {
         "asymmetric_observations": False, "successTolerance": 0.1, "printNumSuccesses": False,
         "maxConsecutiveSuccesses": 0,
         "asset": {"assetFileName": "mjcf/open_ai_assets/hand/shadow_hand.xml",
-                  "assetFileNameBlock": "urdf/objects/cube_multicolor.urdf"},
+                  "assetFileNameBlock": "urdf/objects/cube_multicolor.urdf",
+                  "assetFileNameEgg": "mjcf/open_ai_assets/hand/egg.xml",
+                  "assetFileNamePen": "mjcf/open_ai_assets/hand/pen.xml"},
         "enableCameraSensors": False,
     },
     "sim": _sim(dt=0.01667, num_position_iterations=8, contact_offset=0.002, rest_offset=0.0,

@@ -290,6 +290,45 @@ class VecTask(DomainRandomizationMixin, Env):
     def post_step_extras(self):
         """Task-specific extras (e.g. Ant's true_objective); cheap device views only."""
 
+    # ---------------------------------------------------------------------------------- env state
+    # device tensors that carry a rollout from one step to the next (the gym-visible state and the task
+    # buffers the fused kernel reads back); subclasses extend the list
+    env_state_tensors = ("root_states", "dof_state", "dof_actuation", "sensor_tensor", "dof_force_tensor",
+                         "obs_buf", "obs_clamped", "states_buf", "rew_buf", "reset_buf", "timeout_buf",
+                         "progress_buf", "randomize_buf", "actions", "potentials", "prev_potentials", "up_vec",
+                         "heading_vec", "env_props", "randomize_buf_actors")
+    env_state_scalars = ("control_steps", "frame_count", "last_step", "last_rand_step")
+
+    def get_env_state(self):
+        """Serializable env state for a checkpoint (the reference's hook, vec_task.py:197-205, returns None;
+        SURVEY.md §5 asks for the SoA state tensors): a dict of clones of every per-env device tensor that
+        carries the rollout, plus the step counters.  ``set_env_state`` of it resumes the rollout exactly
+        (the reset RNG is keyed by (seed, env, control step), so the counters are part of the state)."""
+        out, seen = {}, set()
+        for k in self.env_state_tensors:
+            t = getattr(self, k, None)
+            if isinstance(t, torch.Tensor) and t.data_ptr() not in seen:
+                seen.add(t.data_ptr())
+                out[k] = t.detach().clone()
+        for k in self.env_state_scalars:
+            if hasattr(self, k):
+                out[k] = getattr(self, k)
+        return out
+
+    def set_env_state(self, env_state):
+        """Restore ``get_env_state``'s dict in place (the sim keeps pointers to these tensors). ``None`` (what
+        a reference checkpoint holds) is a no-op."""
+        if env_state is None:
+            return
+        for k, v in env_state.items():
+            cur = getattr(self, k, None)
+            if isinstance(cur, torch.Tensor):
+                if tuple(cur.shape) != tuple(v.shape):
+                    raise ValueError(f"set_env_state: {k} has shape {tuple(v.shape)}, expected {tuple(cur.shape)}")
+                cur.copy_(v.to(cur.device, cur.dtype))
+            elif k in self.env_state_scalars:
+                setattr(self, k, v)
+
     # ---------------------------------------------------------------------------------- API
     def get_state(self):
         return torch.clamp(self.states_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
@@ -304,10 +343,24 @@ class VecTask(DomainRandomizationMixin, Env):
             self.obs_dict["states"] = self.get_state()
         return self.obs_dict
 
-    def reset_idx(self, env_ids):
-        """Marks ``env_ids`` for reset; the fused step applies it before its observations
-        (same point in the step as the reference's reset_idx, ant.py:291-293)."""
-        self.reset_buf[env_ids] = 1
+    def reset_idx(self, env_ids, goal_env_ids=None):
+        """reset_idx (ant.py:252-279, humanoid.py:251-278, cartpole.py:122-136, shadow_hand.py:586-668):
+        the listed envs (actor rows for MA layouts) get their reset state written now, by one device launch
+        (``mg_reset_idx``): DOF noise, root rows and potentials, or ShadowHand's goal, object, hand DOFs and
+        PD targets; progress / reset (/ successes) cleared.  A caller reading ``root_states`` right after
+        sees the reset state, as with the reference.  Inside ``step`` the fused kernel applies
+        ``reset_buf``'s resets itself.  ``goal_env_ids`` (ShadowHand) are reset with the env (their goal is
+        redrawn as part of the env reset)."""
+        ids = torch.as_tensor(env_ids, device=self.device).flatten().to(torch.int32).contiguous()
+        n = int(ids.numel())
+        if n == 0:
+            return
+        self._reset_ids = ids   # alive until the launch has consumed it
+        tb = self._tb
+        tb.step_counter = self.control_steps
+        tb.noise = _abi.ptr(self._noise)
+        _abi.check(self._lib.mg_reset_idx(self.sim, _abi.C.byref(self.task_params), _abi.C.byref(tb), ids.data_ptr(),
+                                          n, self._stream()), self._lib)
 
     def reset_done(self):
         done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()

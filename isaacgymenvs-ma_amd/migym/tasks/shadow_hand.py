@@ -113,6 +113,10 @@ class ShadowHand(VecTask):
         self._views = v
         _abi.check(self._lib.mg_sim_bind(self.sim, _abi.C.byref(v)), self._lib)
 
+    env_state_tensors = VecTask.env_state_tensors + (
+        "root_state_tensor", "rigid_body_states", "prev_targets", "cur_targets", "goal_states", "reset_goal_buf",
+        "successes", "consecutive_successes", "rb_forces", "random_force_prob")
+
     def allocate_buffers(self):
         super().allocate_buffers()
         dev, N = self.device, self.num_envs
