@@ -62,9 +62,12 @@ extern "C" {
 #define MG_MAX_SENSORS 8
 #define MG_MAX_TENDONS 8
 #define MG_MAX_HAND_DOFS 32
+#define MG_MAX_HULL_VERTS 64    /* the convex-mesh geom's hull (mg_model.hull_*) */
+#define MG_MAX_HULL_PLANES 128
 
 enum { MG_JT_FREE = 0, MG_JT_FIXED = 1, MG_JT_HINGE = 2, MG_JT_SLIDE = 3 };
-enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4, MG_GT_ELLIPSOID = 5 };
+enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4, MG_GT_ELLIPSOID = 5,
+       MG_GT_CONVEX = 6 /* convex mesh: the model's hull_* tables */ };
 enum { MG_OK = 0, MG_EINVAL = -1, MG_EDEVICE = -2, MG_ENOMEM = -3, MG_ECAPACITY = -4 };
 enum { MG_TASK_CARTPOLE = 0, MG_TASK_ANT = 1, MG_TASK_HUMANOID = 2, MG_TASK_SHADOW_HAND = 3 };
 #define MG_MAX_AGENTS 8
@@ -131,6 +134,12 @@ typedef struct mg_model {
   float obj_lin_damping;
   float obj_ang_damping;
   float obj_gravity;                 /* 1 = the object falls under sim gravity */
+  /* The convex-mesh collision geom (MG_GT_CONVEX; ShadowHand's robot0:C_forearm = mesh robot0:forearm_cvx,
+   * robot.xml:8, shared_asset.xml:15), one per model: its hull in the geom frame (vertices, and outward
+   * face planes n.x <= d inside).  geom_size of that geom = the hull's half extents about geom_pos. */
+  int32_t hull_num_verts, hull_num_planes;
+  float hull_vert[MG_MAX_HULL_VERTS][3];
+  float hull_plane[MG_MAX_HULL_PLANES][4];
 } mg_model;
 
 /* Simulation parameters (cfg['sim'] of the task YAML: Ant.yaml:42-61). */

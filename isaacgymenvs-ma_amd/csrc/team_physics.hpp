@@ -54,6 +54,7 @@ struct alignas(16) ModelTile {
   float gf[MG][17];   // 0-2 pos, 3-11 R, 12-14 size, 15 bounding radius
   int pairs[MP > 0 ? MP : 1][2];
   int nn, ng, np;
+  int hnv;            // vertices of the convex-mesh geom's hull (mg_model.hull_*), 0 if none
 };
 
 // host: the finished tile image of model m (child masks, rest rotations as matrices, geom frames)
@@ -99,14 +100,14 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model
       for (int b = 0; b < 3; b++) f[3 + 3 * a + b] = Rg.m[a][b];
     const float* sz = m->geom_size[g];
     const int ty = m->geom_type[g];
-    f[15] = ty == MG_GT_BOX ? sqrtf(sz[0] * sz[0] + sz[1] * sz[1] + sz[2] * sz[2])
+    f[15] = (ty == MG_GT_BOX || ty == MG_GT_CONVEX) ? sqrtf(sz[0] * sz[0] + sz[1] * sz[1] + sz[2] * sz[2])
                             : (ty == MG_GT_CAPSULE ? sz[0] + sz[1] : sz[0]);
   }
   for (int q = tid; q < np; q += nt) {
     t->pairs[q][0] = m->pair[q][0];
     t->pairs[q][1] = m->pair[q][1];
   }
-  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; }
+  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; t->hnv = m->hull_num_verts; }
 }
 
 // device: the block copies the prebuilt image (global) into its LDS tile, 16 bytes per lane and load
@@ -293,6 +294,16 @@ __device__ __forceinline__ int team_incl_scan(int v) {
   }
   return v;
 }
+// team argmax of (v, i): the largest v, the smallest i among equal v (a serial loop's first maximum)
+template <int T>
+__device__ __forceinline__ void team_argmax(float& v, int& i) {
+#pragma unroll
+  for (int d = 1; d < T; d <<= 1) {
+    const float ov = __shfl_xor(v, d, T);
+    const int oi = __shfl_xor(i, d, T);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
 template <int T>
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
@@ -391,6 +402,96 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
     if (f < best_f) { best_f = f; best_t = t; }
   }
   return best_t;
+}
+
+// ---- the convex-mesh geom (MG_GT_CONVEX; oracle point_hull / hull_box_near): the model's hull tables are read
+// from global memory (only the few candidates near the hull touch them)
+// largest plane distance of pl (geom frame) over the hull's faces (*f = the face): the signed distance inside
+// and where a face is the nearest feature, a lower bound outside near edges / vertices
+__device__ __forceinline__ float point_hull(const mg_model* m, V3 pl, int* f) {
+  float best = -3.0e38f;
+  int bf = 0;
+  const int np = m->hull_num_planes;
+  for (int i = 0; i < np; i++) {
+    const float* q = m->hull_plane[i];
+    const float sd = q[0] * pl.x + q[1] * pl.y + q[2] * pl.z - q[3];
+    if (sd > best) { best = sd; bf = i; }
+  }
+  *f = bf;
+  return best;
+}
+// the hull's bounding box (half extents hg about the geom centre c, axes Rg) within off of a sphere (w, r)
+__device__ __forceinline__ bool hull_box_near(V3 c, const M3& Rg, V3 hg, V3 w, float r, float off) {
+  const V3 l = mulT(Rg, w - c);
+  const float ex = fmaxf(fabsf(l.x) - hg.x, 0.0f), ey = fmaxf(fabsf(l.y) - hg.y, 0.0f), ez = fmaxf(fabsf(l.z) - hg.z, 0.0f);
+  return sqrtf(ex * ex + ey * ey + ez * ez) - r < off;
+}
+
+// box-box edge-edge contact in the object box's frame (oracle box_box_edge): hand box centre c, axes = the
+// columns of R, half extents hg; object half extents hb.  SAT over the 15 axes (edge axes within ~11 deg of a
+// face normal left to the face contacts); an edge axis better than every face axis by 1e-5 m with a
+// separation below off gives one contact at the supporting edges' closest points, normal from B to A.
+__device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, float off, V3* pt, V3* nrm, float* dist) {
+  const float cv[3] = {c.x, c.y, c.z}, hgv[3] = {hg.x, hg.y, hg.z}, hbv[3] = {hb.x, hb.y, hb.z};
+  float face = -3.0e38f;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float ra = hgv[0] * fabsf(R.m[i][0]) + hgv[1] * fabsf(R.m[i][1]) + hgv[2] * fabsf(R.m[i][2]);
+    face = fmaxf(face, fabsf(cv[i]) - hbv[i] - ra);
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const float t = R.m[0][j] * cv[0] + R.m[1][j] * cv[1] + R.m[2][j] * cv[2];
+    const float rb = hbv[0] * fabsf(R.m[0][j]) + hbv[1] * fabsf(R.m[1][j]) + hbv[2] * fabsf(R.m[2][j]);
+    face = fmaxf(face, fabsf(t) - hgv[j] - rb);
+  }
+  // edge axes e_i x a_j in closed form from the entries of R (oracle box_box_edge)
+  float best = -3.0e38f;
+  int bi = -1, bj = -1;
+  float L[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const float ln = sqrtf(R.m[i1][j] * R.m[i1][j] + R.m[i2][j] * R.m[i2][j]);
+      if (ln < 1e-6f) continue;
+      const float near = fmaxf(fmaxf(fabsf(R.m[i1][j]), fabsf(R.m[i2][j])), fmaxf(fabsf(R.m[i][j1]), fabsf(R.m[i][j2]))) / ln;
+      if (near > 0.98f) continue;
+      const float tl = cv[i2] * R.m[i1][j] - cv[i1] * R.m[i2][j];
+      const float rb = hbv[i1] * fabsf(R.m[i2][j]) + hbv[i2] * fabsf(R.m[i1][j]);
+      const float ra = hgv[j1] * fabsf(R.m[i][j2]) + hgv[j2] * fabsf(R.m[i][j1]);
+      const float sep = (fabsf(tl) - ra - rb) / ln;
+      if (sep > best) {
+        const float sg = tl < 0.0f ? -1.0f : 1.0f;
+        best = sep; bi = i; bj = j;
+        L[i] = 0.0f;
+        L[i1] = -sg * R.m[i2][j] / ln;
+        L[i2] = sg * R.m[i1][j] / ln;
+      }
+    }
+  if (bi < 0 || !(best > face + 1e-5f) || !(best < off)) return false;
+  float pb[3], pa[3] = {cv[0], cv[1], cv[2]};
+#pragma unroll
+  for (int a = 0; a < 3; a++) pb[a] = a == bi ? 0.0f : (L[a] >= 0.0f ? hbv[a] : -hbv[a]);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    if (k == bj) continue;
+    const float sg = (L[0] * R.m[0][k] + L[1] * R.m[1][k] + L[2] * R.m[2][k]) >= 0.0f ? -hgv[k] : hgv[k];
+#pragma unroll
+    for (int a = 0; a < 3; a++) pa[a] += sg * R.m[a][k];
+  }
+  const V3 ua = v3(R.m[0][bj], R.m[1][bj], R.m[2][bj]);
+  const V3 ub = v3(bi == 0 ? 1.0f : 0.0f, bi == 1 ? 1.0f : 0.0f, bi == 2 ? 1.0f : 0.0f);
+  const V3 PA = v3(pa[0], pa[1], pa[2]), PB = v3(pb[0], pb[1], pb[2]), w0 = PA - PB;
+  const float b = dot(ua, ub), dd = dot(ua, w0), e = dot(ub, w0), den = 1.0f - b * b;
+  if (den < 1e-12f) return false;
+  const float sa = (b * e - dd) / den, tb = (e - b * dd) / den;
+  if (fabsf(sa) > hgv[bj] || fabsf(tb) > hbv[bi]) return false;
+  *pt = ((PA + ua * sa) + (PB + ub * tb)) * 0.5f;
+  *nrm = v3(L[0], L[1], L[2]);
+  *dist = best;
+  return true;
 }
 
 // Per-lane context of one team.
@@ -1027,6 +1128,18 @@ struct Team {
     }
     const V3 hg = v3(gs[0], gs[1], gs[2]);
     const int v = q & 7;
+    if (q == 16) {  // edge against edge, in the object frame
+      M3 Rt;
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Rt.m[a][b] = oR.m[b][a];
+      V3 pe, ne;
+      float de;
+      if (!box_box_edge(mulT(oR, c - op), mul(Rt, Rg), hg, hb, p->contact_offset, &pe, &ne, &de)) return false;
+      *pt = mul(oR, pe) + op;
+      *nrm = mul(oR, ne);
+      *dist = de;
+      return true;
+    }
     if (q < 8) {
       const V3 l = v3((v & 1 ? 1.f : -1.f) * hg.x, (v & 2 ? 1.f : -1.f) * hg.y, (v & 4 ? 1.f : -1.f) * hg.z);
       const V3 pl = mulT(oR, (c + mul(Rg, l)) - op);
@@ -1045,14 +1158,72 @@ struct Team {
     return true;
   }
 
+  // The convex-mesh geom against the object (oracle geom_object / geom_object_convex, MG_GT_CONVEX branches):
+  //   block: the hull's vertices against the box, then the box's 8 vertices against the hull's faces;
+  //   pen:   the hull's vertices against its segment, then its two end spheres against the faces;
+  //   egg:   the faces against the ellipsoid's support points.
+  // Normal from the object to the geom.  Hull vertex q against the object (block / pen), lane per vertex:
+  __device__ bool hull_vertex_candidate(int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
+    const V3 w = c + mul(Rg, ld3(m->hull_vert[q]));
+    if constexpr (OBJ == MG_GT_BOX) {
+      const V3 pl = mulT(oR, w - op);
+      V3 nb, cb;
+      *dist = point_box(pl, osize(), &nb, &cb);
+      *pt = mul(oR, (pl + cb) * 0.5f) + op;
+      *nrm = mul(oR, nb);
+      return true;
+    } else {
+      const V3 os = osize();
+      const float ro = os.x;
+      const V3 oz = v3(oR.m[0][2], oR.m[1][2], oR.m[2][2]) * os.y;
+      const V3 p0 = op - oz, p1 = op + oz;
+      float ss, tt;
+      closest_seg_seg_t(w, w, p0, p1, &ss, &tt);
+      const V3 qq = p0 + (p1 - p0) * tt, dv = w - qq;
+      const float dl = sqrtf(dot(dv, dv));
+      if (!(dl > 1e-9f)) return false;
+      *nrm = dv * (1.0f / dl);
+      *pt = (w + (qq + *nrm * ro)) * 0.5f;
+      *dist = dl - ro;
+      return true;
+    }
+  }
+  // object point k (block: box vertex k; pen: end k; egg: unused) in the geom frame
+  __device__ V3 hull_object_point(int k, V3 c, const M3& Rg) const {
+    const V3 os = osize();
+    if constexpr (OBJ == MG_GT_BOX) {
+      const V3 l = v3((k & 1 ? 1.f : -1.f) * os.x, (k & 2 ? 1.f : -1.f) * os.y, (k & 4 ? 1.f : -1.f) * os.z);
+      return mulT(Rg, (mul(oR, l) + op) - c);
+    } else {
+      const V3 oz = v3(oR.m[0][2], oR.m[1][2], oR.m[2][2]) * os.y;
+      return mulT(Rg, (k == 0 ? op - oz : op + oz) - c);
+    }
+  }
+  // egg: its support point (geom frame) farthest along -n (n a geom-frame face normal); cl / Rl: the egg's
+  // centre and axes in the geom frame
+  __device__ V3 egg_support_geom(V3 n, V3 cl, const M3& Rl) const {
+    const V3 os = osize();
+    const V3 ne = mulT(Rl, n * -1.0f);
+    const V3 qe = v3(os.x * os.x * ne.x, os.y * os.y * ne.y, os.z * os.z * ne.z);
+    const float nn = sqrtf(qe.x * ne.x + qe.y * ne.y + qe.z * ne.z);
+    const V3 se = nn < 1e-30f ? v3(0, 0, 0) : qe * (1.0f / nn);
+    return mul(Rl, se) + cl;
+  }
+
   // object-contact candidates of an articulation geom of type ty (oracle obj_candidates): block
-  // sphere/capsule 1, box 16 (vertex tests both ways); pen sphere/capsule 1 (segment-segment), box 3
-  // (closest point + the two ends); egg 1 (GJK / MPR)
+  // sphere/capsule 1, box 17 (vertex tests both ways, edge-edge); pen sphere/capsule 1 (segment-segment),
+  // box 3 (closest point + the two ends); egg 1 (GJK / MPR); the convex-mesh geom as counted below
   __device__ int ocand_count(int ty) const {
     const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
-    if (!round && ty != MG_GT_BOX) return 0;
     constexpr int ot = OBJ;
+    if (ty == MG_GT_CONVEX)  // block: hull vertices + the box's 8; pen: hull vertices + its 2 ends; egg: GJK
+      return ot == MG_GT_BOX ? mt->hnv + 8 : (ot == MG_GT_CAPSULE ? mt->hnv + 2 : 1);
+    if (!round && ty != MG_GT_BOX) return 0;
+#ifdef MG_NO_EDGE  // A/B only: without the edge-edge candidate (the oracle always has it)
     if (ot == MG_GT_BOX) return round ? 1 : 16;
+#else
+    if (ot == MG_GT_BOX) return round ? 1 : 17;  // box: 8 + 8 vertex-face, 1 edge-edge
+#endif
     if (ot == MG_GT_CAPSULE) return round ? 1 : 3;
     return 1;
   }
@@ -1175,7 +1346,7 @@ struct Team {
           slot0 = base + incl - cnt;
           base += __shfl(incl, tb + T - 1);
         }
-        const int nc = ty == MG_GT_SPHERE ? 1 : (ty == MG_GT_CAPSULE ? 2 : (ty == MG_GT_BOX ? 8 : 0));
+        const int nc = ty == MG_GT_SPHERE ? 1 : (ty == MG_GT_CAPSULE ? 2 : (ty == MG_GT_BOX ? 8 : (ty == MG_GT_CONVEX ? mt->hnv : 0)));
         for (int q = 0; q < nc; q++) {
           V3 e;
           float r;
@@ -1186,6 +1357,9 @@ struct Team {
             V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * gs[1];
             e = q == 0 ? c - ax : c + ax;
             r = gs[0];
+          } else if (ty == MG_GT_CONVEX) {  // the hull's vertices
+            e = c + mul(Rg, ld3(m->hull_vert[q]));
+            r = 0.0f;
           } else {
             V3 l = v3((q & 1 ? 1.f : -1.f) * gs[0], (q & 2 ? 1.f : -1.f) * gs[1], (q & 4 ? 1.f : -1.f) * gs[2]);
             e = c + mul(Rg, l);
@@ -1281,15 +1455,98 @@ struct Team {
       for (int g0 = 0; g0 < G; g0 += T) {
         const int g = g0 + tl;
         bool ok = false;
+        const int gt = g < G ? mt->gtype[g] : -1;
         if (g < G && (mt->gfil[g] & MG_COLLIDE_OBJECT) &&
-            (mt->gtype[g] == MG_GT_SPHERE || mt->gtype[g] == MG_GT_CAPSULE || mt->gtype[g] == MG_GT_BOX)) {
+            (gt == MG_GT_SPHERE || gt == MG_GT_CAPSULE || gt == MG_GT_BOX || gt == MG_GT_CONVEX)) {
           const V3 c = ld3(gw_tile() + GW * g);
           const V3 dc = c - op;
           const float reach = mt->gf[g][15] + ro + off;
           ok = dot(dc, dc) <= reach * reach;
+          if (ok && gt == MG_GT_CONVEX) {  // the hull's bounding box against the object's sphere (oracle)
+            V3 cc;
+            M3 Rg;
+            geom_staged(g, &cc, &Rg);
+            ok = hull_box_near(cc, Rg, ld3(mt->gf[g] + 12), op, ro, off);
+          }
         }
         const unsigned long long b = __ballot(ok);
         live |= ((b >> tb) & (T >= 64 ? ~0ull : ((1ull << T) - 1ull))) << g0;
+      }
+      // the convex-mesh geom first, in a pass of its own (its candidates precede the other geoms' object
+      // contacts, as in the oracle's collide; rarely live, and kept out of the main loop's code)
+      unsigned long long hull_live = 0ull;
+      for (unsigned long long mm = live; mm; mm &= mm - 1)
+        if (mt->gtype[__builtin_ctzll(mm)] == MG_GT_CONVEX) hull_live |= mm & (~mm + 1ull);
+      live &= ~hull_live;
+#ifdef MG_NO_HULL  // A/B only: the convex-mesh geom's object contacts skipped
+      hull_live = 0ull;
+#endif
+      for (unsigned long long hm = hull_live; hm; hm &= hm - 1) {
+        const int g = __builtin_ctzll(hm);
+        V3 c;
+        M3 Rg;
+        geom_staged(g, &c, &Rg);
+        // (1) the hull's vertices against the object (block, pen): lane per vertex
+        if constexpr (OBJ != MG_GT_ELLIPSOID) {
+          const int nhv = mt->hnv;
+          for (int f0 = 0; f0 < nhv; f0 += T) {
+            const int q = f0 + tl;
+            int cnt = 0;
+            V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
+            float d = 0.0f;
+            if (q < nhv) cnt = hull_vertex_candidate(q, c, Rg, &pt, &nrm, &d) && d < off ? 1 : 0;
+            const int incl = team_incl_scan<T>(cnt);
+            const int tot = __shfl(incl, tb + T - 1);
+            if (cnt) {
+              const int slot = base + incl - 1;
+              if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
+            }
+            base += tot;
+          }
+        }
+        // (2) the object's points against the hull's faces, the faces spread over the team (team argmax;
+        // ties -> the lowest face, as the oracle's serial loop): lane k keeps point k's face and distance
+        constexpr int K = OBJ == MG_GT_BOX ? 8 : (OBJ == MG_GT_CAPSULE ? 2 : 1);
+        const int np = m->hull_num_planes;
+        const V3 cl = mulT(Rg, op - c);
+        M3 Rl;  // object axes in the geom frame: Rg^T oR
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) Rl.m[a][b] = Rg.m[0][a] * oR.m[0][b] + Rg.m[1][a] * oR.m[1][b] + Rg.m[2][a] * oR.m[2][b];
+        float dk = 0.0f;
+        int fk = 0;
+#pragma unroll 1
+        for (int k = 0; k < K; k++) {
+          const V3 pk = OBJ == MG_GT_ELLIPSOID ? cl : hull_object_point(k, c, Rg);
+          float best = -3.0e38f;
+          int bf = 0x7fffffff;
+          for (int f = tl; f < np; f += T) {
+            const float* hp = m->hull_plane[f];
+            const V3 x = OBJ == MG_GT_ELLIPSOID ? egg_support_geom(ld3(hp), cl, Rl) : pk;
+            const float sd = hp[0] * x.x + hp[1] * x.y + hp[2] * x.z - hp[3];
+            if (sd > best) { best = sd; bf = f; }
+          }
+          team_argmax<T>(best, bf);
+          if (tl == k) { dk = best; fk = bf; }
+        }
+        int cnt = 0;
+        V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
+        float d = 0.0f;
+        if (tl < K) {
+          const V3 ng = ld3(m->hull_plane[fk]);
+          const float ro = OBJ == MG_GT_CAPSULE ? osize().x : 0.0f;
+          d = dk - ro;
+          const V3 x = OBJ == MG_GT_ELLIPSOID ? egg_support_geom(ng, cl, Rl) : hull_object_point(tl, c, Rg);
+          pt = mul(Rg, x - ng * (ro + 0.5f * d)) + c;
+          nrm = mul(Rg, ng) * -1.0f;
+          cnt = d < off ? 1 : 0;
+        }
+        const int incl = team_incl_scan<T>(cnt);
+        const int tot = __shfl(incl, tb + T - 1);
+        if (cnt) {
+          const int slot = base + incl - 1;
+          if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
+        }
+        base += tot;
       }
       int NC = 0;
       for (unsigned long long mm = live; mm; mm &= mm - 1) NC += ocand_count(mt->gtype[__builtin_ctzll(mm)]);

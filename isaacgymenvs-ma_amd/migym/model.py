@@ -45,10 +45,12 @@ MAX_GEOMS = 48
 MAX_PAIRS = 192
 MAX_SENSORS = 8
 MAX_TENDONS = 8
+MAX_HULL_VERTS = 64
+MAX_HULL_PLANES = 128
 COLLIDE_GROUND, COLLIDE_OBJECT = 1, 2
 
 JT_FREE, JT_FIXED, JT_HINGE, JT_SLIDE = 0, 1, 2, 3
-GT_PLANE, GT_SPHERE, GT_CAPSULE, GT_BOX, GT_CYLINDER, GT_ELLIPSOID = 0, 1, 2, 3, 4, 5
+GT_PLANE, GT_SPHERE, GT_CAPSULE, GT_BOX, GT_CYLINDER, GT_ELLIPSOID, GT_CONVEX = 0, 1, 2, 3, 4, 5, 6
 _GEOM_TYPES = {"plane": GT_PLANE, "sphere": GT_SPHERE, "capsule": GT_CAPSULE, "box": GT_BOX,
                "cylinder": GT_CYLINDER, "ellipsoid": GT_ELLIPSOID}
 
@@ -198,6 +200,7 @@ class ModelSpec:
     tendons: List[Dict] = field(default_factory=list)   # {name, dofs[2], coefs[2], range[2], limit_stiffness, damping}
     gravity_off: int = 0
     obj: Optional[Dict] = None     # free object sharing the env: {type, size, mass, inertia, lin_damping, ...}
+    hull: Optional[Dict] = None    # the convex-mesh geom: {geom, verts [[x,y,z]], planes [[nx,ny,nz,d]]}, geom frame
 
     @property
     def num_dofs(self):
@@ -350,13 +353,15 @@ def _orientation(a, angle_scale):
 
 
 def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, collapse_fixed=False,
-              mesh_boxes=None) -> ModelSpec:
+              mesh_boxes=None, mesh_hulls=None) -> ModelSpec:
     """Parse an MJCF file (with <include>) into a :class:`ModelSpec`.
 
     ``collapse_fixed``: a jointless body is merged into its parent *body* (gym
     ``AssetOptions.collapse_fixed_joints``, shadow_hand.py:236) instead of becoming a
-    rigid body of its own.  ``mesh_boxes``: {mesh name: (center, half extents)} box
-    stand-ins for convex-mesh collision geoms (the build has no convex-mesh narrowphase).
+    rigid body of its own.  ``mesh_hulls``: {mesh name: {center, half, verts, planes}} convex
+    hulls of mesh collision geoms (mesh frame about ``center``; tools/build_models.py), imported as
+    one MG_GT_CONVEX geom (``spec.hull``); ``mesh_boxes``: {mesh name: (center, half extents)} box
+    stand-ins for the others.
     A fixed-base root body keeps its MJCF orientation (its translation is replaced by the
     actor start pose): the reference places the object on the palm with the hand mount's
     rotation applied and its position ignored (shadow_hand.py:306-318, robot.xml:3)."""
@@ -380,6 +385,7 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, co
     dof_names: List[str] = []
     mass_acc: Dict[int, _MassAccum] = {}
     body_mass: Dict[int, _MassAccum] = {}
+    hulls: List[Dict] = []
 
     def joint_list(b, cls):
         out = []
@@ -404,8 +410,14 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, co
             a.update(g.attrib)
             if a.get("type", "sphere") == "plane":
                 continue
-            if a.get("type") == "mesh" and mesh_boxes and a.get("mesh") in mesh_boxes and \
-                    not (a.get("contype", "1") == "0" and a.get("conaffinity", "1") == "0"):
+            collides = not (a.get("contype", "1") == "0" and a.get("conaffinity", "1") == "0")
+            if a.get("type") == "mesh" and mesh_hulls and a.get("mesh") in mesh_hulls and collides:
+                mh = mesh_hulls[a["mesh"]]
+                Xm = Xform(np.array(_floats(a.get("pos", "0 0 0"))), _orientation(a, angle_scale))
+                gtype, size, Xg = GT_CONVEX, [float(v) for v in mh["half"]], Xm.compose(Xform(np.array(mh["center"])))
+                hulls.append(dict(geom=len(geoms), verts=[list(map(float, v)) for v in mh["verts"]],
+                                  planes=[list(map(float, q)) for q in mh["planes"]]))
+            elif a.get("type") == "mesh" and mesh_boxes and a.get("mesh") in mesh_boxes and collides:
                 ctr, half = mesh_boxes[a["mesh"]]
                 Xm = Xform(np.array(_floats(a.get("pos", "0 0 0"))), _orientation(a, angle_scale))
                 gtype, size, Xg = GT_BOX, [float(v) for v in half], Xm.compose(Xform(np.array(ctr)))
@@ -564,6 +576,9 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, co
                      fixed_base=int(nodes[0].jtype == JT_FIXED), nodes=nodes, bodies=bodies, geoms=geoms,
                      pairs=[], actuators=actuators, dof_names=dof_names, self_collision=int(self_collision),
                      tendons=tendons)
+    if len(hulls) > 1:
+        raise ValueError("mg_model holds one convex-mesh geom")
+    spec.hull = hulls[0] if hulls else None
     if self_collision:
         spec.pairs = self_collision_pairs(spec)
     return spec
@@ -762,6 +777,8 @@ def _model_dtype():
         ("tendon_limit_stiffness", f4, TD), ("tendon_damping", f4, TD),
         ("obj_type", i4), ("obj_pad", i4), ("obj_mass", f4), ("obj_inertia", f4, 3), ("obj_size", f4, 3),
         ("obj_lin_damping", f4), ("obj_ang_damping", f4), ("obj_gravity", f4),
+        ("hull_num_verts", i4), ("hull_num_planes", i4),
+        ("hull_vert", f4, (MAX_HULL_VERTS, 3)), ("hull_plane", f4, (MAX_HULL_PLANES, 4)),
     ])
 
 
@@ -836,6 +853,16 @@ def pack_model(spec: ModelSpec) -> np.ndarray:
         m["obj_lin_damping"] = o.get("lin_damping", 0.0)
         m["obj_ang_damping"] = o.get("ang_damping", 0.0)
         m["obj_gravity"] = o.get("gravity", 1)
+    if spec.hull:
+        h = spec.hull
+        if len(h["verts"]) > MAX_HULL_VERTS or len(h["planes"]) > MAX_HULL_PLANES:
+            raise ValueError("convex hull exceeds mg_model capacity")
+        if spec.geoms[h["geom"]].gtype != GT_CONVEX:
+            raise ValueError("hull geom index does not name an MG_GT_CONVEX geom")
+        m["hull_num_verts"] = len(h["verts"])
+        m["hull_num_planes"] = len(h["planes"])
+        m["hull_vert"][:len(h["verts"])] = h["verts"]
+        m["hull_plane"][:len(h["planes"])] = h["planes"]
     return m
 
 

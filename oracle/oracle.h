@@ -55,6 +55,11 @@ int orc_contacts(const mg_model* m, const mg_sim_params* p, const float* root13,
 /* egg narrowphase KAT hook (GJK + shrunk-core retry): kind 0 segment p0,p1 / kind 1 box c, R (row-major),
  * h, plus radius, vs the origin-centred ellipsoid e; out = point(3), normal(3), distance */
 int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, const double* e, double* out);
+/* edge-edge KAT hook: hand box c (3), R row-major (9), h (3) in the object box's frame (half extents hb);
+ * out = point(3), normal(3), separation; returns 1 when generated */
+int orc_box_box_edge(const double* shape, const double* hb, double off, double* out);
+/* the convex-mesh geom's plane distance of n geom-frame points: out = (distance, face) per point */
+int orc_hull_distance(const mg_model* m, const double* pl, int32_t n, double* out);
 /* world poses of the gym rigid bodies (n_bodies x 13, velocity at body COM) */
 int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out);
 

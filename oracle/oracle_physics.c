@@ -588,6 +588,112 @@ static void from_obj_pt(const kin* k, const real* pl, real* pw) {
   for (int a = 0; a < 3; a++) pw[a] += k->op[a];
 }
 
+/* ---- the convex-mesh geom (MG_GT_CONVEX): the model's hull_* tables, geom frame ----------------------
+ * (ShadowHand's robot0:C_forearm = mesh robot0:forearm_cvx, robot.xml:8, shared_asset.xml:15; the hull's
+ * 64 kept vertices and 124 outward face planes come from tools/build_models.py) */
+
+/* largest plane distance of point pl (geom frame) over the hull's faces: the signed distance inside and
+ * where a face is the nearest feature, a lower bound of the distance outside near edges and vertices;
+ * *f = the face */
+static real point_hull(const mg_model* m, const real* pl, int* f) {
+  real best = -1e300;
+  int bf = 0;
+  for (int i = 0; i < m->hull_num_planes; i++) {
+    const float* q = m->hull_plane[i];
+    const real s = q[0] * pl[0] + q[1] * pl[1] + q[2] * pl[2] - q[3];
+    if (s > best) { best = s; bf = i; }
+  }
+  *f = bf;
+  return best;
+}
+
+/* broadphase of the hull geom (centre c, axes R, half extents hg = its bounding box) against a sphere
+ * (centre w, radius r): 1 if the sphere comes within `off` of the box (the kernel applies the same test) */
+static int hull_box_near(const real* c, real R[3][3], const real* hg, const real* w, real r, real off) {
+  real d[3] = {w[0] - c[0], w[1] - c[1], w[2] - c[2]}, l[3], s = 0.0;
+  mattvec3(R, d, l);
+  for (int a = 0; a < 3; a++) {
+    const real e = fabs(l[a]) - hg[a];
+    if (e > 0) s += e * e;
+  }
+  return sqrt(s) - r < off;
+}
+
+/* Box-box edge-edge contact (object frame: the object box B at the origin, axis aligned, half extents hb;
+ * the hand box A: centre c, axes = columns of R, half extents hg).  Separating-axis test over the 15 axes
+ * (3 + 3 face normals, 9 edge cross products; an edge axis within ~11 deg of a face normal is left to the
+ * face contacts); when the best axis (largest separation, or least
+ * penetration) is an edge-edge axis by more than 1e-5 m over the best face axis and the separation is
+ * below `off`, one contact at the closest points of the two supporting edges, provided both lie within
+ * their edges (otherwise the vertex-face candidates cover the configuration).  Normal from B to A, gap =
+ * the separation along it.  Returns 1 with *pt, *nrm, *d set, else 0. */
+static int box_box_edge(const real* c, real R[3][3], const real* hg, const real* hb, real off, real* pt, real* nrm,
+                        real* d) {
+  real face = -1e300;
+  for (int i = 0; i < 3; i++) { /* B's face axes e_i */
+    real ra = 0.0;
+    for (int k = 0; k < 3; k++) ra += hg[k] * fabs(R[i][k]);
+    const real sep = fabs(c[i]) - hb[i] - ra;
+    if (sep > face) face = sep;
+  }
+  for (int j = 0; j < 3; j++) { /* A's face axes a_j */
+    const real t = R[0][j] * c[0] + R[1][j] * c[1] + R[2][j] * c[2];
+    real rb = 0.0;
+    for (int i = 0; i < 3; i++) rb += hb[i] * fabs(R[i][j]);
+    const real sep = fabs(t) - hg[j] - rb;
+    if (sep > face) face = sep;
+  }
+  /* edge axes L = e_i x a_j in closed form (the classic OBB test, R[i][j] = e_i . a_j):
+   * L = (.., -R[i2][j] at i1, R[i1][j] at i2), |L|^2 = R[i1][j]^2 + R[i2][j]^2, T.L = T[i2] R[i1][j] - T[i1] R[i2][j],
+   * B's radius hb[i1] |R[i2][j]| + hb[i2] |R[i1][j]|, A's hg[j1] |R[i][j2]| + hg[j2] |R[i][j1]| (L.a_k = e_i.(a_j x a_k)) */
+  real best = -1e300, L[3] = {0, 0, 0};
+  int bi = -1, bj = -1;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const real ln = sqrt(R[i1][j] * R[i1][j] + R[i2][j] * R[i2][j]);
+      if (ln < 1e-6) continue; /* parallel edges: the face axes decide */
+      /* an axis within ~11 deg of a face normal of either box is a face configuration (a box resting
+       * tilted on a face): the vertex-face contacts describe it */
+      const real near = fmax(fmax(fabs(R[i1][j]), fabs(R[i2][j])), fmax(fabs(R[i][j1]), fabs(R[i][j2]))) / ln;
+      if (near > 0.98) continue;
+      const real tl = c[i2] * R[i1][j] - c[i1] * R[i2][j];
+      const real rb = hb[i1] * fabs(R[i2][j]) + hb[i2] * fabs(R[i1][j]);
+      const real ra = hg[j1] * fabs(R[i][j2]) + hg[j2] * fabs(R[i][j1]);
+      const real sep = (fabs(tl) - ra - rb) / ln;
+      if (sep > best) {
+        const real sg = tl < 0 ? -1.0 : 1.0; /* orient L from B towards A */
+        best = sep; bi = i; bj = j;
+        L[i] = 0.0;
+        L[i1] = -sg * R[i2][j] / ln;
+        L[i2] = sg * R[i1][j] / ln;
+      }
+    }
+  if (bi < 0 || !(best > face + 1e-5) || !(best < off)) return 0;
+  /* B's supporting edge: parallel to e_bi, the corner towards +L; A's: parallel to a_bj, towards -L */
+  real pb[3], pa[3], ub[3] = {0, 0, 0}, ua[3] = {R[0][bj], R[1][bj], R[2][bj]};
+  ub[bi] = 1.0;
+  for (int a = 0; a < 3; a++) pb[a] = a == bi ? 0.0 : (L[a] >= 0 ? hb[a] : -hb[a]);
+  for (int a = 0; a < 3; a++) pa[a] = c[a];
+  for (int k = 0; k < 3; k++) {
+    if (k == bj) continue;
+    const real s = (L[0] * R[0][k] + L[1] * R[1][k] + L[2] * R[2][k]) >= 0 ? -hg[k] : hg[k];
+    for (int a = 0; a < 3; a++) pa[a] += s * R[a][k];
+  }
+  /* closest points of the lines pa + s ua and pb + t ub */
+  real w0[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+  const real b = dot3(ua, ub), dd = dot3(ua, w0), e = dot3(ub, w0), den = 1.0 - b * b;
+  if (den < 1e-12) return 0;
+  const real sa = (b * e - dd) / den, tb = (e - b * dd) / den;
+  if (fabs(sa) > hg[bj] || fabs(tb) > hb[bi]) return 0;
+  for (int a = 0; a < 3; a++) {
+    pt[a] = 0.5 * ((pa[a] + sa * ua[a]) + (pb[a] + tb * ub[a]));
+    nrm[a] = L[a];
+  }
+  *d = best;
+  return 1;
+}
+
 /* hand geom g (A) vs the object box (B); normal points from the object to the geom */
 static int geom_object(const mg_model* m, const kin* k, int g, real off, contact* out, int n, int cap) {
   const real hb[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
@@ -611,6 +717,45 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
       from_obj_pt(k, pm, pw);
       from_obj_dir(k, nb, nw);
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+    return n;
+  }
+  if (ty == MG_GT_CONVEX) {
+    const real hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
+    if (!hull_box_near(c, R, hg, k->op, sqrt(dot3(hb, hb)), off)) return n;
+    /* the hull's vertices against the object */
+    for (int v = 0; v < m->hull_num_verts; v++) {
+      real l[3] = {m->hull_vert[v][0], m->hull_vert[v][1], m->hull_vert[v][2]}, w[3], pl[3];
+      matvec3(R, l, w);
+      for (int a = 0; a < 3; a++) w[a] += c[a];
+      to_obj(k, w, pl);
+      real nb[3], cb[3], d = point_box(pl, hb, nb, cb);
+      if (d < off) {
+        real pm[3], pw[3], nw[3];
+        for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
+        from_obj_pt(k, pm, pw);
+        from_obj_dir(k, nb, nw);
+        n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+      }
+    }
+    /* the object's vertices against the hull's faces (normal: minus the face normal) */
+    for (int v = 0; v < 8; v++) {
+      real l[3] = {(v & 1 ? 1 : -1) * hb[0], (v & 2 ? 1 : -1) * hb[1], (v & 4 ? 1 : -1) * hb[2]}, w[3], dl[3], pl[3];
+      from_obj_pt(k, l, w);
+      for (int a = 0; a < 3; a++) dl[a] = w[a] - c[a];
+      mattvec3(R, dl, pl);
+      int f;
+      const real d = point_hull(m, pl, &f);
+      if (d < off) {
+        const real ng[3] = {m->hull_plane[f][0], m->hull_plane[f][1], m->hull_plane[f][2]};
+        real pm[3], pw[3], nw[3];
+        for (int a = 0; a < 3; a++) pm[a] = pl[a] - 0.5 * d * ng[a];
+        matvec3(R, pm, pw);
+        for (int a = 0; a < 3; a++) pw[a] += c[a];
+        matvec3(R, ng, nw);
+        for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+        n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+      }
     }
     return n;
   }
@@ -646,6 +791,20 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
       matvec3(R, nb, nw);
       for (int a = 0; a < 3; a++) nw[a] = -nw[a];
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+    }
+  }
+  /* edge against edge (the vertex-face tests above miss an edge resting across an edge) */
+  {
+    real cl[3], Rt[3][3], Rl[3][3], pe[3], ne[3], de;
+    to_obj(k, c, cl);
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) Rt[a][b] = k->oR[b][a];
+    matmul3(Rt, R, Rl);
+    if (box_box_edge(cl, Rl, hg, hb, off, pe, ne, &de)) {
+      real pw[3], nw[3];
+      from_obj_pt(k, pe, pw);
+      from_obj_dir(k, ne, nw);
+      n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, de);
     }
   }
   return n;
@@ -1031,10 +1190,12 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
 }
 
 /* number of object-contact candidates of an articulation geom (the HIP kernel enumerates the same) */
-static int obj_candidates(int otype, int gtype) {
+static int obj_candidates(int otype, int gtype, int hull_verts) {
   const int round = gtype == MG_GT_SPHERE || gtype == MG_GT_CAPSULE;
+  if (gtype == MG_GT_CONVEX) /* block: hull vertices + the box's 8; pen: hull vertices + its 2 ends; egg: planes */
+    return otype == MG_GT_BOX ? hull_verts + 8 : (otype == MG_GT_CAPSULE ? hull_verts + 2 : 1);
   if (!round && gtype != MG_GT_BOX) return 0;
-  if (otype == MG_GT_BOX) return round ? 1 : 16;
+  if (otype == MG_GT_BOX) return round ? 1 : 17; /* box: 8 + 8 vertex-face, 1 edge-edge */
   if (otype == MG_GT_CAPSULE) return round ? 1 : 3;
   return 1; /* ellipsoid */
 }
@@ -1046,10 +1207,89 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
   real c[3], R[3][3];
   geom_world(m, k, g, c, R);
   const int round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
-  if (!round && ty != MG_GT_BOX) return n;
+  if (!round && ty != MG_GT_BOX && ty != MG_GT_CONVEX) return n;
   real pw[3], nw[3];
+  if (ty == MG_GT_CONVEX) {
+    const real hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
+    const real orad = ot == MG_GT_ELLIPSOID ? fmax(os[0], fmax(os[1], os[2])) : os[0] + os[1];
+    if (!hull_box_near(c, R, hg, k->op, orad, off)) return n;
+    if (ot == MG_GT_ELLIPSOID) {
+      /* egg: the hull's face planes against the ellipsoid's support points (the plane distance of the egg's
+       * point farthest along -n_f, largest over the faces): exact where a hull face is the nearest feature,
+       * a lower bound near hull edges; normal minus that face's normal, point halfway across the gap */
+      real cl[3], dl[3];
+      for (int a = 0; a < 3; a++) dl[a] = k->op[a] - c[a];
+      mattvec3(R, dl, cl); /* egg centre, geom frame */
+      real Rl[3][3]; /* egg axes in the geom frame: R^T oR */
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Rl[a][b] = R[0][a] * k->oR[0][b] + R[1][a] * k->oR[1][b] + R[2][a] * k->oR[2][b];
+      real best = -1e300, bs[3] = {0, 0, 0};
+      int bf = 0;
+      for (int f = 0; f < m->hull_num_planes; f++) {
+        const float* q = m->hull_plane[f];
+        real ne[3]; /* -n_f in the egg frame */
+        for (int b = 0; b < 3; b++) ne[b] = -(Rl[0][b] * q[0] + Rl[1][b] * q[1] + Rl[2][b] * q[2]);
+        real se[3], sg[3];
+        ell_support(os, ne, se);
+        matvec3(Rl, se, sg);
+        for (int a = 0; a < 3; a++) sg[a] += cl[a];
+        const real sd = q[0] * sg[0] + q[1] * sg[1] + q[2] * sg[2] - q[3];
+        if (sd > best) { best = sd; bf = f; bs[0] = sg[0]; bs[1] = sg[1]; bs[2] = sg[2]; }
+      }
+      if (best < off) {
+        const real ng[3] = {m->hull_plane[bf][0], m->hull_plane[bf][1], m->hull_plane[bf][2]};
+        real pm[3];
+        for (int a = 0; a < 3; a++) pm[a] = bs[a] - 0.5 * best * ng[a];
+        matvec3(R, pm, pw);
+        for (int a = 0; a < 3; a++) pw[a] += c[a];
+        matvec3(R, ng, nw);
+        for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+        n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, best);
+      }
+      return n;
+    }
+    /* pen: the hull's vertices against the pen's segment, then the pen's end spheres against the faces */
+    const real ro = os[0];
+    real p0[3], p1[3];
+    for (int a = 0; a < 3; a++) { p0[a] = k->op[a] - k->oR[a][2] * os[1]; p1[a] = k->op[a] + k->oR[a][2] * os[1]; }
+    for (int v = 0; v < m->hull_num_verts; v++) {
+      real l[3] = {m->hull_vert[v][0], m->hull_vert[v][1], m->hull_vert[v][2]}, w[3], s, t, q[3], dv[3];
+      matvec3(R, l, w);
+      for (int a = 0; a < 3; a++) w[a] += c[a];
+      closest_seg_seg(w, w, p0, p1, &s, &t);
+      for (int a = 0; a < 3; a++) { q[a] = p0[a] + t * (p1[a] - p0[a]); dv[a] = w[a] - q[a]; }
+      const real dist = sqrt(dot3(dv, dv)), d = dist - ro;
+      if (d < off && dist > 1e-9) {
+        for (int a = 0; a < 3; a++) {
+          nw[a] = dv[a] / dist;
+          pw[a] = 0.5 * (w[a] + (q[a] + nw[a] * ro));
+        }
+        n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+      }
+    }
+    for (int e = 0; e < 2; e++) {
+      const real* pe = e == 0 ? p0 : p1;
+      real dl[3], pl[3];
+      for (int a = 0; a < 3; a++) dl[a] = pe[a] - c[a];
+      mattvec3(R, dl, pl);
+      int f;
+      const real d = point_hull(m, pl, &f) - ro;
+      if (d < off) {
+        const real ng[3] = {m->hull_plane[f][0], m->hull_plane[f][1], m->hull_plane[f][2]};
+        real pm[3];
+        for (int a = 0; a < 3; a++) pm[a] = pl[a] - (ro + 0.5 * d) * ng[a];
+        matvec3(R, pm, pw);
+        for (int a = 0; a < 3; a++) pw[a] += c[a];
+        matvec3(R, ng, nw);
+        for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+        n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
+      }
+    }
+    return n;
+  }
   if (ot == MG_GT_ELLIPSOID) {
     cvx_shape A;
+    memset(&A, 0, sizeof(A));
     real r = 0.0;
     if (round) {
       real hl = ty == MG_GT_CAPSULE ? m->geom_size[g][1] : 0.0, aw[3], bw[3];
@@ -1129,7 +1369,7 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
 
 /* contact order (the HIP kernel emits the same list): ground contacts of the articulation's geoms
  * in geom order, the object's box corners on the ground, self-collision pairs in pair order, then
- * articulation geoms against the object in geom order */
+ * articulation geoms against the object: the convex-mesh geom, then the others in geom order */
 static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, contact* out, int cap) {
   int n = 0;
   real off = p->contact_offset;
@@ -1145,6 +1385,13 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       for (int s = -1; s <= 1; s += 2) {
         for (int a = 0; a < 3; a++) e[a] = c[a] + s * R[a][2] * hl;
         n = sphere_plane(out, n, cap, nd, g, e, r, off);
+      }
+    } else if (ty == MG_GT_CONVEX) { /* the hull's vertices (the box of geom_size culls them in the kernel) */
+      for (int v = 0; v < m->hull_num_verts; v++) {
+        real l[3] = {m->hull_vert[v][0], m->hull_vert[v][1], m->hull_vert[v][2]}, w[3], e[3];
+        matvec3(R, l, w);
+        for (int a = 0; a < 3; a++) e[a] = c[a] + w[a];
+        n = sphere_plane(out, n, cap, nd, g, e, 0.0, off);
       }
     } else if (ty == MG_GT_BOX) {
       for (int corner = 0; corner < 8; corner++) {
@@ -1196,11 +1443,13 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pt, nrm, d);
     }
   }
+  /* articulation geoms against the object: the convex-mesh geom first, then the others in geom order */
   if (m->obj_type)
-    for (int g = 0; g < m->num_geoms; g++)
-      if (m->geom_filter[g] & MG_COLLIDE_OBJECT)
-        n = m->obj_type == MG_GT_BOX ? geom_object(m, k, g, off, out, n, cap)
-                                     : geom_object_convex(m, k, g, off, out, n, cap);
+    for (int pass = 0; pass < 2; pass++)
+      for (int g = 0; g < m->num_geoms; g++)
+        if ((m->geom_filter[g] & MG_COLLIDE_OBJECT) && ((m->geom_type[g] == MG_GT_CONVEX) == (pass == 0)))
+          n = m->obj_type == MG_GT_BOX ? geom_object(m, k, g, off, out, n, cap)
+                                       : geom_object_convex(m, k, g, off, out, n, cap);
   return n;
 }
 
@@ -1713,6 +1962,29 @@ int orc_ellipsoid_contact(int32_t kind, const real* shape, real radius, const re
     }
   }
   cvx_contact(&A, radius, e, 1e300, out, out + 3, out + 6);
+  return MG_OK;
+}
+
+/* KAT hook: box-box edge-edge contact (box_box_edge) in the object box's frame: shape = hand box centre (3),
+ * axes R row-major (9), half extents (3); hb = object half extents.  out = point (3), normal from the object
+ * to the hand box (3), separation; returns 1 when an edge-edge contact is generated. */
+int orc_box_box_edge(const real* shape, const real* hb, real off, real* out) {
+  real c[3], R[3][3], hg[3];
+  for (int a = 0; a < 3; a++) {
+    c[a] = shape[a];
+    hg[a] = shape[12 + a];
+    for (int b = 0; b < 3; b++) R[a][b] = shape[3 + 3 * a + b];
+  }
+  return box_box_edge(c, R, hg, hb, off, out, out + 3, out + 6);
+}
+
+/* KAT hook: the hull's plane distance (point_hull) of points pl (n x 3, geom frame); out = distance, face */
+int orc_hull_distance(const mg_model* m, const real* pl, int32_t n, real* out) {
+  for (int i = 0; i < n; i++) {
+    int f;
+    out[2 * i] = point_hull(m, pl + 3 * i, &f);
+    out[2 * i + 1] = f;
+  }
   return MG_OK;
 }
 #endif

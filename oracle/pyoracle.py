@@ -59,6 +59,8 @@ def lib():
                                         C.c_int32]
         l.orc_hand_finalize.argtypes = [C.POINTER(_abi.TaskParams), C.POINTER(_abi.TaskBuffers)]
         l.orc_ellipsoid_contact.argtypes = [C.c_int32, P, C.c_double, P, P]
+        l.orc_box_box_edge.argtypes = [P, P, C.c_double, P]
+        l.orc_hull_distance.argtypes = [P, P, C.c_int32, P]
         l.orc_dr_apply.argtypes = [C.POINTER(_abi.DrApplyArgs)]
         l.orc_dr_noise.argtypes = [C.POINTER(_abi.DrNoiseArgs)]
         _lib = l
@@ -115,6 +117,23 @@ def contacts(model_np, sp, root13, dof2, cap=64):
     out = np.zeros(9 * cap)
     n = lib().orc_contacts(model_np.ctypes.data, C.byref(sp), p(f32(root13)), p(f32(dof2)), p(out), cap)
     return out[: 9 * n].reshape(n, 9)
+
+
+def box_box_edge(c, R, h, hb, off):
+    """edge-edge contact of hand box (c, R, h) against the object box hb (object frame): None or
+    (point, normal from the object to the hand box, separation)"""
+    sh = np.concatenate([np.asarray(c, np.float64), np.asarray(R, np.float64).ravel(), np.asarray(h, np.float64)])
+    out = np.zeros(7)
+    ok = lib().orc_box_box_edge(p(sh), p(np.ascontiguousarray(hb, dtype=np.float64)), float(off), p(out))
+    return (out[0:3], out[3:6], out[6]) if ok else None
+
+
+def hull_distance(model_np, pts):
+    """plane distance of geom-frame points to the model's convex-mesh hull: (distances, faces)"""
+    pl = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 3)
+    out = np.zeros((len(pl), 2))
+    lib().orc_hull_distance(model_np.ctypes.data, p(pl), len(pl), p(out))
+    return out[:, 0], out[:, 1].astype(int)
 
 
 def ellipsoid_contact(kind, shape, radius, e):

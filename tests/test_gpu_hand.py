@@ -176,13 +176,8 @@ def env_agreement(a, b, atol, rtol):
     return ok.mean()
 
 
-@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
-def test_hand_physics_step_matches_oracle(lib, kind):
-    """One simulate from random states; egg = GJK / MPR narrowphase, pen = capsule contacts."""
-    spec, sp, tp = setup(kind=kind)
-    n = 256
-    rng = np.random.default_rng(5)
-    h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
+def _physics_vs_oracle(lib, spec, sp, h, rng, n):
+    """one simulate of the states h on the GPU and in the oracle; asserts determinism and per-env agreement"""
     # applied object forces (LOCAL_SPACE) on half of the envs
     h.rb_forces[: n // 2, len(spec.bodies)] = rng.normal(0, 0.3, (n // 2, 3))
     e = DevHandEnv(h)
@@ -215,9 +210,59 @@ def test_hand_physics_step_matches_oracle(lib, kind):
     assert env_agreement(np_(e.rbs), h.rbs, 2e-3, 2e-3) >= 0.97
     scale = max(1.0, np.abs(h.sensors).max())
     assert env_agreement(np_(e.sensors), h.sensors, 1e-2 * scale, 0) >= 0.97
+    return mnp, h0
+
+
+@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
+def test_hand_physics_step_matches_oracle(lib, kind):
+    """One simulate from random states; egg = GJK / MPR narrowphase, pen = capsule contacts."""
+    spec, sp, tp = setup(kind=kind)
+    n = 256
+    rng = np.random.default_rng(5)
+    h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
+    mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n)
     # the states exercise the object contacts
-    ncon = [len(O.contacts(mnp, sp, h.root[i].ravel(), h.dof[i], 64)) for i in range(32)]
+    ncon = [len(O.contacts(mnp, sp, h0.root[i].ravel(), h0.dof[i], 64)) for i in range(32)]
     assert max(ncon) >= 3
+
+
+def forearm_top(spec, h):
+    """world position of the forearm hull's highest vertex (geom frame of node 0 = the hand's root row)"""
+    g = spec.geoms[spec.hull["geom"]]
+
+    def rot(q):
+        a, b, c, w = q
+        return np.array([[1 - 2 * (b * b + c * c), 2 * (a * b - c * w), 2 * (a * c + b * w)],
+                         [2 * (a * b + c * w), 1 - 2 * (a * a + c * c), 2 * (b * c - a * w)],
+                         [2 * (a * c - b * w), 2 * (b * c + a * w), 1 - 2 * (a * a + b * b)]])
+    Rn = rot(h.root[0, 0, 3:7].astype(np.float64))
+    c = h.root[0, 0, 0:3] + Rn @ np.asarray(g.pos)
+    vw = c + np.array(spec.hull["verts"]) @ (Rn @ rot(g.quat)).T
+    return vw[np.argmax(vw[:, 2])]
+
+
+@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
+def test_hand_physics_near_forearm_matches_oracle(lib, kind):
+    """The forearm's convex-hull geom (robot.xml:8): objects dropped on / into the hull top
+    (block: vertex-face both ways; egg: GJK / MPR on the hull's support function; pen: hull vertices vs its
+    segment, its ends vs the hull's faces), GPU vs oracle like the palm states."""
+    spec, sp, tp = setup(kind=kind)
+    n = 256
+    rng = np.random.default_rng(11)
+    h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
+    top = forearm_top(spec, h)
+    ob = h.root[:, 1]
+    reach = {"block": 0.025, "egg": 0.03, "pen": 0.008}[kind]
+    ob[:, 0:3] = top + np.c_[rng.normal(0, 0.02, (n, 2)), reach * rng.uniform(0.6, 1.4, n)]
+    ob[:, 7:13] = rng.normal(0, 0.1, (n, 6))
+    h.dof[:, :, 0] = 0.0   # fingers straight and away from the forearm
+    mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n)
+    hull_geom = spec.hull["geom"]
+    touching = 0
+    for i in range(64):
+        cs = O.contacts(mnp, sp, h0.root[i].ravel(), h0.dof[i], 64)
+        touching += any(int(c[0]) == spec.geoms[hull_geom].node and int(c[8]) == -2 for c in cs)
+    assert touching >= 16, touching
 
 
 @pytest.mark.parametrize("kind", ["block", "egg", "pen"])

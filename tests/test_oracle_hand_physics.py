@@ -266,3 +266,97 @@ def test_egg_and_pen_land_on_the_palm():
         assert sum(1 for c in con if c[8] == -2 and c[0] >= 0) >= 2, (kind, con)
         if kind == "pen":
             assert np.abs(obj[7:13]).max() < 0.05, obj
+
+
+# ---------------------------------------------------------------------------------------------------- A6
+def _edge_config(s, h=0.02, hl=0.05, hb=0.025):
+    """hand box A whose edge (parallel to its long axis a1 = (0, 1, -1)/sqrt2) passes a distance s above the
+    object box's edge along x at (y, z) = (hb, hb), crossing it; L = (0, 1, 1)/sqrt2 points from B to A"""
+    L = np.array([0.0, 1.0, 1.0]) / np.sqrt(2)
+    x = np.array([1.0, 0.0, 0.0])
+    a1 = np.array([0.0, 1.0, -1.0]) / np.sqrt(2)
+    a0, a2 = (x + L) / np.sqrt(2), (-x + L) / np.sqrt(2)
+    R = np.stack([a0, a1, a2], axis=1)          # columns = A's axes
+    p0 = np.array([0.0, hb, hb])
+    c = p0 + (s + h * np.sqrt(2)) * L
+    return c, R, np.array([h, hl, h]), np.full(3, hb), p0, L
+
+
+def test_box_edge_edge_contact_crossed_edges():
+    """An edge resting across an edge: no vertex lies near the other box, so only the SAT edge-edge candidate
+    sees it (normal = the edges' common perpendicular, gap = their distance, point halfway)."""
+    for s in (0.001, 0.0, -0.0005):
+        c, R, h, hb, p0, L = _edge_config(s)
+        r = O.box_box_edge(c, R, h, hb, 0.002)
+        assert r is not None, s
+        pt, n, d = r
+        np.testing.assert_allclose(n, L, atol=1e-9)
+        np.testing.assert_allclose(d, s, atol=1e-9)
+        np.testing.assert_allclose(pt, p0 + 0.5 * s * L, atol=1e-9)
+    # beyond the contact offset: nothing
+    c, R, h, hb, _, _ = _edge_config(0.003)
+    assert O.box_box_edge(c, R, h, hb, 0.002) is None
+    # a box lying (slightly tilted) on the object's top face is a face configuration: no edge contact
+    t = 0.02
+    Rf = np.array([[1, 0, 0], [0, np.cos(t), -np.sin(t)], [0, np.sin(t), np.cos(t)]])
+    assert O.box_box_edge([0.0, 0.0, 0.025 + 0.0111 - 0.0002], Rf, [0.032, 0.049, 0.0111], np.full(3, 0.025),
+                          0.002) is None
+
+
+def _forearm_frame(mnp, h, spec):
+    """world centre and axes of the convex forearm geom: geom_pos / geom_quat are in the frame of node 0, the
+    fixed root, whose pose is the hand's root row"""
+    g = spec.geoms[spec.hull["geom"]]
+
+    def rot(qq):
+        a, b, c_, w = qq
+        return np.array([[1 - 2 * (b * b + c_ * c_), 2 * (a * b - c_ * w), 2 * (a * c_ + b * w)],
+                         [2 * (a * b + c_ * w), 1 - 2 * (a * a + c_ * c_), 2 * (b * c_ - a * w)],
+                         [2 * (a * c_ - b * w), 2 * (b * c_ + a * w), 1 - 2 * (a * a + b * b)]])
+    x, q = h.root[0, 0, 0:3].astype(np.float64), h.root[0, 0, 3:7].astype(np.float64)
+    Rn = rot(q)
+    return x + Rn @ np.asarray(g.pos), Rn @ rot(g.quat)
+
+
+def test_forearm_hull_tables():
+    """The forearm's convex mesh (shared_asset.xml:15) is a hull of 64 vertices with outward planes: every
+    kept vertex lies on or inside every plane, the centre is inside, points beyond the bounding box are
+    outside, and the plane distance never exceeds the true distance to the kept vertices' hull."""
+    spec = M.load_builtin("shadow_hand")
+    mnp = M.pack_model(spec)
+    assert spec.geoms[spec.hull["geom"]].gtype == M.GT_CONVEX and spec.geoms[spec.hull["geom"]].name == "robot0:C_forearm"
+    v = np.array(spec.hull["verts"])
+    d, _ = O.hull_distance(mnp, v)
+    assert d.max() < 1e-6 and len(v) == 64
+    d0, _ = O.hull_distance(mnp, np.zeros((1, 3)))
+    assert d0[0] < -0.03
+    hb = np.array(spec.geoms[spec.hull["geom"]].size)
+    rng = np.random.default_rng(1)
+    dirs = rng.normal(size=(200, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    far = dirs * (np.linalg.norm(hb) + 0.01)
+    df, _ = O.hull_distance(mnp, far)
+    assert (df > 0).all()
+    # lower bound: the plane distance <= the distance to any hull vertex
+    dv = np.linalg.norm(far[:, None, :] - v[None], axis=2).min(1)
+    assert (df <= dv + 1e-9).all()
+
+
+def test_cube_contacts_and_rests_on_the_forearm_hull():
+    """A cube dropped 1 mm above the forearm hull's highest vertex gets contacts from the convex geom (node 0)
+    and is held up by them (the bounding box this replaced would put it 0.1-2 mm higher)."""
+    spec, tp, sp, mnp, h = setup()
+    c, R = _forearm_frame(mnp, h, spec)
+    vw = c + np.array(spec.hull["verts"]) @ R.T
+    top = vw[np.argmax(vw[:, 2])]
+    h.root[:, 1, 0:3] = top + np.array([0.0, 0.0, 0.025 + 0.001])
+    h.root[:, 1, 3:7] = (0, 0, 0, 1)
+    h.root[:, 1, 7:] = 0
+    cs = O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)
+    fore = [x for x in cs if int(x[0]) == 0 and int(x[8]) == -2]
+    assert len(fore) >= 1
+    z0 = float(h.root[0, 1, 2])
+    for _ in range(10):
+        h.simulate(mnp, sp)
+    # held up by the hull: no deeper than a few mm below the start (free fall would drop ~12 mm)
+    assert h.root[0, 1, 2] > z0 - 0.004, (h.root[0, 1, 2], z0)

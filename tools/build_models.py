@@ -13,7 +13,10 @@ them from migym/assets/*.json.
             (tasks/shadow_hand.py:220-396: fix_base_link, collapse_fixed_joints, disable_gravity,
              tendon limit_stiffness 30 / damping 0.1 on the four T_*J1c tendons, fingertip force
              sensors; the object keeps gym's default AssetOptions: angular_damping 0.5, gravity on).
-            The forearm's convex collision mesh is replaced by its bounding box.
+            The forearm's convex collision mesh (forearm_electric_cvx.stl, 455 hull vertices) is
+            imported as a convex hull of 64 of its vertices (greedy: the 26 axis / diagonal extremes,
+            then repeatedly the vertex farthest outside the current hull; every dropped vertex lies
+            within 1.9 mm of the kept hull) with its face planes (coplanar facets merged).
   hand_objects.json  the free object of each ShadowHand objectType (shadow_hand.py:86-100):
             block = urdf/objects/cube_multicolor.urdf, egg = mjcf/open_ai_assets/hand/egg.xml
             (ellipsoid), pen = mjcf/open_ai_assets/hand/pen.xml (capsule along the body z); mass and
@@ -35,8 +38,8 @@ from migym import model as M  # noqa: E402
 REF = os.environ.get("MIGYM_REFERENCE", "/root/reference")
 
 
-def stl_bounds(path, scale=(1.0, 1.0, 1.0)):
-    """axis-aligned bounds of an STL mesh (binary or ASCII), mesh frame, scaled."""
+def stl_vertices(path, scale=(1.0, 1.0, 1.0)):
+    """unique vertices of an STL mesh (binary or ASCII), mesh frame, scaled."""
     data = open(path, "rb").read()
     n = struct.unpack("<I", data[80:84])[0] if len(data) >= 84 else 0
     if len(data) == 84 + 50 * n:
@@ -45,8 +48,35 @@ def stl_bounds(path, scale=(1.0, 1.0, 1.0)):
     else:
         v = np.array([[float(x) for x in ln.split()[1:4]] for ln in data.decode().splitlines()
                       if ln.strip().startswith("vertex")])
-    v = v * np.asarray(scale)
-    return v.min(0), v.max(0)
+    return np.unique(v * np.asarray(scale), axis=0)
+
+
+def reduced_hull(v, max_verts=64, tol=1e-5):
+    """a convex hull of at most max_verts of the points v: the extremes along the 26 axis / diagonal
+    directions, then greedily the point farthest outside the current hull.  Returns (kept vertices,
+    merged outward face planes [n, d] with n.x <= d inside, largest distance of a dropped point
+    outside the kept hull)."""
+    from scipy.spatial import ConvexHull
+    v = v[ConvexHull(v).vertices]
+    dirs = [np.array(d, float) - 1.0 for d in np.ndindex(3, 3, 3) if d != (1, 1, 1)]
+    sel = []
+    for d in dirs:
+        i = int(np.argmax(v @ d))
+        if i not in sel:
+            sel.append(i)
+    while True:
+        eq = ConvexHull(v[sel]).equations          # n.x + off <= 0 inside
+        out = (v @ eq[:, :3].T + eq[:, 3]).max(1)
+        i = int(np.argmax(out))
+        if out[i] < tol or len(sel) >= max_verts:
+            break
+        sel.append(i)
+    planes = []
+    for e in eq:
+        q = [float(e[0]), float(e[1]), float(e[2]), float(-e[3])]
+        if not any(np.allclose(q, p2, atol=1e-7) for p2 in planes):
+            planes.append(q)
+    return v[sel], planes, float(max(out.max(), 0.0))
 
 
 HAND_FINGERTIPS = ["robot0:ffdistal", "robot0:mfdistal", "robot0:rfdistal", "robot0:lfdistal", "robot0:thdistal"]
@@ -56,15 +86,21 @@ HAND_TENDONS = ["robot0:T_FFJ1c", "robot0:T_MFJ1c", "robot0:T_RFJ1c", "robot0:T_
 def shadow_hand():
     hand_dir = os.path.join(REF, "assets/mjcf/open_ai_assets/hand")
     mesh_dir = os.path.join(hand_dir, "../stls/hand")
-    boxes = {}
+    hulls = {}
     for m in ET.parse(os.path.join(hand_dir, "shared_asset.xml")).getroot().iter("mesh"):
         if "cvx" not in m.get("file", ""):
             continue
         sc = [float(x) for x in m.get("scale", "1 1 1").split()]
-        lo, hi = stl_bounds(os.path.join(mesh_dir, m.get("file")), sc)
-        boxes[m.get("name")] = ((lo + hi) / 2, (hi - lo) / 2)
+        v = stl_vertices(os.path.join(mesh_dir, m.get("file")), sc)
+        lo, hi = v.min(0), v.max(0)
+        ctr = (lo + hi) / 2
+        kept, planes, err = reduced_hull(v - ctr)
+        print(f"{m.get('name')}: {len(v)} vertices -> hull of {len(kept)} ({len(planes)} planes), "
+              f"max dropped-vertex distance {err * 1e3:.2f} mm")
+        hulls[m.get("name")] = dict(center=ctr.tolist(), half=((hi - lo) / 2).tolist(), verts=kept.tolist(),
+                                    planes=planes)
     hand = M.load_mjcf(os.path.join(hand_dir, "shadow_hand.xml"), "shadow_hand", collapse_fixed=True,
-                       mesh_boxes=boxes)
+                       mesh_hulls=hulls)
     hand.sensors = [hand.body_index(n) for n in HAND_FINGERTIPS]
     hand.gravity_off = 1
     for t in hand.tendons:
