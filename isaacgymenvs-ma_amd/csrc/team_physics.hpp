@@ -471,30 +471,42 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
       }
     }
   if (bi < 0 || !(best > face + 1e-5f) || !(best < off)) return false;
-  float pb[3], pa[3] = {cv[0], cv[1], cv[2]};
+  // the supporting edges (B: parallel to e_bi, the corner towards +L; A: parallel to a_bj, towards -L);
+  // bi / bj are data dependent, so columns and extents are selected by unrolled compares (no dynamic
+  // register indexing, which would put R in scratch)
+  float pb[3], pa[3] = {cv[0], cv[1], cv[2]}, hga = 0.0f, hbb = 0.0f;
+  V3 ua = v3(0, 0, 0);
 #pragma unroll
-  for (int a = 0; a < 3; a++) pb[a] = a == bi ? 0.0f : (L[a] >= 0.0f ? hbv[a] : -hbv[a]);
+  for (int a = 0; a < 3; a++) {
+    pb[a] = a == bi ? 0.0f : (L[a] >= 0.0f ? hbv[a] : -hbv[a]);
+    if (a == bi) hbb = hbv[a];
+  }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    if (k == bj) continue;
+    if (k == bj) {
+      ua = v3(R.m[0][k], R.m[1][k], R.m[2][k]);
+      hga = hgv[k];
+      continue;
+    }
     const float sg = (L[0] * R.m[0][k] + L[1] * R.m[1][k] + L[2] * R.m[2][k]) >= 0.0f ? -hgv[k] : hgv[k];
 #pragma unroll
     for (int a = 0; a < 3; a++) pa[a] += sg * R.m[a][k];
   }
-  const V3 ua = v3(R.m[0][bj], R.m[1][bj], R.m[2][bj]);
   const V3 ub = v3(bi == 0 ? 1.0f : 0.0f, bi == 1 ? 1.0f : 0.0f, bi == 2 ? 1.0f : 0.0f);
   const V3 PA = v3(pa[0], pa[1], pa[2]), PB = v3(pb[0], pb[1], pb[2]), w0 = PA - PB;
   const float b = dot(ua, ub), dd = dot(ua, w0), e = dot(ub, w0), den = 1.0f - b * b;
   if (den < 1e-12f) return false;
   const float sa = (b * e - dd) / den, tb = (e - b * dd) / den;
-  if (fabsf(sa) > hgv[bj] || fabsf(tb) > hbv[bi]) return false;
+  if (fabsf(sa) > hga || fabsf(tb) > hbb) return false;
   *pt = ((PA + ua * sa) + (PB + ub * tb)) * 0.5f;
   *nrm = v3(L[0], L[1], L[2]);
   *dist = best;
   return true;
 }
 
-// Per-lane context of one team.
+// Per-lane context of one team.  Every member function is force-inlined: one that the inliner leaves as a
+// call (it declined fk() once the egg kernel grew) takes `this`, which puts the whole Team object in scratch
+// memory, and every phase then runs from scratch (egg: 7.4 -> 4.7 M env-steps/s until this was found).
 template <int T, int MN, int MC, int MG, int MP, int OBJ = 0>  // OBJ: the free object's type (0: none)
 struct Team {
   using L = TeamLDS<T, MN, MC, OBJ>;
@@ -530,18 +542,18 @@ struct Team {
   // 32-bit accumulators so they stay in SGPRs and do not disturb the vector register budget
   unsigned int ph[16];
   unsigned long long tmark;
-  __device__ void ph_start() {
+  __device__ __forceinline__ void ph_start() {
     for (int i = 0; i < 16; i++) ph[i] = 0u;
     tmark = __builtin_amdgcn_s_memtime();
   }
-  __device__ void ph_mark(int i) {
+  __device__ __forceinline__ void ph_mark(int i) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     ph[i] = __builtin_amdgcn_readfirstlane(ph[i] + (unsigned int)(t1 - tmark));
     tmark = t1;
   }
 #else
-  __device__ void ph_start() {}
-  __device__ void ph_mark(int) {}
+  __device__ __forceinline__ void ph_start() {}
+  __device__ __forceinline__ void ph_mark(int) {}
 #endif
   // drives / tendons (node lanes)
   float tgt;           // PD target of the own DOF
@@ -553,17 +565,17 @@ struct Team {
   const float* drt;    // tendons (stride 2)
   const float* dro;    // object [mass, friction, scale]
   // node property row [mass, armature, damping, stiffness, lower, upper, drive kp, effort]
-  __device__ const float* nprop(int i) const { return drn ? drn + 9 * i : &mt->nf[i][24]; }
-  __device__ float omass() const { return dro ? dro[0] : m->obj_mass; }
-  __device__ float oscale() const { return dro ? dro[2] : 1.0f; }
-  __device__ V3 osize() const { return ld3(m->obj_size) * oscale(); }
+  __device__ __forceinline__ const float* nprop(int i) const { return drn ? drn + 9 * i : &mt->nf[i][24]; }
+  __device__ __forceinline__ float omass() const { return dro ? dro[0] : m->obj_mass; }
+  __device__ __forceinline__ float oscale() const { return dro ? dro[2] : 1.0f; }
+  __device__ __forceinline__ V3 osize() const { return ld3(m->obj_size) * oscale(); }
   // object principal moments: model inertia x (mass / model mass) x scale^2 (uniform density)
-  __device__ V3 oinertia() const {
+  __device__ __forceinline__ V3 oinertia() const {
     const float f = dro ? (dro[0] / m->obj_mass) * dro[2] * dro[2] : 1.0f;
     return ld3(m->obj_inertia) * f;
   }
   // friction coefficient of a contact side's geom (-1 ground plane, -2 the object)
-  __device__ float gmu(int g) const { return g >= 0 ? drg[g] : (g == -2 ? dro[1] : p->friction); }
+  __device__ __forceinline__ float gmu(int g) const { return g >= 0 ? drg[g] : (g == -2 ? dro[1] : p->friction); }
   // free object (OBJ): pose replicated on every lane, velocity column on lanes ob0..ob0+5
   int ob0;
   bool objl;
@@ -571,9 +583,9 @@ struct Team {
   float oq[4];
   M3 oR;
 
-  __device__ int col_of(int i) const { return ncol0 - 1 + i; }
+  __device__ __forceinline__ int col_of(int i) const { return ncol0 - 1 + i; }
 
-  __device__ void init(L* lds, const MT* tile, const mg_model* mm, const mg_sim_params* pp) {
+  __device__ __forceinline__ void init(L* lds, const MT* tile, const mg_model* mm, const mg_sim_params* pp) {
     s = lds;
     mt = tile;
     m = mm;
@@ -614,11 +626,11 @@ struct Team {
     oq[0] = oq[1] = oq[2] = 0.0f;
     oq[3] = 1.0f;
   }
-  __device__ float gscale() const { return m->gravity_off ? 0.0f : 1.0f; }
-  __device__ bool in_path(int target, int k) const { return target >= 0 && ((s->anc[target] >> k) & 1ull); }
+  __device__ __forceinline__ float gscale() const { return m->gravity_off ? 0.0f : 1.0f; }
+  __device__ __forceinline__ bool in_path(int target, int k) const { return target >= 0 && ((s->anc[target] >> k) & 1ull); }
 
   // ---------------------------------------------------------------- FK (level-synchronous)
-  __device__ void fk() {
+  __device__ __forceinline__ void fk() {
     if (OBJ) oR = quat_to_mat(oq[0], oq[1], oq[2], oq[3]);
     if (tl == 0) {
       M3 R0 = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
@@ -674,7 +686,7 @@ struct Team {
     }
   }
 
-  __device__ void set_axis() {
+  __device__ __forceinline__ void set_axis() {
     if (freeb && tl < 6) {
       for (int k = 0; k < 6; k++) Sl[k] = k == tl ? 1.0f : 0.0f;
     } else {
@@ -683,7 +695,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- ABA (unconstrained step)
-  __device__ void aba() {
+  __device__ __forceinline__ void aba() {
     if (node >= 0) {
       const V3 o = ld3(s->x[0]);
       const float* nf = mt->nf[node];
@@ -795,7 +807,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- fixed tendons (explicit soft limits)
-  __device__ void tendons() {
+  __device__ __forceinline__ void tendons() {
     ttend = 0.0f;
     for (int q = 0; q < mt->nten; q++) {
       const int d0 = mt->tdof[q][0], d1 = mt->tdof[q][1];
@@ -813,12 +825,12 @@ struct Team {
 
   // ---------------------------------------------------------------- free object: unconstrained step
   // I_w = R diag(I) R^T; every lane evaluates the 3-vectors, object lane k keeps component k.
-  __device__ V3 obj_inv_inertia(V3 x) const {
+  __device__ __forceinline__ V3 obj_inv_inertia(V3 x) const {
     const V3 I = oinertia();
     V3 b = mulT(oR, x);
     return mul(oR, v3(b.x / I.x, b.y / I.y, b.z / I.z));
   }
-  __device__ void obj_free() {
+  __device__ __forceinline__ void obj_free() {
     if (!OBJ) return;
     const V3 w = v3(__shfl(nu, tb + ob0), __shfl(nu, tb + ob0 + 1), __shfl(nu, tb + ob0 + 2));
     const V3 I = oinertia();
@@ -838,7 +850,7 @@ struct Team {
   }
   // object part of contact row r on the object's columns [w; v_com]: +-[(p - c_obj) x d; d] (d = the
   // row's direction: normal or a tangent; sign + when the object is side A)
-  __device__ void obj_jrow(int r, V3* wo, V3* d) const {
+  __device__ __forceinline__ void obj_jrow(int r, V3* wo, V3* d) const {
     const int c = r / 3, q = r - 3 * c;
     const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
     const V3 dir = ld3(q == 0 ? s->cn[c] : (q == 1 ? s->ct1[c] : s->ct2[c]));
@@ -846,7 +858,7 @@ struct Team {
     *d = dir * so;
   }
   // object part of the response column Y_r = M^-1 J_r^T (object lanes)
-  __device__ float obj_response(int r) const {
+  __device__ __forceinline__ float obj_response(int r) const {
     const int k = tl - ob0;
     if constexpr (L::OROWS > 1) {
       const float* J = s->rwo[r];
@@ -868,7 +880,7 @@ struct Team {
   // pass is then written in joint space, y_j = (ut_j - U_j.a0 - sum_{i in anc(j)} (U_j.S_i) y_i) / D_j:
   // level by level, each lane gathers its ancestor's y values with one bpermute per column (no LDS
   // round trip or barrier per level).  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
-  __device__ void test_solve(int r0, int nrows_, const float* Wv, float* y) {
+  __device__ __forceinline__ void test_solve(int r0, int nrows_, const float* Wv, float* y) {
     auto& ts = s->u.sv.ts.ts;
     for (int i = tl; i < L::RB * MN; i += T) (&ts.ut[0][0])[i] = 0.0f;
     wsync();
@@ -978,13 +990,13 @@ struct Team {
   }
 
   // side k of contact c: 0 node A, 1 node B, 2 geom A, 3 geom B
-  __device__ int cside(int c, int k) const { return (int)(int8_t)(s->cside[c] >> (8 * k)); }
+  __device__ __forceinline__ int cside(int c, int k) const { return (int)(int8_t)(s->cside[c] >> (8 * k)); }
   // row r -> kind (0 normal, 1 friction, 2 lower limit, 3 upper limit) and ref (contact / node).
   // Rows are [n, t1, t2] per contact, then the joint limits (oracle order).
-  __device__ int row_kind(int r) const { return r < 3 * ncr ? (r % 3 == 0 ? 0 : 1) : (s->lmeta[r - 3 * ncr] & 3); }
-  __device__ int row_ref(int r) const { return r < 3 * ncr ? r / 3 : (s->lmeta[r - 3 * ncr] >> 4); }
+  __device__ __forceinline__ int row_kind(int r) const { return r < 3 * ncr ? (r % 3 == 0 ? 0 : 1) : (s->lmeta[r - 3 * ncr] & 3); }
+  __device__ __forceinline__ int row_ref(int r) const { return r < 3 * ncr ? r / 3 : (s->lmeta[r - 3 * ncr] >> 4); }
   // spatial direction of contact row r at the team origin: w = [(p - o) x d; d]
-  __device__ void row_w(int r, float* w) const {
+  __device__ __forceinline__ void row_w(int r, float* w) const {
     const int c = r / 3, k = r - 3 * c;
     const float* dp = k == 0 ? s->cn[c] : (k == 1 ? s->ct1[c] : s->ct2[c]);
     const V3 d = ld3(dp), q = ld3(s->cp[c]) - org, mo = cross(q, d);
@@ -992,7 +1004,7 @@ struct Team {
   }
   // Jacobian code of this lane for row r: 0 none, 1 +, 2 - (contact rows: +-Sl.w; limit rows: +-1
   // on the DOF's lane)
-  __device__ int jac_code(int r) const {
+  __device__ __forceinline__ int jac_code(int r) const {
     if (tl >= nv || (OBJ && objl)) return 0;
     const int kind = row_kind(r);
     if (kind >= 2) return (node > 0 && node == row_ref(r)) ? (kind == 2 ? 1 : 2) : 0;
@@ -1004,7 +1016,7 @@ struct Team {
     return sgn > 0.0f ? 1 : (sgn < 0.0f ? 2 : 0);
   }
   // J_r[tl] from the lane's code (object lanes: the stored object part)
-  __device__ float jac_value(int r, int code) const {
+  __device__ __forceinline__ float jac_value(int r, int code) const {
     if (OBJ && objl) {
       if constexpr (L::OROWS > 1) return r >= 3 * ncr ? 0.0f : s->rwo[r][tl - ob0];
       if (r >= 3 * ncr) return 0.0f;
@@ -1025,7 +1037,7 @@ struct Team {
   // triples (n, t1, t2 of contact r0 / 3): they share the lane's sign and the point-velocity vector
   // g = Sl_ang x (p - o) + Sl_lin, so J_r = sign (d_r . g) (= sign Sl . [(p - o) x d_r; d_r]).
   // Limit rows: +-1 on the DOF's lane.  Object lanes: the stored object part of the contact rows.
-  __device__ void batch_jacobians(int r0, int nrows_, float* J) const {
+  __device__ __forceinline__ void batch_jacobians(int r0, int nrows_, float* J) const {
 #pragma unroll
     for (int q = 0; q < 3; q++) J[q] = 0.0f;
     if (OBJ && objl) {
@@ -1069,7 +1081,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- collision -> LDS contact list
-  __device__ void geom_world(int g, V3* cw, M3* Rg) const {
+  __device__ __forceinline__ void geom_world(int g, V3* cw, M3* Rg) const {
     const int nd = mt->gnode[g];
     const float* gf = mt->gf[g];
     M3 Rn, Rl;
@@ -1084,14 +1096,14 @@ struct Team {
   // world frames of the geoms, staged once per substep by collide() (lane per geom) in the team's
   // union storage (dead between the ABA and build_rows); rows of 13 floats (odd stride): centre, R
   static constexpr int GW = 13;
-  __device__ float* gw_tile() const { return &s->u.slot[0][0]; }
-  __device__ void geom_staged(int g, V3* c, M3* Rg) const {
+  __device__ __forceinline__ float* gw_tile() const { return &s->u.slot[0][0]; }
+  __device__ __forceinline__ void geom_staged(int g, V3* c, M3* Rg) const {
     const float* w = gw_tile() + GW * g;
     *c = v3(w[0], w[1], w[2]);
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) Rg->m[a][b] = w[3 + 3 * a + b];
   }
-  __device__ bool geom_segment(int g, V3* a, V3* b, float* r) const {
+  __device__ __forceinline__ bool geom_segment(int g, V3* a, V3* b, float* r) const {
     V3 c;
     M3 Rg;
     geom_staged(g, &c, &Rg);
@@ -1109,7 +1121,7 @@ struct Team {
   // candidate q of articulation geom g against the object box (oracle geom_object): sphere/capsule
   // -> one closest-point candidate; box -> its 8 vertices vs the object, then the object's 8 vertices
   // vs the geom (normal flipped).  Normal points from the object (B) to the geom (A).
-  __device__ bool obj_candidate(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
+  __device__ __forceinline__ bool obj_candidate(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
     const V3 hb = osize();
     const int ty = mt->gtype[g];
     const float* gs = mt->gf[g] + 12;
@@ -1163,7 +1175,7 @@ struct Team {
   //   pen:   the hull's vertices against its segment, then its two end spheres against the faces;
   //   egg:   the faces against the ellipsoid's support points.
   // Normal from the object to the geom.  Hull vertex q against the object (block / pen), lane per vertex:
-  __device__ bool hull_vertex_candidate(int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
+  __device__ __forceinline__ bool hull_vertex_candidate(int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
     const V3 w = c + mul(Rg, ld3(m->hull_vert[q]));
     if constexpr (OBJ == MG_GT_BOX) {
       const V3 pl = mulT(oR, w - op);
@@ -1189,7 +1201,7 @@ struct Team {
     }
   }
   // object point k (block: box vertex k; pen: end k; egg: unused) in the geom frame
-  __device__ V3 hull_object_point(int k, V3 c, const M3& Rg) const {
+  __device__ __forceinline__ V3 hull_object_point(int k, V3 c, const M3& Rg) const {
     const V3 os = osize();
     if constexpr (OBJ == MG_GT_BOX) {
       const V3 l = v3((k & 1 ? 1.f : -1.f) * os.x, (k & 2 ? 1.f : -1.f) * os.y, (k & 4 ? 1.f : -1.f) * os.z);
@@ -1201,7 +1213,7 @@ struct Team {
   }
   // egg: its support point (geom frame) farthest along -n (n a geom-frame face normal); cl / Rl: the egg's
   // centre and axes in the geom frame
-  __device__ V3 egg_support_geom(V3 n, V3 cl, const M3& Rl) const {
+  __device__ __forceinline__ V3 egg_support_geom(V3 n, V3 cl, const M3& Rl) const {
     const V3 os = osize();
     const V3 ne = mulT(Rl, n * -1.0f);
     const V3 qe = v3(os.x * os.x * ne.x, os.y * os.y * ne.y, os.z * os.z * ne.z);
@@ -1213,7 +1225,7 @@ struct Team {
   // object-contact candidates of an articulation geom of type ty (oracle obj_candidates): block
   // sphere/capsule 1, box 17 (vertex tests both ways, edge-edge); pen sphere/capsule 1 (segment-segment),
   // box 3 (closest point + the two ends); egg 1 (GJK / MPR); the convex-mesh geom as counted below
-  __device__ int ocand_count(int ty) const {
+  __device__ __forceinline__ int ocand_count(int ty) const {
     const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
     constexpr int ot = OBJ;
     if (ty == MG_GT_CONVEX)  // block: hull vertices + the box's 8; pen: hull vertices + its 2 ends; egg: GJK
@@ -1228,7 +1240,7 @@ struct Team {
     return 1;
   }
   // bounding radius of the object (broadphase cull)
-  __device__ float obj_radius() const {
+  __device__ __forceinline__ float obj_radius() const {
     const V3 e = osize();
     constexpr int ot = OBJ;
     if (ot == MG_GT_BOX) return sqrtf(dot(e, e));
@@ -1236,7 +1248,7 @@ struct Team {
     return fmaxf(e.x, fmaxf(e.y, e.z));
   }
   // candidate q of geom g against the pen / egg (oracle geom_object_convex); false = no candidate
-  __device__ bool obj_candidate_convex(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
+  __device__ __forceinline__ bool obj_candidate_convex(int g, int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
     const V3 os = osize();
     const int ty = mt->gtype[g];
     const float* gs = mt->gf[g] + 12;
@@ -1302,14 +1314,14 @@ struct Team {
     return true;
   }
 
-  __device__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
+  __device__ __forceinline__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
     s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
     s->cn[slot][0] = n.x; s->cn[slot][1] = n.y; s->cn[slot][2] = n.z;
     s->cd[slot] = d;
     s->cside[slot] = (A & 0xff) | ((B & 0xff) << 8) | ((gA & 0xff) << 16) | ((gB & 0xff) << 24);
   }
 
-  __device__ void collide() {
+  __device__ __forceinline__ void collide() {
     const int cap = p->max_contacts < MC ? p->max_contacts : MC;
     const float off = p->contact_offset;
     int base = 0;
@@ -1619,7 +1631,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- constraint rows
-  __device__ void build_rows() {
+  __device__ __forceinline__ void build_rows() {
     const int ncon = ncr;
     for (int c = tl; c < ncon; c += T) {
       V3 n = ld3(s->cn[c]), pt = ld3(s->cp[c]), t1, t2;
@@ -1670,7 +1682,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- one substep
-  __device__ void substep() {
+  __device__ __forceinline__ void substep() {
     ph_mark(15);
     fk();
     set_axis();
@@ -1828,7 +1840,7 @@ struct Team {
     ph_mark(7);
   }
 
-  __device__ void integrate() {
+  __device__ __forceinline__ void integrate() {
     // root pose (lane 0 gathers the twist from lanes 0..5)
     float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
     float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
@@ -1883,7 +1895,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- sensors & DOF forces (last substep)
-  __device__ void outputs(float* sens_out, float* dforce_out) {
+  __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out) {
     fk();  // post-step pose for the sensor body frames
     const int NS = m->num_sensors;
     if (sens_out && tl < NS) {
@@ -1929,7 +1941,7 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- state I/O (gym layouts)
-  __device__ void load(const float* root, const float* dof, const float* act_tau, const float* orow = nullptr,
+  __device__ __forceinline__ void load(const float* root, const float* dof, const float* act_tau, const float* orow = nullptr,
                        const float* tg = nullptr) {
     // root pose/twist: every lane reads the 13 floats (one cache line pair per actor)
     if (tl == 0) {
@@ -1965,7 +1977,7 @@ struct Team {
   }
 
   // writes the post-step state into the team's LDS staging (root[13], dof[2 nD])
-  __device__ void stage_state() {
+  __device__ __forceinline__ void stage_state() {
     float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
     float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
     if (tl == 0) {
@@ -1998,7 +2010,7 @@ struct Team {
 
   // gym rigid-body state of articulation body `b` (post-step FK in LDS): body-origin pose, COM linear
   // velocity, angular velocity (oracle body_states)
-  __device__ void body_state(int b, float* o) const {
+  __device__ __forceinline__ void body_state(int b, float* o) const {
     const int nd = m->body_node[b];
     M3 Rn;
     for (int a = 0; a < 3; a++)
