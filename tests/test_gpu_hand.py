@@ -17,6 +17,7 @@ import numpy as np
 import pytest
 import torch
 
+import parity_stats as PS
 import pyoracle as O
 from migym import _abi, configs, model as M, taskdefs
 from test_oracle_golden import HAND_TRACES, hand_noise, hand_trace_setup
@@ -202,14 +203,28 @@ def _physics_vs_oracle(lib, spec, sp, h, rng, n):
     assert np.isfinite(rg).all() and np.isfinite(dg).all()
     np.testing.assert_array_equal(rg[:, 0], h.root[:, 0])       # fixed hand root untouched
     np.testing.assert_array_equal(rg[:, 2], h.root[:, 2])       # goal actor untouched
-    assert env_agreement(rg[:, 1, 0:7], h.root[:, 1, 0:7], 2e-4, 0) >= 0.97
-    assert env_agreement(rg[:, 1, 7:13], h.root[:, 1, 7:13], 2e-3, 2e-3) >= 0.97
-    assert env_agreement(dg[..., 0], h.dof[..., 0], 2e-4, 0) >= 0.97
-    assert env_agreement(dg[..., 1], h.dof[..., 1], 2e-3, 2e-3) >= 0.97
-    assert env_agreement(np_(e.dof_force), h.dof_force, 1e-2, 1e-2) >= 0.97
-    assert env_agreement(np_(e.rbs), h.rbs, 2e-3, 2e-3) >= 0.97
+    # every env must agree, unless it sits at a discontinuity of the physics (contact offset, joint-limit
+    # margin, drive saturation: tests/parity_stats.py); the error statistics go to MIGYM_PARITY_REPORT
+    test = os.environ.get("PYTEST_CURRENT_TEST", "hand").split(" ")[0]
     scale = max(1.0, np.abs(h.sensors).max())
-    assert env_agreement(np_(e.sensors), h.sensors, 1e-2 * scale, 0) >= 0.97
+    checks = [("object pose", rg[:, 1, 0:7], h.root[:, 1, 0:7], 2e-4, 0), ("object twist", rg[:, 1, 7:13], h.root[:, 1, 7:13], 2e-3, 2e-3),
+              ("dof pos", dg[..., 0], h.dof[..., 0], 2e-4, 0), ("dof vel", dg[..., 1], h.dof[..., 1], 2e-3, 2e-3),
+              ("dof force", np_(e.dof_force), h.dof_force, 1e-2, 1e-2), ("rigid bodies", np_(e.rbs), h.rbs, 2e-3, 2e-3),
+              ("sensors", np_(e.sensors), h.sensors, 1e-2 * scale, 0)]
+    bad = np.zeros(n, bool)
+    for name, a, b, atol, rtol in checks:
+        eb = PS.env_bad(a, b, atol, rtol)
+        PS.record(test, name, a, b, envs_outside=int(eb.sum()), atol=atol, rtol=rtol)
+        bad |= eb
+    if bad.any():
+        mnp0 = M.pack_model(spec)
+        lo, hi = np.array([x.lower for x in spec.nodes[1:]]), np.array([x.upper for x in spec.nodes[1:]])
+        kp, bd = np.array([x.drive_kp for x in spec.nodes[1:]]), np.array([x.damping for x in spec.nodes[1:]])
+        eff = np.array([x.effort_limit for x in spec.nodes[1:]])
+        why = (PS.contact_flips(mnp0, sp, h0.root, h0.dof, 1e-4) | PS.limit_flips(h0.dof[..., 0], lo, hi, sp.limit_margin)
+               | PS.drive_flips(h0.dof[..., 0], h0.dof[..., 1], h0.targets, kp, bd, eff)
+               | PS.deep_contacts(mnp0, sp, h0.root, h0.dof))
+        PS.assert_explained(bad, why, test)
     return mnp, h0
 
 
@@ -267,8 +282,9 @@ def test_hand_physics_near_forearm_matches_oracle(lib, kind):
 
 @pytest.mark.parametrize("kind", ["block", "egg", "pen"])
 def test_hand_fused_env_step_matches_oracle(lib, kind):
-    """mg_env_step (the bench path) vs orc_hand_env_step over 3 control steps, device RNG resets (pen:
-    randomize_rotation_pen, ignore_z_rot success tolerance)."""
+    """mg_env_step (the bench path) vs orc_hand_env_step over 12 control steps (the block and the egg start
+    0.1 m above the palm and land on it after ~9), device RNG resets (pen: randomize_rotation_pen, ignore_z_rot
+    success tolerance)."""
     spec, sp, tp = setup(kind=kind)
     n = 192
     h = O.HandHostEnv(tp, spec, n)
@@ -278,21 +294,46 @@ def test_hand_fused_env_step_matches_oracle(lib, kind):
     _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
     _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
     rng = np.random.default_rng(3)
-    for t in range(3):
+    pre, acts = [], []
+    for t in range(12):
         a = rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32)
+        acts.append(a)
         h.actions[:] = a
         e.actions.copy_(T(a))
+        pre.append(copy.deepcopy(h))
         h.env_step(mnp, sp, tp, seed=5, step=t, threads=8)
         _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=5, step=t)), stream()), lib)
     torch.cuda.synchronize()
     lib.mg_sim_destroy(sim)
     np.testing.assert_array_equal(np_(e.progress), h.progress)
-    assert (np_(e.reset) == h.reset).mean() >= 0.97
     np.testing.assert_allclose(np_(e.targets), h.targets, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(np_(e.prev_targets), h.prev_targets, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(np_(e.goal_states), h.goal_states, rtol=1e-5, atol=1e-6)
-    assert env_agreement(np_(e.obs), h.obs, 2e-2, 2e-2) >= 0.97
-    assert env_agreement(np_(e.rew), h.rew, 5e-2, 5e-2) >= 0.97
+    # every env: obs within 2e-3 + 2e-3 |x|, reward within 5e-3, same reset -- unless one of the steps
+    # started at a discontinuity (tests/parity_stats.py)
+    test = f"test_hand_fused_env_step_matches_oracle[{kind}]"
+    bad_o = PS.env_bad(np_(e.obs), h.obs, 2e-3, 2e-3)
+    bad_r = PS.env_bad(np_(e.rew)[:, None], h.rew[:, None], 5e-3, 5e-3)
+    bad_d = np_(e.reset) != h.reset
+    ncon = sum(len(O.contacts(mnp, sp, h.root[i].ravel(), h.dof[i], 64)) > 0 for i in range(n))
+    PS.record(test, "obs (12 steps)", np_(e.obs), h.obs, envs_outside=int(bad_o.sum()), envs_in_contact=int(ncon))
+    PS.record(test, "rew (12 steps)", np_(e.rew), h.rew, envs_outside=int(bad_r.sum()), reset_differs=int(bad_d.sum()))
+    assert ncon >= n // 2   # the objects are on the hand by now
+    bad = bad_o | bad_r | bad_d
+    if bad.any():
+        lo, hi = np.array([x.lower for x in spec.nodes[1:]]), np.array([x.upper for x in spec.nodes[1:]])
+        kp, bd = np.array([x.drive_kp for x in spec.nodes[1:]]), np.array([x.damping for x in spec.nodes[1:]])
+        eff = np.array([x.effort_limit for x in spec.nodes[1:]])
+        why = np.zeros(n, bool)
+        for q in pre:
+            why |= (PS.contact_flips(mnp, sp, q.root, q.dof, 1e-4) | PS.limit_flips(q.dof[..., 0], lo, hi, sp.limit_margin)
+                    | PS.drive_flips(q.dof[..., 0], q.dof[..., 1], q.targets, kp, bd, eff)
+                    | PS.deep_contacts(mnp, sp, q.root, q.dof))
+        og = np_(e.obs)
+        for i in np.flatnonzero(bad & ~why):
+            why[i] = PS.oracle_sensitive(mnp, sp, tp, pre, acts, i, og[i], h.obs[i], seed=5, hand=True)
+        PS.record(test, "explained", og[bad], h.obs[bad], disagreeing=int(bad.sum()), explained=int((bad & why).sum()))
+        PS.assert_explained(bad, why, test)
     np.testing.assert_allclose(np_(e.cons), h.cons, atol=2e-2)
 
 
