@@ -40,7 +40,7 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(task, seconds=10.0, n=65536):
+def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
     """The oracle's fp32 restatement of the same step (oracle/build/liboracle_f32.so: fp32 physics, fp32 task
     layer, OpenMP over envs), timed on this box's host cores at the workload's own env count on a bounded
     sample of steps: once with every thread this process may use (OMP_NUM_THREADS, the box's CPU share for
@@ -55,7 +55,9 @@ def cpu_baseline(task, seconds=10.0, n=65536):
     cfg = configs.task_config(task, n)
     base = "Ant" if task == "MAAnt" else task
     A = int(cfg["env"].get("numAgents", 1)) if task == "MAAnt" else 1
-    spec = taskdefs.hand_spec("block") if task == "ShadowHand" else M.load_builtin(taskdefs.TASK_INFO[base][1])
+    if task == "ShadowHand":
+        cfg["env"]["objectType"] = object_type
+    spec = taskdefs.hand_spec(object_type) if task == "ShadowHand" else M.load_builtin(taskdefs.TASK_INFO[base][1])
     sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[base][5], A)
     tp = taskdefs.task_params(task, cfg, spec)
     mnp = M.pack_model(spec)
@@ -83,14 +85,15 @@ def cpu_baseline(task, seconds=10.0, n=65536):
             "single_core": {"value": v1, "unit": "env-steps/s", "cores": 1, "sample": smp1}}
 
 
-def pmc_traffic(task, n, kern_ms):
+def pmc_traffic(task, n, kern_ms, object_type="block"):
     """Measured HBM traffic of the dominant kernel for this workload, from the committed rocprofv3 --pmc
     passes of the same bench command (tools/gpu_prof.sh -> tools/pmc_summary.py --json): FETCH_SIZE x2
     (gfx950 correction) + WRITE_SIZE per launch, expressed over this run's launch time like `achieved`.
     None when no pass was recorded for this workload."""
     path = None
+    tag = task if (task != "ShadowHand" or object_type == "block") else f"{task}-{object_type}"   # per kernel instance
     for rnd in ("r02", "r01"):   # the newest round's passes of this workload
-        cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{task}_{n}.json")
+        cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_{n}.json")
         if os.path.exists(cand):
             path = cand
             break
@@ -217,14 +220,14 @@ def main():
                        "parallelism": f"env-sharded x{world}",
                        **({"object_type": args.object_type} if args.task == "ShadowHand" else {})},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms),
+                         "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms, args.object_type),
                          "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",
                          "kernel_ms": kern_ms,
                          "algo_bytes_per_env_step": ALGO_BYTES[args.task]},
         }
         if not args.no_cpu_baseline and world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n)
+                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n, args.object_type)
             except Exception as ex:  # noqa: BLE001
                 out["cpu_baseline"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
