@@ -25,6 +25,18 @@ Supported actor properties (everything the shipped task configs randomize):
   color                ignored (no renderer)
 Anything else raises ``NotImplementedError`` at setup.
 
+External samples (vec_task.py:566-604, 736-760, 832-840): ``get_actor_params_info`` lists the randomized
+actor parameters (values of an env's row, names ``<prop>_<element>_<attr>[_<dof>]``, uniform ranges or
++-inf) in the reference's draw order, and an ``actor_params_generator`` (any object with ``sample()``
+returning one flat vector of that length per env) replaces the per-attribute draws of every env being
+randomized: the value is scheduled like dr_utils.generate_random_samples' ``extern_sample`` branch and
+applied with the attribute's operation and buckets.  The reference resolves the vector's slices with a
+helper it never defines (``get_attr_val_from_sample`` is not in its tree), so the slicing here is this
+build's: the vector has get_actor_params_info's length and order (a generator sized from it fits), the
+entries of setup_only attributes are ignored after setup, and a vector of any other length raises.  The
+generator path needs the host to know which envs are randomized, so it costs one synchronisation per
+resetting step (like ``dr_exact_trigger``).
+
 The reference evaluates apply_randomizations only on steps where some env resets; without a host
 synchronisation this build evaluates it every step (identical once any env resets each step, which is
 the case at the benchmark sizes).  ``VecTask.dr_exact_trigger = True`` restores the reference's rule
@@ -244,6 +256,8 @@ class DomainRandomizationMixin:
         offsets = tuple(int(x) for x in offs)
         actors = dict(self.dr_actor_names)
         descs, attrs, names = build_actor_attrs(dr.get("actor_params", {}), actors, spec, offsets)
+        self._dr_offsets = offsets
+        self._dr_attrs = attrs
         row = np.zeros(stride, np.float32)
         _abi.check(self._lib.mg_env_props_defaults(self._model_np.ctypes.data, row.ctypes.data), self._lib)
         dev = self.device
@@ -298,11 +312,81 @@ class DomainRandomizationMixin:
             a.reset_mask = None if reset_mask is None else reset_mask.data_ptr()
             a.randomize_buf = self.randomize_buf_actors.data_ptr()
             smp = d["samples"]
+            if smp is None and self.actor_params_generator is not None and not self.first_randomization:
+                smp = self._extern_samples(dr_params, reset_mask, increment, int(rand_freq))
             a.samples = None if smp is None else smp.data_ptr()
             a.seed, a.counter, a.env_offset = self.seed, d["calls"], self.env_offset * self.num_agents
             _abi.check(self._lib.mg_dr_apply(_abi.C.byref(a), self._stream()), self._lib)
             d["calls"] += 1
         self.first_randomization = False
+
+    def get_actor_params_info(self, dr_params: Dict[str, Any], env: int = 0):
+        """vec_task.py:566-604: (params, names, lows, highs) of the randomized actor attributes, one entry per
+        element in the reference's order; ``params`` are env ``env``'s current values (its first actor's
+        env_props row).  lows / highs: the range for uniform / loguniform draws, +-inf otherwise."""
+        if "actor_params" not in dr_params:
+            return None
+        _, attrs, names = build_actor_attrs(dr_params["actor_params"], dict(self.dr_actor_names), self.model_spec,
+                                            self._dr_offsets)
+        row = self.env_props[env * self.num_agents].cpu().numpy() if self._dr is not None else None
+        params, out_names, lows, highs = [], [], [], []
+        for (slot, _, og), (actor, prop, elem, attr) in zip(attrs, names):
+            if prop == "scale":
+                continue
+            rp = dr_params["actor_params"][actor][prop][attr]
+            if prop == "dof_properties":
+                out_names.append(f"{prop}_0_{attr}_{elem}")
+            else:
+                out_names.append(f"{prop}_{elem}_{attr}")
+            params.append(float(row[slot]) if (row is not None and slot is not None) else float(og))
+            lo, hi = rp["range"] if "uniform" in rp["distribution"] else (-float("inf"), float("inf"))
+            lows.append(lo)
+            highs.append(hi)
+        return params, out_names, lows, highs
+
+    def _extern_layout(self, dr_params):
+        """per live attribute column: (index into the extern vector or -1 for a setup_only attribute, schedule
+        scale, op is scaling), and the vector length (get_actor_params_info's)"""
+        names = self._dr_names
+        pos, n = {}, 0
+        for j, (actor, prop, elem, attr) in enumerate(names):
+            if prop == "scale":
+                continue
+            if not dr_params["actor_params"][actor][prop][attr].get("setup_only", False):
+                pos[j] = n
+            n += 1
+        cols = []
+        for j in self._dr_live:
+            actor, prop, elem, attr = names[j]
+            rp = dr_params["actor_params"][actor][prop][attr] if prop != "scale" else dr_params["actor_params"][actor][prop]
+            cols.append((pos.get(j, -1), sched_scaling(rp, self.last_step), rp["operation"] == "scaling"))
+        return cols, n
+
+    def _extern_samples(self, dr_params, reset_mask, increment, freq) -> torch.Tensor:
+        """vec_task.py:736-760: actor_params_generator.sample() for every env the kernel will randomize on
+        this call (randomize_buf >= frequency on a resetting env), scheduled as dr_utils' extern_sample
+        branch, as the (num_actors, live attributes) sample table mg_dr_apply reads."""
+        cols, n = self._extern_layout(dr_params)
+        rb = self.randomize_buf_actors + (1 if increment else 0)
+        doit = (rb >= freq) & (reset_mask != 0)
+        ids = torch.nonzero(doit).flatten().cpu().numpy()
+        smp = np.zeros((self.num_actors, max(len(cols), 1)), np.float32)
+        env_ids = np.unique(ids // self.num_agents)
+        ext = np.zeros((len(env_ids), n), np.float64)
+        for k, env_id in enumerate(env_ids):
+            v = np.asarray(self.actor_params_generator.sample(), np.float64).ravel()
+            if v.shape[0] != n:
+                raise Exception(f"Invalid extern_sample size: env {env_id} needs {n} values, got {v.shape[0]}")
+            self.extern_actor_params[int(env_id)] = v
+            ext[k] = v
+        row = np.searchsorted(env_ids, ids // self.num_agents)
+        for i, (p, s, scaling) in enumerate(cols):
+            if p >= 0:
+                x = ext[row, p]
+                smp[ids, i] = x * s + (1.0 - s) if scaling else x * s
+        t = torch.from_numpy(smp).to(self.device)
+        self._dr_extern_keep = t          # alive until the kernel has read it (stream order)
+        return t
 
     def _dr_nonphysical(self, name, p):
         """vec_task.py:646-720: the noise parameters after the schedule; the correlated noise is redrawn."""

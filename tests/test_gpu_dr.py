@@ -202,3 +202,68 @@ def test_make_with_randomize(task, n):
     if task == "ShadowHand":   # gravity noise without a schedule (Humanoid's starts at scale 0)
         assert tuple(env.sim_params.gravity) != (0.0, 0.0, -9.81)
     env.close()
+
+
+class _Gen:
+    """actor_params_generator stand-in: a known vector per call (vec_task.py:736-760)"""
+
+    def __init__(self, n):
+        self.n, self.calls = n, 0
+
+    def sample(self):
+        self.calls += 1
+        return 1.0 + 0.01 * np.arange(self.n) + 0.1 * self.calls
+
+
+def test_actor_params_generator_ant():
+    """get_actor_params_info + actor_params_generator: the randomized envs take og * sample (scaling) /
+    og + sample (additive) from the generator's vector, setup_only entries (mass) are ignored, the other
+    envs keep their rows, and a vector of the wrong length raises."""
+    import migym
+    n = 64
+    cfg = configs.task_config("Ant", n, sim_device=DEV)
+    cfg["task"]["randomize"] = True
+    env = migym.make(seed=3, task="Ant", num_envs=n, sim_device=DEV, rl_device=DEV, headless=True, cfg={"task": cfg})
+    dr = env.randomization_params
+    params, names, lows, highs = env.get_actor_params_info(dr, 5)
+    assert len(params) == len(names) == len(lows) == len(highs)
+    nd = env.num_dof
+    assert "dof_properties_0_damping_0" in names and f"dof_properties_0_damping_{nd - 1}" in names
+    assert "rigid_body_properties_0_mass" in names
+    i_lo = names.index("dof_properties_0_lower_0")
+    assert lows[i_lo] == -np.inf and highs[i_lo] == np.inf          # gaussian: unbounded
+    i_d = names.index("dof_properties_0_damping_3")
+    assert (lows[i_d], highs[i_d]) == (0.5, 1.5)
+    spec = env.model_spec
+    base = defaults(spec)
+    stride, offs = layout(spec)
+    assert params[i_d] == pytest.approx(float(env.env_props[5, offs[0] + 8 * 4 + 2]), rel=0, abs=0)
+    before = env.env_props.clone()
+    gen = _Gen(len(names))
+    env.actor_params_generator = gen
+    ids = torch.tensor([2, 9, 40], device=DEV)
+    mask = torch.zeros(n, dtype=torch.long, device=DEV)
+    mask[ids] = 1
+    env.randomize_buf_actors[:] = 10 ** 6
+    env.apply_randomizations(dr, reset_mask=mask, increment=False)
+    torch.cuda.synchronize()
+    assert gen.calls == 3 and sorted(env.extern_actor_params) == [2, 9, 40]
+    props = env.env_props.cpu().numpy()
+    keep = np.ones(n, bool)
+    keep[ids.cpu().numpy()] = False
+    assert np.array_equal(props[keep], before.cpu().numpy()[keep])
+    for e in (2, 9, 40):
+        ext = env.extern_actor_params[e]
+        for d in range(nd):
+            col = offs[0] + 8 * (d + 1)
+            j = names.index(f"dof_properties_0_damping_{d}")
+            assert props[e, col + 2] == pytest.approx(base[col + 2] * ext[j], rel=1e-6, abs=1e-7)
+            j = names.index(f"dof_properties_0_lower_{d}")
+            assert props[e, col + 4] == pytest.approx(base[col + 4] + ext[j], rel=1e-6, abs=1e-6)
+        # mass is setup_only: unchanged by the generator
+        assert np.array_equal(props[e, offs[0]::8][:len(spec.nodes)], before.cpu().numpy()[e, offs[0]::8][:len(spec.nodes)])
+    env.actor_params_generator = _Gen(len(names) + 1)
+    env.randomize_buf_actors[:] = 10 ** 6      # the call above restarted the randomized envs' counters
+    with pytest.raises(Exception, match="extern_sample size"):
+        env.apply_randomizations(dr, reset_mask=mask, increment=False)
+    env.close()
