@@ -140,6 +140,9 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #ifndef MG_PGS_EARLY
 #define MG_PGS_EARLY 1  // issue a block's private J/Y loads one whole block ahead (compiler barrier)
 #endif
+#ifndef MG_DROP_TREE
+#define MG_DROP_TREE 1  // free the tree phases' per-lane state before the PGS sweeps (drop_tree_state)
+#endif
 #ifndef MG_PGS_JY2
 #define MG_PGS_JY2 0  // rows' (J, Y) private columns interleaved as float2
 #endif
@@ -1767,6 +1770,9 @@ struct Team {
     // (so a row's impulse is never read ahead of its previous visit's write, and the unrolled loop
     // needs no per-visit guards): the padding rows have J = Y = 0 and 1/W = 0, i.e. they are skipped
     // as the oracle skips W = 0 rows.
+#if MG_DROP_TREE
+    drop_tree_state();
+#endif
     constexpr int PF = MG_PGS_PREFETCH;
     static_assert(MR % PF == 0, "row capacity must be a multiple of the PGS prefetch depth");
     const int prow = wave_rows == 0 ? 0 : ((wave_rows + PF - 1) / PF) * PF;
@@ -1838,6 +1844,20 @@ struct Team {
     ph_mark(6);
     integrate();
     ph_mark(7);
+  }
+
+  // The tree phases assign R, x, S, V, c, U, pA, IA, D^-1, u only on the lanes of the level being
+  // processed, so without help the compiler keeps every lane's previous value alive across the whole
+  // substep loop.  None is read again before the next substep's fk()/aba() rewrite them (outputs()
+  // reruns fk()), so they are set to constants once the rows are built: their registers are free
+  // for the PGS sweep.
+  __device__ __forceinline__ void drop_tree_state() {
+    R = M3{};
+    x = v3(0, 0, 0);
+    S = V = c = U = pA = szero();
+    IA = Sym6{};
+    Dinv = u = 0.0f;
+    for (int k = 0; k < 6; k++) Sl[k] = 0.0f;
   }
 
   __device__ __forceinline__ void integrate() {
