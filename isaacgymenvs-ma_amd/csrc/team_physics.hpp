@@ -143,8 +143,8 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #ifndef MG_DROP_TREE
 #define MG_DROP_TREE 1  // free the tree phases' per-lane state before the PGS sweeps (drop_tree_state)
 #endif
-#ifndef MG_PGS_JY2
-#define MG_PGS_JY2 0  // rows' (J, Y) private columns interleaved as float2
+#ifndef MG_JY_REGS
+#define MG_JY_REGS 16  // rows of (J, Y) columns kept in registers; the rest in private (scratch) arrays
 #endif
 #ifndef MG_RB_WIDE
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
@@ -154,7 +154,9 @@ template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + MG_PGS_PREFETCH - 1) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;
-  static constexpr int RB = (T >= 32 && !OBJ) ? MG_RB_WIDE : 6;  // right-hand sides per test solve (rows of 2-4 contacts)
+  static constexpr int RB = (T >= 32 && !OBJ) ? MG_RB_WIDE : 6;
+  // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
+  static constexpr int KR = (MG_JY_REGS < MR ? MG_JY_REGS : MR) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -1723,18 +1725,20 @@ struct Team {
         }
       }
     }
-#if MG_PGS_JY2
-    // (J, Y) of a row interleaved: one 8-byte private load per visit instead of two 4-byte ones
-    float2 JYcol[MR];
-#define MG_JSET(r, j, y) (JYcol[r] = make_float2((j), (y)))
-#define MG_JGET(r) (JYcol[r].x)
-#define MG_YGET(r) (JYcol[r].y)
-#else
-    float Jcol[MR], Ycol[MR];
-#define MG_JSET(r, j, y) (Jcol[r] = (j), Ycol[r] = (y))
-#define MG_JGET(r) (Jcol[r])
-#define MG_YGET(r) (Ycol[r])
-#endif
+    // (J_r[j], Y_r[j]) of the first KR rows live in registers (the index is wave-uniform, so the compiler
+    // promotes the arrays to VGPRs and addresses them with relative moves); the remaining rows are
+    // private arrays in scratch.  Wave-uniform branches pick the side.
+    constexpr int KR = L::KR;
+    float Jr[KR > 0 ? KR : 1], Yr[KR > 0 ? KR : 1];
+    float Js[MR - KR > 0 ? MR - KR : 1], Ys[MR - KR > 0 ? MR - KR : 1];
+#define MG_JSET(r, j, y)                 \
+  do {                                   \
+    if ((r) < KR) {                      \
+      Jr[r] = (j); Yr[r] = (y);          \
+    } else {                             \
+      Js[(r) - KR] = (j); Ys[(r) - KR] = (y); \
+    }                                    \
+  } while (0)
     for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
       float jb[L::RB], yb[L::RB];
 #pragma unroll
@@ -1788,50 +1792,81 @@ struct Team {
     // occupant's last use.  The friction bound uses the contact's normal impulse of this sweep (the
     // normal row precedes its two friction rows), carried in a register.  Every lane of the team
     // computes the same impulse, so all of them store it (no exec-mask switch per visit).
+    // Rows below KR take their (J, Y) from registers in a fully unrolled part A (static indices; the LDS
+    // row records are loaded one block ahead); the rows from KR on run part B, whose scratch columns and
+    // row records rotate through PF registers loaded a block ahead and wrap into the next sweep's part B.
+    float lamn = 0.0f;
+    auto visit = [&](float J, float Y, const typename L::Row& R, int r) {
+      const float v = team_sum<T>(J * nu, tb);
+      const float lam = R.lam, m = R.mu;
+      // friction rows (m = mu >= 0): [-mu lambda_n, mu lambda_n]; normal / limit rows (m < 0):
+      // [0, inf).  Rows with 1/W = 0 keep lambda = 0: lam + (b - v) * 0 = 0 clamps to 0.
+      const bool fric = m >= 0.0f;
+      const float t = fric ? m * lamn : 0.0f;
+      const float hi = fric ? t : __builtin_inff();
+      const float lnew = __builtin_amdgcn_fmed3f(lam + (R.b - v) * R.iw, -t, hi);
+      lamn = m == -1.0f ? lnew : lamn;
+      s->u.sv.rows[r].lam = lnew;
+      nu += Y * (lnew - lam);
+    };
+    const int pa = prow < KR ? prow : KR;  // rows of part A
     float pJ[PF], pY[PF];
     typename L::Row pR[PF];
-    if (prow > 0) {
+    if (prow > KR) {
 #pragma unroll
       for (int k = 0; k < PF; k++) {
-        pJ[k] = MG_JGET(k);
-        pY[k] = MG_YGET(k);
-        pR[k] = s->u.sv.rows[k];
+        pJ[k] = Js[k];
+        pY[k] = Ys[k];
+        pR[k] = s->u.sv.rows[KR + k];
       }
     }
-    float lamn = 0.0f;
     for (int it = 0; it < p->pos_iters; it++) {
-      for (int r0 = 0; r0 < prow; r0 += PF) {
-        const int rn = r0 + PF == prow ? 0 : r0 + PF;  // next block of rows (wraps into the next sweep)
+      if constexpr (KR > 0) {
+        typename L::Row cR[PF];
+        if (pa > 0) {
+#pragma unroll
+          for (int k = 0; k < PF; k++) cR[k] = s->u.sv.rows[k];
+        }
+#pragma unroll
+        for (int r0 = 0; r0 < KR; r0 += PF) {
+          if (r0 < pa) {
+            typename L::Row nR[PF];
+            const bool more = r0 + PF < pa;
+            if (more) {
+#pragma unroll
+              for (int k = 0; k < PF; k++) nR[k] = s->u.sv.rows[r0 + PF + k];
+            }
+#pragma unroll
+            for (int k = 0; k < PF; k++) visit(Jr[r0 + k], Yr[r0 + k], cR[k], r0 + k);
+            if (more) {
+#pragma unroll
+              for (int k = 0; k < PF; k++) cR[k] = nR[k];
+            }
+          }
+        }
+      }
+      for (int r0 = KR; r0 < prow; r0 += PF) {
+        const int rn = r0 + PF == prow ? KR : r0 + PF;  // next block of part B (wraps into the next sweep)
 #if MG_PGS_EARLY
         // the next block's private J/Y (scratch, L2 latency) are issued before this block's visits; the
         // compiler barrier keeps the scheduler from sinking them behind the first visits
         float nJ[PF], nY[PF];
 #pragma unroll
         for (int k = 0; k < PF; k++) {
-          nJ[k] = MG_JGET(rn + k);
-          nY[k] = MG_YGET(rn + k);
+          nJ[k] = Js[rn - KR + k];
+          nY[k] = Ys[rn - KR + k];
         }
         asm volatile("" ::: "memory");
 #endif
 #pragma unroll
         for (int k = 0; k < PF; k++) {
-          const float v = team_sum<T>(pJ[k] * nu, tb);
-          const float lam = pR[k].lam, m = pR[k].mu;
-          // friction rows (m = mu >= 0): [-mu lambda_n, mu lambda_n]; normal / limit rows (m < 0):
-          // [0, inf).  Rows with 1/W = 0 keep lambda = 0: lam + (b - v) * 0 = 0 clamps to 0.
-          const bool fric = m >= 0.0f;
-          const float t = fric ? m * lamn : 0.0f;
-          const float hi = fric ? t : __builtin_inff();
-          const float lnew = __builtin_amdgcn_fmed3f(lam + (pR[k].b - v) * pR[k].iw, -t, hi);
-          lamn = m == -1.0f ? lnew : lamn;
-          s->u.sv.rows[r0 + k].lam = lnew;
-          nu += pY[k] * (lnew - lam);
+          visit(pJ[k], pY[k], pR[k], r0 + k);
 #if MG_PGS_EARLY
           pJ[k] = nJ[k];
           pY[k] = nY[k];
 #else
-          pJ[k] = MG_JGET(rn + k);
-          pY[k] = MG_YGET(rn + k);
+          pJ[k] = Js[rn - KR + k];
+          pY[k] = Ys[rn - KR + k];
 #endif
           pR[k] = s->u.sv.rows[rn + k];
         }
@@ -1839,8 +1874,6 @@ struct Team {
     }
     wsync();
 #undef MG_JSET
-#undef MG_JGET
-#undef MG_YGET
     ph_mark(6);
     integrate();
     ph_mark(7);
