@@ -1422,35 +1422,56 @@ struct Team {
       }
       base += tot;
     }
-    // self-collision pairs: lane per pair, pair order preserved
+    // self-collision pairs, pair order preserved.  Pass 1, lane per pair: the bounding-sphere test of the
+    // two cores; the survivors' indices are compacted (team scan) into a list in the union storage behind
+    // the geom frames.  Pass 2, lane per survivor: the segment-segment narrowphase, so the divergent
+    // narrowphase runs over a few dense chunks instead of every chunk of pairs.
     const int P = mt->np;
+    static_assert(MN * 27 >= MG * GW + MP, "the pair list must fit behind the geom frames");
+    int* plist = reinterpret_cast<int*>(gw_tile() + GW * MG);
+    int npc = 0;
     for (int p0 = 0; p0 < P; p0 += T) {
       const int pi = p0 + tl;
+      int ok = 0;
+      if (pi < P) {
+        V3 a0, a1, b0, b1;
+        float ra, rb;
+        if (geom_segment(mt->pairs[pi][0], &a0, &a1, &ra) && geom_segment(mt->pairs[pi][1], &b0, &b1, &rb)) {
+          V3 ca = (a0 + a1) * 0.5f, cb = (b0 + b1) * 0.5f, dc = ca - cb;
+          float ha = sqrtf(dot(a1 - a0, a1 - a0)) * 0.5f, hb = sqrtf(dot(b1 - b0, b1 - b0)) * 0.5f;
+          float reach = ha + hb + ra + rb + off;
+          ok = dot(dc, dc) <= reach * reach ? 1 : 0;
+        }
+      }
+      const int incl = team_incl_scan<T>(ok);
+      if (ok) plist[npc + incl - 1] = pi;
+      npc += __shfl(incl, tb + T - 1);
+    }
+    wsync();
+    const int npw = __builtin_amdgcn_readfirstlane(wave_max<T>(npc));  // wave-uniform trip count
+    for (int c0 = 0; c0 < npw; c0 += T) {
+      const int ci = c0 + tl;
       int cnt = 0;
       V3 pt, nrm;
       float d = 0.0f;
       int ga = 0, gb = 0;
-      if (pi < P) {
+      if (ci < npc) {
+        const int pi = plist[ci];
         ga = mt->pairs[pi][0];
         gb = mt->pairs[pi][1];
         V3 a0, a1, b0, b1;
         float ra, rb;
-        if (geom_segment(ga, &a0, &a1, &ra) && geom_segment(gb, &b0, &b1, &rb)) {
-          V3 ca = (a0 + a1) * 0.5f, cb = (b0 + b1) * 0.5f, dc = ca - cb;
-          float ha = sqrtf(dot(a1 - a0, a1 - a0)) * 0.5f, hb = sqrtf(dot(b1 - b0, b1 - b0)) * 0.5f;
-          float reach = ha + hb + ra + rb + off;
-          if (dot(dc, dc) <= reach * reach) {
-            float ss, tt;
-            closest_seg_seg_t(a0, a1, b0, b1, &ss, &tt);
-            V3 pa = a0 + (a1 - a0) * ss, pb = b0 + (b1 - b0) * tt, dv = pa - pb;
-            float dist = sqrtf(dot(dv, dv));
-            d = dist - ra - rb;
-            if (d < off && dist > 1e-9f) {
-              nrm = dv * (1.0f / dist);
-              pt = ((pa - nrm * ra) + (pb + nrm * rb)) * 0.5f;
-              cnt = 1;
-            }
-          }
+        geom_segment(ga, &a0, &a1, &ra);
+        geom_segment(gb, &b0, &b1, &rb);
+        float ss, tt;
+        closest_seg_seg_t(a0, a1, b0, b1, &ss, &tt);
+        V3 pa = a0 + (a1 - a0) * ss, pb = b0 + (b1 - b0) * tt, dv = pa - pb;
+        float dist = sqrtf(dot(dv, dv));
+        d = dist - ra - rb;
+        if (d < off && dist > 1e-9f) {
+          nrm = dv * (1.0f / dist);
+          pt = ((pa - nrm * ra) + (pb + nrm * rb)) * 0.5f;
+          cnt = 1;
         }
       }
       const int incl = team_incl_scan<T>(cnt);

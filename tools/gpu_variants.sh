@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/var
 SPECS=${VAR_SPECS:-Ant:65536 Humanoid:32768 ShadowHand:16384}
-for lib in default isaacgymenvs-ma_amd/migym/_lib/var/*.so; do
+for lib in default $(ls isaacgymenvs-ma_amd/migym/_lib/var/*.so 2>/dev/null); do
   name=$(basename "$lib" .so)
   for spec in $SPECS; do
     t=${spec%%:*}; n=${spec##*:}
