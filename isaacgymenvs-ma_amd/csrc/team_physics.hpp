@@ -143,6 +143,9 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #ifndef MG_DROP_TREE
 #define MG_DROP_TREE 1  // free the tree phases' per-lane state before the PGS sweeps (drop_tree_state)
 #endif
+#ifndef MG_TS_LDS
+#define MG_TS_LDS 1  // test-solve forward pass: ancestors' y rows through LDS (0: one bpermute per column)
+#endif
 #ifndef MG_JY_REGS
 #define MG_JY_REGS 16  // rows of (J, Y) columns kept in registers; the rest in private (scratch) arrays
 #endif
@@ -968,6 +971,31 @@ struct Team {
     ph_mark(11);
     // proper ancestors below the root, visited in increasing depth (= increasing index)
     unsigned long long path = node > 0 ? (s->anc[node] & ~1ull & ~(1ull << node)) : 0ull;
+#if MG_TS_LDS
+    // the level's y values are published in the (now read) ut slab, RB floats per node, and every deeper
+    // lane reads its ancestor's row: a few wide LDS accesses per level instead of RB bpermutes
+    float* ybuf = &ts.ut[0][0];
+    static_assert(sizeof(ts.ut) >= sizeof(float) * L::RB * MN, "y rows must fit the ut slab");
+    wsync();
+    for (int lev = 1; lev <= maxdepth; lev++) {
+      if (node > 0 && depth == lev) {
+#pragma unroll
+        for (int q = 0; q < L::RB; q++) {
+          yv[q] = rem[q] * Dinv;
+          ybuf[L::RB * node + q] = yv[q];
+        }
+      }
+      wsync();
+      if (lev < maxdepth && node > 0 && depth > lev) {
+        const int an = __builtin_ctzll(path);
+        path &= path - 1;
+        const float C = dot(U, sv(ld3(s->S[an]), ld3(s->S[an] + 3)));
+        const float* ya = ybuf + L::RB * an;
+#pragma unroll
+        for (int q = 0; q < L::RB; q++) rem[q] -= C * ya[q];
+      }
+    }
+#else
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
 #pragma unroll
@@ -986,6 +1014,7 @@ struct Team {
         }
       }
     }
+#endif
     ph_mark(12);
 #pragma unroll
     for (int q = 0; q < L::RB; q++) {
