@@ -1,0 +1,59 @@
+"""GPU test of the 8-GPU sharding on one card (BASELINE configs 4 and 5).
+
+The multi-GPU configs run one process per GPU, each stepping the envs [rank * n, (rank + 1) * n) of the
+node with `env_offset = rank * n` (migym/utils/rlgames_utils.py): every random draw (reset noise,
+ShadowHand goal / object resets and random forces) is keyed by the global env / actor id, so a shard is
+the corresponding slice of one big rollout.  Here the full node-size rollout and rank shards run on the
+same GPU, with the same actions, and must agree bit for bit on obs, rew and reset at every step:
+
+  * MA-Ant, 65,536 envs x 4 agents, shards of 8,192 envs (ranks 0, 3 and 7 of 8);
+  * ShadowHand, 32,768 envs, shards of 4,096 (ranks 0 and 7 of 8);
+  * Ant, 65,536 envs, shards of 8,192 (rank 5).
+
+(The per-rank consecutive_successes mean is reduced across ranks by the dist layer and is not part of
+obs / rew / reset.)
+"""
+import pytest
+import torch
+
+import migym
+from migym import configs
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _make(task, n, offset):
+    cfg = configs.task_config(task, n, sim_device=DEV)
+    cfg["env_offset"] = offset
+    return migym.make(seed=11, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                      cfg={"task": cfg})
+
+
+@pytest.mark.parametrize("task,world,per_rank,ranks", [("MAAnt", 8, 8192, (0, 3, 7)),
+                                                        ("ShadowHand", 8, 4096, (0, 7)),
+                                                        ("Ant", 8, 8192, (5,))])
+def test_rank_shards_equal_slices_of_the_node_rollout(task, world, per_rank, ranks):
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    steps = 6
+    full = _make(task, world * per_rank, 0)
+    A = full.num_agents
+    g = torch.Generator(device=DEV).manual_seed(5)
+    acts = [torch.rand((full.num_actors, full.num_actions), device=DEV, generator=g) * 2.4 - 1.2 for _ in range(steps)]
+    ref = []
+    for a in acts:
+        obs, rew, reset, _ = full.step(a)
+        ref.append((obs["obs"].clone(), rew.clone(), reset.clone()))
+    full.close()
+    del full
+    for r in ranks:
+        sh = _make(task, per_rank, r * per_rank)
+        lo, hi = r * per_rank * A, (r + 1) * per_rank * A
+        for k, a in enumerate(acts):
+            obs, rew, reset, _ = sh.step(a[lo:hi].contiguous())
+            o, w, d = ref[k]
+            assert torch.equal(obs["obs"], o[lo:hi]), f"{task} rank {r} step {k}: obs differ"
+            assert torch.equal(rew, w[lo:hi]), f"{task} rank {r} step {k}: rew differ"
+            assert torch.equal(reset, d[lo:hi]), f"{task} rank {r} step {k}: reset differ"
+        assert int(d[lo:hi].sum()) >= 0
+        sh.close()
