@@ -37,6 +37,17 @@
 
 namespace mg {
 
+// The physics may contract a * b + c into FMAs (the oracle it is checked against is fp64; the task layer's
+// reference arithmetic in task.hpp / hand_task.hpp keeps contraction off).  The caller's FP state is
+// restored at the end of this header.
+#pragma float_control(push)
+#ifndef MG_PHYS_FMA
+#define MG_PHYS_FMA 1
+#endif
+#if MG_PHYS_FMA
+#pragma clang fp contract(fast)
+#endif
+
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
 // every per-node / per-geom constant is an LDS read (~64 cycles) instead of a dependent global load.
 // Rows padded to odd strides.  The image is built once on the host (build_tile, at mg_sim_create) and
@@ -281,6 +292,9 @@ __device__ __forceinline__ constexpr unsigned long long team_bits() {
 // end with bit-identical sums (fp add is commutative) and no broadcast is needed.
 template <int T>
 __device__ __forceinline__ float team_sum(float v, int) {
+  // no contraction into the butterfly: a lane's product fused into its first add would differ from the
+  // rounded product its partner receives, and the team's lanes would no longer hold identical sums
+#pragma clang fp contract(off)
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad xor 1
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad xor 2
   if (T >= 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
@@ -2132,5 +2146,7 @@ struct Team {
     o[10] = w.x; o[11] = w.y; o[12] = w.z;
   }
 };
+
+#pragma float_control(pop)
 
 }  // namespace mg
