@@ -144,6 +144,32 @@ __device__ __forceinline__ Sym6 body_inertia(float m, V3 c, const float* Ic) {
   I.c[0] = m; I.c[1] = 0; I.c[2] = 0; I.c[3] = m; I.c[4] = 0; I.c[5] = m;
   return I;
 }
+// reciprocal / square root / inverse square root of the physics: the 1-ulp hardware instructions instead
+// of the correctly rounded sequences (~10 instructions each); the task layer keeps IEEE division
+#ifndef MG_FAST_RCP
+#define MG_FAST_RCP 1
+#endif
+__device__ __forceinline__ float prcp(float x) {
+#if MG_FAST_RCP
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+__device__ __forceinline__ float psqrt(float x) {
+#if MG_FAST_RCP
+  return __builtin_amdgcn_sqrtf(x);
+#else
+  return sqrtf(x);
+#endif
+}
+__device__ __forceinline__ float prsq(float x) {
+#if MG_FAST_RCP
+  return __builtin_amdgcn_rsqf(x);
+#else
+  return 1.0f / sqrtf(x);
+#endif
+}
 // Cholesky of a Sym6 into a packed lower-triangular 6x6 (21 floats); returns false if not SPD
 __device__ __forceinline__ bool chol6(const Sym6& I, float* L) {
   float M[6][6];
@@ -164,9 +190,9 @@ __device__ __forceinline__ bool chol6(const Sym6& I, float* L) {
 #pragma unroll
     for (int k = 0; k < j; k++) s -= M[j][k] * M[j][k];
     ok = ok && (s > 0.0f);
-    float d = sqrtf(fmaxf(s, 1e-30f));
+    float d = psqrt(fmaxf(s, 1e-30f));
     M[j][j] = d;
-    float inv = 1.0f / d;
+    float inv = prcp(d);
 #pragma unroll
     for (int i = j + 1; i < 6; i++) {
       float t = M[i][j];
@@ -190,7 +216,7 @@ __device__ __forceinline__ SV chol6_solve(const float* L, const SV& b) {
     float s = x[i];
 #pragma unroll
     for (int k = 0; k < i; k++) s -= L[i * (i + 1) / 2 + k] * x[k];
-    x[i] = s / L[i * (i + 1) / 2 + i];
+    x[i] = s * prcp(L[i * (i + 1) / 2 + i]);
   }
   // backward: L^T x = y
 #pragma unroll
@@ -198,7 +224,7 @@ __device__ __forceinline__ SV chol6_solve(const float* L, const SV& b) {
     float s = x[i];
 #pragma unroll
     for (int k = i + 1; k < 6; k++) s -= L[k * (k + 1) / 2 + i] * x[k];
-    x[i] = s / L[i * (i + 1) / 2 + i];
+    x[i] = s * prcp(L[i * (i + 1) / 2 + i]);
   }
   return sv(v3(x[0], x[1], x[2]), v3(x[3], x[4], x[5]));
 }

@@ -337,7 +337,7 @@ __device__ __forceinline__ int wave_max(int v) {
 __device__ __forceinline__ void tangent_basis_t(V3 n, V3* t1, V3* t2) {
   V3 a = fabsf(n.x) < 0.57735f ? v3(1, 0, 0) : v3(0, 1, 0);
   V3 t = cross(a, n);
-  t = t * (1.0f / sqrtf(dot(t, t)));
+  t = t * prsq(dot(t, t));
   *t1 = t;
   *t2 = cross(n, t);
 }
@@ -352,7 +352,7 @@ __device__ __forceinline__ float point_box(V3 p, V3 hb, V3* nb, V3* cb) {
   if (q.x != p.x || q.y != p.y || q.z != p.z) {
     V3 d = p - q;
     float l = sqrtf(dot(d, d));
-    *nb = d * (1.0f / l);
+    *nb = d * prcp(l);
     *cb = q;
     return l;
   }
@@ -759,7 +759,7 @@ struct Team {
           }
         }
         float D = dot(S, U) + np[1] + h * bb + h * h * kk;
-        Dinv = 1.0f / D;
+        Dinv = prcp(D);
         float t = tau + tadd + ttend - bb * nu - kk * (qj - ref + h * nu);
         u = t - dot(S, pA);
         Sym6 Ia = IA;
@@ -1243,7 +1243,7 @@ struct Team {
       const V3 qq = p0 + (p1 - p0) * tt, dv = w - qq;
       const float dl = sqrtf(dot(dv, dv));
       if (!(dl > 1e-9f)) return false;
-      *nrm = dv * (1.0f / dl);
+      *nrm = dv * prcp(dl);
       *pt = (w + (qq + *nrm * ro)) * 0.5f;
       *dist = dl - ro;
       return true;
@@ -1345,7 +1345,7 @@ struct Team {
       const V3 pa = a0 + (a1 - a0) * ss, pb = p0 + (p1 - p0) * tt, dv = pa - pb;
       const float dl = sqrtf(dot(dv, dv));
       if (!(dl > 1e-9f)) return false;
-      *nrm = dv * (1.0f / dl);
+      *nrm = dv * prcp(dl);
       *pt = ((pa - *nrm * r) + (pb + *nrm * ro)) * 0.5f;
       *dist = dl - r - ro;
       return true;
@@ -1513,7 +1513,7 @@ struct Team {
         float dist = sqrtf(dot(dv, dv));
         d = dist - ra - rb;
         if (d < off && dist > 1e-9f) {
-          nrm = dv * (1.0f / dist);
+          nrm = dv * prcp(dist);
           pt = ((pa - nrm * ra) + (pb + nrm * rb)) * 0.5f;
           cnt = 1;
         }
@@ -1703,13 +1703,14 @@ struct Team {
   // ---------------------------------------------------------------- constraint rows
   __device__ __forceinline__ void build_rows() {
     const int ncon = ncr;
+    const float ih = prcp(h);
     for (int c = tl; c < ncon; c += T) {
       V3 n = ld3(s->cn[c]), pt = ld3(s->cp[c]), t1, t2;
       tangent_basis_t(n, &t1, &t2);
       s->ct1[c][0] = t1.x; s->ct1[c][1] = t1.y; s->ct1[c][2] = t1.z;
       s->ct2[c][0] = t2.x; s->ct2[c][1] = t2.y; s->ct2[c][2] = t2.z;
       float deff = s->cd[c] - p->rest_offset;
-      float bn = deff >= 0.0f ? -deff / h : fminf(-p->baumgarte * deff / h, p->max_depen_vel);
+      float bn = deff >= 0.0f ? -deff * ih : fminf(-p->baumgarte * deff * ih, p->max_depen_vel);
       s->u.sv.rows[3 * c].b = bn;
       s->u.sv.rows[3 * c + 1].b = 0.0f;
       s->u.sv.rows[3 * c + 2].b = 0.0f;
@@ -1743,7 +1744,7 @@ struct Team {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
       float d = side == 0 ? dl : du;
-      s->u.sv.rows[3 * ncon + li].b = d >= 0.0f ? -d / h : fminf(-p->baumgarte * d / h, p->max_depen_vel);
+      s->u.sv.rows[3 * ncon + li].b = d >= 0.0f ? -d * ih : fminf(-p->baumgarte * d * ih, p->max_depen_vel);
       s->lmeta[li] = (2 + side) | (node << 4);
       li++;
     }
@@ -1824,7 +1825,7 @@ struct Team {
           const float Wr = team_sum<T>(J * y, tb);
           if (tl == 0) {
             typename L::Row& rw = s->u.sv.rows[r];
-            rw.iw = (active && Wr > 1e-12f) ? 1.0f / Wr : 0.0f;
+            rw.iw = (active && Wr > 1e-12f) ? prcp(Wr) : 0.0f;
             rw.lam = 0.0f;
             // DR: a contact's friction is the mean of its two shapes' (vec_task.py rigid_shape_properties)
             const float muc = (drg && contact) ? 0.5f * (gmu(cside(r / 3, 2)) + gmu(cside(r / 3, 3))) : p->friction;
@@ -1968,7 +1969,7 @@ struct Team {
       float wn = sqrtf(dot(om, om));
       float dq[4];
       if (wn * h > 1e-12f) {
-        float ha = 0.5f * wn * h, sn = sinf(ha) / wn;
+        float ha = 0.5f * wn * h, sn = sinf(ha) * prcp(wn);
         dq[0] = om.x * sn; dq[1] = om.y * sn; dq[2] = om.z * sn; dq[3] = cosf(ha);
       } else {
         dq[0] = 0.5f * h * om.x; dq[1] = 0.5f * h * om.y; dq[2] = 0.5f * h * om.z; dq[3] = 1.0f;
@@ -1979,7 +1980,7 @@ struct Team {
                      a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0],
                      a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3],
                      a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2]};
-      float l = 1.0f / sqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+      float l = prsq(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
       for (int k = 0; k < 4; k++) q0[k] = qn[k] * l;
       V3 dp = pn - p0;
       p0 = pn;
@@ -1995,7 +1996,7 @@ struct Team {
       const float wn = sqrtf(dot(om, om));
       float dq[4];
       if (wn * h > 1e-12f) {
-        const float ha = 0.5f * wn * h, sn = sinf(ha) / wn;
+        const float ha = 0.5f * wn * h, sn = sinf(ha) * prcp(wn);
         dq[0] = om.x * sn; dq[1] = om.y * sn; dq[2] = om.z * sn; dq[3] = cosf(ha);
       } else {
         dq[0] = 0.5f * h * om.x; dq[1] = 0.5f * h * om.y; dq[2] = 0.5f * h * om.z; dq[3] = 1.0f;
@@ -2006,7 +2007,7 @@ struct Team {
                      a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0],
                      a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3],
                      a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2]};
-      const float l = 1.0f / sqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+      const float l = prsq(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
       for (int k = 0; k < 4; k++) oq[k] = qn[k] * l;
       op = op + vc * h;
     }
