@@ -13,7 +13,9 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "build", "liboracle.so")
+# MG_ORACLE_LIB: an alternative build of the checker (the sanitizer build, `make sanitize`;
+# tests/test_oracle_sanitize.py runs the oracle tests against it)
+LIB = os.environ.get("MG_ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 sys.path.insert(0, os.path.join(HERE, "..", "isaacgymenvs-ma_amd"))
 from migym import _abi  # noqa: E402  (struct mirrors only)
 
