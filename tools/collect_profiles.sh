@@ -9,7 +9,7 @@ mkdir -p profiles/$R
 for f in gpurun_out/bench/*.json; do cp "$f" profiles/$R/; done
 cp gpurun_out/prof/trace_kernel_stats.csv profiles/$R/ant65536_kernel_stats.csv
 [ -f gpurun_out/rocprof_trace.log ] && cp gpurun_out/rocprof_trace.log profiles/$R/ant65536_bench.log
-for spec in "Ant 65536 k_env_step" "Humanoid 32768 k_env_step" "ShadowHand 16384 k_hand_step"; do
+for spec in "Ant 65536 k_env_step" "Humanoid 32768 k_env_step" "ShadowHand 16384 k_hand_step" "ShadowHand-egg 16384 k_hand_step" "ShadowHand-pen 16384 k_hand_step"; do
   set -- $spec
   [ -d gpurun_out/pmc/$1 ] || continue
   mkdir -p profiles/$R/pmc_$1
