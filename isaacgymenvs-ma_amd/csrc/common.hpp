@@ -11,6 +11,7 @@ struct mg_sim {
   mg_model host_model;
   mg_model* d_model;
   void* d_tile;     // the launched instance's model tile image (mgi::BuildTile), nullptr if none fits
+  unsigned* d_wq;   // the step kernels' work-queue counters [dequeues, finished waves] (step_kernels.hpp)
   mg_sim_params params;
   int32_t n;        // actors
   int32_t device;

@@ -553,10 +553,17 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   // the LDS model tile of the instance that will run this model, prebuilt once on the host; a model no
   // instance fits is still created (its launches report MG_ECAPACITY)
   s->d_tile = nullptr;
+  // the step kernels' work-queue counters: zero here, and zeroed again by the last wave of every launch
+  if (hipMalloc(&s->d_wq, 2 * sizeof(unsigned)) != hipSuccess || hipMemset(s->d_wq, 0, 2 * sizeof(unsigned)) != hipSuccess) {
+    (void)hipFree(s->d_model);
+    delete s;
+    return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(work queue) failed");
+  }
   if (mgi::team_size(s->host_model, s->params.max_contacts) > 0) {
     const int rc = mgi::dispatch<mgi::BuildTile>(s->host_model, s->params.max_contacts, s);
     if (rc) {
       (void)hipFree(s->d_model);
+      (void)hipFree(s->d_wq);
       delete s;
       return rc;
     }
@@ -642,6 +649,7 @@ int mg_sim_destroy(mg_sim* sim) {
   if (!sim) return MG_OK;
   (void)hipFree(sim->d_model);
   if (sim->d_tile) (void)hipFree(sim->d_tile);
+  (void)hipFree(sim->d_wq);
   delete sim;
   return MG_OK;
 }

@@ -19,9 +19,9 @@ namespace mgi {
 constexpr int kPhaseCap = 1 << 16;  // waves tracked
 // one copy per instance translation unit (each is its own code object): phase_buf_publish<I> sets it
 static __device__ unsigned long long* g_phase_buf;
-#define MG_PHASE_FLUSH(t, W)                                                           \
+#define MG_PHASE_FLUSH(t, item)                                                        \
   {                                                                                    \
-    const unsigned gw_ = blockIdx.x * (W) + threadIdx.x / 64, l_ = threadIdx.x & 63;    \
+    const unsigned gw_ = (unsigned)(item), l_ = threadIdx.x & 63;                      \
     if (g_phase_buf && gw_ < kPhaseCap && l_ < 16) {                                   \
       unsigned int v_ = 0;                                                             \
       for (int i_ = 0; i_ < 16; i_++)                                                  \
@@ -30,7 +30,7 @@ static __device__ unsigned long long* g_phase_buf;
     }                                                                                  \
   }
 #else
-#define MG_PHASE_FLUSH(t, W)
+#define MG_PHASE_FLUSH(t, item)
 #endif
 
 #ifndef MG_EXP
@@ -67,6 +67,35 @@ struct Shape {
   static constexpr int E = E1 * W;  // teams per block
   static_assert(per_cu(W) >= 1, "one block must fit the CU's LDS");
 };
+
+// ------------------------------------------------------------------------------------------------ work queue
+// The step kernels launch the resident capacity (as many blocks as the CUs hold at once, launch_wq) and
+// each wave loops over work items (one item = the E1 teams of one wave): its own index in the grid first,
+// then items dequeued from a device counter until they run out.  A CU thus refills a wave's slot as soon
+// as that wave is done; with one block per W waves launched over the whole batch, a block's LDS stays held
+// until its slowest wave finishes (Humanoid: 4-wave blocks, 23 % of the wave slots idle),
+// and the model tile is copied once per resident block instead of once per W waves of work.
+// wq[0] counts dequeues, wq[1] finished waves; the last wave to finish zeroes both (every other wave has
+// made its final dequeue before its wq[1] add), so the next launch on the stream starts from zero.
+// a zero the compiler cannot see through, redrawn per work item: every address of the item's body is offset by it,
+// so nothing the body loads (LDS tile, model, kernel arguments) is hoisted out of the work loop and kept in
+// registers across all items (that hoisting took the Ant kernel from 11 to 107 spilled registers)
+__device__ __forceinline__ int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+__device__ __forceinline__ int wq_next(unsigned* wq, int grid_waves) {
+  unsigned v = 0u;
+  if ((threadIdx.x & 63) == 0) v = atomicAdd(&wq[0], 1u);
+  return grid_waves + (int)__builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
+  if ((threadIdx.x & 63) == 0 && atomicAdd(&wq[1], 1u) == (unsigned)grid_waves - 1u) {
+    atomicExch(&wq[0], 0u);
+    atomicExch(&wq[1], 0u);
+  }
+}
 
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
@@ -142,30 +171,22 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
 // are latency-bound; occupancy is the lever — DESIGN.md §3)
 // RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
 // post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
+// one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(
-    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
-    mg_task_buffers tb, int n, mg_replay rp) {
+__device__ __forceinline__ void env_step_item(
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC>, T>* lds,
+    mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
+    const mg_task_buffers& tb, int n, const mg_replay& rp, int item) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
-  constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP> tile;
-  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
-  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
-#else
-  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
-#endif
-  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   const int team = threadIdx.x / T;
   const int wt = (threadIdx.x & 63) / T;  // team index within the wave (ballot / shuffle positions)
-  const int a = blockIdx.x * E + team;
+  const int a = item * SH::E1 + wt;
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
   mg::TeamLDS<T, MN, MC>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP> t;
-  t.init(&L, &tile, m, &p);
+  t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
     t.drn = &drt[team].node[0][0];
@@ -342,7 +363,37 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
   t.ph_mark(9);
-  MG_PHASE_FLUSH(t, W)
+  MG_PHASE_FLUSH(t, item)
+}
+
+template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(
+    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
+    mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq) {
+  using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
+  constexpr int E = SH::E, W = SH::W;
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP> tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
+  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
+#else
+  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
+#endif
+  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
+  if constexpr (W == 1) {
+    // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
+    if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
+  } else {
+    // multi-wave blocks: the work queue (wq_next), the grid being the resident capacity
+    const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
+    for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
+      const int z = opaque_zero();
+      env_step_item<T, MN, MC, MG, MP, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
+                                               (&rp)[z], item);
+    }
+    wq_done(wq, gwv);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------ hand tasks
@@ -357,30 +408,22 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // PD targets) -> simulate x substeps -> post_physics_step (full_state obs, reward, partial sums of
 // the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
 // RP: physics-bypass replay instance (mg_env_step_replay), as k_env_step's.
+// one work item of k_hand_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(
-    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
-    mg_task_buffers tb, int n, mg_replay rp) {
+__device__ __forceinline__ void hand_step_item(
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, 16 * MG>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T>* lds,
+    mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
+    const mg_task_buffers& tb, int n, const mg_replay& rp, int item) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
-  constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
-  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
-  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
-#else
-  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, 16 * MG>*>(timg));
-#endif
-  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   const int team = threadIdx.x / T;
-  const int e = blockIdx.x * E + team;
+  const int e = item * SH::E1 + (int)(threadIdx.x & 63) / T;
   const bool valid = e < n;
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
   mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, OT> t;
-  t.init(&L, &tile, m, &p);
+  t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
     t.drn = &drt[team].node[0][0];
@@ -608,13 +651,72 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
     }
   }
   t.ph_mark(9);
-  MG_PHASE_FLUSH(t, W)
+  MG_PHASE_FLUSH(t, item)
+}
+
+template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(
+    const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
+    mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq) {
+  using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
+  constexpr int E = SH::E, W = SH::W;
+  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
+  __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
+  __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
+  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
+#else
+  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, 16 * MG>*>(timg));
+#endif
+  __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
+  if constexpr (W == 1) {  // as k_env_step
+    if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
+  } else {
+    const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
+    for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
+      const int z = opaque_zero();
+      hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z],
+                                                    (&tb)[z], n, (&rp)[z], item);
+    }
+    wq_done(wq, gwv);
+  }
 }
 
 // launch helper: grid of ceil(n / teams-per-block) blocks of the instance's shape
 template <class SH, class K, class... A>
 static void launch(K kern, hipStream_t s, int n, A... args) {
   hipLaunchKernelGGL(kern, dim3((n + SH::E - 1) / SH::E), dim3(SH::kThreads), 0, s, args...);
+}
+
+// launch of a step kernel: multi-wave blocks get min(blocks of the whole batch, resident blocks) blocks (the
+// work queue; occupancy query cached per kernel and device), one-wave blocks one block per item
+template <class SH, class K, class... A>
+static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
+  struct Entry { const void* k; int dev, blocks; };
+  static Entry cache[32];  // (kernel, device) -> resident blocks
+  const void* kp = reinterpret_cast<const void*>(kern);
+  int resident = 0;
+  for (const Entry& c : cache)
+    if (c.k == kp && c.dev == sim->device) resident = c.blocks;
+  if (resident <= 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, SH::kThreads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sim->device) != hipSuccess || per_cu <= 0 ||
+        cus <= 0)
+      return fail(MG_EDEVICE, "mg_env_step: occupancy query failed");
+    resident = per_cu * cus;
+    for (Entry& c : cache)
+      if (!c.k) { c = Entry{kp, sim->device, resident}; break; }
+  }
+  const int items = (sim->n + SH::E1 - 1) / SH::E1;
+  const int need = (items + SH::W - 1) / SH::W;
+  if (SH::W == 1) {  // the kernels' one-wave-block path: the static grid, one block per item
+    hipLaunchKernelGGL(kern, dim3(need), dim3(SH::kThreads), 0, s, args..., sim->d_wq);
+    return MG_OK;
+  }
+  const int blocks = need < resident ? need : resident;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), 0, s, args..., sim->d_wq);
+  return MG_OK;
 }
 
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
@@ -671,23 +773,23 @@ int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, co
     mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
     mg::h_fill_maps(&tpm);
     if (rp)
-      launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>, s, sim->n,
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>, s, sim,
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>, s, sim->n,
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>, s, sim,
                                                    sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else
-      launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>, s, sim->n,
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>, s, sim,
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
   } else {
     if (rp)
-      launch<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim->n, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      launch<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim->n, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim, sim->d_model,
                                                  ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else
-      launch<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim->n, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
   }
   return MG_OK;

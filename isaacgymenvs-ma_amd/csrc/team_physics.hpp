@@ -608,13 +608,18 @@ struct Team {
 
   __device__ __forceinline__ int col_of(int i) const { return ncol0 - 1 + i; }
 
-  __device__ __forceinline__ void init(L* lds, const MT* tile, const mg_model* mm, const mg_sim_params* pp) {
+  __device__ __forceinline__ void init(L* lds, const MT* tile, const mg_model* mm, const mg_sim_params* pp,
+                                       bool opaque_lane = false) {
     s = lds;
     mt = tile;
     m = mm;
     p = pp;
     drn = drg = drt = dro = nullptr;
     tl = threadIdx.x % T;
+    // opaque_lane: tl made opaque to the optimizer.  The work-queue step kernels call init() once per work
+    // item, and every lane-dependent constant derived from tl would otherwise be hoisted out of their work
+    // loop and held in registers across it
+    if (opaque_lane) asm volatile("" : "+v"(tl));
     tb = (threadIdx.x & 63) - tl;  // first lane of the team within its wave
     freeb = !m->fixed_base;
     nn = m->num_nodes;

@@ -57,3 +57,41 @@ def test_rank_shards_equal_slices_of_the_node_rollout(task, world, per_rank, ran
             assert torch.equal(reset, d[lo:hi]), f"{task} rank {r} step {k}: reset differ"
         assert int(d[lo:hi].sum()) >= 0
         sh.close()
+
+
+@pytest.mark.parametrize("task,obj", [("Humanoid", "block"), ("ShadowHand", "egg"), ("ShadowHand", "pen")])
+def test_work_queue_items_equal_the_static_grid(task, obj):
+    """Multi-wave-block instances (Humanoid: 4 waves per block, hand block / pen 2, egg 8) run a work queue
+    (step_kernels.hpp wq_next): at 16,384 envs the waves dequeue most of their items from the device counter;
+    a 2,048-env shard fits the resident grid and runs static items only.  Both must give the same envs the same
+    bits, over consecutive launches (the counters are re-zeroed by the last wave of every launch)."""
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    steps, n, per = 4, 16384, 2048
+
+    def make(num, offset):
+        cfg = configs.task_config(task, num, sim_device=DEV)
+        cfg["env_offset"] = offset
+        if task == "ShadowHand":
+            cfg["env"]["objectType"] = obj
+        return migym.make(seed=3, task=task, num_envs=num, sim_device=DEV, rl_device=DEV, headless=True,
+                          cfg={"task": cfg})
+
+    full = make(n, 0)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    acts = [torch.rand((full.num_actors, full.num_actions), device=DEV, generator=g) * 2.4 - 1.2 for _ in range(steps)]
+    ref = []
+    for a in acts:
+        obs, rew, reset, _ = full.step(a)
+        ref.append((obs["obs"].clone(), rew.clone(), reset.clone()))
+    full.close()
+    del full
+    for r in (0, n // per - 1):
+        sh = make(per, r * per)
+        lo, hi = r * per, (r + 1) * per
+        for k, a in enumerate(acts):
+            obs, rew, reset, _ = sh.step(a[lo:hi].contiguous())
+            o, w, d = ref[k]
+            assert torch.equal(obs["obs"], o[lo:hi]), f"{task}/{obj} shard {r} step {k}: obs differ"
+            assert torch.equal(rew, w[lo:hi]), f"{task}/{obj} shard {r} step {k}: rew differ"
+            assert torch.equal(reset, d[lo:hi]), f"{task}/{obj} shard {r} step {k}: reset differ"
+        sh.close()
