@@ -69,6 +69,9 @@ struct Shape {
 };
 
 // ------------------------------------------------------------------------------------------------ work queue
+#ifndef MG_WQ_ALL
+#define MG_WQ_ALL 0  // A/B: the work queue for one-wave blocks too
+#endif
 // The step kernels launch the resident capacity (as many blocks as the CUs hold at once, launch_wq) and
 // each wave loops over work items (one item = the E1 teams of one wave): its own index in the grid first,
 // then items dequeued from a device counter until they run out.  A CU thus refills a wave's slot as soon
@@ -186,7 +189,7 @@ __device__ __forceinline__ void env_step_item(
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
   mg::TeamLDS<T, MN, MC>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP> t;
-  t.init(&L, &tile, m, &p, SH::W > 1);
+  t.init(&L, &tile, m, &p, SH::W > 1 || MG_WQ_ALL);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
     t.drn = &drt[team].node[0][0];
@@ -381,7 +384,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
 #endif
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
-  if constexpr (W == 1) {
+  if constexpr (W == 1 && !MG_WQ_ALL) {
     // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
     if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
   } else {
@@ -423,7 +426,7 @@ __device__ __forceinline__ void hand_step_item(
   const int nb = m->num_bodies, nbe = nb + 2;
   mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, OT> t;
-  t.init(&L, &tile, m, &p, SH::W > 1);
+  t.init(&L, &tile, m, &p, SH::W > 1 || MG_WQ_ALL);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
     t.drn = &drt[team].node[0][0];
@@ -669,7 +672,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, 16 * MG>*>(timg));
 #endif
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
-  if constexpr (W == 1) {  // as k_env_step
+  if constexpr (W == 1 && !MG_WQ_ALL) {  // as k_env_step
     if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
   } else {
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
@@ -710,7 +713,7 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
   }
   const int items = (sim->n + SH::E1 - 1) / SH::E1;
   const int need = (items + SH::W - 1) / SH::W;
-  if (SH::W == 1) {  // the kernels' one-wave-block path: the static grid, one block per item
+  if (SH::W == 1 && !MG_WQ_ALL) {  // the kernels' one-wave-block path: the static grid, one block per item
     hipLaunchKernelGGL(kern, dim3(need), dim3(SH::kThreads), 0, s, args..., sim->d_wq);
     return MG_OK;
   }
