@@ -126,7 +126,8 @@ typedef struct mg_model {
    * kinematic goal actor.  Root-state rows per env are then [articulation, object, goal] and
    * rigid-body rows [articulation bodies..., object, goal]. */
   int32_t obj_type;                  /* 0 = none, MG_GT_BOX (block), MG_GT_ELLIPSOID (egg), MG_GT_CAPSULE (pen) */
-  int32_t obj_pad;
+  int32_t pair_mjcf;                 /* 1 = the pairs are explicit MJCF <pair>s (condim 1, margin 0): frictionless,
+                                      * and in contact from zero distance (not the sim's contact offset) */
   float obj_mass;
   float obj_inertia[3];              /* principal moments, object frame (COM at the origin) */
   float obj_size[3];                 /* box half extents | ellipsoid semi-axes | capsule (radius, half length

@@ -10,8 +10,8 @@
 // instance that fits the model is launched.
 #define MG_INSTANCES(X)                                                                                     \
   X(8, 4, 8, 4, 0, 0) X(16, 9, 16, 16, 0, 0) X(16, 16, 24, 24, 32, 0) X(32, 24, 32, 24, 160, 0)            \
-  X(32, 32, 48, 48, 192, 0) X(64, 40, 48, 48, 192, 0) X(32, 25, 24, 24, 0, MG_GT_BOX)                       \
-  X(32, 25, 24, 24, 0, MG_GT_CAPSULE) X(32, 25, 24, 24, 0, MG_GT_ELLIPSOID)
+  X(32, 32, 48, 48, 192, 0) X(64, 40, 48, 48, 192, 0) X(32, 25, 24, 24, 24, MG_GT_BOX)                      \
+  X(32, 25, 24, 24, 24, MG_GT_CAPSULE) X(32, 25, 24, 24, 24, MG_GT_ELLIPSOID)
 #define MG_NUM_INST 9
 
 namespace mgi {

@@ -1471,11 +1471,14 @@ struct Team {
       }
       base += tot;
     }
-    // self-collision pairs, pair order preserved.  Pass 1, lane per pair: the bounding-sphere test of the
-    // two cores; the survivors' indices are compacted (team scan) into a list in the union storage behind
-    // the geom frames.  Pass 2, lane per survivor: the segment-segment narrowphase, so the divergent
-    // narrowphase runs over a few dense chunks instead of every chunk of pairs.
+    // self-collision pairs, pair order preserved (Humanoid: every non-adjacent pair; ShadowHand: the MJCF's
+    // explicit <contact><pair>s).  Pass 1, lane per pair: the bounding-sphere test of the two cores; the
+    // survivors' indices are compacted (team scan) into a list in the union storage behind the geom frames.
+    // Pass 2, lane per survivor: the segment-segment narrowphase (or segment-box when one side is a box, as
+    // the hand's palm against the thumb), so the divergent narrowphase runs over a few dense chunks instead
+    // of every chunk of pairs.
     const int P = mt->np;
+    const float poff = m->pair_mjcf ? 0.0f : off;  // explicit MJCF pairs: in contact from zero distance (margin 0)
     static_assert(MN * 27 >= MG * GW + MP, "the pair list must fit behind the geom frames");
     int* plist = reinterpret_cast<int*>(gw_tile() + GW * MG);
     int npc = 0;
@@ -1485,10 +1488,17 @@ struct Team {
       if (pi < P) {
         V3 a0, a1, b0, b1;
         float ra, rb;
-        if (geom_segment(mt->pairs[pi][0], &a0, &a1, &ra) && geom_segment(mt->pairs[pi][1], &b0, &b1, &rb)) {
+        const bool sa = geom_segment(mt->pairs[pi][0], &a0, &a1, &ra), sb = geom_segment(mt->pairs[pi][1], &b0, &b1, &rb);
+        if (sa && sb) {
           V3 ca = (a0 + a1) * 0.5f, cb = (b0 + b1) * 0.5f, dc = ca - cb;
           float ha = sqrtf(dot(a1 - a0, a1 - a0)) * 0.5f, hb = sqrtf(dot(b1 - b0, b1 - b0)) * 0.5f;
-          float reach = ha + hb + ra + rb + off;
+          float reach = ha + hb + ra + rb + poff;
+          ok = dot(dc, dc) <= reach * reach ? 1 : 0;
+        } else if (sa != sb) {  // a box (bounding radius about its centre) and a sphere / capsule
+          const int gx = mt->pairs[pi][sa ? 1 : 0];
+          const V3 p0 = sa ? a0 : b0, p1 = sa ? a1 : b1;
+          const V3 dc = (p0 + p1) * 0.5f - ld3(gw_tile() + GW * gx);
+          const float reach = mt->gf[gx][15] + sqrtf(dot(p1 - p0, p1 - p0)) * 0.5f + (sa ? ra : rb) + poff;
           ok = dot(dc, dc) <= reach * reach ? 1 : 0;
         }
       }
@@ -1510,17 +1520,35 @@ struct Team {
         gb = mt->pairs[pi][1];
         V3 a0, a1, b0, b1;
         float ra, rb;
-        geom_segment(ga, &a0, &a1, &ra);
-        geom_segment(gb, &b0, &b1, &rb);
-        float ss, tt;
-        closest_seg_seg_t(a0, a1, b0, b1, &ss, &tt);
-        V3 pa = a0 + (a1 - a0) * ss, pb = b0 + (b1 - b0) * tt, dv = pa - pb;
-        float dist = sqrtf(dot(dv, dv));
-        d = dist - ra - rb;
-        if (d < off && dist > 1e-9f) {
-          nrm = dv * prcp(dist);
-          pt = ((pa - nrm * ra) + (pb + nrm * rb)) * 0.5f;
-          cnt = 1;
+        const bool sa = geom_segment(ga, &a0, &a1, &ra), sb = geom_segment(gb, &b0, &b1, &rb);
+        if (sa && sb) {
+          float ss, tt;
+          closest_seg_seg_t(a0, a1, b0, b1, &ss, &tt);
+          V3 pa = a0 + (a1 - a0) * ss, pb = b0 + (b1 - b0) * tt, dv = pa - pb;
+          float dist = sqrtf(dot(dv, dv));
+          d = dist - ra - rb;
+          if (d < poff && dist > 1e-9f) {
+            nrm = dv * prcp(dist);
+            pt = ((pa - nrm * ra) + (pb + nrm * rb)) * 0.5f;
+            cnt = 1;
+          }
+        } else {  // box vs sphere / capsule (oracle collide): the segment's closest point to the box
+          const int gx = sa ? gb : ga;
+          V3 cx;
+          M3 Rx;
+          geom_staged(gx, &cx, &Rx);
+          const float* gs = mt->gf[gx] + 12;
+          const V3 hg = v3(gs[0], gs[1], gs[2]);
+          const float r = sa ? ra : rb;
+          const V3 al = mulT(Rx, (sa ? a0 : b0) - cx), u = mulT(Rx, (sa ? a1 : b1) - cx) - al;
+          const V3 P = al + u * seg_box_t(al, u, hg);
+          V3 nb, cbx;
+          d = point_box(P, hg, &nb, &cbx) - r;
+          if (d < poff) {
+            pt = mul(Rx, ((P - nb * r) + cbx) * 0.5f) + cx;
+            nrm = mul(Rx, nb) * (sa ? 1.0f : -1.0f);  // from B to A; nb points from the box to the segment
+            cnt = 1;
+          }
         }
       }
       const int incl = team_incl_scan<T>(cnt);
@@ -1833,7 +1861,8 @@ struct Team {
             rw.iw = (active && Wr > 1e-12f) ? prcp(Wr) : 0.0f;
             rw.lam = 0.0f;
             // DR: a contact's friction is the mean of its two shapes' (vec_task.py rigid_shape_properties)
-            const float muc = (drg && contact) ? 0.5f * (gmu(cside(r / 3, 2)) + gmu(cside(r / 3, 3))) : p->friction;
+            float muc = (drg && contact) ? 0.5f * (gmu(cside(r / 3, 2)) + gmu(cside(r / 3, 3))) : p->friction;
+            if (contact && m->pair_mjcf && cside(r / 3, 1) >= 0) muc = 0.0f;  // explicit MJCF pair: condim 1
             rw.mu = contact ? (q % 3 == 0 ? -1.0f : muc) : -2.0f;
             if (!active) rw.b = 0.0f;
           }

@@ -200,6 +200,7 @@ class ModelSpec:
     tendons: List[Dict] = field(default_factory=list)   # {name, dofs[2], coefs[2], range[2], limit_stiffness, damping}
     gravity_off: int = 0
     obj: Optional[Dict] = None     # free object sharing the env: {type, size, mass, inertia, lin_damping, ...}
+    pair_mjcf: int = 0             # 1: the pairs are explicit MJCF <pair>s (condim 1: frictionless; margin 0)
     hull: Optional[Dict] = None    # the convex-mesh geom: {geom, verts [[x,y,z]], planes [[nx,ny,nz,d]]}, geom frame
 
     @property
@@ -581,7 +582,43 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, co
     spec.hull = hulls[0] if hulls else None
     if self_collision:
         spec.pairs = self_collision_pairs(spec)
+    explicit, spec.pair_mjcf = mjcf_contact_pairs(root, geoms)
+    for pr in explicit:
+        if pr not in spec.pairs and pr[::-1] not in spec.pairs:
+            spec.pairs.append(pr)
     return spec
+
+
+def mjcf_contact_pairs(root, geoms):
+    """Explicit ``<contact><pair geom1 geom2 condim margin>`` elements of an MJCF: geom index pairs in file order
+    (a repeated pair once), and ``mg_model.pair_mjcf``.  MuJoCo collides these pairs whatever contype /
+    conaffinity say (the ShadowHand's collision geoms are contype 1 / conaffinity 0, so its only hand-hand
+    contacts are the 19 finger / thumb pairs of shared.xml:31-51), with the pair's own attributes: condim 1 =
+    frictionless, margin (default 0) = the distance below which the pair is in contact -- not the sim's
+    contact offset (at rest the hand's adjacent proximal capsules sit exactly 2 mm apart).  Pairs name sphere
+    / capsule geoms, or one box and one sphere / capsule (the kernel's pair narrowphase)."""
+    contact = root.find("contact")
+    if contact is None:
+        return [], 0
+    names = [g.name for g in geoms]
+    out, condims = [], set()
+    for pe in contact.findall("pair"):
+        g1, g2 = pe.get("geom1"), pe.get("geom2")
+        if g1 not in names or g2 not in names:
+            raise ValueError(f"MJCF contact pair names a geom that is not a collision geom: {g1!r}, {g2!r}")
+        pr = [names.index(g1), names.index(g2)]
+        if pr in out or pr[::-1] in out:
+            continue
+        types = sorted(geoms[i].gtype for i in pr)
+        if types[0] not in (GT_SPHERE, GT_CAPSULE) or types[1] not in (GT_SPHERE, GT_CAPSULE, GT_BOX):
+            raise NotImplementedError(f"MJCF contact pair {g1!r} / {g2!r}: geom types {types} have no pair narrowphase")
+        out.append(pr)
+        condims.add(int(pe.get("condim", "3")))
+        if float(pe.get("margin", "0")) != 0.0:
+            raise NotImplementedError(f"MJCF contact pair {g1!r} / {g2!r}: margin != 0")
+    if condims != {1}:
+        raise NotImplementedError(f"MJCF contact pairs with condim {sorted(condims)} (only condim 1 is built)")
+    return out, 1
 
 
 def _read_mjcf_tree(path):
@@ -775,7 +812,7 @@ def _model_dtype():
         ("num_tendons", i4), ("gravity_off", i4),
         ("tendon_dof", i4, (TD, 2)), ("tendon_coef", f4, (TD, 2)), ("tendon_range", f4, (TD, 2)),
         ("tendon_limit_stiffness", f4, TD), ("tendon_damping", f4, TD),
-        ("obj_type", i4), ("obj_pad", i4), ("obj_mass", f4), ("obj_inertia", f4, 3), ("obj_size", f4, 3),
+        ("obj_type", i4), ("pair_mjcf", i4), ("obj_mass", f4), ("obj_inertia", f4, 3), ("obj_size", f4, 3),
         ("obj_lin_damping", f4), ("obj_ang_damping", f4), ("obj_gravity", f4),
         ("hull_num_verts", i4), ("hull_num_planes", i4),
         ("hull_vert", f4, (MAX_HULL_VERTS, 3)), ("hull_plane", f4, (MAX_HULL_PLANES, 4)),
@@ -797,6 +834,7 @@ def pack_model(spec: ModelSpec) -> np.ndarray:
     m["num_bodies"] = len(spec.bodies)
     m["num_geoms"] = len(spec.geoms)
     m["num_pairs"] = len(spec.pairs)
+    m["pair_mjcf"] = int(getattr(spec, "pair_mjcf", 0))
     m["num_sensors"] = len(spec.sensors)
     m["nv"] = (0 if spec.fixed_base else 6) + len(spec.nodes) - 1
     m["parent"][:] = -1

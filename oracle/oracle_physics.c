@@ -1368,7 +1368,8 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
 }
 
 /* contact order (the HIP kernel emits the same list): ground contacts of the articulation's geoms
- * in geom order, the object's box corners on the ground, self-collision pairs in pair order, then
+ * in geom order, the object's box corners on the ground, self-collision pairs in pair order (capsule /
+ * sphere pairs; a box against a capsule / sphere; ShadowHand's explicit MJCF pairs are frictionless), then
  * articulation geoms against the object: the convex-mesh geom, then the others in geom order */
 static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, contact* out, int cap) {
   int n = 0;
@@ -1424,10 +1425,36 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
     from_obj_pt(k, sl, e);
     n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
   }
+  const real poff = m->pair_mjcf ? 0.0 : off; /* explicit MJCF pairs: in contact from zero distance (margin 0) */
   for (int pi = 0; pi < m->num_pairs; pi++) {
     int ga = m->pair[pi][0], gb = m->pair[pi][1];
     real a0[3], a1[3], b0[3], b1[3], ra, rb;
-    if (!geom_segment(m, k, ga, a0, a1, &ra) || !geom_segment(m, k, gb, b0, b1, &rb)) continue;
+    const int sa = geom_segment(m, k, ga, a0, a1, &ra), sb = geom_segment(m, k, gb, b0, b1, &rb);
+    if (sa != sb) { /* a box against a sphere / capsule (the hand's palm vs the thumb, shared.xml:39) */
+      const int gx = sa ? gb : ga;
+      const real* p0 = sa ? a0 : b0;
+      const real* p1 = sa ? a1 : b1;
+      const real r = sa ? ra : rb;
+      real c[3], R[3][3], d0[3], du[3], al[3], u[3], P[3], nb[3], cb[3], pm[3], pw[3], nw[3];
+      geom_world(m, k, gx, c, R);
+      const real hg[3] = {m->geom_size[gx][0], m->geom_size[gx][1], m->geom_size[gx][2]};
+      for (int a = 0; a < 3; a++) { d0[a] = p0[a] - c[a]; du[a] = p1[a] - p0[a]; }
+      mattvec3(R, d0, al);
+      mattvec3(R, du, u);
+      int inside;
+      const real t = seg_box_t(al, u, hg, &inside);
+      for (int a = 0; a < 3; a++) P[a] = al[a] + t * u[a];
+      const real d = point_box(P, hg, nb, cb) - r;
+      if (d < poff) {
+        for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - nb[a] * r) + cb[a]);
+        matvec3(R, pm, pw);
+        matvec3(R, nb, nw);
+        for (int a = 0; a < 3; a++) { pw[a] += c[a]; nw[a] = sa ? nw[a] : -nw[a]; } /* normal from B to A */
+        n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pw, nw, d);
+      }
+      continue;
+    }
+    if (!sa) continue;
     real s, t, pa[3], pb[3], dv[3];
     closest_seg_seg(a0, a1, b0, b1, &s, &t);
     for (int a = 0; a < 3; a++) {
@@ -1437,7 +1464,7 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
     }
     real dist = sqrt(dot3(dv, dv));
     real d = dist - ra - rb;
-    if (d < off && dist > 1e-9) {
+    if (d < poff && dist > 1e-9) {
       real nrm[3] = {dv[0] / dist, dv[1] / dist, dv[2] / dist}, pt[3];
       for (int a = 0; a < 3; a++) pt[a] = 0.5 * (pa[a] - ra * nrm[a] + pb[a] + rb * nrm[a]);
       n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pt, nrm, d);
@@ -1621,6 +1648,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
             sum += g2[k] >= 0 ? s->gmu[g2[k]] : (g2[k] == -2 ? s->gmu[m->num_geoms] : p->friction);
           mu = 0.5 * sum;
         }
+        if (m->pair_mjcf && so->con[so->row_ref[r]].nodeB >= 0) mu = 0.0; /* explicit MJCF pair: condim 1 */
         real lim = mu * so->lam[3 * so->row_ref[r]];  /* normal row of this contact */
         lnew = lnew < -lim ? -lim : (lnew > lim ? lim : lnew);
       } else if (lnew < 0) {

@@ -3,7 +3,8 @@ discontinuities of the build's physics that let an fp32 (GPU) and an fp64 (oracl
 part ways:
 
   * contact threshold: a candidate whose gap lies within `delta` of contact_offset is a contact on one side
-    and not on the other (detected by regenerating the oracle's contacts with the offset moved by +-delta);
+    and not on the other (detected by regenerating the oracle's contacts with the offset moved by +-delta; the hand's explicit
+    MJCF pairs switch on at distance 0, and their threshold is moved by +-delta the same way);
   * joint-limit rows: a DOF within `dq` of the limit margin (limit_margin 0.1 rad from a limit);
   * PD drive saturation (hand tasks): an explicit drive force within `df` of its effort limit;
   * deep penetration (a contact deeper than 5 mm, reachable only where a reset places the object into hand
@@ -71,6 +72,20 @@ def contact_flips(mnp, sp, roots, dofs, delta=1e-4, cap=64):
         r = np.ascontiguousarray(roots[i], np.float32).ravel()
         d = np.ascontiguousarray(dofs[i], np.float32)
         out[i] = len(O.contacts(mnp, lo, r, d, cap)) != len(O.contacts(mnp, hi, r, d, cap))
+    if int(mnp["pair_mjcf"]) and int(mnp["num_pairs"]) > 0:
+        # explicit MJCF pairs switch on at distance 0, not at the offset: count the pair contacts alone (the
+        # model with pairs minus the model without) with the pairs' threshold moved to +-delta
+        mp, m0 = mnp.copy(), mnp.copy()
+        mp["pair_mjcf"] = 0
+        m0["num_pairs"] = 0
+        lo0, hi0 = copy.copy(sp), copy.copy(sp)
+        lo0.contact_offset, hi0.contact_offset = -delta, delta
+        for i in range(len(roots)):
+            r = np.ascontiguousarray(roots[i], np.float32).ravel()
+            d = np.ascontiguousarray(dofs[i], np.float32)
+            npl = len(O.contacts(mp, lo0, r, d, cap)) - len(O.contacts(m0, lo0, r, d, cap))
+            nph = len(O.contacts(mp, hi0, r, d, cap)) - len(O.contacts(m0, hi0, r, d, cap))
+            out[i] |= npl != nph
     return out
 
 

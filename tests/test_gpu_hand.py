@@ -241,6 +241,27 @@ def test_hand_physics_step_matches_oracle(lib, kind):
     assert max(ncon) >= 3
 
 
+def test_hand_finger_pairs_match_oracle(lib):
+    """Curled fingers and thumb (60-95 % of their flexion range, object parked away): the MJCF's explicit
+    finger / thumb / palm pairs (frictionless, from zero distance) are in contact in most envs; one simulate on
+    the GPU against the oracle, every env, as _physics_vs_oracle."""
+    spec, sp, tp = setup(kind="block")
+    n = 256
+    rng = np.random.default_rng(17)
+    h = hand_states(spec, tp, n, rng)
+    lo = np.array([x.lower for x in spec.nodes[1:]])
+    hi = np.array([x.upper for x in spec.nodes[1:]])
+    h.dof[:, :, 0] = lo + (hi - lo) * rng.uniform(0.6, 0.95, (n, spec.num_dofs))
+    h.root[:, 1, 0:3] = (5.0, 5.0, 3.0)
+    mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n)
+    spec0 = copy.deepcopy(spec)
+    spec0.pairs = []
+    m0 = M.pack_model(spec0)
+    npair = [len(O.contacts(mnp, sp, h0.root[i].ravel(), h0.dof[i], 64)) - len(O.contacts(m0, sp, h0.root[i].ravel(), h0.dof[i], 64))
+             for i in range(64)]
+    assert sum(1 for k in npair if k > 0) >= 32, npair
+
+
 def forearm_top(spec, h):
     """world position of the forearm hull's highest vertex (geom frame of node 0 = the hand's root row)"""
     g = spec.geoms[spec.hull["geom"]]

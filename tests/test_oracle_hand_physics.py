@@ -84,6 +84,10 @@ def test_cube_settles_on_the_palm():
 
 def test_drives_track_targets():
     spec, tp, sp, mnp, h = setup()
+    # the drives alone: at 70 % flexion the ring and little fingers meet (the MJCF's explicit contact pairs,
+    # test_flexed_fingers_meet_through_the_explicit_pairs), so the self pairs are left out here
+    spec.pairs = []
+    mnp = M.pack_model(spec)
     park_object(h)
     act = [tp.actuated_dof[i] for i in range(tp.num_actions)]
     lo = np.array([tp.dof_lower[j] for j in range(24)])
@@ -247,7 +251,8 @@ def test_egg_and_pen_rest_on_the_ground():
     np.testing.assert_allclose(obj[2], 0.04, atol=5e-4)
     assert np.abs(obj[7:10]).max() < 1e-2, obj
     con = O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)
-    assert len(con) >= 1 and abs(con[-1][7]) < 5e-4
+    ground = [c for c in con if c[0] == -2]   # the object's side first: the egg on the plane
+    assert len(ground) == 1 and abs(ground[0][7]) < 5e-4, con
 
 
 def test_egg_and_pen_land_on_the_palm():
@@ -360,3 +365,40 @@ def test_cube_contacts_and_rests_on_the_forearm_hull():
         h.simulate(mnp, sp)
     # held up by the hull: no deeper than a few mm below the start (free fall would drop ~12 mm)
     assert h.root[0, 1, 2] > z0 - 0.004, (h.root[0, 1, 2], z0)
+
+
+def test_explicit_contact_pairs_imported():
+    """shared.xml:31-51 lists 19 <pair>s (condim 1), one of them twice: 18 pairs, frictionless; the palm's box
+    against the thumb's distal capsule is the one box pair."""
+    spec = M.load_builtin("shadow_hand")
+    names = [g.name for g in spec.geoms]
+    assert len(spec.pairs) == 18 and spec.pair_mjcf == 1
+    assert [names[i] for i in spec.pairs[0]] == ["robot0:C_ffdistal", "robot0:C_thdistal"]
+    assert [names[i] for i in spec.pairs[7]] == ["robot0:C_palm0", "robot0:C_thdistal"]
+    assert spec.geoms[spec.pairs[7][0]].gtype == M.GT_BOX
+    assert int(M.pack_model(spec)["pair_mjcf"]) == 1
+
+
+def test_flexed_fingers_meet_through_the_explicit_pairs():
+    """At 70 % flexion the ring and little fingers touch: with the explicit pairs their drives stall short of
+    the target and the contact list holds finger-finger contacts; without the pairs (no hand self-collision
+    otherwise: contype 1 / conaffinity 0) they pass through each other and track."""
+    res = {}
+    for pairs in (True, False):
+        spec, tp, sp, mnp, h = setup()
+        if not pairs:
+            spec.pairs = []
+            mnp = M.pack_model(spec)
+        park_object(h)
+        lo = np.array([tp.dof_lower[j] for j in range(24)])
+        hi = np.array([tp.dof_upper[j] for j in range(24)])
+        tgt = (0.3 * lo + 0.7 * hi).astype(np.float32)
+        h.targets[:] = tgt
+        for _ in range(300):
+            park_object(h)
+            h.simulate(mnp, sp)
+        rf = [spec.dof_names.index(n) for n in ("robot0:RFJ2", "robot0:LFJ2")]
+        con = O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)
+        res[pairs] = (np.abs(h.dof[0, rf, 0] - tgt[rf]).max(), len(con))
+    assert res[True][0] > 0.02 and res[True][1] >= 1, res
+    assert res[False][0] < 0.02 and res[False][1] == 0, res
