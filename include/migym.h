@@ -459,7 +459,9 @@ int mg_hand_finalize(const mg_task_params* tp, const mg_task_buffers* tb, void* 
 int mg_reset_idx(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const int32_t* ids, int32_t n,
                  void* stream);
 
-/* Whole VecTask.step: actions -> actuation -> simulate -> post_physics. */
+/* Whole VecTask.step: actions -> actuation -> simulate -> post_physics.  Launches of one sim must be
+ * stream-ordered: the multi-wave kernel instances dequeue work items from the sim's device counters,
+ * which the last wave of each launch zeroes for the next. */
 int mg_env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, void* stream);
 
 /* Physics-bypass replay of mg_env_step (test infrastructure: pins the fused kernels' own task layer
