@@ -85,6 +85,9 @@ def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
             "single_core": {"value": v1, "unit": "env-steps/s", "cores": 1, "sample": smp1}}
 
 
+VALU_SIMDS, CLOCK_HZ = 256 * 4, 2.4e9   # MI355X: 256 CUs x 4 SIMD-32, peak engine clock (MI355X_MICROARCH.md)
+
+
 def pmc_traffic(task, n, kern_ms, object_type="block"):
     """Measured HBM traffic of the dominant kernel for this workload, from the committed rocprofv3 --pmc
     passes of the same bench command (tools/gpu_prof.sh -> tools/pmc_summary.py --json): FETCH_SIZE x2
@@ -112,7 +115,12 @@ def pmc_traffic(task, n, kern_ms, object_type="block"):
         with open(path) as f:
             issue = json.load(f).get("issue")
         if issue:
-            out["pmc_issue"] = issue   # VALU-active / wait fractions of the same launches
+            out["pmc_issue"] = dict(issue)   # VALU-active / wait fractions of the same launches
+            vi = issue.get("valu_insts_per_launch")
+            if vi:
+                # the bound that does apply: VALU issue against its peak, one wave64 instruction
+                # per 2 cycles on each of the 1,024 SIMD-32s at the 2.4 GHz peak clock
+                out["pmc_issue"]["valu_issue_frac_of_peak"] = vi * 2.0 / (VALU_SIMDS * kern_ms * 1e-3 * CLOCK_HZ)
     except (OSError, ValueError):
         pass
     return out

@@ -42,6 +42,8 @@ if jout:
                                                      ("any_active_frac", "SQ_ACTIVE_INST_ANY"),
                                                      ("wait_any_frac", "SQ_WAIT_ANY"),
                                                      ("wait_inst_lds_frac", "SQ_WAIT_INST_LDS")) if c in med}
+        if "SQ_INSTS_VALU" in med:
+            out["issue"]["valu_insts_per_launch"] = med["SQ_INSTS_VALU"]
         if "SQ_INSTS_LDS" in med and "SQ_LDS_BANK_CONFLICT" in med:
             out["issue"]["lds_bank_conflict_cycles_per_lds_inst"] = med["SQ_LDS_BANK_CONFLICT"] / med["SQ_INSTS_LDS"]
     json.dump(out, open(jout, "w"), indent=1)
