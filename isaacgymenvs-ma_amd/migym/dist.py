@@ -114,6 +114,9 @@ class PackedGather:
         self.works = [None] * depth
         self.k = 0
         self.last = None
+        # one full-group collective before the first point-to-point message, so every rank has created
+        # the group's communicator before the root's batched receives (torch's batch_isend_irecv rule)
+        dist.barrier(group=group)
 
     def next_pack(self) -> torch.Tensor:
         """The slot the next step writes; waits (stream-ordered) for the gather that last used it."""
@@ -127,7 +130,7 @@ class PackedGather:
         buf = self.pack[i]
         if self.mode == "root":
             if self.rank != self.root:
-                works = [dist.isend(buf, dst=self.root, group=self.group)]
+                works = dist.batch_isend_irecv([dist.P2POp(dist.isend, buf, self.root, self.group)])
             else:
                 parts = self.full[i].chunk(self.world, 0)
                 ops = [dist.P2POp(dist.irecv, parts[r], r, self.group) for r in range(self.world) if r != self.root]
