@@ -163,12 +163,17 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #ifndef MG_RB_WIDE
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
 #endif
+#ifndef MG_RB_NARROW
+#define MG_RB_NARROW 12  // test-solve columns per batch for 16-lane locomotion teams (a multiple of 3, <= T):
+                         // 12 walkers instead of 6 halve the batches per substep (same-box A/B, 400 steps:
+                         // Ant 129.3 -> 130.2 M, MA-Ant 29.3 -> 29.6 M env-steps/s); hand teams and Cartpole keep 6
+#endif
 
 template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + MG_PGS_PREFETCH - 1) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;
-  static constexpr int RB = (T >= 32 && !OBJ) ? MG_RB_WIDE : 6;
+  static constexpr int RB = OBJ ? 6 : (T >= 32 ? MG_RB_WIDE : (MG_RB_NARROW <= T ? MG_RB_NARROW : 6));
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
   // (not for the egg instance, whose fp64 narrowphase already spills: 7.46 vs 7.71 M env-steps/s measured)
   static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (MG_JY_REGS < MR ? MG_JY_REGS : MR) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;  // right-hand sides per test solve (rows of 2-4 contacts)

@@ -10,7 +10,7 @@ for lib in default $(ls isaacgymenvs-ma_amd/migym/_lib/var/*.so 2>/dev/null); do
   for spec in $SPECS; do
     IFS=: read t n o <<< "$spec"; o=${o:-block}
     if [ "$lib" = default ]; then unset MIGYM_LIB; else export MIGYM_LIB=$PWD/$lib; fi
-    timeout -k 10 200 python bench.py --task $t --num-envs $n --object-type $o --steps 100 --warmup 10 --no-cpu-baseline \
+    timeout -k 10 200 python bench.py --task $t --num-envs $n --object-type $o --steps ${STEPS:-100} --warmup 10 --no-cpu-baseline \
       > gpurun_out/var/${name}_${t}_$o.json 2> gpurun_out/var/${name}_${t}_$o.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "$name $t rc=$rc"; tail -3 gpurun_out/var/${name}_${t}_$o.err; exit $rc; fi
