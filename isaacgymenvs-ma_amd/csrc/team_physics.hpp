@@ -161,6 +161,12 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #define MG_JY_REGS 12  // rows of (J, Y) columns kept in registers; the rest in private (scratch) arrays
                        // (same-box A/B vs 16: Ant +0.8 %, Humanoid +0.8 %, ShadowHand +0.6 %; 8 and 20 slower)
 #endif
+#ifndef MG_JY_REGS_WIDE
+#define MG_JY_REGS_WIDE MG_JY_REGS  // the same for 32- and 64-lane locomotion teams (Humanoid)
+#endif
+#ifndef MG_JY_REGS_OBJ
+#define MG_JY_REGS_OBJ MG_JY_REGS  // hand teams (block, pen; the egg keeps every row in scratch)
+#endif
 #ifndef MG_RB_WIDE
 #define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
 #endif
@@ -177,7 +183,8 @@ struct TeamLDS {
   static constexpr int RB = OBJ ? 6 : (T >= 32 ? MG_RB_WIDE : (MG_RB_NARROW <= T ? MG_RB_NARROW : 6));
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
   // (not for the egg instance, whose fp64 narrowphase already spills: 7.46 vs 7.71 M env-steps/s measured)
-  static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (MG_JY_REGS < MR ? MG_JY_REGS : MR) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;  // right-hand sides per test solve (rows of 2-4 contacts)
+  static constexpr int KRW = OBJ ? MG_JY_REGS_OBJ : (T >= 32 ? MG_JY_REGS_WIDE : MG_JY_REGS);
+  static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (KRW < MR ? KRW : MR) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -2054,10 +2061,73 @@ struct Team {
   }
 
   // ---------------------------------------------------------------- sensors & DOF forces (last substep)
+  // Sensor wrenches lane-parallel over the contacts (wide locomotion teams: Humanoid's 2 sensors against up to
+  // 32 contacts).  Contact c sits on lane c mod T: its impulse as a world force f_c and the bodies of its two
+  // sides (+ side A, - side B, A first, as the per-sensor scan).  Sensor k's wrench about its body origin x_k is
+  // the team sum of +-[f_c; (p_c - x_k) x f_c]; the six sums of a sensor are independent, so a sensor costs a
+  // few pipelined reductions instead of a serial scan over the contacts.  The sensor tables are read with
+  // wave-uniform indices (scalar loads).  Same-box A/B: Humanoid +1.1 %; Ant -1.3 % and ShadowHand -0.9 %
+  // (4-5 sensors against a handful of contacts), which keep the scan.
+  __device__ __forceinline__ void sensors_by_team_sums(float* sens_out, int NS) {
+    constexpr int CPL = (MC + T - 1) / T;  // contacts per lane
+    const int nc = s->ncon;
+    V3 f[CPL], pc[CPL];
+    int ba[CPL], bb[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; j++) {
+      const int c = tl + j * T;
+      f[j] = v3(0, 0, 0);
+      pc[j] = v3(0, 0, 0);
+      ba[j] = bb[j] = -1;
+      if (c < nc) {
+        const int ga = cside(c, 2), gb = cside(c, 3);
+        ba[j] = ga >= 0 ? mt->gbody[ga] : -1;
+        bb[j] = gb >= 0 ? mt->gbody[gb] : -1;
+        const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
+        f[j] = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) *
+               (1.0f / h);
+        pc[j] = ld3(s->cp[c]);
+      }
+    }
+    V3 F = v3(0, 0, 0), Tq = v3(0, 0, 0);
+    M3 Rb;
+#pragma unroll
+    for (int k = 0; k < MG_MAX_SENSORS; k++) {
+      if (k >= NS) break;  // wave-uniform
+      const int body = m->sensor_body[k], nd = m->body_node[body];
+      M3 Rn;
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Rn.m[a][b] = s->R[nd][3 * a + b];
+      const V3 xb = ld3(s->x[nd]) + mul(Rn, ld3(m->body_pos[body]));
+      V3 fs = v3(0, 0, 0), ts = v3(0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < CPL; j++) {
+        const float sg = ba[j] == body ? 1.0f : (bb[j] == body ? -1.0f : 0.0f);
+        const V3 fk = f[j] * sg;
+        fs = fs + fk;
+        ts = ts + cross(pc[j] - xb, fk);
+      }
+      const float s0 = team_sum<T>(fs.x, tb), s1 = team_sum<T>(fs.y, tb), s2 = team_sum<T>(fs.z, tb);
+      const float s3 = team_sum<T>(ts.x, tb), s4 = team_sum<T>(ts.y, tb), s5 = team_sum<T>(ts.z, tb);
+      if (tl == k) {
+        F = v3(s0, s1, s2);
+        Tq = v3(s3, s4, s5);
+        Rb = mul(Rn, quat_to_mat(m->body_quat[body][0], m->body_quat[body][1], m->body_quat[body][2],
+                                 m->body_quat[body][3]));
+      }
+    }
+    if (tl < NS) {
+      const V3 Fl = mulT(Rb, F), Tl = mulT(Rb, Tq);
+      float* o = sens_out + 6 * tl;
+      o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
+    }
+  }
   __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out) {
     fk();  // post-step pose for the sensor body frames
     const int NS = m->num_sensors;
-    if (sens_out && tl < NS) {
+    if constexpr (T >= 32 && !OBJ) {
+      if (sens_out && NS > 0) sensors_by_team_sums(sens_out, NS);
+    } else if (sens_out && tl < NS) {
       const int body = m->sensor_body[tl], nd = m->body_node[body];
       M3 Rn;
       for (int a = 0; a < 3; a++)
