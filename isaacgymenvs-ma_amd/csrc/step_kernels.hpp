@@ -12,6 +12,17 @@
 #include "task.hpp"
 #include "team_physics.hpp"
 
+// Write-back of the per-step outputs (obs, state rows): read by the next kernel or the caller, never again by
+// this launch.  MG_NT_STORES=1 marks them non-temporal so they do not push the waves' scratch lines out of L2.
+#ifndef MG_NT_STORES
+#define MG_NT_STORES 0
+#endif
+#if MG_NT_STORES
+#define MG_STREAM_ST(p, x) __builtin_nontemporal_store((x), (p))
+#else
+#define MG_STREAM_ST(p, x) (*(p) = (x))
+#endif
+
 namespace mgi {
 #ifdef MG_PHASE_TIMING
 // per-wave accumulators (one row of 16 per block; plain read-modify-writes by the block's own wave,
@@ -346,24 +357,24 @@ __device__ __forceinline__ void env_step_item(
     float* o = tb.obs + (size_t)no * a;
     for (int q = t.tl; q < no; q += T) {
       const float x = bad ? 0.0f : ost[q];
-      o[q] = x;
-      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(x, tp.clip_obs);
+      MG_STREAM_ST(&o[q], x);
+      if (tb.obs_clamped) MG_STREAM_ST(&tb.obs_clamped[(size_t)no * a + q], mg::clampf(x, tp.clip_obs));
     }
     if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset] (migym/dist.py)
       float* pk = tb.out_pack + (size_t)(no + 2) * a;
-      for (int q = t.tl; q < no; q += T) pk[q] = bad ? 0.0f : mg::clampf(ost[q], tp.clip_obs);
+      for (int q = t.tl; q < no; q += T) MG_STREAM_ST(&pk[q], bad ? 0.0f : mg::clampf(ost[q], tp.clip_obs));
       if (t.tl == 0) { pk[no] = rew; pk[no + 1] = (float)reset; }
     }
   }
   mg::wsync();
   if (valid) {  // state write-back (gym layouts), team-cooperative
     if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
-      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
-    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.u.sv.st.dof[q];
+      for (int q = t.tl; q < 13; q += T) MG_STREAM_ST(&v.root_states[(size_t)13 * a + q], L.u.sv.st.root[q]);
+    for (int q = t.tl; q < 2 * nd; q += T) MG_STREAM_ST(&v.dof_state[(size_t)2 * nd * a + q], L.u.sv.st.dof[q]);
     if (v.sensors)
-      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.u.sv.st.sens[q];
+      for (int q = t.tl; q < 6 * ns; q += T) MG_STREAM_ST(&v.sensors[(size_t)6 * ns * a + q], L.u.sv.st.sens[q]);
     if (v.dof_force)
-      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
+      for (int q = t.tl; q < nd; q += T) MG_STREAM_ST(&v.dof_force[(size_t)nd * a + q], L.u.sv.st.dforce[q]);
   }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
