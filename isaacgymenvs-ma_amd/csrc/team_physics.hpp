@@ -164,6 +164,9 @@ static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packe
 #ifndef MG_JY_REGS_WIDE
 #define MG_JY_REGS_WIDE MG_JY_REGS  // the same for 32- and 64-lane locomotion teams (Humanoid)
 #endif
+#ifndef MG_ROWREC_LANES
+#define MG_ROWREC_LANES 1  // a test-solve block's row records written lane-parallel (0: team lane 0, row by row)
+#endif
 #ifndef MG_JY_REGS_OBJ
 #define MG_JY_REGS_OBJ MG_JY_REGS  // hand teams (block, pen; the egg keeps every row in scratch)
 #endif
@@ -1857,9 +1860,24 @@ struct Team {
       for (int g = 0; g < L::RB; g += 3) batch_jacobians(r0 + g, nrows, jb + g);
       ph_mark(4);
       test_solve(r0, nrows, Wv, yb);
+      // the row record of row r (written by one lane): 1/W, impulse 0, mu; inactive rows get b = 0
+      auto row_record = [&](int r, float Wr) {
+        const bool active = r < nrows;
+        const bool contact = r < 3 * ncr;
+        typename L::Row& rw = s->u.sv.rows[r];
+        rw.iw = (active && Wr > 1e-12f) ? prcp(Wr) : 0.0f;
+        rw.lam = 0.0f;
+        // DR: a contact's friction is the mean of its two shapes' (vec_task.py rigid_shape_properties)
+        float muc = (drg && contact) ? 0.5f * (gmu(cside(r / 3, 2)) + gmu(cside(r / 3, 3))) : p->friction;
+        if (contact && m->pair_mjcf && cside(r / 3, 1) >= 0) muc = 0.0f;  // explicit MJCF pair: condim 1
+        rw.mu = contact ? (r % 3 == 0 ? -1.0f : muc) : -2.0f;
+        if (!active) rw.b = 0.0f;
+      };
+      float wq[L::RB];
 #pragma unroll
       for (int q = 0; q < L::RB; q++) {
         const int r = r0 + q;
+        wq[q] = 0.0f;
         if (r < wave_rows) {
           const bool active = r < nrows;
           const bool contact = r < 3 * ncr;
@@ -1869,18 +1887,20 @@ struct Team {
           const float J = jb[q];
           MG_JSET(r, J, y);
           const float Wr = team_sum<T>(J * y, tb);
-          if (tl == 0) {
-            typename L::Row& rw = s->u.sv.rows[r];
-            rw.iw = (active && Wr > 1e-12f) ? prcp(Wr) : 0.0f;
-            rw.lam = 0.0f;
-            // DR: a contact's friction is the mean of its two shapes' (vec_task.py rigid_shape_properties)
-            float muc = (drg && contact) ? 0.5f * (gmu(cside(r / 3, 2)) + gmu(cside(r / 3, 3))) : p->friction;
-            if (contact && m->pair_mjcf && cside(r / 3, 1) >= 0) muc = 0.0f;  // explicit MJCF pair: condim 1
-            rw.mu = contact ? (q % 3 == 0 ? -1.0f : muc) : -2.0f;
-            if (!active) rw.b = 0.0f;
-          }
+          wq[q] = Wr;
+#if !MG_ROWREC_LANES
+          if (tl == 0) row_record(r, Wr);
+#endif
         }
       }
+#if MG_ROWREC_LANES
+      {  // the block's row records, lane q writes row r0 + q: one divergent region instead of RB
+        float Wr = wq[0];
+#pragma unroll
+        for (int q = 1; q < L::RB; q++) Wr = tl == q ? wq[q] : Wr;
+        if (tl < L::RB && r0 + tl < wave_rows) row_record(r0 + tl, Wr);
+      }
+#endif
       ph_mark(5);
     }
     // The sweep runs over prow rows, the row count rounded up to a multiple of the prefetch depth PF
