@@ -299,10 +299,11 @@ __device__ __forceinline__ void env_step_item(
   if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
     const float px = L.u.sv.st.root[0], py = L.u.sv.st.root[1], pz = L.u.sv.st.root[2];
     const int base = no - 3 * (A - 1);
-    for (int j = 1; j < A; j++) {
+    {  // lane j - 1 of the team writes agent j's three entries (one shuffle per coordinate, per-lane sources)
+      const int j = t.tl + 1 < A ? t.tl + 1 : 0;
       const int src = (wt - k + (k + j) % A) * T;
       const float qx = __shfl(px, src), qy = __shfl(py, src), qz = __shfl(pz, src);
-      if (t.tl == 0) {
+      if (t.tl + 1 < A) {
         ost[base + 3 * (j - 1) + 0] = qx - px;
         ost[base + 3 * (j - 1) + 1] = qy - py;
         ost[base + 3 * (j - 1) + 2] = qz - pz;

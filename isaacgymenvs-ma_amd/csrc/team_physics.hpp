@@ -1913,10 +1913,8 @@ struct Team {
     constexpr int PF = MG_PGS_PREFETCH;
     static_assert(MR % PF == 0, "row capacity must be a multiple of the PGS prefetch depth");
     const int prow = wave_rows == 0 ? 0 : ((wave_rows + PF - 1) / PF) * PF;
-    for (int r = wave_rows; r < prow; r++) {
-      MG_JSET(r, 0.0f, 0.0f);
-      if (tl == 0) s->u.sv.rows[r] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};
-    }
+    for (int r = wave_rows; r < prow; r++) MG_JSET(r, 0.0f, 0.0f);
+    if (tl < prow - wave_rows) s->u.sv.rows[wave_rows + tl] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};  // PF - 1 <= T
     wsync();
     ph_mark(5);
     // PGS sweeps: per visit one team dot product (DPP), a branch-free clamp (med3), one multiply-add
