@@ -595,7 +595,9 @@ __device__ __forceinline__ void hand_step_item(
       tb.progress[e] = prog;
       tb.successes[e] = succ;
       tb.timeout[e] = (uint8_t)((prog >= (int64_t)tp.max_episode_length - 1) && (ro != 0));
-      fin = succ * (float)ro;
+      // a guard-forced reset counts as a reset of the running mean, with no successes (its succ comes
+      // from a non-finite state)
+      fin = bad ? 0.0f : succ * (float)ro;
       if (tb.out_pack) {
         tb.out_pack[(size_t)(no + 2) * e + no] = rew;
         tb.out_pack[(size_t)(no + 2) * e + no + 1] = (float)ro;
@@ -661,7 +663,7 @@ __device__ __forceinline__ void hand_step_item(
           x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
                               L.obs + (no - na));
         }
-        tb.states[(size_t)tp.num_states * e + k] = x;
+        tb.states[(size_t)tp.num_states * e + k] = bad ? 0.0f : x;   // NaN guard, as for obs
       }
     }
   }

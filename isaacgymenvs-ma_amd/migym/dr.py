@@ -441,6 +441,46 @@ class DomainRandomizationMixin:
         _abi.check(self._lib.mg_sim_set_params(self.sim, _abi.C.byref(sp)), self._lib)
 
     # -------------------------------------------------------------------------------------------
+    def _dr_get_state(self):
+        """The randomization state a resumed rollout needs to draw the same samples as an uninterrupted one:
+        the counters that key the device draws (``mg_dr_apply``'s call counter, each noise lambda's call
+        counter and its correlated-noise tensor), the schedule / first-call flags, the current noise
+        parameters, the randomized sim params and the extern samples.  None without randomization."""
+        if self._dr is None:
+            return None
+        noise = {}
+        for name, p in self.dr_randomizations.items():
+            lam = p.get("noise_lambda")
+            noise[name] = {k: v for k, v in p.items() if k != "noise_lambda"}
+            if lam is not None:
+                noise[name]["_lambda"] = (lam.calls, lam.refresh, None if lam.corr is None else lam.corr.clone())
+        return {"calls": self._dr["calls"], "first_randomization": self.first_randomization, "noise": noise,
+                "gravity": tuple(float(x) for x in self.sim_params.gravity),
+                "rest_offset": float(self.sim_params.rest_offset), "og_gravity": self._og_sim_params["gravity"],
+                "extern_actor_params": {k: np.array(v, copy=True) for k, v in self.extern_actor_params.items()}}
+
+    def _dr_set_state(self, st):
+        if st is None or self._dr is None:
+            return
+        self._dr["calls"] = st["calls"]
+        self.first_randomization = st["first_randomization"]
+        for name, p in st["noise"].items():
+            p = dict(p)
+            calls, refresh, corr = p.pop("_lambda", (0, True, None))
+            lam = self.dr_randomizations.get(name, {}).get("noise_lambda") or \
+                NoiseLambda(self, name, 1 if name == "actions" else 2)
+            lam.calls, lam.refresh = calls, refresh
+            lam.corr = None if corr is None else corr.to(self.device).clone()
+            p["noise_lambda"] = lam
+            self.dr_randomizations[name] = p
+        sp = self.sim_params
+        for k in range(3):
+            sp.gravity[k] = st["gravity"][k]
+        sp.rest_offset = st["rest_offset"]
+        self._og_sim_params["gravity"] = st["og_gravity"]
+        _abi.check(self._lib.mg_sim_set_params(self.sim, _abi.C.byref(sp)), self._lib)
+        self.extern_actor_params = {k: np.array(v, copy=True) for k, v in st["extern_actor_params"].items()}
+
     def _dr_any_reset(self) -> bool:
         return (not self.dr_exact_trigger) or bool(self.reset_buf.any())
 

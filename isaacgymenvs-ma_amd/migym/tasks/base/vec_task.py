@@ -303,7 +303,8 @@ class VecTask(DomainRandomizationMixin, Env):
         """Serializable env state for a checkpoint (the reference's hook, vec_task.py:197-205, returns None;
         SURVEY.md §5 asks for the SoA state tensors): a dict of clones of every per-env device tensor that
         carries the rollout, plus the step counters.  ``set_env_state`` of it resumes the rollout exactly
-        (the reset RNG is keyed by (seed, env, control step), so the counters are part of the state)."""
+        (the reset RNG is keyed by (seed, env, control step), so the counters are part of the state); with
+        domain randomization the draw counters, noise state and randomized sim params are part of it too."""
         out, seen = {}, set()
         for k in self.env_state_tensors:
             t = getattr(self, k, None)
@@ -313,6 +314,9 @@ class VecTask(DomainRandomizationMixin, Env):
         for k in self.env_state_scalars:
             if hasattr(self, k):
                 out[k] = getattr(self, k)
+        dr = self._dr_get_state()
+        if dr is not None:
+            out["domain_randomization"] = dr
         return out
 
     def set_env_state(self, env_state):
@@ -328,6 +332,8 @@ class VecTask(DomainRandomizationMixin, Env):
                 cur.copy_(v.to(cur.device, cur.dtype))
             elif k in self.env_state_scalars:
                 setattr(self, k, v)
+            elif k == "domain_randomization":
+                self._dr_set_state(v)
 
     # ---------------------------------------------------------------------------------- API
     def get_state(self):
@@ -350,11 +356,28 @@ class VecTask(DomainRandomizationMixin, Env):
         PD targets; progress / reset (/ successes) cleared.  A caller reading ``root_states`` right after
         sees the reset state, as with the reference.  Inside ``step`` the fused kernel applies
         ``reset_buf``'s resets itself.  ``goal_env_ids`` (ShadowHand) are reset with the env (their goal is
-        redrawn as part of the env reset)."""
-        ids = torch.as_tensor(env_ids, device=self.device).flatten().to(torch.int32).contiguous()
-        n = int(ids.numel())
-        if n == 0:
+        redrawn as part of the env reset).
+
+        Multi-agent layouts (num_agents > 1) take agent ids, as the fork's MA tasks do
+        (franka_reach_MA.py:616-621, 875-889): ``_agent_ids_to_env_ids(use_AND_filter=True)`` keeps the envs
+        whose ids count at least num_agents times (``bincount(agent_ids // A) >= A``), and every agent of
+        those envs is reset (``_env_ids_to_agent_ids``).  The filter runs on the device: the launch gets all
+        N*A actor rows, -1 for the rows it skips, so there is no host synchronisation.
+
+        With domain randomization on, ``apply_randomizations`` runs first, as the reference's reset_idx does
+        (ant.py:254-256); like the reference's, it selects the envs to randomize from ``reset_buf``."""
+        ids = torch.as_tensor(env_ids, device=self.device).flatten().to(torch.int64)
+        if ids.numel() == 0:
             return
+        if self.num_agents > 1:
+            A, N = self.num_agents, self.num_envs
+            full = torch.bincount(ids // A, minlength=N)[:N] >= A
+            rows = torch.arange(N * A, device=self.device, dtype=torch.int64)
+            ids = torch.where(full.repeat_interleave(A), rows, torch.full_like(rows, -1))
+        ids = ids.to(torch.int32).contiguous()
+        n = int(ids.numel())
+        if self.randomize and self._dr is not None:
+            self.apply_randomizations(self.randomization_params, reset_mask=self.reset_buf, increment=False)
         self._reset_ids = ids   # alive until the launch has consumed it
         tb = self._tb
         tb.step_counter = self.control_steps

@@ -136,10 +136,10 @@ class ShadowHand(VecTask):
         tb.states = _abi.ptr(self.states_buf) if self.num_states > 0 else None
         # multi-GPU: the running mean over the envs of all ranks; the step leaves its
         # partial sums, post_launch all-reduces them (16 bytes) and applies shadow_hand.py:795-798.
-        # env.globalConsecutiveSuccesses: False keeps the reference's per-rank statistic.
-        self._global_cons = bool(self.cfg["env"].get("globalConsecutiveSuccesses", True)) and \
-            torch.distributed.is_available() and torch.distributed.is_initialized() and \
-            torch.distributed.get_world_size() > 1
+        # Off by default: the reference's statistic is per rank (shadow_hand.py:795-798); set
+        # env.globalConsecutiveSuccesses: True to opt in to the node-wide mean (one 16-byte all-reduce per step).
+        self._global_cons = bool(self.cfg["env"].get("globalConsecutiveSuccesses", False)) and \
+            torch.distributed.is_available() and torch.distributed.is_initialized()
         tb.defer_finalize = 1 if self._global_cons else 0
 
     def post_launch(self):

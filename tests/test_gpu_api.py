@@ -2,13 +2,19 @@
 
   * get_env_state / set_env_state: a rollout restored from a checkpointed state continues bit for bit;
   * reset_idx(env_ids): the listed envs hold their reset state right after the call (the reference
-    writes it immediately, ant.py:252-279, shadow_hand.py:586-668), the other envs are untouched.
+    writes it immediately, ant.py:252-279, shadow_hand.py:586-668), the other envs are untouched;
+    multi-agent layouts take agent ids through the AND filter (franka_reach_MA.py:616-621, 875-889);
+  * with domain randomization, the checkpointed state includes the draw counters, so a resumed rollout
+    draws the same samples.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
 import migym
+from migym import configs
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -139,4 +145,64 @@ def test_reset_idx_shadow_hand():
     assert torch.equal(root[keep], root_before[keep])
     env.step(actions(env, 5))
     assert torch.isfinite(env.obs_buf).all()
+    env.close()
+
+
+def test_reset_idx_multi_agent_and_filter():
+    """MA reset_idx(agent_ids): an env resets only when its ids count num_agents times (bincount, so a
+    repeated id counts twice, as in the reference), and then every agent of it resets; a partially listed
+    env is untouched (franka_reach_MA.py:875-885)."""
+    n = 64
+    env = make("MAAnt", n)
+    A = env.num_agents
+    assert A == 4
+    for k in range(3):
+        env.step(actions(env, k))
+    before = env.root_states.clone()
+    prog_before = env.progress_buf.clone()
+    assert (prog_before > 0).all()
+    # env 0 fully listed; env 1 three of four agents; env 2 two agents listed twice each; env 3 three
+    # agents; plus random ids: the envs to reset are what the reference returned for this list
+    G = np.load(os.path.join(os.path.dirname(__file__), "golden", "ma_conventions.npz"))
+    ids = torch.tensor(G["A4_dup_ids"], device=DEV)
+    full = set(G["A4_dup_env_ids"].tolist())
+    assert 0 in full and 2 in full and 1 not in full and 3 not in full
+    env.reset_idx(ids)
+    torch.cuda.synchronize()
+    for e in range(n):
+        rows = slice(A * e, A * e + A)
+        if e in full:
+            torch.testing.assert_close(env.root_states[rows], env.initial_root_states[rows], rtol=0, atol=0)
+            assert (env.progress_buf[rows] == 0).all() and (env.reset_buf[rows] == 0).all()
+        else:
+            assert torch.equal(env.root_states[rows], before[rows])
+            assert torch.equal(env.progress_buf[rows], prog_before[rows])
+    env.step(actions(env, 7))
+    assert torch.isfinite(env.obs_buf).all()
+    env.close()
+
+
+def test_env_state_round_trip_with_randomization():
+    n = 512
+    cfg = configs.task_config("Ant", n, sim_device=DEV)
+    cfg["task"]["randomize"] = True
+    cfg["task"]["randomization_params"]["frequency"] = 1   # every reset re-randomizes
+    cfg["env"]["episodeLength"] = 4                        # resets inside the resumed window
+    env = make("Ant", n, cfg={"task": cfg})
+    assert env.randomize
+    for k in range(5):
+        env.step(actions(env, k))
+    state = env.get_env_state()
+    assert "domain_randomization" in state
+    ref = []
+    for k in range(5, 12):
+        obs, rew, reset, _ = env.step(actions(env, k))
+        ref.append((obs["obs"].clone(), rew.clone(), reset.clone(), env.env_props.clone()))
+    assert any(bool(r[2].any()) for r in ref), "the resumed window must contain resets (re-randomization)"
+    env.set_env_state(state)
+    for k in range(5, 12):
+        obs, rew, reset, _ = env.step(actions(env, k))
+        o, r, d, p = ref[k - 5]
+        assert torch.equal(obs["obs"], o) and torch.equal(rew, r) and torch.equal(reset, d)
+        assert torch.equal(env.env_props, p)
     env.close()

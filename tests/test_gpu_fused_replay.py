@@ -24,7 +24,7 @@ from migym import _abi, configs, model as M, taskdefs
 from test_oracle_golden import HAND_TRACES, hand_noise, hand_trace_setup
 
 pytestmark = pytest.mark.gpu
-G = os.path.join(os.path.dirname(__file__), "golden")
+G = G_DIR = os.path.join(os.path.dirname(__file__), "golden")
 DEV = "cuda:0"
 
 
@@ -164,8 +164,12 @@ def test_fused_cartpole_replays_reference_trace(lib):
 @pytest.mark.parametrize("A", [2, 4])
 def test_fused_multi_agent_replay_matches_oracle_task_layer(lib, A):
     """MA-Ant through k_env_step's wave-ballot AND filter and shuffle-based others block, replayed on
-    random post-simulate states, vs the oracle's MA task layer (pinned to franka_reach_MA.py's
-    conventions by tests/test_multi_agent.py) at the same 1e-4 bar; potentials bit-exact."""
+    random post-simulate states, vs the oracle's MA task layer at the same 1e-4 bar; potentials
+    bit-exact.  Step 3 takes the reset_buf of tests/golden/ma_conventions.npz and must reset exactly the
+    agents the reference's reset_idx resets for it (franka_reach_MA.py:616-621, 875-889); step 4 places
+    the agents at the fixture's positions and the others block must give the reference's cyclic shift
+    (franka_reach_MA.py:604-608) once the agent's own position is added back."""
+    G = np.load(os.path.join(G_DIR, "ma_conventions.npz"))
     cfg = configs.task_config("MAAnt", 16)
     cfg["env"]["numAgents"] = A
     spec = M.load_builtin("ant")
@@ -189,10 +193,15 @@ def test_fused_multi_agent_replay_matches_oracle_task_layer(lib, A):
             dof = np.stack([lo + (hi - lo) * rng.uniform(-0.02, 1.02, (n, nd)), rng.normal(0, 2, (n, nd))], -1)
             sens = rng.normal(0, 5, h.sensors.shape).astype(np.float32)
             noise = rng.uniform(0, 1, (n, 2 * nd)).astype(np.float32)
-            if t == 3:   # a mix of fully- and partially-done envs for the AND filter
-                m = (rng.random(n) < 0.7).astype(np.int64)
+            if t == 3:   # the fixture's mix of fully- and partially-done envs for the AND filter
+                m = G[f"A{A}_mask"]
+                assert len(m) == n
                 h.reset[:] = m
                 e.reset.copy_(T(m, torch.int64))
+            if t == 4:   # no resets; the agents at the fixture's positions
+                h.reset[:] = 0
+                e.reset.zero_()
+                root[:, 0:3] = G[f"A{A}_pos"].reshape(n, 3)
             # oracle: post-simulate state in place, then post_physics_step
             h.actions[:] = a
             h.root[:], h.dof[:], h.sensors[:] = root, dof, sens
@@ -215,6 +224,13 @@ def test_fused_multi_agent_replay_matches_oracle_task_layer(lib, A):
             np.testing.assert_array_equal(np_(e.potentials), h.potentials)
             np.testing.assert_array_equal(np_(e.timeout).astype(np.uint8), h.timeout)
             assert np_(e.obs).shape[1] == 60 + 3 * (A - 1)
+            if t == 3:
+                reset_agents = np.zeros(n, bool)
+                reset_agents[G[f"A{A}_agent_ids"]] = True
+                np.testing.assert_array_equal(np_(e.progress) == 0, reset_agents)
+            if t == 4:
+                others = np_(e.obs)[:, 60:] + np.tile(np_(e.root)[:, 0:3], (1, A - 1))
+                np.testing.assert_allclose(others, G[f"A{A}_others"], atol=2e-6)
     finally:
         lib.mg_sim_destroy(sim)
 

@@ -130,13 +130,19 @@ def test_control_freq_inv_runs_simulate_twice(lib, task, n):
     assert bad.mean() < 1e-3, (bad.sum(), np.argwhere(bad)[:10])
 
 
-@pytest.mark.parametrize("task", ["Ant", "MAAnt", "ShadowHand"])
+@pytest.mark.parametrize("task", ["Ant", "MAAnt", "ShadowHand", "ShadowHand-asym"])
 def test_non_finite_state_flags_reset(task):
     """NaN guard: a NaN injected into one env's state gives that env reset = 1 (all its
-    agents under MA), reward 0 and a zero observation row; the next step's reset restores a finite state;
-    the other envs are untouched."""
+    agents under MA), reward 0 and a zero observation row (and, with asymmetric_observations, a zero
+    states row); the next step's reset restores a finite state; the other envs are untouched."""
     n = 64
-    env = migym.make(seed=0, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True)
+    asym = task.endswith("-asym")
+    task = task.split("-")[0]
+    cfg = configs.task_config(task, n, sim_device=DEV)
+    if asym:
+        cfg["env"]["asymmetric_observations"] = True
+    env = migym.make(seed=0, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True, cfg={"task": cfg})
+    assert env.num_states == (211 if asym else 0)
     A = env.num_agents
     g = torch.Generator(device=DEV).manual_seed(0)
     act = lambda: torch.rand((env.num_actors, env.num_actions), device=DEV, generator=g) * 2 - 1  # noqa: E731
@@ -155,6 +161,11 @@ def test_non_finite_state_flags_reset(task):
     others = torch.ones(env.num_actors, dtype=torch.bool, device=DEV)
     others[rows] = False
     assert bool(torch.isfinite(obs["obs"][others]).all())
+    if asym:
+        assert bool((obs["states"][e] == 0).all())
+        keep = torch.ones(n, dtype=torch.bool, device=DEV)
+        keep[e] = False
+        assert bool(torch.isfinite(obs["states"][keep]).all()) and bool((obs["states"][keep] != 0).any())
     for _ in range(2):   # ShadowHand resets in pre_physics (1 step), the locomotion tasks in post_physics
         obs, rew, reset, _ = env.step(act())
     torch.cuda.synchronize()

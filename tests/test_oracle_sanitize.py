@@ -1,5 +1,5 @@
 """The CPU oracle (the repo's only physics truth, SURVEY.md §5 "Race detection / sanitizers") under
-AddressSanitizer + UndefinedBehaviorSanitizer: `make -C oracle sanitize` builds build/liboracle_san.so and the
+AddressSanitizer + UndefinedBehaviorSanitizer: `make -C oracle sanitize` builds build_san/liboracle_san.so and the
 oracle test files run against it in a child python with the sanitizer runtimes preloaded (host code only; the
 GPU pool has no device sanitizers).  Any heap/stack overflow, use-after-free or UB aborts the child."""
 import os
@@ -23,7 +23,7 @@ def test_oracle_tests_clean_under_asan_ubsan():
     if not (asan and ubsan):
         pytest.skip("gcc sanitizer runtimes not installed")
     subprocess.check_call(["make", "-s", "-C", ORACLE, "sanitize"])
-    lib = os.path.join(ORACLE, "build", "liboracle_san.so")
+    lib = os.path.join(ORACLE, "build_san", "liboracle_san.so")
     env = dict(os.environ, MG_ORACLE_LIB=lib, LD_PRELOAD=f"{asan}:{ubsan}",
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     files = ["test_oracle_physics.py", "test_oracle_hand_physics.py", "test_oracle_golden.py", "test_dr.py"]
