@@ -40,18 +40,40 @@ def _cpu_model():
     return None
 
 
+def usable_cores():
+    """(threads to time on, how they were found): the CPUs this process may run on (sched_getaffinity),
+    capped by the cgroup CPU quota (cpu.max: quota / period, the box's CPU share) and by OMP_NUM_THREADS
+    when the launcher sets it.  nproc alone overstates it on the GPU boxes (the whole machine's CPUs)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n, how = aff, [f"sched_getaffinity {aff}"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            c = max(1, int(int(q) // int(per)))
+            how.append(f"cgroup cpu.max {c}")
+            n = min(n, c)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        how.append(f"OMP_NUM_THREADS {omp}")
+        n = min(n, int(omp))
+    return max(1, n), ", ".join(how)
+
+
 def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
     """The oracle's fp32 restatement of the same step (oracle/build/liboracle_f32.so: fp32 physics, fp32 task
     layer, OpenMP over envs), timed on this box's host cores at the workload's own env count on a bounded
-    sample of steps: once with every thread this process may use (OMP_NUM_THREADS, the box's CPU share for
-    one GPU; nproc and the CPU model are reported beside it) and once on 1 core.  The reference's
+    sample of steps: once with every core this process may use (``usable_cores``: affinity, cgroup quota,
+    OMP_NUM_THREADS; nproc and the CPU model are reported beside it) and once on 1 core.  The reference's
     pipeline=cpu PhysX path cannot run anywhere here (no isaacgym), so this is a port, not the reference."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     from migym import configs, model as M, taskdefs
     nproc = os.cpu_count() or 1
-    threads = max(1, min(nproc, int(os.environ.get("OMP_NUM_THREADS", str(nproc)))))
+    threads, usable = usable_cores()
     cfg = configs.task_config(task, n)
     base = "Ant" if task == "MAAnt" else task
     A = int(cfg["env"].get("numAgents", 1)) if task == "MAAnt" else 1
@@ -79,9 +101,9 @@ def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
     v, smp = leg(threads, n, seconds)
     v1, smp1 = leg(1, min(n, 8192), seconds)
     return {"value": v, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{smp}, {threads} OpenMP threads; oracle/ fp32 CPU restatement of the same step "
-                      f"(liboracle_f32.so), not PhysX",
-            "nproc": nproc, "cpu_model": _cpu_model(),
+            "sample": f"{smp}, {threads} OpenMP threads (every core this process may use: {usable}); oracle/ fp32 "
+                      f"CPU restatement of the same step (liboracle_f32.so), not PhysX",
+            "usable_cores": usable, "nproc": nproc, "cpu_model": _cpu_model(),
             "single_core": {"value": v1, "unit": "env-steps/s", "cores": 1, "sample": smp1}}
 
 

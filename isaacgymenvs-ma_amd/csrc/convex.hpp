@@ -24,17 +24,8 @@
 
 namespace mg {
 
-// the narrowphase scalar type: fp64 (an fp32 build, -DMG_CVX_REAL=float, is a host-harness experiment:
-// its GJK / MPR decisions near contact drift from the fp64 oracle)
-#ifndef MG_CVX_REAL
-#define MG_CVX_REAL double
-#endif
-typedef MG_CVX_REAL creal;
-// cvx_contact_v is inlined into the team kernel.  A real call (-DMG_CVX_INLINE='__attribute__((noinline))',
-// A/B only) is not safe in these kernels: see the note at cvx_contact_v.
-#ifndef MG_CVX_INLINE
-#define MG_CVX_INLINE __forceinline__
-#endif
+// the narrowphase scalar type (fp64, see the header note)
+typedef double creal;
 struct D3 {
   creal x, y, z;
 };
@@ -396,21 +387,20 @@ __device__ __forceinline__ CvxHit cvx_contact_body(CvxShape A, creal rA, D3 e, c
 }
 
 // The narrowphase entry: the core as five 3-vectors (segment: p0, p1; box: centre, half extents, the three
-// axis columns), the result by value.
-// Why it is inlined (NaN / wrong-state history of the egg kernels):
-//   * as a real call taking the shape by value (an aggregate past the register budget, passed through
-//     the caller's stack) and writing its outputs through generic pointers into the caller's private
-//     frame, its results changed with unrelated edits to the calling kernel: round 1 saw order-dependent
-//     NaN object states; in round 2, replacing the model-tile prologue (no change to any code the egg
-//     path runs) turned k_simulate's egg step nondeterministic and wrong in 84 % of envs
-//     (tools/egg_diag.py: run-to-run differences of metres, identical source of the narrowphase);
-//   * this pointer-free signature as a real call did not finish a 256-env step within a 120 s limit;
-//   * inlined, every variant is deterministic and follows the oracle to 2e-7 m.
-// Every one of the kernels carries ~350 spilled VGPRs and a 2.2 KB private frame, and the callee's
-// 48-byte frame sits above it; the failures are consistent with the call's frame or return address being
-// clobbered, which no source-level defect of the narrowphase explains.  cvx_tri's 0 / 0 on coincident
-// vertices is a separate, real edge case, guarded in both the kernel and the oracle.
-__device__ MG_CVX_INLINE CvxHit cvx_contact_v(int kind, D3 a0, D3 a1, D3 a2, D3 a3, D3 a4, creal rA, D3 e,
+// axis columns), the result by value.  A real call: the fp64 working set then lives in the callee's own
+// registers instead of spilling across the whole calling kernel (egg k_hand_step: 190 -> 98 spilled VGPRs,
+// +3.3 % env-steps/s, same-box A/B).
+//
+// The instance TUs are compiled with -mllvm -enable-ipra=false (build.py).  With interprocedural register
+// allocation on (the ROCm 7.2 LLVM default for AMDGPU), the caller keeps values across this call in
+// registers that IPRA's register-usage summary reports as preserved, and the callee clobbers some of them:
+// k_simulate's egg step then returned wrong object states in 222 of 256 envs (metres off, some NaN), and
+// an earlier build hung.  Measured (tools/gpu_egg_ab.sh on the states of egg_diag.py): the same source with
+// IPRA off is bit-reproducible and within 2.4e-7 m of the fp64 oracle; with IPRA on it fails with 8-wave
+// blocks and with 1-wave blocks alike (so no cross-wave LDS race is involved); the kernel descriptor's
+// private segment (1,600 B caller frame + 40 B callee frame = .private_segment_fixed_size 1,640, no dynamic
+// stack) covers the frames.  The earlier workaround was to force-inline the narrowphase.
+__device__ __attribute__((noinline)) CvxHit cvx_contact_v(int kind, D3 a0, D3 a1, D3 a2, D3 a3, D3 a4, creal rA, D3 e,
                                               creal cut) {
   CvxShape A;
   A.kind = kind;

@@ -146,30 +146,9 @@ __device__ __forceinline__ Sym6 body_inertia(float m, V3 c, const float* Ic) {
 }
 // reciprocal / square root / inverse square root of the physics: the 1-ulp hardware instructions instead
 // of the correctly rounded sequences (~10 instructions each); the task layer keeps IEEE division
-#ifndef MG_FAST_RCP
-#define MG_FAST_RCP 1
-#endif
-__device__ __forceinline__ float prcp(float x) {
-#if MG_FAST_RCP
-  return __builtin_amdgcn_rcpf(x);
-#else
-  return 1.0f / x;
-#endif
-}
-__device__ __forceinline__ float psqrt(float x) {
-#if MG_FAST_RCP
-  return __builtin_amdgcn_sqrtf(x);
-#else
-  return sqrtf(x);
-#endif
-}
-__device__ __forceinline__ float prsq(float x) {
-#if MG_FAST_RCP
-  return __builtin_amdgcn_rsqf(x);
-#else
-  return 1.0f / sqrtf(x);
-#endif
-}
+__device__ __forceinline__ float prcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float psqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float prsq(float x) { return __builtin_amdgcn_rsqf(x); }
 // Cholesky of a Sym6 into a packed lower-triangular 6x6 (21 floats); returns false if not SPD
 __device__ __forceinline__ bool chol6(const Sym6& I, float* L) {
   float M[6][6];

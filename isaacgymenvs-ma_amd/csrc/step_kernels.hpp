@@ -12,16 +12,6 @@
 #include "task.hpp"
 #include "team_physics.hpp"
 
-// Write-back of the per-step outputs (obs, state rows): read by the next kernel or the caller, never again by
-// this launch.  MG_NT_STORES=1 marks them non-temporal so they do not push the waves' scratch lines out of L2.
-#ifndef MG_NT_STORES
-#define MG_NT_STORES 0
-#endif
-#if MG_NT_STORES
-#define MG_STREAM_ST(p, x) __builtin_nontemporal_store((x), (p))
-#else
-#define MG_STREAM_ST(p, x) (*(p) = (x))
-#endif
 
 namespace mgi {
 #ifdef MG_PHASE_TIMING
@@ -44,9 +34,6 @@ static __device__ unsigned long long* g_phase_buf;
 #define MG_PHASE_FLUSH(t, item)
 #endif
 
-#ifndef MG_EXP
-#define MG_EXP 0  // profiling experiments only (phase attribution): skip parts of the hand post-physics
-#endif
 // ------------------------------------------------------------------------------------------------ launch shape
 // Waves per block W.  A block's W waves share one LDS model tile (each team's own LDS is per wave), so a
 // larger W leaves more of the CU's 160 KB LDS for resident waves; a smaller W lets the CU refill sooner
@@ -69,20 +56,13 @@ struct Shape {
       if (per_cu(w) > per_cu(best)) best = w;
     return best;
   }
-#ifdef MG_WAVES
-  static constexpr int W = MG_WAVES;  // A/B builds (tools/gpu_variants.sh)
-#else
   static constexpr int W = pick();
-#endif
   static constexpr int kThreads = 64 * W;
   static constexpr int E = E1 * W;  // teams per block
   static_assert(per_cu(W) >= 1, "one block must fit the CU's LDS");
 };
 
 // ------------------------------------------------------------------------------------------------ work queue
-#ifndef MG_WQ_ALL
-#define MG_WQ_ALL 0  // A/B: the work queue for one-wave blocks too
-#endif
 // The step kernels launch the resident capacity (as many blocks as the CUs hold at once, launch_wq) and
 // each wave loops over work items (one item = the E1 teams of one wave): its own index in the grid first,
 // then items dequeued from a device counter until they run out.  A CU thus refills a wave's slot as soon
@@ -123,11 +103,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
-  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
-#else
   mg::copy_tile(&tile, static_cast<const typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT*>(timg));
-#endif
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   const int team = threadIdx.x / T;
   const int a = blockIdx.x * E + team;
@@ -200,7 +176,7 @@ __device__ __forceinline__ void env_step_item(
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
   mg::TeamLDS<T, MN, MC>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP> t;
-  t.init(&L, &tile, m, &p, SH::W > 1 || MG_WQ_ALL);
+  t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
     t.drn = &drt[team].node[0][0];
@@ -358,24 +334,24 @@ __device__ __forceinline__ void env_step_item(
     float* o = tb.obs + (size_t)no * a;
     for (int q = t.tl; q < no; q += T) {
       const float x = bad ? 0.0f : ost[q];
-      MG_STREAM_ST(&o[q], x);
-      if (tb.obs_clamped) MG_STREAM_ST(&tb.obs_clamped[(size_t)no * a + q], mg::clampf(x, tp.clip_obs));
+      o[q] = x;
+      if (tb.obs_clamped) tb.obs_clamped[(size_t)no * a + q] = mg::clampf(x, tp.clip_obs);
     }
     if (tb.out_pack) {  // the gather's message row [clamped obs | rew | reset] (migym/dist.py)
       float* pk = tb.out_pack + (size_t)(no + 2) * a;
-      for (int q = t.tl; q < no; q += T) MG_STREAM_ST(&pk[q], bad ? 0.0f : mg::clampf(ost[q], tp.clip_obs));
+      for (int q = t.tl; q < no; q += T) pk[q] = bad ? 0.0f : mg::clampf(ost[q], tp.clip_obs);
       if (t.tl == 0) { pk[no] = rew; pk[no + 1] = (float)reset; }
     }
   }
   mg::wsync();
   if (valid) {  // state write-back (gym layouts), team-cooperative
     if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
-      for (int q = t.tl; q < 13; q += T) MG_STREAM_ST(&v.root_states[(size_t)13 * a + q], L.u.sv.st.root[q]);
-    for (int q = t.tl; q < 2 * nd; q += T) MG_STREAM_ST(&v.dof_state[(size_t)2 * nd * a + q], L.u.sv.st.dof[q]);
+      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
+    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.u.sv.st.dof[q];
     if (v.sensors)
-      for (int q = t.tl; q < 6 * ns; q += T) MG_STREAM_ST(&v.sensors[(size_t)6 * ns * a + q], L.u.sv.st.sens[q]);
+      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.u.sv.st.sens[q];
     if (v.dof_force)
-      for (int q = t.tl; q < nd; q += T) MG_STREAM_ST(&v.dof_force[(size_t)nd * a + q], L.u.sv.st.dforce[q]);
+      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
@@ -390,13 +366,9 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
-  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
-#else
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
-#endif
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
-  if constexpr (W == 1 && !MG_WQ_ALL) {
+  if constexpr (W == 1) {
     // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
     if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
   } else {
@@ -438,7 +410,7 @@ __device__ __forceinline__ void hand_step_item(
   const int nb = m->num_bodies, nbe = nb + 2;
   mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, OT> t;
-  t.init(&L, &tile, m, &p, SH::W > 1 || MG_WQ_ALL);
+  t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
     t.drn = &drt[team].node[0][0];
@@ -546,15 +518,12 @@ __device__ __forceinline__ void hand_step_item(
   // rigid-body states of the hand once (one lane per body) into the dead row storage: the fingertip
   // observations and the rigid_body_states write-back both read them
   float* bst = &L.u.sv.rows[0].b;
-#if !(MG_EXP & 1)
   if constexpr (RP) {
     for (int k = t.tl; k < 13 * nb; k += T) bst[k] = rp.rigid_body_states[(size_t)13 * nbe * ec + k];
   } else {
     for (int b = t.tl; b < nb; b += T) t.body_state(b, bst + 13 * b);
   }
-#endif
   mg::wsync();
-#if !(MG_EXP & 2)
   {
     const float* gs = L.goal + 13;
     float qdiff[4];
@@ -575,11 +544,10 @@ __device__ __forceinline__ void hand_step_item(
       L.obs[k] = x;
     }
   }
-#endif
   mg::wsync();
   int64_t ro = 0;
   float fin = 0.0f;
-  if (!(MG_EXP & 4) && t.tl == 0) {
+  if (t.tl == 0) {
     const float* gs = L.goal + 13;
     float succ = env_reset ? 0.0f : tb.successes[ec], rew;
     int64_t prog = progress_in + 1, go;
@@ -616,7 +584,7 @@ __device__ __forceinline__ void hand_step_item(
     atomicAdd((unsigned long long*)&tb.reduce_scratch[0], cr);
     atomicAdd((unsigned long long*)&tb.reduce_scratch[1], cf);
   }
-  if (!(MG_EXP & 8) && valid) {  // write-back (gym layouts), team-cooperative
+  if (valid) {  // write-back (gym layouts), team-cooperative
     float* o = tb.obs + (size_t)no * e;
     for (int k = t.tl; k < no; k += T) {
       const float x = bad ? 0.0f : L.obs[k];
@@ -680,13 +648,9 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  #ifdef MG_TILE_DEVICE  // A/B: derive the tile in every block from the model tables
-  mg::build_tile(&tile, m, threadIdx.x, blockDim.x);
-#else
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, 16 * MG>*>(timg));
-#endif
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
-  if constexpr (W == 1 && !MG_WQ_ALL) {  // as k_env_step
+  if constexpr (W == 1) {  // as k_env_step
     if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
   } else {
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
@@ -727,7 +691,7 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
   }
   const int items = (sim->n + SH::E1 - 1) / SH::E1;
   const int need = (items + SH::W - 1) / SH::W;
-  if (SH::W == 1 && !MG_WQ_ALL) {  // the kernels' one-wave-block path: the static grid, one block per item
+  if (SH::W == 1) {  // the kernels' one-wave-block path: the static grid, one block per item
     hipLaunchKernelGGL(kern, dim3(need), dim3(SH::kThreads), 0, s, args..., sim->d_wq);
     return MG_OK;
   }

@@ -41,12 +41,7 @@ namespace mg {
 // reference arithmetic in task.hpp / hand_task.hpp keeps contraction off).  The caller's FP state is
 // restored at the end of this header.
 #pragma float_control(push)
-#ifndef MG_PHYS_FMA
-#define MG_PHYS_FMA 1
-#endif
-#if MG_PHYS_FMA
 #pragma clang fp contract(fast)
-#endif
 
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
 // every per-node / per-geom constant is an LDS read (~64 cycles) instead of a dependent global load.
@@ -134,10 +129,6 @@ __device__ __forceinline__ void copy_tile(MT* t, const MT* img) {
 // a wave's LDS operations complete in order; the wavefront-scope fences keep the compiler from moving
 // LDS accesses across the point).  No s_barrier: the other waves of the block run on independently.
 __device__ __forceinline__ void wsync() {
-#ifdef MG_WSYNC_BLOCK  // A/B: the block barrier (one-wave blocks only)
-  __syncthreads();
-  return;
-#endif
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -145,49 +136,24 @@ __device__ __forceinline__ void wsync() {
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
 
-#ifndef MG_PGS_PREFETCH
-#define MG_PGS_PREFETCH 4  // PGS visits per block of the sweep (their data are loaded one block ahead)
-#endif
-#ifndef MG_PGS_EARLY
-#define MG_PGS_EARLY 1  // issue a block's private J/Y loads one whole block ahead (compiler barrier)
-#endif
-#ifndef MG_DROP_TREE
-#define MG_DROP_TREE 1  // free the tree phases' per-lane state before the PGS sweeps (drop_tree_state)
-#endif
-#ifndef MG_TS_LDS
-#define MG_TS_LDS 1  // test-solve forward pass: ancestors' y rows through LDS (0: one bpermute per column)
-#endif
-#ifndef MG_JY_REGS
-#define MG_JY_REGS 12  // rows of (J, Y) columns kept in registers; the rest in private (scratch) arrays
-                       // (same-box A/B vs 16: Ant +0.8 %, Humanoid +0.8 %, ShadowHand +0.6 %; 8 and 20 slower)
-#endif
-#ifndef MG_JY_REGS_WIDE
-#define MG_JY_REGS_WIDE MG_JY_REGS  // the same for 32- and 64-lane locomotion teams (Humanoid)
-#endif
-#ifndef MG_ROWREC_LANES
-#define MG_ROWREC_LANES 1  // a test-solve block's row records written lane-parallel (0: team lane 0, row by row)
-#endif
-#ifndef MG_JY_REGS_OBJ
-#define MG_JY_REGS_OBJ MG_JY_REGS  // hand teams (block, pen; the egg keeps every row in scratch)
-#endif
-#ifndef MG_RB_WIDE
-#define MG_RB_WIDE 12  // test-solve columns per batch for 32-lane locomotion teams (a multiple of 3)
-#endif
-#ifndef MG_RB_NARROW
-#define MG_RB_NARROW 12  // test-solve columns per batch for 16-lane locomotion teams (a multiple of 3, <= T):
-                         // 12 walkers instead of 6 halve the batches per substep (same-box A/B, 400 steps:
-                         // Ant 129.3 -> 130.2 M, MA-Ant 29.3 -> 29.6 M env-steps/s); hand teams and Cartpole keep 6
-#endif
+// PGS visits per block of the sweep (their data are loaded one block ahead; 2 and 8 measured slower)
+constexpr int kPgsPrefetch = 4;
+// rows whose (J, Y) columns stay in registers; the rest live in private (scratch) arrays (same-box A/B vs 16:
+// Ant +0.8 %, Humanoid +0.8 %, ShadowHand +0.6 %; 8 and 20 slower).  The egg keeps every row in scratch.
+constexpr int kJYRegs = 12;
+// test-solve columns per batch (a multiple of 3): 12 for the 16- and 32-lane locomotion teams (12 walkers
+// instead of 6 halve the batches per substep: Ant +0.7 %, MA-Ant +1.0 %; 15 columns -3.5 %, 9 or 18 for
+// 32-lane teams -5 % / -34 %); hand teams and Cartpole keep 6
+constexpr int kRBLoco = 12;
 
 template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
-  static constexpr int MR = (3 * MC + 2 * (MN - 1) + MG_PGS_PREFETCH - 1) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;
-  static constexpr int RB = OBJ ? 6 : (T >= 32 ? MG_RB_WIDE : (MG_RB_NARROW <= T ? MG_RB_NARROW : 6));
+  static constexpr int MR = (3 * MC + 2 * (MN - 1) + kPgsPrefetch - 1) / kPgsPrefetch * kPgsPrefetch;
+  static constexpr int RB = OBJ ? 6 : (kRBLoco <= T ? kRBLoco : 6);
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
   // (not for the egg instance, whose fp64 narrowphase already spills: 7.46 vs 7.71 M env-steps/s measured)
-  static constexpr int KRW = OBJ ? MG_JY_REGS_OBJ : (T >= 32 ? MG_JY_REGS_WIDE : MG_JY_REGS);
-  static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (KRW < MR ? KRW : MR) / MG_PGS_PREFETCH * MG_PGS_PREFETCH;  // right-hand sides per test solve (rows of 2-4 contacts)
+  static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (kJYRegs < MR ? kJYRegs : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -1007,7 +973,6 @@ struct Team {
     ph_mark(11);
     // proper ancestors below the root, visited in increasing depth (= increasing index)
     unsigned long long path = node > 0 ? (s->anc[node] & ~1ull & ~(1ull << node)) : 0ull;
-#if MG_TS_LDS
     // the level's y values are published in the (now read) ut slab, RB floats per node, and every deeper
     // lane reads its ancestor's row: a few wide LDS accesses per level instead of RB bpermutes
     float* ybuf = &ts.ut[0][0];
@@ -1031,26 +996,6 @@ struct Team {
         for (int q = 0; q < L::RB; q++) rem[q] -= C * ya[q];
       }
     }
-#else
-    for (int lev = 1; lev <= maxdepth; lev++) {
-      if (node > 0 && depth == lev) {
-#pragma unroll
-        for (int q = 0; q < L::RB; q++) yv[q] = rem[q] * Dinv;
-      }
-      if (lev < maxdepth) {
-        const bool deeper = node > 0 && depth > lev;
-        const int an = deeper ? __builtin_ctzll(path) : 1;
-        if (deeper) path &= path - 1;
-        const int src = deeper ? tb + ncol0 + an - 1 : (int)(threadIdx.x & 63);
-        const float C = deeper ? dot(U, sv(ld3(s->S[an]), ld3(s->S[an] + 3))) : 0.0f;
-#pragma unroll
-        for (int q = 0; q < L::RB; q++) {
-          const float ya = __shfl(yv[q], src);
-          rem[q] -= C * ya;
-        }
-      }
-    }
-#endif
     ph_mark(12);
 #pragma unroll
     for (int q = 0; q < L::RB; q++) {
@@ -1301,11 +1246,7 @@ struct Team {
     if (ty == MG_GT_CONVEX)  // block: hull vertices + the box's 8; pen: hull vertices + its 2 ends; egg: GJK
       return ot == MG_GT_BOX ? mt->hnv + 8 : (ot == MG_GT_CAPSULE ? mt->hnv + 2 : 1);
     if (!round && ty != MG_GT_BOX) return 0;
-#ifdef MG_NO_EDGE  // A/B only: without the edge-edge candidate (the oracle always has it)
-    if (ot == MG_GT_BOX) return round ? 1 : 16;
-#else
     if (ot == MG_GT_BOX) return round ? 1 : 17;  // box: 8 + 8 vertex-face, 1 edge-edge
-#endif
     if (ot == MG_GT_CAPSULE) return round ? 1 : 3;
     return 1;
   }
@@ -1609,9 +1550,6 @@ struct Team {
       for (unsigned long long mm = live; mm; mm &= mm - 1)
         if (mt->gtype[__builtin_ctzll(mm)] == MG_GT_CONVEX) hull_live |= mm & (~mm + 1ull);
       live &= ~hull_live;
-#ifdef MG_NO_HULL  // A/B only: the convex-mesh geom's object contacts skipped
-      hull_live = 0ull;
-#endif
       for (unsigned long long hm = hull_live; hm; hm &= hm - 1) {
         const int g = __builtin_ctzll(hm);
         V3 c;
@@ -1888,29 +1826,22 @@ struct Team {
           MG_JSET(r, J, y);
           const float Wr = team_sum<T>(J * y, tb);
           wq[q] = Wr;
-#if !MG_ROWREC_LANES
-          if (tl == 0) row_record(r, Wr);
-#endif
         }
       }
-#if MG_ROWREC_LANES
       {  // the block's row records, lane q writes row r0 + q: one divergent region instead of RB
         float Wr = wq[0];
 #pragma unroll
         for (int q = 1; q < L::RB; q++) Wr = tl == q ? wq[q] : Wr;
         if (tl < L::RB && r0 + tl < wave_rows) row_record(r0 + tl, Wr);
       }
-#endif
       ph_mark(5);
     }
     // The sweep runs over prow rows, the row count rounded up to a multiple of the prefetch depth PF
     // (so a row's impulse is never read ahead of its previous visit's write, and the unrolled loop
     // needs no per-visit guards): the padding rows have J = Y = 0 and 1/W = 0, i.e. they are skipped
     // as the oracle skips W = 0 rows.
-#if MG_DROP_TREE
     drop_tree_state();
-#endif
-    constexpr int PF = MG_PGS_PREFETCH;
+    constexpr int PF = kPgsPrefetch;
     static_assert(MR % PF == 0, "row capacity must be a multiple of the PGS prefetch depth");
     const int prow = wave_rows == 0 ? 0 : ((wave_rows + PF - 1) / PF) * PF;
     for (int r = wave_rows; r < prow; r++) MG_JSET(r, 0.0f, 0.0f);
@@ -1978,7 +1909,6 @@ struct Team {
       }
       for (int r0 = KR; r0 < prow; r0 += PF) {
         const int rn = r0 + PF == prow ? KR : r0 + PF;  // next block of part B (wraps into the next sweep)
-#if MG_PGS_EARLY
         // the next block's private J/Y (scratch, L2 latency) are issued before this block's visits; the
         // compiler barrier keeps the scheduler from sinking them behind the first visits
         float nJ[PF], nY[PF];
@@ -1988,17 +1918,11 @@ struct Team {
           nY[k] = Ys[rn - KR + k];
         }
         asm volatile("" ::: "memory");
-#endif
 #pragma unroll
         for (int k = 0; k < PF; k++) {
           visit(pJ[k], pY[k], pR[k], r0 + k);
-#if MG_PGS_EARLY
           pJ[k] = nJ[k];
           pY[k] = nY[k];
-#else
-          pJ[k] = Js[rn - KR + k];
-          pY[k] = Ys[rn - KR + k];
-#endif
           pR[k] = s->u.sv.rows[rn + k];
         }
       }

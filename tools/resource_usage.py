@@ -11,7 +11,7 @@ src = sys.argv[1] if len(sys.argv) > 1 else "isaacgymenvs-ma_amd/csrc/migym.hip"
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-c", "--cuda-device-only",
        "-Rpass-analysis=kernel-resource-usage", "-o", "/dev/null", src] + sys.argv[2:]
 if src.endswith("inst.hip"):  # the instance TUs' build flags (build.py)
-    cmd += ["-mllvm", "-disable-machine-licm"]
+    cmd += ["-mllvm", "-disable-machine-licm", "-mllvm", "-enable-ipra=false"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
