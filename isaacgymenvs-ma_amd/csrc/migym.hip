@@ -533,6 +533,13 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
       return fail(MG_EINVAL, "mg_sim_create: nodes must be topologically ordered (parent < child)");
   if (params->substeps < 1 || params->dt <= 0.0f || params->max_contacts < 0)
     return fail(MG_EINVAL, "mg_sim_create: bad sim params");
+  // the exact hull-object candidates are computed before the tree phases (team_physics.hpp hull_stage), from
+  // the fixed root's pose: a convex-mesh geom colliding with a block / pen object must sit on that root
+  if (model->obj_type == MG_GT_BOX || model->obj_type == MG_GT_CAPSULE)
+    for (int g = 0; g < model->num_geoms; g++)
+      if (model->geom_type[g] == MG_GT_CONVEX && (model->geom_filter[g] & MG_COLLIDE_OBJECT) &&
+          (model->geom_node[g] != 0 || !model->fixed_base))
+        return fail(MG_EINVAL, "mg_sim_create: a convex-mesh geom against the object must be on the fixed root");
   if (hipSetDevice(device) != hipSuccess) return fail(MG_EDEVICE, "mg_sim_create: hipSetDevice failed");
   mg_sim* s = new (std::nothrow) mg_sim();
   if (!s) return fail(MG_ENOMEM, "mg_sim_create: out of host memory");

@@ -42,7 +42,7 @@ static __device__ unsigned long long* g_phase_buf;
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
 struct Shape {
   static constexpr int E1 = 64 / T;  // teams (actors) per wave
-  static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP>);
+  static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>);
   static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T>) +
                                         (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
   static constexpr int per_cu(int w) {
@@ -702,7 +702,7 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
 
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int BuildTile<T, MN, MC, MG, MP, OBJ>::run(mg_sim* sim) {
-  using MT = mg::ModelTile<MN, MG, MP>;
+  using MT = mg::ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>;   // the kernels' tile type (Team::MT)
   MT* img = new (std::nothrow) MT();
   if (!img) return fail(MG_ENOMEM, "mg_sim_create: out of host memory (model tile)");
   mg::build_tile(img, &sim->host_model);

@@ -32,6 +32,7 @@
 #include "../../include/migym.h"
 #include "convex.hpp"
 #include "device_math.hpp"
+#include "hull.hpp"
 
 #include <type_traits>
 
@@ -47,7 +48,7 @@ namespace mg {
 // every per-node / per-geom constant is an LDS read (~64 cycles) instead of a dependent global load.
 // Rows padded to odd strides.  The image is built once on the host (build_tile, at mg_sim_create) and
 // each block copies it with 16-byte loads; the W waves of a block share one copy.
-template <int MN, int MG, int MP, int OC = 1>  // OC: unused (kept in the instance signatures)
+template <int MN, int MG, int MP, int OC = 1>  // OC > 1: the free-object (hand) instances
 struct alignas(16) ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
@@ -61,6 +62,11 @@ struct alignas(16) ModelTile {
   int pairs[MP > 0 ? MP : 1][2];
   int nn, ng, np;
   int hnv;            // vertices of the convex-mesh geom's hull (mg_model.hull_*), 0 if none
+  int hullg;          // the convex-mesh geom (-1 if none)
+  // hand instances: the hull's vertices and their centroid for the exact hull candidates (hull.hpp), read by
+  // every GJK support; its planes stay in global memory (one pass per call)
+  float hv[OC > 1 ? MG_MAX_HULL_VERTS : 1][3];
+  float hctr[4];
 };
 
 // host: the finished tile image of model m (child masks, rest rotations as matrices, geom frames)
@@ -113,7 +119,25 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model
     t->pairs[q][0] = m->pair[q][0];
     t->pairs[q][1] = m->pair[q][1];
   }
-  if (tid == 0) { t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; t->hnv = m->hull_num_verts; }
+  if (tid == 0) {
+    t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; t->hnv = m->hull_num_verts;
+    t->hullg = -1;
+    for (int g = ng - 1; g >= 0; g--)
+      if (m->geom_type[g] == MG_GT_CONVEX) t->hullg = g;
+    t->hctr[0] = t->hctr[1] = t->hctr[2] = t->hctr[3] = 0.0f;
+    if (OC > 1 && m->hull_num_verts > 0) {
+      float cx = 0.0f, cy = 0.0f, cz = 0.0f;
+      for (int v = 0; v < m->hull_num_verts; v++) {
+        for (int k = 0; k < 3; k++) t->hv[v][k] = m->hull_vert[v][k];
+        cx += m->hull_vert[v][0];
+        cy += m->hull_vert[v][1];
+        cz += m->hull_vert[v][2];
+      }
+      t->hctr[0] = cx / (float)m->hull_num_verts;
+      t->hctr[1] = cy / (float)m->hull_num_verts;
+      t->hctr[2] = cz / (float)m->hull_num_verts;
+    }
+  }
 }
 
 // device: the block copies the prebuilt image (global) into its LDS tile, 16 bytes per lane and load
@@ -222,6 +246,10 @@ struct TeamLDS {
   float oroot[OBJ ? 13 : 1];
   float goal[OBJ ? 26 : 1];   // goal actor root row, goal_states row
   float oforce[OBJ ? 4 : 1];  // external force on the object (apply_rigid_body_force_tensors), [3] = local
+  // block / pen: the exact hull candidates of this substep (Team::hull_stage -> collide), world frame
+  static constexpr int HX = (OBJ == MG_GT_BOX || OBJ == MG_GT_CAPSULE) ? 2 : 0;
+  float hx[HX > 0 ? HX : 1][7];
+  int hxn;
 };
 
 // A team's LDS region padded so that consecutive teams start 4*T bytes apart modulo 128 B.  A
@@ -1243,8 +1271,8 @@ struct Team {
   __device__ __forceinline__ int ocand_count(int ty) const {
     const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
     constexpr int ot = OBJ;
-    if (ty == MG_GT_CONVEX)  // block: hull vertices + the box's 8; pen: hull vertices + its 2 ends; egg: GJK
-      return ot == MG_GT_BOX ? mt->hnv + 8 : (ot == MG_GT_CAPSULE ? mt->hnv + 2 : 1);
+    if (ty == MG_GT_CONVEX)  // block: hull vertices + the box's 8 + exact; pen: hull vertices + its 2 ends + exact
+      return ot == MG_GT_BOX ? mt->hnv + 9 : (ot == MG_GT_CAPSULE ? mt->hnv + 3 : 1);
     if (!round && ty != MG_GT_BOX) return 0;
     if (ot == MG_GT_BOX) return round ? 1 : 17;  // box: 8 + 8 vertex-face, 1 edge-edge
     if (ot == MG_GT_CAPSULE) return round ? 1 : 3;
@@ -1323,6 +1351,82 @@ struct Team {
     *pt = mul(Rg, ((P - nb * ro) + cb) * 0.5f) + c;
     *nrm = mul(Rg, nb) * -1.0f;
     return true;
+  }
+
+  // The exact hull candidates of this substep (hull.hpp), before the tree phases: the convex-mesh geom is on the
+  // hand's fixed root (checked at launch), so its world frame (built as fk() + geom_world() build it) and the
+  // object's pose are the ones collide() sees, and the fp64 narrowphase runs where little else is live.  The
+  // broadphase is collide()'s (the geom's bounding sphere, then its box against the object's sphere).
+  __device__ __forceinline__ void hull_stage() {
+    if constexpr (L::HX > 0) {
+      const int g = mt->hullg;
+      int nx = 0;
+      float res[14];
+      V3 c = v3(0, 0, 0);
+      M3 Rg;
+      if (g >= 0 && (mt->gfil[g] & MG_COLLIDE_OBJECT)) {
+        const M3 R0 = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
+        const float* gf = mt->gf[g];
+        M3 Rl;
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) Rl.m[a][b] = gf[3 + 3 * a + b];
+        c = p0 + mul(R0, ld3(gf));
+        Rg = mul(R0, Rl);
+        const float ro = obj_radius(), off = p->contact_offset;
+        const V3 dc = c - op;
+        const float reach = gf[15] + ro + off;
+        if (dot(dc, dc) <= reach * reach && hull_box_near(c, Rg, ld3(gf + 12), op, ro, off)) {
+          const M3 oRs = quat_to_mat(oq[0], oq[1], oq[2], oq[3]);
+          HullCore B;
+          float rB;
+          const V3 os = osize();
+          if constexpr (OBJ == MG_GT_BOX) {
+            B.kind = 1;
+            B.c = mulT(Rg, op - c);
+            for (int a = 0; a < 3; a++)
+              for (int b = 0; b < 3; b++)
+                B.R.m[a][b] = Rg.m[0][a] * oRs.m[0][b] + Rg.m[1][a] * oRs.m[1][b] + Rg.m[2][a] * oRs.m[2][b];
+            const float mg = fminf(HULL_MARGIN, 0.5f * fminf(os.x, fminf(os.y, os.z)));
+            B.h = v3(os.x - mg, os.y - mg, os.z - mg);
+            rB = mg;
+          } else {
+            const V3 oz = v3(oRs.m[0][2], oRs.m[1][2], oRs.m[2][2]) * os.y;
+            B.kind = 0;
+            B.p0 = mulT(Rg, (op - oz) - c);
+            B.p1 = mulT(Rg, (op + oz) - c);
+            rB = os.x;
+          }
+          // a lower bound of the object's distance to the hull from its plane distances (each plane's distance is
+          // at most the true one): the cube's centre minus its circumradius, or the pen's segment by max over the
+          // planes of the nearer end (max_f min_t <= min_t max_f); at or beyond the offset there is no contact
+          float lb = -3.0e38f;
+          const int np = m->hull_num_planes;
+#pragma unroll
+          for (int k = 0; k < (MG_MAX_HULL_PLANES + T - 1) / T; k++) {  // one batch of loads, then the reduction
+            const int f = tl + k * T;
+            if (f < np) {
+              const float4 q = *reinterpret_cast<const float4*>(m->hull_plane[f]);
+              const V3 nf = v3(q.x, q.y, q.z);
+              const float sd = B.kind == 1 ? dot(nf, B.c) - q.w : fminf(dot(nf, B.p0), dot(nf, B.p1)) - q.w;
+              lb = fmaxf(lb, sd);
+            }
+          }
+          lb = team_max_dpp<T>(lb);
+          lb -= B.kind == 1 ? sqrtf(dot(os, os)) : rB;
+          if (lb < off)
+            nx = hull_core_contacts<T>(mt->hv, mt->hnv, ld3(mt->hctr), m->hull_plane, np, tl, tb, B, rB, off, res);
+        }
+      }
+      if (tl == 0) {
+        for (int i = 0; i < nx; i++) {
+          const V3 pw = mul(Rg, ld3(res + 7 * i)) + c, nw = mul(Rg, ld3(res + 7 * i + 3));
+          s->hx[i][0] = pw.x; s->hx[i][1] = pw.y; s->hx[i][2] = pw.z;
+          s->hx[i][3] = nw.x; s->hx[i][4] = nw.y; s->hx[i][5] = nw.z;
+          s->hx[i][6] = res[7 * i + 6];
+        }
+        s->hxn = nx;
+      }
+    }
   }
 
   __device__ __forceinline__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
@@ -1616,6 +1720,13 @@ struct Team {
           if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
         }
         base += tot;
+        // (3) block / pen: the exact candidates, computed at the start of the substep (hull_stage)
+        if constexpr (L::HX > 0) {
+          const int nx = s->hxn;
+          if (tl < nx && base + tl < cap)
+            put_contact(base + tl, ld3(s->hx[tl]), ld3(s->hx[tl] + 3), s->hx[tl][6], mt->gnode[g], g, OBJ_NODE, -2);
+          base += nx;
+        }
       }
       int NC = 0;
       for (unsigned long long mm = live; mm; mm &= mm - 1) NC += ocand_count(mt->gtype[__builtin_ctzll(mm)]);
@@ -1742,6 +1853,7 @@ struct Team {
   // ---------------------------------------------------------------- one substep
   __device__ __forceinline__ void substep() {
     ph_mark(15);
+    hull_stage();
     fk();
     set_axis();
     ph_mark(0);

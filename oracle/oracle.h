@@ -60,6 +60,7 @@ int orc_ellipsoid_contact(int32_t kind, const double* shape, double radius, cons
 int orc_box_box_edge(const double* shape, const double* hb, double off, double* out);
 /* the convex-mesh geom's plane distance of n geom-frame points: out = (distance, face) per point */
 int orc_hull_distance(const mg_model* m, const double* pl, int32_t n, double* out);
+int orc_hull_core_contact(const mg_model* m, const double* shape, double rB, double off, double* out);
 /* world poses of the gym rigid bodies (n_bodies x 13, velocity at body COM) */
 int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out);
 

@@ -694,6 +694,10 @@ static int box_box_edge(const real* c, real R[3][3], const real* hg, const real*
   return 1;
 }
 
+/* the hull against the object's core, exactly (defined with the convex narrowphase below) */
+static int hull_object_exact(const mg_model* m, const kin* k, int g, const real* c, real R[3][3], real off,
+                             contact* out, int n, int cap);
+
 /* hand geom g (A) vs the object box (B); normal points from the object to the geom */
 static int geom_object(const mg_model* m, const kin* k, int g, real off, contact* out, int n, int cap) {
   const real hb[3] = {m->obj_size[0], m->obj_size[1], m->obj_size[2]};
@@ -757,7 +761,8 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
         n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
       }
     }
-    return n;
+    /* edge against edge / edge across a face: the exact distance of the hull and the box */
+    return hull_object_exact(m, k, g, c, R, off, out, n, cap);
   }
   if (ty != MG_GT_BOX) return n;
   const real hg[3] = {m->geom_size[g][0], m->geom_size[g][1], m->geom_size[g][2]};
@@ -1189,11 +1194,389 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
   *d = -rA;
 }
 
+/* ---- the convex-mesh hull against the object's core, exactly (ShadowHand block / pen) --
+ * The vertex-face candidates above (hull vertices against the object, the object's vertices / end spheres
+ * against the hull's faces) miss the configurations whose closest features are both interior: a cube edge
+ * across a hull edge, the pen across a ridge of the hull, the pen lying across a face its ends overhang.
+ *
+ * GJK on the Minkowski difference hull - core in the hull's geom frame, fp64: A = the hull (support: its
+ * vertices, ties to the lowest index), B = the object's core: the cube shrunk by HULL_MARGIN and rounded by it
+ * (the rounded core finds the features; an edge-edge contact is then placed on the sharp edges), or the pen's segment with the
+ * pen's radius.  When the cores overlap, MPR from the interior point (hull vertex centroid - core centre) gives
+ * the penetration (so with the 1 mm rounding a cube resting up to 1 mm deep stays with GJK, whose closest
+ * features are unique; MPR's portal point is not).  The features at the witnesses decide: on the hull, the planes within HULL_FEAT_EPS of the
+ * hull witness (1 = a face, 2 = an edge: their cross product its direction, >= 3 = a vertex); on the core, the
+ * box's face planes through its witness (1, 2, 3), or the segment parameter (an end or the interior).
+ *   * edge against edge: one contact, unless the edges are within 5 deg of parallel or one
+ *     edge is within 2 deg of parallel to a face of the other shape (then the closest pair is not unique and
+ *     the configuration is an edge lying on a face, whose ends are vertex-face candidates; for the pen, the
+ *     face case below);
+ *   * the pen's interior over a hull face (the face, or a face of the witness edge the pen lies parallel to):
+ *     the segment, projected onto the face's plane, is clipped by every other plane of the hull to the part
+ *     over the face, [t0, t1]; each end strictly inside the segment (an end of the pen over the face is its end
+ *     sphere's candidate) is a contact with the face's normal and its own plane gap.  A pen lying flat across a
+ *     face rests on two points, and the contacts move continuously with the pose;
+ *   * anything else has a vertex among its closest features: the vertex-face candidates' case.
+ * Normal from the object to the hull, point halfway between the surfaces. */
+#define HULL_MAXV 256
+#define HULL_MARGIN 1e-3       /* rounding of the cube's core against the hull (m) */
+#define HULL_FEAT_EPS 1e-6     /* a witness lies on a plane within this (m) */
+#define HULL_SIN_PARALLEL 0.0871557427476582  /* sin 5 deg: edges closer to parallel are no edge-edge contact */
+#define HULL_SIN_ON_FACE 0.0348994967025010   /* sin 2 deg: an edge closer to a face's plane lies on the face */
+#define HULL_CLIP_EPS 1e-9     /* slack of the face clipping (m) */
+static void hull_support(const real (*hv)[3], int nv, const cvx_shape* B, const real* d, real* w) {
+  real best = -1e300;
+  int bi = 0;
+  for (int v = 0; v < nv; v++) {
+    const real s = hv[v][0] * d[0] + hv[v][1] * d[1] + hv[v][2] * d[2];
+    if (s > best) { best = s; bi = v; }
+  }
+  real nd[3] = {-d[0], -d[1], -d[2]}, b[3];
+  cvx_support(B, nd, b);
+  for (int a = 0; a < 3; a++) w[a] = hv[bi][a] - b[a];
+  (void)0;
+}
+/* the hull-side support point (the vertex) of direction d: GJK / MPR keep it for the witness */
+static void hull_vertex_of(const real (*hv)[3], int nv, const real* d, real* o) {
+  real best = -1e300;
+  int bi = 0;
+  for (int v = 0; v < nv; v++) {
+    const real s = hv[v][0] * d[0] + hv[v][1] * d[1] + hv[v][2] * d[2];
+    if (s > best) { best = s; bi = v; }
+  }
+  v3cp(o, hv[bi]);
+}
+/* 2 = farther than cut, 1 = separated (pa, pb: hull / core witnesses, dist), 0 = overlapping */
+static int hull_gjk(const real (*hv)[3], int nv, const real* v0, const cvx_shape* B, real cut, real* pa, real* pb,
+                    real* dist) {
+  real W[4][3], P[4][3], v[3] = {v0[0], v0[1], v0[2]};
+  if (dot3(v, v) < 1e-20) { v[0] = 0; v[1] = 0; v[2] = 1; }
+  int n = 0;
+  real vv = dot3(v, v);
+  real lam[4] = {0, 0, 0, 0};
+  for (int it = 0; it < 64; it++) {
+    real nd[3] = {-v[0], -v[1], -v[2]}, w[3], a[3];
+    hull_support(hv, nv, B, nd, w);
+    const real vw = dot3(v, w);
+    if (vw > 0 && vw * vw > vv * cut * cut) {
+      *dist = vw / sqrt(vv);
+      return 2;
+    }
+    if (n > 0 && vv - vw <= 1e-10 * vv + 1e-24) break;
+    int dup = 0;
+    for (int i = 0; i < n; i++) {
+      real dd[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
+      if (dot3(dd, dd) <= 1e-24) dup = 1;
+    }
+    if (dup) break;
+    hull_vertex_of(hv, nv, nd, a);
+    for (int k = 0; k < 3; k++) { W[n][k] = w[k]; P[n][k] = a[k]; }
+    n++;
+    if (cvx_simplex(W, P, &n, v, lam)) return 0;
+    const real vn = dot3(v, v);
+    if (vn <= 1e-20) return 0;
+    const int stall = it > 0 && vn >= vv * (1.0 - 1e-14);
+    vv = vn;
+    if (stall) break;
+  }
+  for (int k = 0; k < 3; k++) {
+    pa[k] = 0;
+    for (int i = 0; i < n; i++) pa[k] += lam[i] * P[i][k];
+    pb[k] = pa[k] - v[k];
+  }
+  *dist = sqrt(vv);
+  return 1;
+}
+/* MPR on hull - core from the interior point v0: x = the boundary point (moving the hull by -x separates),
+ * pa = the hull-side witness; 0 if the portal search degenerates */
+static void hull_mpr_support(const real (*hv)[3], int nv, const cvx_shape* B, const real* d, real* w, real* a) {
+  hull_support(hv, nv, B, d, w);
+  hull_vertex_of(hv, nv, d, a);
+}
+static int hull_mpr(const real (*hv)[3], int nv, const real* v0, const cvx_shape* B, real* x, real* pa) {
+  real V[5][3], Pa[5][3], dir[3];
+  v3cp(V[0], v0);
+  if (dot3(V[0], V[0]) < 1e-20) { V[0][0] = 1e-6; V[0][1] = 0; V[0][2] = 0; }
+  for (int k = 0; k < 3; k++) dir[k] = -V[0][k];
+  v3unit(dir);
+  hull_mpr_support(hv, nv, B, dir, V[1], Pa[1]);
+  if (dot3(V[1], dir) <= 0) return 0;
+  cross3(V[0], V[1], dir);
+  if (dot3(dir, dir) <= 1e-24) {
+    v3cp(x, V[1]);
+    v3cp(pa, Pa[1]);
+    return 1;
+  }
+  v3unit(dir);
+  hull_mpr_support(hv, nv, B, dir, V[2], Pa[2]);
+  if (dot3(V[2], dir) <= 0) return 0;
+  real va[3], vb[3];
+  v3sub(V[1], V[0], va);
+  v3sub(V[2], V[0], vb);
+  cross3(va, vb, dir);
+  v3unit(dir);
+  if (dot3(dir, V[0]) > 0) {
+    real t[3];
+    v3cp(t, V[1]); v3cp(V[1], V[2]); v3cp(V[2], t);
+    v3cp(t, Pa[1]); v3cp(Pa[1], Pa[2]); v3cp(Pa[2], t);
+    for (int k = 0; k < 3; k++) dir[k] = -dir[k];
+  }
+  int it;
+  for (it = 0; it < 64; it++) {
+    hull_mpr_support(hv, nv, B, dir, V[3], Pa[3]);
+    if (dot3(V[3], dir) <= 0) return 0;
+    real c[3];
+    cross3(V[1], V[3], c);
+    if (dot3(c, V[0]) < -MPR_EPS) {
+      v3cp(V[2], V[3]); v3cp(Pa[2], Pa[3]);
+    } else {
+      cross3(V[3], V[2], c);
+      if (dot3(c, V[0]) < -MPR_EPS) { v3cp(V[1], V[3]); v3cp(Pa[1], Pa[3]); }
+      else break;
+    }
+    v3sub(V[1], V[0], va);
+    v3sub(V[2], V[0], vb);
+    cross3(va, vb, dir);
+    v3unit(dir);
+  }
+  if (it == 64) return 0;
+  for (it = 0;; it++) {
+    mpr_portal_dir(V, dir);
+    if (it >= 64) return 0;
+    if (dot3(V[1], dir) >= 0) break;
+    hull_mpr_support(hv, nv, B, dir, V[4], Pa[4]);
+    if (dot3(V[4], dir) < 0 || mpr_reached(V, dir)) return 0;
+    mpr_expand(V, Pa);
+  }
+  for (it = 0;; it++) {
+    mpr_portal_dir(V, dir);
+    hull_mpr_support(hv, nv, B, dir, V[4], Pa[4]);
+    if (mpr_reached(V, dir) || it >= 64) break;
+    mpr_expand(V, Pa);
+  }
+  real lam[3];
+  cvx_tri(V[1], V[2], V[3], lam);
+  for (int k = 0; k < 3; k++) {
+    x[k] = lam[0] * V[1][k] + lam[1] * V[2][k] + lam[2] * V[3][k];
+    pa[k] = lam[0] * Pa[1][k] + lam[1] * Pa[2][k] + lam[2] * Pa[3][k];
+  }
+  return 1;
+}
+/* the pen's segment (p0 + t u, radius rB) over face f: the clipped part's inner ends as contacts */
+static int hull_face_clip(const float (*pl)[4], int np, int f, const real* p0, const real* u, real rB, real off,
+                          real* out) {
+  const real nf[3] = {pl[f][0], pl[f][1], pl[f][2]}, df = pl[f][3];
+  const real s0 = dot3(nf, p0) - df, su = dot3(nf, u);
+  real q0[3], qu[3];
+  for (int a = 0; a < 3; a++) { q0[a] = p0[a] - s0 * nf[a]; qu[a] = u[a] - su * nf[a]; }
+  real t0 = 0.0, t1 = 1.0;
+  for (int i = 0; i < np; i++) {
+    if (i == f) continue;
+    const real a = pl[i][0] * q0[0] + pl[i][1] * q0[1] + pl[i][2] * q0[2] - pl[i][3] - HULL_CLIP_EPS;
+    const real b = pl[i][0] * qu[0] + pl[i][1] * qu[1] + pl[i][2] * qu[2];
+    if (b > 0) t1 = fmin(t1, -a / b); /* a + t b <= 0 */
+    else if (b < 0) t0 = fmax(t0, -a / b);
+    else if (a > 0) return 0;
+  }
+  if (!(t0 <= t1)) return 0;
+  int n = 0;
+  for (int e = 0; e < 2; e++) {
+    const real t = e == 0 ? t0 : t1;
+    if (!(t > 1e-6 && t < 1.0 - 1e-6) || (e == 1 && t1 - t0 < 1e-9)) continue;
+    const real g = s0 + t * su - rB;
+    if (!(g < off)) continue;
+    real* o = out + 7 * n;
+    for (int a = 0; a < 3; a++) {
+      o[a] = p0[a] + t * u[a] - nf[a] * (rB + 0.5 * g);
+      o[3 + a] = -nf[a];
+    }
+    o[6] = g;
+    n++;
+  }
+  return n;
+}
+/* the exact candidates in the hull's geom frame: core B (+ radius rB); up to 2 contacts (point, normal from the
+ * object to the hull, gap) written to out[7 * i], their count returned */
+static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4], int np, const cvx_shape* B, real rB,
+                              real off, real* out) {
+  real ctr[3] = {0, 0, 0}, cb[3], v0[3], pa[3], pb[3], x[3], dist, nrm[3], pt[3], d;
+  for (int v = 0; v < nv; v++)
+    for (int a = 0; a < 3; a++) ctr[a] += hv[v][a];
+  for (int a = 0; a < 3; a++) ctr[a] /= nv;
+  if (B->kind == 0) for (int a = 0; a < 3; a++) cb[a] = 0.5 * (B->p0[a] + B->p1[a]);
+  else v3cp(cb, B->c);
+  v3sub(ctr, cb, v0);
+  const int gk = hull_gjk(hv, nv, v0, B, rB + off, pa, pb, &dist);
+  if (gk == 2) return 0;
+  if (gk == 1) {
+    if (!(dist > 1e-9)) return 0;
+    for (int a = 0; a < 3; a++) {
+      nrm[a] = (pa[a] - pb[a]) / dist;
+      pt[a] = 0.5 * (pa[a] + pb[a] + nrm[a] * rB);
+    }
+    d = dist - rB;
+  } else {
+    if (!hull_mpr(hv, nv, v0, B, x, pa)) return 0;
+    const real l = sqrt(dot3(x, x));
+    if (!(l > 1e-9)) return 0;
+    for (int a = 0; a < 3; a++) {
+      nrm[a] = -x[a] / l;
+      pb[a] = pa[a] - x[a];
+      pt[a] = pa[a] - 0.5 * x[a] + 0.5 * nrm[a] * rB;
+    }
+    d = -l - rB;
+  }
+  if (!cvx_finite(pt, nrm, d)) return 0;
+  /* no contact can be made at or beyond the offset: a face-clip gap is at least the distance, and the cube's
+   * sharp edge is at most (sqrt2 - 1) of its rounding nearer than the rounded core */
+  if (!(d - (B->kind == 1 ? 0.41422 * rB : 0.0) < off)) return 0;
+  /* the hull's features at pa: the planes through it (the first two kept) */
+  int kA = 0, fa[2] = {0, 0};
+  for (int i = 0; i < np; i++)
+    if (fabs(pl[i][0] * pa[0] + pl[i][1] * pa[1] + pl[i][2] * pa[2] - pl[i][3]) < HULL_FEAT_EPS) {
+      if (kA < 2) fa[kA] = i;
+      kA++;
+    }
+  if (kA == 0 || kA >= 3) return 0; /* a hull vertex (or a witness off the surface) */
+  /* the core's feature at pb: the edge direction ub (0 for a box face / vertex or a segment end) */
+  real ub[3] = {0, 0, 0}, u[3];
+  int kB;
+  if (B->kind == 0) {
+    v3sub(B->p1, B->p0, u);
+    const real uu = dot3(u, u);
+    real dp[3];
+    v3sub(pb, B->p0, dp);
+    const real t = uu > 0 ? dot3(dp, u) / uu : 0.0;
+    if (!(t * sqrt(uu) > HULL_FEAT_EPS && (1.0 - t) * sqrt(uu) > HULL_FEAT_EPS)) return 0; /* an end */
+    v3cp(ub, u);
+    kB = 2;
+  } else {
+    real dl[3], l[3];
+    v3sub(pb, B->c, dl);
+    mattvec3((real(*)[3])B->R, dl, l);
+    kB = 0;
+    int free_ax = -1;
+    for (int k = 0; k < 3; k++) {
+      if (fabs(l[k]) > B->h[k] - HULL_FEAT_EPS) kB++;
+      else free_ax = k;
+    }
+    if (kB != 2) return 0; /* a face of the box (an edge of the hull lying on it) or a corner */
+    for (int a = 0; a < 3; a++) ub[a] = B->R[a][free_ax];
+  }
+  const real lub = sqrt(dot3(ub, ub));
+  /* the pen's interior parallel to a face of the hull at the witness: the face case */
+  int face = -1;
+  real falign = -2.0;
+  for (int i = 0; i < kA; i++) { /* the parallel face best aligned with the contact normal */
+    const real nn[3] = {pl[fa[i]][0], pl[fa[i]][1], pl[fa[i]][2]};
+    const real al = -dot3(nn, nrm);
+    if (fabs(dot3(nn, ub)) < HULL_SIN_ON_FACE * lub && al > falign) { face = fa[i]; falign = al; }
+  }
+  if (face >= 0 || kA == 1) {
+    if (B->kind != 0) return 0; /* a box edge on a hull face: its ends are vertex-face candidates */
+    return hull_face_clip(pl, np, face >= 0 ? face : fa[0], B->p0, u, rB, off, out);
+  }
+  /* edge against edge: the hull edge's direction, the core edge not near parallel to it nor to the box's faces */
+  const real n1[3] = {pl[fa[0]][0], pl[fa[0]][1], pl[fa[0]][2]}, n2[3] = {pl[fa[1]][0], pl[fa[1]][1], pl[fa[1]][2]};
+  real ua[3], cx[3];
+  cross3(n1, n2, ua);
+  cross3(ua, ub, cx);
+  if (!(dot3(cx, cx) > HULL_SIN_PARALLEL * HULL_SIN_PARALLEL * dot3(ua, ua) * dot3(ub, ub))) return 0;
+  if (B->kind == 1) /* the hull edge lying on a face of the box: the hull edge's ends are vertex candidates */
+    for (int k = 0; k < 3; k++) {
+      const real col[3] = {B->R[0][k], B->R[1][k], B->R[2][k]};
+      if (fabs(dot3(col, ub)) < 0.5 && fabs(dot3(col, ua)) < HULL_SIN_ON_FACE * sqrt(dot3(ua, ua))) {
+        /* col is a face normal of the box adjacent to its witness edge */
+        real dl[3], l[3];
+        v3sub(pb, B->c, dl);
+        mattvec3((real(*)[3])B->R, dl, l);
+        if (fabs(l[k]) > B->h[k] - HULL_FEAT_EPS) return 0;
+      }
+    }
+  if (B->kind == 1) {
+    /* the cube's sharp edge: the core edge moved out by the margin along its two faces' normals; the contact on
+     * the common perpendicular of the hull edge's line (pa, ua) and that edge's line (q, ub) */
+    real dl[3], l[3], q[3];
+    v3sub(pb, B->c, dl);
+    mattvec3((real(*)[3])B->R, dl, l);
+    v3cp(q, pb);
+    for (int k = 0; k < 3; k++) {
+      if (!(fabs(l[k]) > B->h[k] - HULL_FEAT_EPS)) continue;
+      const real sg = l[k] < 0 ? -rB : rB;
+      for (int a = 0; a < 3; a++) q[a] += sg * B->R[a][k];
+    }
+    real np_[3], w0[3];
+    cross3(ua, ub, np_);
+    v3unit(np_);
+    if (dot3(np_, nrm) < 0) for (int a = 0; a < 3; a++) np_[a] = -np_[a];
+    v3sub(pa, q, w0);
+    const real a_ = dot3(ua, ua), b_ = dot3(ua, ub), c_ = dot3(ub, ub), d_ = dot3(ua, w0), e_ = dot3(ub, w0);
+    const real den = a_ * c_ - b_ * b_;
+    const real sa = (b_ * e_ - c_ * d_) / den, tb = (a_ * e_ - b_ * d_) / den;
+    for (int a = 0; a < 3; a++) {
+      pt[a] = 0.5 * ((pa[a] + sa * ua[a]) + (q[a] + tb * ub[a]));
+      nrm[a] = np_[a];
+    }
+    d = dot3(w0, np_);
+  }
+  if (!(d < off)) return 0;
+  v3cp(out, pt);
+  v3cp(out + 3, nrm);
+  out[6] = d;
+  return 1;
+}
+/* the object's core in the hull's geom frame (centre c, axes R) */
+static void hull_object_core(const mg_model* m, const kin* k, const real* c, real R[3][3], cvx_shape* B, real* rB) {
+  memset(B, 0, sizeof(*B));
+  real dl[3];
+  if (m->obj_type == MG_GT_BOX) {
+    B->kind = 1;
+    for (int a = 0; a < 3; a++) dl[a] = k->op[a] - c[a];
+    mattvec3(R, dl, B->c);
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) B->R[a][b] = R[0][a] * k->oR[0][b] + R[1][a] * k->oR[1][b] + R[2][a] * k->oR[2][b];
+    const real h0 = m->obj_size[0], h1 = m->obj_size[1], h2 = m->obj_size[2];
+    const real mg = fmin(HULL_MARGIN, 0.5 * fmin(h0, fmin(h1, h2)));
+    B->h[0] = h0 - mg; B->h[1] = h1 - mg; B->h[2] = h2 - mg;
+    *rB = mg;
+  } else { /* pen: segment along the object's z, half length obj_size[1], radius obj_size[0] */
+    B->kind = 0;
+    real e0[3], e1[3];
+    for (int a = 0; a < 3; a++) {
+      e0[a] = k->op[a] - k->oR[a][2] * m->obj_size[1] - c[a];
+      e1[a] = k->op[a] + k->oR[a][2] * m->obj_size[1] - c[a];
+    }
+    mattvec3(R, e0, B->p0);
+    mattvec3(R, e1, B->p1);
+    *rB = m->obj_size[0];
+  }
+}
+static int hull_object_exact(const mg_model* m, const kin* k, int g, const real* c, real R[3][3], real off,
+                             contact* out, int n, int cap) {
+  real hv[HULL_MAXV][3], res[14];
+  const int nv = m->hull_num_verts < HULL_MAXV ? m->hull_num_verts : HULL_MAXV;
+  for (int v = 0; v < nv; v++)
+    for (int a = 0; a < 3; a++) hv[v][a] = m->hull_vert[v][a];
+  cvx_shape B;
+  real rB;
+  hull_object_core(m, k, c, R, &B, &rB);
+  const int nc = hull_core_contacts((const real(*)[3])hv, nv, m->hull_plane, m->hull_num_planes, &B, rB, off, res);
+  for (int i = 0; i < nc; i++) {
+    real pw[3], nw[3];
+    matvec3(R, res + 7 * i, pw);
+    for (int a = 0; a < 3; a++) pw[a] += c[a];
+    matvec3(R, res + 7 * i + 3, nw);
+    n = push_contact(out, n, cap, m->geom_node[g], g, OBJ_NODE, -2, pw, nw, res[7 * i + 6]);
+  }
+  return n;
+}
+
 /* number of object-contact candidates of an articulation geom (the HIP kernel enumerates the same) */
 static int obj_candidates(int otype, int gtype, int hull_verts) {
   const int round = gtype == MG_GT_SPHERE || gtype == MG_GT_CAPSULE;
-  if (gtype == MG_GT_CONVEX) /* block: hull vertices + the box's 8; pen: hull vertices + its 2 ends; egg: planes */
-    return otype == MG_GT_BOX ? hull_verts + 8 : (otype == MG_GT_CAPSULE ? hull_verts + 2 : 1);
+  if (gtype == MG_GT_CONVEX) /* block: hull vertices + the box's 8 + exact; pen: hull vertices + its 2 ends + exact;
+                                egg: planes */
+    return otype == MG_GT_BOX ? hull_verts + 9 : (otype == MG_GT_CAPSULE ? hull_verts + 3 : 1);
   if (!round && gtype != MG_GT_BOX) return 0;
   if (otype == MG_GT_BOX) return round ? 1 : 17; /* box: 8 + 8 vertex-face, 1 edge-edge */
   if (otype == MG_GT_CAPSULE) return round ? 1 : 3;
@@ -1285,7 +1668,8 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
         n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
       }
     }
-    return n;
+    /* the pen's segment interior across the hull (a ridge, or a face its ends overhang): exact distance */
+    return hull_object_exact(m, k, g, c, R, off, out, n, cap);
   }
   if (ot == MG_GT_ELLIPSOID) {
     cvx_shape A;
@@ -2016,3 +2400,28 @@ int orc_hull_distance(const mg_model* m, const real* pl, int32_t n, real* out) {
   return MG_OK;
 }
 #endif
+
+/* KAT hook: the exact hull candidates (hull_core_contacts) of the model's hull against a core given in the hull's
+ * geom frame: shape = [kind, p0 (3), p1 (3)] (segment) or [kind, c (3), R (9, row-major), h (3)] (box);
+ * out = up to 2 x [point (3), normal (3), gap].  Returns the number of contacts. */
+int orc_hull_core_contact(const mg_model* m, const double* shape, double rB, double off, double* out) {
+  real hv[HULL_MAXV][3];
+  const int nv = m->hull_num_verts < HULL_MAXV ? m->hull_num_verts : HULL_MAXV;
+  for (int v = 0; v < nv; v++)
+    for (int a = 0; a < 3; a++) hv[v][a] = m->hull_vert[v][a];
+  cvx_shape B;
+  memset(&B, 0, sizeof(B));
+  B.kind = (int)shape[0];
+  if (B.kind == 0) {
+    for (int a = 0; a < 3; a++) { B.p0[a] = shape[1 + a]; B.p1[a] = shape[4 + a]; }
+  } else {
+    for (int a = 0; a < 3; a++) B.c[a] = shape[1 + a];
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) B.R[a][b] = shape[4 + 3 * a + b];
+    for (int a = 0; a < 3; a++) B.h[a] = shape[13 + a];
+  }
+  real res[14];
+  const int nc = hull_core_contacts((const real(*)[3])hv, nv, m->hull_plane, m->hull_num_planes, &B, rB, off, res);
+  for (int i = 0; i < 7 * nc; i++) out[i] = res[i];
+  return nc;
+}

@@ -63,6 +63,7 @@ def lib():
         l.orc_ellipsoid_contact.argtypes = [C.c_int32, P, C.c_double, P, P]
         l.orc_box_box_edge.argtypes = [P, P, C.c_double, P]
         l.orc_hull_distance.argtypes = [P, P, C.c_int32, P]
+        l.orc_hull_core_contact.argtypes = [P, P, C.c_double, C.c_double, P]
         l.orc_dr_apply.argtypes = [C.POINTER(_abi.DrApplyArgs)]
         l.orc_dr_noise.argtypes = [C.POINTER(_abi.DrNoiseArgs)]
         _lib = l
@@ -136,6 +137,16 @@ def hull_distance(model_np, pts):
     out = np.zeros((len(pl), 2))
     lib().orc_hull_distance(model_np.ctypes.data, p(pl), len(pl), p(out))
     return out[:, 0], out[:, 1].astype(int)
+
+
+def hull_core_contact(model_np, kind, shape, radius, off):
+    """the exact hull candidates (oracle hull_core_contacts) against a core in the hull's geom frame: kind 0 =
+    segment (shape = p0, p1), 1 = box (shape = c, R row-major, h); a list of (point, normal from the core to the
+    hull, gap), at most 2"""
+    sh = np.concatenate([[float(kind)], np.asarray(shape, np.float64).ravel()])
+    out = np.zeros(14)
+    n = lib().orc_hull_core_contact(model_np.ctypes.data, p(sh), float(radius), float(off), p(out))
+    return [(out[7 * i:7 * i + 3], out[7 * i + 3:7 * i + 6], out[7 * i + 6]) for i in range(n)]
 
 
 def ellipsoid_contact(kind, shape, radius, e):

@@ -301,6 +301,60 @@ def test_hand_physics_near_forearm_matches_oracle(lib, kind):
     assert touching >= 16, touching
 
 
+def _forearm_world(spec, h):
+    """world centre and axes of the forearm hull's geom frame (node 0 = the hand's fixed root row)"""
+    g = spec.geoms[spec.hull["geom"]]
+    from scipy.spatial.transform import Rotation
+    Rn = Rotation.from_quat(h.root[0, 0, 3:7].astype(np.float64)).as_matrix()
+    return h.root[0, 0, 0:3] + Rn @ np.asarray(g.pos), Rn @ Rotation.from_quat(np.asarray(g.quat, np.float64)).as_matrix()
+
+
+@pytest.mark.parametrize("kind", ["block", "pen"])
+def test_hand_physics_hull_exact_matches_oracle(lib, kind):
+    """A6, the exact hull candidate (hull.hpp / oracle hull_core_contact): the cube with an edge across one of the
+    hull's upper edges, or the pen lying across one of its upper faces with its ends overhanging, at gaps of
+    -0.5 .. 1.5 mm, where the vertex-face candidates see nothing (test_oracle_hand_physics.py KATs).  GPU vs
+    oracle like the palm states; most envs must be in contact with the hull."""
+    from scipy.spatial.transform import Rotation
+    from test_oracle_hand_physics import _cube_across_edge, _hull_edges
+    spec, sp, tp = setup(kind=kind)
+    n = 256
+    rng = np.random.default_rng(13)
+    h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
+    h.dof[:, :, 0] = 0.0   # fingers straight and away from the forearm
+    c, R = _forearm_world(spec, h)
+    edges, V, P, on = _hull_edges(spec)
+    ob = h.root[:, 1]
+    if kind == "block":
+        up = [e for e in edges if e[1] > 10 and e[0] > 0.03 and (R @ (P[e[4], :3] + P[e[5], :3]))[2] > 0]
+        assert len(up) >= 4
+        for i in range(n):
+            (_, _, a, b, f1, f2) = up[i % len(up)]
+            cl, Rl, _, _ = _cube_across_edge(V, P, a, b, f1, f2, rng.uniform(-5e-4, 1.5e-3))
+            ob[i, 0:3] = c + R @ cl
+            ob[i, 3:7] = Rotation.from_matrix(R @ Rl).as_quat()
+    else:
+        faces = [f for f in range(len(P)) if (R @ P[f, :3])[2] > 0.3]
+        assert len(faces) >= 8
+        for i in range(n):
+            f = faces[i % len(faces)]
+            nf = P[f, :3]
+            t = np.cross(nf, rng.normal(size=3))
+            t /= np.linalg.norm(t)
+            ctr = V[on[:, f]].mean(0) + nf * (0.008 + rng.uniform(-5e-4, 1.5e-3))
+            Rl = np.stack([nf, np.cross(t, nf), t], 1)      # the pen's axis (object z) along t
+            ob[i, 0:3] = c + R @ ctr
+            ob[i, 3:7] = Rotation.from_matrix(R @ Rl).as_quat()
+    ob[:, 7:13] = rng.normal(0, 0.05, (n, 6))
+    mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n)
+    node = spec.geoms[spec.hull["geom"]].node
+    touching = 0
+    for i in range(n):
+        cs = O.contacts(mnp, sp, h0.root[i].ravel(), h0.dof[i], 64)
+        touching += any(int(x[0]) == node and int(x[8]) == -2 for x in cs)
+    assert touching >= n // 2, touching
+
+
 @pytest.mark.parametrize("kind", ["block", "egg", "pen"])
 def test_hand_fused_env_step_matches_oracle(lib, kind):
     """mg_env_step (the bench path) vs orc_hand_env_step over 12 control steps (the block and the egg start

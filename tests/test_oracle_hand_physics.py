@@ -367,6 +367,148 @@ def test_cube_contacts_and_rests_on_the_forearm_hull():
     assert h.root[0, 1, 2] > z0 - 0.004, (h.root[0, 1, 2], z0)
 
 
+def _hull_edges(spec):
+    """the hull's edges (vertex pairs on two face planes): (length, dihedral deg, i, j, f1, f2), longest first"""
+    V, P = np.array(spec.hull["verts"]), np.array(spec.hull["planes"])
+    on = np.abs(V @ P[:, :3].T - P[:, 3]) < 1e-6
+    out = []
+    for i in range(len(V)):
+        for j in range(i + 1, len(V)):
+            f = np.nonzero(on[i] & on[j])[0]
+            if len(f) >= 2:
+                ang = np.degrees(np.arccos(np.clip(P[f[0], :3] @ P[f[1], :3], -1, 1)))
+                out.append((np.linalg.norm(V[j] - V[i]), ang, i, j, f[0], f[1]))
+    return sorted(out, reverse=True), V, P, on
+
+
+def _cube_across_edge(V, P, i, j, f1, f2, gap, h=0.025):
+    """a cube (half extent h) whose edge crosses hull edge (i, j) at right angles, `gap` outside it along the
+    bisector b of the two faces' normals: the cube's edge points at -b (its two faces at 45 deg to b)"""
+    b = P[f1, :3] + P[f2, :3]
+    b /= np.linalg.norm(b)
+    e = (V[j] - V[i]) / np.linalg.norm(V[j] - V[i])
+    m = 0.5 * (V[i] + V[j])
+    u = np.cross(e, b)
+    u /= np.linalg.norm(u)
+    w = np.cross(u, b)
+    R = np.stack([u, (b + w) / np.sqrt(2), (w - b) / np.sqrt(2)], 1)   # right-handed; corner (-h, +h) of (a1, a2) at -sqrt2 h b
+    return m + b * (gap + np.sqrt(2) * h), R, m, b
+
+
+def test_hull_exact_cube_edge_across_hull_edge():
+    """A6: a cube edge resting across a hull edge.  No vertex of either is near the other, so the vertex-face
+    candidates see nothing; the exact candidate (GJK on hull - rounded cube core) gives the contact: normal =
+    minus the faces' bisector (from the cube to the hull), gap = the edges' distance, point halfway."""
+    spec = M.load_builtin("shadow_hand")
+    mnp = M.pack_model(spec)
+    edges, V, P, _ = _hull_edges(spec)
+    mg = 1e-3   # the core's rounding (oracle HULL_MARGIN): it finds the features; the contact is on the sharp edges
+    checked = 0
+    # edges with a real ridge (dihedral > 10 deg: a cube edge across a flatter one lies within 2 deg of the
+    # faces, i.e. on the surface, and is the vertex-face candidates' case)
+    for (ln, ang, i, j, f1, f2) in [e for e in edges if e[1] > 10][:12]:
+        for gap in (0.0015, 0.0, -0.0005):
+            c, R, m, b = _cube_across_edge(V, P, i, j, f1, f2, gap)
+            r = O.hull_core_contact(mnp, 1, np.r_[c, R.ravel(), np.full(3, 0.025 - mg)], mg, 0.002)
+            assert len(r) == 1, (i, j, gap, r)
+            pt, n, d = r[0]
+            np.testing.assert_allclose(n, -b, atol=1e-6)
+            np.testing.assert_allclose(d, gap, atol=1e-8)
+            np.testing.assert_allclose(pt, m + 0.5 * gap * b, atol=1e-6)
+            checked += 1
+        # beyond the contact offset: nothing
+        c, R, _, _ = _cube_across_edge(V, P, i, j, f1, f2, 0.003)
+        assert O.hull_core_contact(mnp, 1, np.r_[c, R.ravel(), np.full(3, 0.025 - mg)], mg, 0.002) == []
+    assert checked == 36
+    # the cube's edge turned parallel to the hull's edge (a near-parallel pair's closest points are not unique):
+    # no edge-edge contact; the edge ends are vertex-face cases
+    (_, _, i, j, f1, f2) = [e for e in edges if e[1] > 10][0]
+    c, R, m, b = _cube_across_edge(V, P, i, j, f1, f2, 0.001)
+    e = (V[j] - V[i]) / np.linalg.norm(V[j] - V[i])
+    Rz = R.copy()
+    Rz[:, 0] = e
+    Rz[:, 1:] = R[:, 1:] - np.outer(e, e @ R[:, 1:])
+    Rz[:, 1:] /= np.linalg.norm(Rz[:, 1:], axis=0)
+    assert O.hull_core_contact(mnp, 1, np.r_[c, Rz.ravel(), np.full(3, 0.025 - mg)], mg, 0.002) == []
+
+
+def test_hull_exact_pen_across_face():
+    """A6: the pen lying across a hull face whose plane its ends overhang: the end spheres' plane distances
+    are centimetres, the segment interior is `gap` above the face; the exact candidate sees it (normal = minus
+    the face normal, gap)."""
+    spec = M.load_builtin("shadow_hand")
+    mnp = M.pack_model(spec)
+    _, V, P, on = _hull_edges(spec)
+    ro, hl = 0.008, 0.1
+    for f in range(0, len(P), 7):
+        n = P[f, :3]
+        ctr = V[on[:, f]].mean(0)
+        t = np.cross(n, [0.3, 0.2, 0.9])
+        t /= np.linalg.norm(t)
+        for gap in (0.001, 0.0, -0.002):
+            p0, p1 = ctr + n * (ro + gap) - t * hl, ctr + n * (ro + gap) + t * hl
+            ends, _ = O.hull_distance(mnp, np.stack([p0, p1]))
+            assert (ends - ro > 0.02).all()          # the end-sphere candidates are far from contact
+            r = O.hull_core_contact(mnp, 0, np.r_[p0, p1], ro, 0.002)
+            assert len(r) == 2, (f, gap, r)   # where the segment leaves the face, on both sides
+            for pt, nn, d in r:
+                np.testing.assert_allclose(nn, -n, atol=1e-9)
+                np.testing.assert_allclose(d, gap, atol=1e-8)   # the float32 plane table
+                # on the face's boundary: the point's projection onto the face satisfies every plane, one tightly
+                q = pt - n * (0.5 * d)
+                dist, _ = O.hull_distance(mnp, q[None])
+                assert abs(dist[0]) < 1e-7, dist
+            # tilted by 1 or 3 deg: the part over the face (or the lower crossing of its boundary ridge, or the
+            # neighbouring face it now lies on) is nearer than the flat gap, with normals near the face's
+            for deg, count in ((1.0, (1, 2)), (3.0, (1, 2))):
+                tt = np.cos(np.radians(deg)) * t + np.sin(np.radians(deg)) * n
+                q0, q1 = ctr + n * (ro + gap) - tt * hl, ctr + n * (ro + gap) + tt * hl
+                r2 = O.hull_core_contact(mnp, 0, np.r_[q0, q1], ro, 0.002)
+                if not r2:   # a vertex is among the closest features: the pen's end (its end sphere's candidate)
+                    de, _ = O.hull_distance(mnp, np.stack([q0, q1]))   # or a hull vertex (the vertex candidates)
+                    w = np.clip(((V - q0) @ (q1 - q0)) / ((q1 - q0) @ (q1 - q0)), 0, 1)
+                    dv = np.linalg.norm(V - (q0 + w[:, None] * (q1 - q0)), axis=1)
+                    assert min(de.min(), dv.min()) - ro < gap, (f, deg, de, dv.min())
+                    continue
+                assert len(r2) in count, (f, deg, r2)
+                assert min(x[2] for x in r2) < gap and all(x[1] @ -n > np.cos(np.radians(15)) for x in r2), r2
+
+
+
+def test_hull_exact_contact_in_collide():
+    """Through the full collide (world frame): the cube posed across a forearm hull edge gets exactly one
+    contact from the convex geom at the edges' distance, and it holds the cube up."""
+    spec, tp, sp, mnp, h = setup()
+    edges, V, P, _ = _hull_edges(spec)
+    c, R = _forearm_frame(mnp, h, spec)
+    # an edge on the hull's upper side (bisector pointing up in the world), long and with a real dihedral
+    best = -1.0
+    for (ln, ang, i, j, f1, f2) in edges:
+        b = P[f1, :3] + P[f2, :3]
+        up = (R @ (b / np.linalg.norm(b)))[2]
+        if ang > 10 and ln > 0.05 and up > best:
+            best, pick = up, (i, j, f1, f2)
+    assert best > 0.9, best
+    cl, Rl, m, b = _cube_across_edge(V, P, *pick, gap=0.001)
+    Rw = R @ Rl
+    from scipy.spatial.transform import Rotation
+    h.root[:, 1, 0:3] = c + R @ cl
+    h.root[:, 1, 3:7] = Rotation.from_matrix(Rw).as_quat()   # xyzw
+    h.root[:, 1, 7:] = 0
+    cs = O.contacts(mnp, sp, h.root[0].ravel(), h.dof[0], 64)
+    fore = [x for x in cs if int(x[0]) == 0 and int(x[8]) == -2]
+    assert len(fore) == 1, fore
+    np.testing.assert_allclose(fore[0][7], 0.001, atol=2e-5)   # gap (fp32 state)
+    np.testing.assert_allclose(fore[0][4:7], -(R @ b), atol=2e-4)             # normal: from the cube to the hull
+    # touching (gap 0), one step: the contact takes the cube's fall (free fall would reach -g dt = -0.16 m/s);
+    # balanced on a point of an edge the cube then tips over, as a real one would
+    cl, Rl, m, b = _cube_across_edge(V, P, *pick, gap=0.0)
+    h.root[:, 1, 0:3] = c + R @ cl
+    z0 = float(h.root[0, 1, 2])
+    h.simulate(mnp, sp)
+    assert h.root[0, 1, 9] > -0.03 and h.root[0, 1, 2] > z0 - 1e-3, h.root[0, 1]
+
+
 def test_explicit_contact_pairs_imported():
     """shared.xml:31-51 lists 19 <pair>s (condim 1), one of them twice: 18 pairs, frictionless; the palm's box
     against the thumb's distal capsule is the one box pair."""
