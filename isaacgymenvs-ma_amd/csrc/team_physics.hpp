@@ -159,6 +159,7 @@ __device__ __forceinline__ void wsync() {
 }
 
 static_assert(MG_MAX_GEOMS < 128 && MG_MAX_NODES < 128, "contact sides are packed as int8");
+constexpr float kBoxBlend = 1e-3f;  // point_box: the band (m) over which an interior point's normal blends faces
 
 // PGS visits per block of the sweep (their data are loaded one block ahead; 2 and 8 measured slower)
 constexpr int kPgsPrefetch = 4;
@@ -366,17 +367,22 @@ __device__ __forceinline__ float point_box(V3 p, V3 hb, V3* nb, V3* cb) {
     *cb = q;
     return l;
   }
-  float dx = hb.x - fabsf(p.x), dy = hb.y - fabsf(p.y), dz = hb.z - fabsf(p.z);
-  int k = 0;
-  float dm = dx;
-  if (dy < dm) { dm = dy; k = 1; }
-  if (dz < dm) { dm = dz; k = 2; }
-  V3 c = p, n = v3(0, 0, 0);
-  if (k == 0) { float sg = p.x < 0 ? -1.f : 1.f; n.x = sg; c.x = sg * hb.x; }
-  else if (k == 1) { float sg = p.y < 0 ? -1.f : 1.f; n.y = sg; c.y = sg * hb.y; }
-  else { float sg = p.z < 0 ? -1.f : 1.f; n.z = sg; c.z = sg * hb.z; }
+  // inside: the depth is the nearest face's; the normal blends the faces within kBoxBlend of the nearest one
+  // (weight 1 - (depth - nearest) / kBoxBlend), so it turns continuously across the box's medial planes instead
+  // of jumping to whichever face fp32 / fp64 rounding makes nearest (oracle point_box, the same rule)
+  const float ex0 = hb.x - p.x, ex1 = hb.x + p.x, ey0 = hb.y - p.y, ey1 = hb.y + p.y, ez0 = hb.z - p.z, ez1 = hb.z + p.z;
+  const float dm = fminf(fminf(fminf(ex0, ex1), fminf(ey0, ey1)), fminf(ez0, ez1));
+  auto wt = [&](float e) { return fmaxf(0.0f, 1.0f - (e - dm) * (1.0f / kBoxBlend)); };
+  V3 n = v3(wt(ex0) - wt(ex1), wt(ey0) - wt(ey1), wt(ez0) - wt(ez1));
+  const float nl = dot(n, n);
+  if (nl < 1e-12f) {  // opposite faces cancel (a thin box entered at its middle): the nearest face, +x +y +z first
+    n = dm == ex0 ? v3(1, 0, 0) : dm == ex1 ? v3(-1, 0, 0) : dm == ey0 ? v3(0, 1, 0) : dm == ey1 ? v3(0, -1, 0)
+      : dm == ez0 ? v3(0, 0, 1) : v3(0, 0, -1);
+  } else {
+    n = n * prsq(nl);
+  }
   *nb = n;
-  *cb = c;
+  *cb = p + n * dm;
   return -dm;
 }
 

@@ -54,6 +54,7 @@ typedef double real;
 #define MAXR (3 * MAXC + 2 * MG_MAX_NODES)
 #define MPR_TOL 1e-7  /* portal reached the boundary (m) */
 #define CVX_MARGIN 1e-3 /* rounding of box cores against the egg (m) */
+#define BOX_BLEND 1e-3  /* point_box: the band (m) over which an interior point's normal blends faces */
 #define MPR_EPS 1e-12 /* origin-side tests */
 
 typedef real v3[3];
@@ -512,16 +513,33 @@ static real point_box(const real* pl, const real* hb, real* nb, real* cb) {
     for (int a = 0; a < 3; a++) { nb[a] = d[a] / l; cb[a] = q[a]; }
     return l;
   }
-  int kmin = 0;
-  real dmin = hb[0] - fabs(pl[0]);
-  for (int a = 1; a < 3; a++) {
-    real dd = hb[a] - fabs(pl[a]);
-    if (dd < dmin) { dmin = dd; kmin = a; }
+  /* inside: the depth is the nearest face's; the normal blends the faces within BOX_BLEND of the nearest one
+   * (weight 1 - (depth - nearest) / BOX_BLEND), so it turns continuously across the box's medial planes instead
+   * of jumping to whichever face rounding makes nearest; the surface point is p moved out along it by the depth */
+  real e[6], dmin = 1e300;
+  for (int a = 0; a < 3; a++) {
+    e[2 * a] = hb[a] - pl[a];
+    e[2 * a + 1] = hb[a] + pl[a];
   }
-  for (int a = 0; a < 3; a++) { nb[a] = 0.0; cb[a] = pl[a]; }
-  real sg = pl[kmin] < 0 ? -1.0 : 1.0;
-  nb[kmin] = sg;
-  cb[kmin] = sg * hb[kmin];
+  for (int i = 0; i < 6; i++) dmin = fmin(dmin, e[i]);
+  real n[3], nl = 0.0;
+  for (int a = 0; a < 3; a++) {
+    n[a] = fmax(0.0, 1.0 - (e[2 * a] - dmin) / BOX_BLEND) - fmax(0.0, 1.0 - (e[2 * a + 1] - dmin) / BOX_BLEND);
+    nl += n[a] * n[a];
+  }
+  if (nl < 1e-12) { /* opposite faces cancel (a thin box entered at its middle): the nearest face, +x +y +z first */
+    int i = 0;
+    while (i < 5 && e[i] != dmin) i++;
+    n[0] = n[1] = n[2] = 0.0;
+    n[i / 2] = (i & 1) ? -1.0 : 1.0;
+  } else {
+    nl = sqrt(nl);
+    for (int a = 0; a < 3; a++) n[a] /= nl;
+  }
+  for (int a = 0; a < 3; a++) {
+    nb[a] = n[a];
+    cb[a] = pl[a] + n[a] * dmin;
+  }
   return -dmin;
 }
 
