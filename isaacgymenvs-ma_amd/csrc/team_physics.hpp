@@ -674,60 +674,71 @@ struct Team {
   __device__ __forceinline__ bool in_path(int target, int k) const { return target >= 0 && ((s->anc[target] >> k) & 1ull); }
 
   // ---------------------------------------------------------------- FK (level-synchronous)
+  // Forward kinematics without a barrier per tree level: every node's lane composes its own path from the
+  // root (proper ancestors in increasing depth = increasing index, then itself) with the ancestors' joint
+  // positions / velocities published once in LDS.  The operations per link are those of a level-by-level pass
+  // (R = R_parent R_rest rot(axis, q), x, S, V = V_parent + S qd), so the results are bit-identical to it; the
+  // deeper lanes repeat their ancestors' few dozen FMAs instead of waiting for one LDS round trip and wave
+  // barrier per level.  R, x, V, S are then stored for the later phases.
   __device__ __forceinline__ void fk() {
     if (OBJ) oR = quat_to_mat(oq[0], oq[1], oq[2], oq[3]);
+    const M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
     if (tl == 0) {
-      M3 R0 = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
       for (int a = 0; a < 3; a++)
-        for (int b = 0; b < 3; b++) s->R[0][3 * a + b] = R0.m[a][b];
+        for (int b = 0; b < 3; b++) s->R[0][3 * a + b] = Rr.m[a][b];
       s->x[0][0] = p0.x; s->x[0][1] = p0.y; s->x[0][2] = p0.z;
       if (!freeb)
         for (int k = 0; k < 6; k++) s->V[0][k] = 0.0f;
     }
     if (freeb && tl < 6) s->V[0][tl] = nu;
+    // (q, qd) per node in the union storage (free here: the ABA's child slots are written after)
+    float* qv = &s->u.slot[0][0];
+    static_assert(sizeof(s->u.slot) >= sizeof(float) * 2 * MN, "joint states must fit the union storage");
+    if (node > 0) {
+      qv[2 * node] = qj;
+      qv[2 * node + 1] = nu;
+    }
     wsync();
-    if (node == 0) {
+    if (node >= 0) {
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) R.m[a][b] = s->R[0][3 * a + b];
       x = ld3(s->x[0]);
       V = sv(ld3(s->V[0]), ld3(s->V[0] + 3));
     }
-    for (int lev = 1; lev <= maxdepth; lev++) {
-      if (node > 0 && depth == lev) {
-        M3 Rp;
-        for (int a = 0; a < 3; a++)
-          for (int b = 0; b < 3; b++) Rp.m[a][b] = s->R[par][3 * a + b];
-        V3 xp = ld3(s->x[par]);
-        SV Vp = sv(ld3(s->V[par]), ld3(s->V[par] + 3));
-        const float* nf = mt->nf[node];
+    if (node > 0) {
+      const V3 x0 = x;
+      for (unsigned long long path = s->anc[node] & ~1ull; path; path &= path - 1) {
+        const int k = __builtin_ctzll(path);
+        const float* nf = mt->nf[k];
         M3 R0;
         for (int a = 0; a < 3; a++)
           for (int b = 0; b < 3; b++) R0.m[a][b] = nf[3 * a + b];
-        M3 Rp0 = mul(Rp, R0);
-        V3 tp = mul(Rp, ld3(nf + 9));
-        V3 ax = ld3(nf + 12);
-        if (mt->jtype[node] == MG_JT_HINGE) {
-          R = mul(Rp0, axis_angle(ax, qj));
-          x = xp + tp;
-          V3 sw = mul(R, ax);
-          S = sv(sw, cross(x - ld3(s->x[0]), sw));
+        const M3 Rp0 = mul(R, R0);
+        const V3 tp = mul(R, ld3(nf + 9));
+        const V3 ax = ld3(nf + 12);
+        const float qk = k == node ? qj : qv[2 * k], vk = k == node ? nu : qv[2 * k + 1];
+        if (mt->jtype[k] == MG_JT_HINGE) {
+          R = mul(Rp0, axis_angle(ax, qk));
+          x = x + tp;
+          const V3 sw = mul(R, ax);
+          S = sv(sw, cross(x - x0, sw));
         } else {
           R = Rp0;
-          V3 sw = mul(Rp0, ax);
-          x = xp + tp + sw * qj;
+          const V3 sw = mul(Rp0, ax);
+          x = x + tp + sw * qk;
           S = sv(v3(0, 0, 0), sw);
         }
-        V = Vp + S * nu;
-        for (int a = 0; a < 3; a++)
-          for (int b = 0; b < 3; b++) s->R[node][3 * a + b] = R.m[a][b];
-        s->x[node][0] = x.x; s->x[node][1] = x.y; s->x[node][2] = x.z;
-        s->V[node][0] = V.a.x; s->V[node][1] = V.a.y; s->V[node][2] = V.a.z;
-        s->V[node][3] = V.l.x; s->V[node][4] = V.l.y; s->V[node][5] = V.l.z;
-        s->S[node][0] = S.a.x; s->S[node][1] = S.a.y; s->S[node][2] = S.a.z;
-        s->S[node][3] = S.l.x; s->S[node][4] = S.l.y; s->S[node][5] = S.l.z;
+        V = V + S * vk;
       }
-      wsync();
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) s->R[node][3 * a + b] = R.m[a][b];
+      s->x[node][0] = x.x; s->x[node][1] = x.y; s->x[node][2] = x.z;
+      s->V[node][0] = V.a.x; s->V[node][1] = V.a.y; s->V[node][2] = V.a.z;
+      s->V[node][3] = V.l.x; s->V[node][4] = V.l.y; s->V[node][5] = V.l.z;
+      s->S[node][0] = S.a.x; s->S[node][1] = S.a.y; s->S[node][2] = S.a.z;
+      s->S[node][3] = S.l.x; s->S[node][4] = S.l.y; s->S[node][5] = S.l.z;
     }
+    wsync();
   }
 
   __device__ __forceinline__ void set_axis() {
