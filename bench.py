@@ -107,6 +107,52 @@ def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
             "single_core": {"value": v1, "unit": "env-steps/s", "cores": 1, "sample": smp1}}
 
 
+def baseline_config0(dev, steps=1000, n=256):
+    """BASELINE.json configs[0]: Cartpole, 256 envs, random actions, 1000 steps.  The reference quotes it
+    on pipeline=cpu; here the same rollout runs through the fused HIP step on `dev` (wall clock of the
+    1000 VecTask.step calls, each host->device action copy included, since that configuration hands actions
+    over from the host) and through the oracle's fp32 CPU restatement on 1 core and on every usable core."""
+    import numpy as np
+    import torch
+    import migym
+    env = migym.make(seed=0, task="Cartpole", num_envs=n, sim_device=dev, rl_device=dev, headless=True)
+    rng = np.random.default_rng(0)
+    host = torch.from_numpy(rng.uniform(-1, 1, (8, n, env.num_actions)).astype(np.float32))
+    for i in range(10):
+        env.step(host[i % 8].to(dev, non_blocking=True))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        env.step(host[i % 8].to(dev, non_blocking=True))
+    torch.cuda.synchronize()
+    gpu_s = time.perf_counter() - t0
+    env.close()
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    from migym import configs, model as M, taskdefs
+    cfg = configs.task_config("Cartpole", n)
+    spec = M.load_builtin(taskdefs.TASK_INFO["Cartpole"][1])
+    sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO["Cartpole"][5], 1)
+    tp = taskdefs.task_params("Cartpole", cfg, spec)
+    mnp = M.pack_model(spec)
+    threads, _ = usable_cores()
+    cpu = {}
+    for nt in sorted({1, threads}):
+        h = O.HostEnv(tp, spec, n)
+        h.actions[:] = host[0].numpy()
+        h.env_step(mnp, sp, tp, 0, 0, nt, fp32=True)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            h.actions[:] = host[i % 8].numpy()
+            h.env_step(mnp, sp, tp, 0, i + 1, nt, fp32=True)
+        cpu[nt] = time.perf_counter() - t0
+    return {"workload": f"Cartpole {n} envs x {steps} random-action steps (BASELINE.json configs[0])",
+            "gpu": {"seconds": gpu_s, "env_steps_per_s": n * steps / gpu_s, "device": dev,
+                    "note": "fused HIP step, host action copy per step included"},
+            "cpu_port": {f"{nt}_cores": {"seconds": s, "env_steps_per_s": n * steps / s} for nt, s in cpu.items()},
+            "cpu_kind": "port (oracle fp32 restatement; the reference's PhysX CPU pipeline is not runnable here)"}
+
+
 VALU_SIMDS, CLOCK_HZ = 256 * 4, 2.4e9   # MI355X: 256 CUs x 4 SIMD-32, peak engine clock (MI355X_MICROARCH.md)
 
 
@@ -117,7 +163,7 @@ def pmc_traffic(task, n, kern_ms, object_type="block"):
     None when no pass was recorded for this workload."""
     path = None
     tag = task if (task != "ShadowHand" or object_type == "block") else f"{task}-{object_type}"   # per kernel instance
-    for rnd in ("r02", "r01"):   # the newest round's passes of this workload
+    for rnd in ("r03", "r02", "r01"):   # the newest round's passes of this workload
         cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_{n}.json")
         if os.path.exists(cand):
             path = cand
@@ -260,6 +306,11 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n, args.object_type)
             except Exception as ex:  # noqa: BLE001
                 out["cpu_baseline"] = {"error": repr(ex)}
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                out["baseline_config0"] = baseline_config0(dev)
+            except Exception as ex:  # noqa: BLE001
+                out["baseline_config0"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
     env.close()
     if world > 1:

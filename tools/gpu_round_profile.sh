@@ -5,7 +5,7 @@
 # which therefore cite this build's traffic.  Copy back with tools/collect_profiles.sh <round>.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-R=${1:-r02}
+R=${1:-r03}
 bash tools/gpu_prof_all.sh > gpurun_out/prof_all.log 2>&1 || { tail -5 gpurun_out/prof_all.log; exit 1; }
 for spec in "Ant 65536 k_env_step" "Humanoid 32768 k_env_step" "ShadowHand 16384 k_hand_step" \
             "ShadowHand-egg 16384 k_hand_step" "ShadowHand-pen 16384 k_hand_step"; do
