@@ -388,40 +388,48 @@ __device__ __forceinline__ float point_box(V3 p, V3 hb, V3* nb, V3* cb) {
 
 // closest parameter of segment a + t u (box frame) to the box (oracle seg_box_t): exact minimum of
 // the convex piecewise-quadratic squared distance over the sorted slab crossings; middle of the
-// inside portion when the segment passes through the box
+// inside portion when the segment passes through the box.  Registers only: a crossing outside (0, 1)
+// is replaced by 1 (the segment's end), so the eight breakpoints [0, six crossings, 1] sort with a fixed
+// 12-comparator network and the pieces are visited with static indices (the repeated 1s only add empty
+// pieces at the end, which the strict comparison never prefers).  The data-dependent count and insertion
+// sort of a literal restatement compile to compare / select chains per dynamic index on this target.
+__device__ __forceinline__ void seg_box_cx(float& a, float& b) {
+  const float lo = fminf(a, b), hi = fmaxf(a, b);
+  a = lo;
+  b = hi;
+}
 __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
   const float av[3] = {a.x, a.y, a.z}, uv[3] = {u.x, u.y, u.z}, hv[3] = {hb.x, hb.y, hb.z};
   float t0 = 0.0f, t1 = 1.0f;
   bool hit = true;
+  float bp[8];
+  bp[0] = 0.0f;
+  bp[7] = 1.0f;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
+    float ta = 1.0f, tb = 1.0f;
     if (fabsf(uv[k]) < 1e-12f) {
       if (av[k] < -hv[k] || av[k] > hv[k]) hit = false;
     } else {
-      float ta = (-hv[k] - av[k]) / uv[k], tb = (hv[k] - av[k]) / uv[k];
-      if (ta > tb) { float x = ta; ta = tb; tb = x; }
-      t0 = fmaxf(t0, ta);
-      t1 = fminf(t1, tb);
+      const float iu = 1.0f / uv[k];
+      ta = (-hv[k] - av[k]) * iu;
+      tb = (hv[k] - av[k]) * iu;
+      t0 = fmaxf(t0, fminf(ta, tb));
+      t1 = fminf(t1, fmaxf(ta, tb));
     }
+    bp[1 + 2 * k] = (ta > 0.0f && ta < 1.0f) ? ta : 1.0f;
+    bp[2 + 2 * k] = (tb > 0.0f && tb < 1.0f) ? tb : 1.0f;
   }
   if (hit && t0 <= t1) return 0.5f * (t0 + t1);
-  float bp[8];
-  int nb = 0;
-  bp[nb++] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    if (fabsf(uv[k]) < 1e-12f) continue;
-#pragma unroll
-    for (int sg = -1; sg <= 1; sg += 2) {
-      float t = ((float)sg * hv[k] - av[k]) / uv[k];
-      if (t > 0.0f && t < 1.0f) bp[nb++] = t;
-    }
-  }
-  bp[nb++] = 1.0f;
-  for (int i = 1; i < nb; i++)
-    for (int j = i; j > 0 && bp[j] < bp[j - 1]; j--) { float x = bp[j]; bp[j] = bp[j - 1]; bp[j - 1] = x; }
+  float* c = bp + 1;  // the six crossings
+  seg_box_cx(c[0], c[5]); seg_box_cx(c[1], c[3]); seg_box_cx(c[2], c[4]);
+  seg_box_cx(c[1], c[2]); seg_box_cx(c[3], c[4]);
+  seg_box_cx(c[0], c[3]); seg_box_cx(c[2], c[5]);
+  seg_box_cx(c[0], c[1]); seg_box_cx(c[2], c[3]); seg_box_cx(c[4], c[5]);
+  seg_box_cx(c[1], c[2]); seg_box_cx(c[3], c[4]);
   float best_t = 0.0f, best_f = 3.0e38f;
-  for (int i = 0; i + 1 < nb; i++) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
     const float lo = bp[i], hi = bp[i + 1], mid = 0.5f * (lo + hi);
     float num = 0.0f, den = 0.0f;
 #pragma unroll
@@ -430,7 +438,7 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
       if (x > hv[k]) { num += (av[k] - hv[k]) * uv[k]; den += uv[k] * uv[k]; }
       else if (x < -hv[k]) { num += (av[k] + hv[k]) * uv[k]; den += uv[k] * uv[k]; }
     }
-    float t = den > 0.0f ? -num / den : lo;
+    float t = den > 0.0f ? -num * prcp(den) : lo;
     t = fminf(fmaxf(t, lo), hi);
     float f = 0.0f;
 #pragma unroll
