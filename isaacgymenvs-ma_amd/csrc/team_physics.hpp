@@ -1753,22 +1753,29 @@ struct Team {
           base += nx;
         }
       }
+      // the survivors' candidates in geom order: lane per geom, a team scan of the counts places each geom's
+      // run, and the geom writes (geom, candidate index) for its run into a map behind the pair list, so a
+      // candidate's lane finds its pair with one LDS read (instead of walking the live mask)
+      static_assert(MN * 27 >= MG * GW + MP + (17 * MG + 1) / 2, "the candidate map must fit behind the pair list");
+      uint16_t* cmap = reinterpret_cast<uint16_t*>(plist + MP);
       int NC = 0;
-      for (unsigned long long mm = live; mm; mm &= mm - 1) NC += ocand_count(mt->gtype[__builtin_ctzll(mm)]);
+      for (int g0 = 0; g0 < G; g0 += T) {
+        const int g = g0 + tl;
+        const int n = (g < G && ((live >> g) & 1ull)) ? ocand_count(mt->gtype[g]) : 0;
+        const int incl = team_incl_scan<T>(n);
+        for (int q = 0; q < n; q++) cmap[NC + incl - n + q] = (uint16_t)(g | (q << 8));
+        NC += __shfl(incl, tb + T - 1);
+      }
+      wsync();
       for (int f0 = 0; f0 < NC; f0 += T) {
         const int f = f0 + tl;
         int cnt = 0, g = 0;
         V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
         float d = 0.0f;
         if (f < NC) {
-          // candidate f of the survivors, in geom order: its geom and candidate index
-          int q = f;
-          for (unsigned long long mm = live; mm; mm &= mm - 1) {
-            g = __builtin_ctzll(mm);
-            const int n = ocand_count(mt->gtype[g]);
-            if (q < n) break;
-            q -= n;
-          }
+          const int e = cmap[f];
+          g = e & 0xff;
+          const int q = e >> 8;
           V3 c;
           M3 Rg;
           geom_staged(g, &c, &Rg);
