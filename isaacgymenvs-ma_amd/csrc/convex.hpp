@@ -387,20 +387,17 @@ __device__ __forceinline__ CvxHit cvx_contact_body(CvxShape A, creal rA, D3 e, c
 }
 
 // The narrowphase entry: the core as five 3-vectors (segment: p0, p1; box: centre, half extents, the three
-// axis columns), the result by value.  A real call: the fp64 working set then lives in the callee's own
-// registers instead of spilling across the whole calling kernel (egg k_hand_step: 190 -> 98 spilled VGPRs,
-// +3.3 % env-steps/s, same-box A/B).
+// axis columns), the result by value.  Force-inlined into collide().
 //
-// The instance TUs are compiled with -mllvm -enable-ipra=false (build.py).  With interprocedural register
-// allocation on (the ROCm 7.2 LLVM default for AMDGPU), the caller keeps values across this call in
-// registers that IPRA's register-usage summary reports as preserved, and the callee clobbers some of them:
-// k_simulate's egg step then returned wrong object states in 222 of 256 envs (metres off, some NaN), and
-// an earlier build hung.  Measured (tools/gpu_egg_ab.sh on the states of egg_diag.py): the same source with
-// IPRA off is bit-reproducible and within 2.4e-7 m of the fp64 oracle; with IPRA on it fails with 8-wave
-// blocks and with 1-wave blocks alike (so no cross-wave LDS race is involved); the kernel descriptor's
-// private segment (1,600 B caller frame + 40 B callee frame = .private_segment_fixed_size 1,640, no dynamic
-// stack) covers the frames.  The earlier workaround was to force-inline the narrowphase.
-__device__ __attribute__((noinline)) CvxHit cvx_contact_v(int kind, D3 a0, D3 a1, D3 a2, D3 a3, D3 a4, creal rA, D3 e,
+// A real call (noinline) was tried in round 3 and is not safe with this toolchain (ROCm 7.2 LLVM): with
+// interprocedural register allocation on, k_simulate's egg step was wrong in 222 of 256 envs; with it off
+// (-mllvm -enable-ipra=false, still passed for the instance TUs) the call passed every egg test, but two
+// unrelated edits of the calling kernel then broke it again -- the narrowphase staged after fk() as a call
+// faulted (illegal address), and a prefetching rewrite of fk()'s ancestor walk left the DR egg test 93 %
+// in agreement -- while the same sources with the narrowphase inlined passed (profiles/r03/egg_call_ab.txt).
+// A static check of that build's code object found the callee's saves and the caller's restores in order,
+// so the miscompile is not pinned down; inlining costs 0.6 % of egg throughput against the call.
+__device__ __forceinline__ CvxHit cvx_contact_v(int kind, D3 a0, D3 a1, D3 a2, D3 a3, D3 a4, creal rA, D3 e,
                                               creal cut) {
   CvxShape A;
   A.kind = kind;

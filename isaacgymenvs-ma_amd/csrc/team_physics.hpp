@@ -1318,7 +1318,7 @@ struct Team {
     const float* gs = mt->gf[g] + 12;
     const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
     if constexpr (OBJ == MG_GT_ELLIPSOID) {
-      // fp64 from here (convex.hpp); the core crosses the call as five 3-vectors (cvx_contact_v)
+      // fp64 from here (convex.hpp): the core as five 3-vectors (cvx_contact_v, inlined)
       int kind;
       D3 a0, a1, a2 = d3(0, 0, 0), a3 = d3(0, 0, 0), a4 = d3(0, 0, 0);
       float r = 0.0f;
@@ -1652,7 +1652,7 @@ struct Team {
       const float ro = obj_radius();
       // pass 1, lane per geom: bounding-sphere cull of the whole geom (its centre only: R . pos + x);
       // the survivors' candidates are then enumerated densely, so culled boxes cost no lanes
-      unsigned long long live = 0ull;
+      unsigned long long live = 0ull, hull_live = 0ull;
       for (int g0 = 0; g0 < G; g0 += T) {
         const int g = g0 + tl;
         bool ok = false;
@@ -1670,14 +1670,12 @@ struct Team {
             ok = hull_box_near(cc, Rg, ld3(mt->gf[g] + 12), op, ro, off);
           }
         }
-        const unsigned long long b = __ballot(ok);
-        live |= ((b >> tb) & (T >= 64 ? ~0ull : ((1ull << T) - 1ull))) << g0;
+        constexpr unsigned long long tmask = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
+        live |= ((__ballot(ok) >> tb) & tmask) << g0;
+        hull_live |= ((__ballot(ok && gt == MG_GT_CONVEX) >> tb) & tmask) << g0;
       }
       // the convex-mesh geom first, in a pass of its own (its candidates precede the other geoms' object
       // contacts, as in the oracle's collide; rarely live, and kept out of the main loop's code)
-      unsigned long long hull_live = 0ull;
-      for (unsigned long long mm = live; mm; mm &= mm - 1)
-        if (mt->gtype[__builtin_ctzll(mm)] == MG_GT_CONVEX) hull_live |= mm & (~mm + 1ull);
       live &= ~hull_live;
       for (unsigned long long hm = hull_live; hm; hm &= hm - 1) {
         const int g = __builtin_ctzll(hm);
