@@ -1380,12 +1380,13 @@ struct Team {
 
   // The exact hull candidates of this substep (hull.hpp), before the tree phases: the convex-mesh geom is on the
   // hand's fixed root (checked at launch), so its world frame (built as fk() + geom_world() build it) and the
-  // object's pose are the ones collide() sees, and the fp64 narrowphase runs where little else is live.  The
+  // object's pose are the ones collide() sees, and the narrowphase runs where little else is live.  The
   // broadphase is collide()'s (the geom's bounding sphere, then its box against the object's sphere).
   __device__ __forceinline__ void hull_stage() {
     if constexpr (L::HX > 0) {
       const int g = mt->hullg;
       int nx = 0;
+      bool near = false;  // the object within the offset of the hull's planes (else collide() skips the hull)
       float res[14];
       V3 c = v3(0, 0, 0);
       M3 Rg;
@@ -1438,8 +1439,10 @@ struct Team {
           }
           lb = team_max_dpp<T>(lb);
           lb -= B.kind == 1 ? sqrtf(dot(os, os)) : rB;
-          if (lb < off)
+          if (lb < off) {
             nx = hull_core_contacts<T>(mt->hv, mt->hnv, ld3(mt->hctr), m->hull_plane, np, tl, tb, B, rB, off, res);
+            near = true;
+          }
         }
       }
       if (tl == 0) {
@@ -1449,7 +1452,7 @@ struct Team {
           s->hx[i][3] = nw.x; s->hx[i][4] = nw.y; s->hx[i][5] = nw.z;
           s->hx[i][6] = res[7 * i + 6];
         }
-        s->hxn = nx;
+        s->hxn = near ? nx : -1;
       }
     }
   }
@@ -1677,6 +1680,11 @@ struct Team {
       // the convex-mesh geom first, in a pass of its own (its candidates precede the other geoms' object
       // contacts, as in the oracle's collide; rarely live, and kept out of the main loop's code)
       live &= ~hull_live;
+      // block / pen: hull_stage()'s plane bound puts the object at least the contact offset from the hull (every
+      // hull candidate's distance is at least that bound), so none of the passes below could emit a contact
+      if constexpr (L::HX > 0) {
+        if (s->hxn < 0) hull_live = 0ull;
+      }
       for (unsigned long long hm = hull_live; hm; hm &= hm - 1) {
         const int g = __builtin_ctzll(hm);
         V3 c;
