@@ -1318,33 +1318,33 @@ struct Team {
     const float* gs = mt->gf[g] + 12;
     const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
     if constexpr (OBJ == MG_GT_ELLIPSOID) {
-      // fp64 from here (convex.hpp): the core as five 3-vectors (cvx_contact_v, inlined)
+      // the core as five 3-vectors in the object frame (convex.hpp cvx_contact_v, inlined)
       int kind;
-      D3 a0, a1, a2 = d3(0, 0, 0), a3 = d3(0, 0, 0), a4 = d3(0, 0, 0);
+      V3 a0, a1, a2 = v3(0, 0, 0), a3 = v3(0, 0, 0), a4 = v3(0, 0, 0);
       float r = 0.0f;
       if (round) {
         const float hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
         const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
         kind = 0;
-        a0 = d3(mulT(oR, (c - ax) - op));
-        a1 = d3(mulT(oR, (c + ax) - op));
+        a0 = mulT(oR, (c - ax) - op);
+        a1 = mulT(oR, (c + ax) - op);
         r = gs[0];
       } else {
         kind = 1;
-        a0 = d3(mulT(oR, c - op));
+        a0 = mulT(oR, c - op);
         M3 Rt;
         for (int a = 0; a < 3; a++)
           for (int b = 0; b < 3; b++) Rt.m[a][b] = oR.m[b][a];
         const M3 Rl = mul(Rt, Rg);  // box axes in the object frame (columns)
-        a1 = d3(gs[0], gs[1], gs[2]);
-        a2 = d3(Rl.m[0][0], Rl.m[1][0], Rl.m[2][0]);
-        a3 = d3(Rl.m[0][1], Rl.m[1][1], Rl.m[2][1]);
-        a4 = d3(Rl.m[0][2], Rl.m[1][2], Rl.m[2][2]);
+        a1 = v3(gs[0], gs[1], gs[2]);
+        a2 = v3(Rl.m[0][0], Rl.m[1][0], Rl.m[2][0]);
+        a3 = v3(Rl.m[0][1], Rl.m[1][1], Rl.m[2][1]);
+        a4 = v3(Rl.m[0][2], Rl.m[1][2], Rl.m[2][2]);
       }
-      const CvxHit hit = cvx_contact_v(kind, a0, a1, a2, a3, a4, r, d3(os), p->contact_offset);
-      *dist = (float)hit.d;
-      *pt = mul(oR, f3(hit.pt)) + op;
-      *nrm = mul(oR, f3(hit.nrm));
+      const CvxHit hit = cvx_contact_v(kind, a0, a1, a2, a3, a4, r, os, p->contact_offset);
+      *dist = hit.d;
+      *pt = mul(oR, hit.pt) + op;
+      *nrm = mul(oR, hit.nrm);
       return true;
     }
     // pen: capsule of radius os.x along the object's z, half length os.y
@@ -1547,7 +1547,7 @@ struct Team {
         r = hb.x;
         cnt = 1;
       } else if (ot == MG_GT_ELLIPSOID && tl == 0) {
-        e = mul(oR, f3(ell_support(d3(hb), d3(-oR.m[2][0], -oR.m[2][1], -oR.m[2][2])))) + op;
+        e = mul(oR, ell_support(hb, v3(-oR.m[2][0], -oR.m[2][1], -oR.m[2][2]))) + op;
         cnt = 1;
       }
       const float d = e.z - r;

@@ -845,8 +845,8 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
  * contact offset, since such a candidate is not a contact).  Box cores are rounded by a 1 mm margin
  * (CVX_MARGIN: edges and corners of a hand box become 1 mm round; penetrations shallower than that
  * stay with GJK).  Overlapping cores (the simplex encloses the origin) go to
- * MPR (below) for the penetration vector.  The HIP kernel
- * (csrc/convex.hpp) runs the same algorithm in fp32. */
+ * MPR (below) for the penetration vector.  GJK's witnesses are then polished by alternating projections
+ * (cvx_polish).  The HIP kernel (csrc/convex.hpp) runs the same algorithm in fp32. */
 typedef struct {
   int kind;                    /* 0 segment [p0, p1], 1 box (c, R columns = axes, h) */
   real p0[3], p1[3];
@@ -1161,6 +1161,171 @@ static int cvx_finite(const real* p, const real* n, real d) {
          isfinite(d);
 }
 
+/* Exact closest points of core A and the ellipsoid (cvx_polish), from GJK's witnesses.  GJK converges linearly
+ * against the curved surface and its stop rule leaves the witness direction accurate to about sqrt(GJK_REL) (the
+ * fp32 kernel's 1e-6: 1e-3).  The polish solves the optimality conditions on the feature of A that holds GJK's
+ * witness, by Newton's method on the ellipsoid point's Lagrange multiplier lam: b_i = e_i^2 a_i / (e_i^2 + lam),
+ * so the separation a - b = lam a_i / (e_i^2 + lam) carries no cancellation at small gaps, and the egg's normal
+ * at b is the direction of a_i / (e_i^2 + lam):
+ *   vertex a:          sum_i b_i^2 / e_i^2 = 1                               (unknown lam)
+ *   edge a0 + t u:     the same and (a - b) . u = 0                          (unknowns t, lam; 2 x 2 Newton)
+ *   box face (n, h):   b = the egg's support point in -n, a = b projected onto the face (closed form)
+ * An active set moves between them: a parameter that leaves its edge or face is clamped (face -> edge ->
+ * vertex), and a clamped box axis through whose face the separation does not point is freed (vertex -> edge
+ * -> face).  (Alternating projections between the two shapes contract the error along an edge nearly tangent
+ * to the egg only by R / (R + gap) per round: measured, no use.)  The kernel (csrc/convex.hpp) runs the same
+ * steps in fp32 with CVX_NEWTON iterations per solve; here each solve runs CVX_NEWTON_ORACLE. */
+#ifdef ORC_FP32
+#define CVX_NEWTON_ORACLE 3
+#else
+#define CVX_NEWTON_ORACLE 12
+#endif
+
+static real vtx_newton(const real* e2, const real* a, real lam, int iters) {
+  for (int it = 0; it < iters; it++) {
+    real F = -1, dF = 0;
+    for (int i = 0; i < 3; i++) {
+      const real q = 1 / (e2[i] + lam), t = e2[i] * a[i] * a[i] * q * q;
+      F += t;
+      dF -= 2 * t * q;
+    }
+    if (!(dF < 0)) break;
+    const real ln = lam - F / dF;
+    lam = ln > 0 ? ln : 0;
+  }
+  return lam;
+}
+
+/* (t, lam) for a(t) = a0 + t u: F1 = sum e2 a^2 q^2 - 1, F2 = (a - b) . u = sum lam q a u */
+static void edge_newton(const real* e2, const real* a0, const real* u, real* t, real* lam, int iters) {
+  for (int it = 0; it < iters; it++) {
+    real F1 = -1, F1t = 0, F1l = 0, F2 = 0, F2t = 0, F2l = 0;
+    for (int i = 0; i < 3; i++) {
+      const real ai = a0[i] + *t * u[i], q = 1 / (e2[i] + *lam), w = e2[i] * ai * q * q; /* w = b_i q_i */
+      F1 += ai * w;
+      F1l -= 2 * ai * w * q;
+      F1t += 2 * w * u[i];
+      F2 += *lam * q * ai * u[i];
+      F2l += u[i] * w;
+      F2t += u[i] * u[i] * *lam * q;
+    }
+    const real det = F1t * F2l - F1l * F2t;
+    if (!(det > 0)) break;
+    *t += (F1l * F2 - F1 * F2l) / det;
+    const real ln = *lam + (F2t * F1 - F1t * F2) / det;
+    *lam = ln > 0 ? ln : 0;
+  }
+}
+
+static void cvx_polish(const cvx_shape* A, const real* e, real* pa, real* pb, real* dist) {
+  const int N = CVX_NEWTON_ORACLE;
+  const real e2[3] = {e[0] * e[0], e[1] * e[1], e[2] * e[2]};
+  real g[3] = {pb[0] / e2[0], pb[1] / e2[1], pb[2] / e2[2]};
+  real dv[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+  const real gg = dot3(g, g);
+  real lam = gg > 0 ? dot3(dv, g) / gg : 0;
+  lam = lam > 0 ? lam : 0;
+  real a[3], b[3];
+  int face = 0;
+  if (A->kind == 0) { /* segment: its interior, else the end on the side the interior solution left by */
+    real u[3] = {A->p1[0] - A->p0[0], A->p1[1] - A->p0[1], A->p1[2] - A->p0[2]};
+    const real uu = dot3(u, u);
+    real w[3] = {pa[0] - A->p0[0], pa[1] - A->p0[1], pa[2] - A->p0[2]};
+    real t = uu > 0 ? dot3(w, u) / uu : 0, l = lam;
+    t = t < 0 ? 0 : (t > 1 ? 1 : t);
+    const real t0 = t;
+    if (uu > 0) edge_newton(e2, A->p0, u, &t, &l, N);
+    if (uu > 0 && t > 0 && t < 1 && isfinite(t) && isfinite(l)) {
+      lam = l;
+    } else {
+      t = (isfinite(t) ? t : t0) < 0.5 ? 0 : 1;
+      for (int i = 0; i < 3; i++) a[i] = A->p0[i] + t * u[i];
+      lam = vtx_newton(e2, a, lam, N);
+    }
+    for (int i = 0; i < 3; i++) a[i] = A->p0[i] + t * u[i];
+  } else { /* box: active set over the axes clamped at +-h (sg), from GJK's witness */
+    const real hmax = fmax(A->h[0], fmax(A->h[1], A->h[2])), tol = 1e-5 * hmax;
+    real lc[3];
+    int sg[3], done = 0;
+    for (int k = 0; k < 3; k++) {
+      lc[k] = A->R[0][k] * (pa[0] - A->c[0]) + A->R[1][k] * (pa[1] - A->c[1]) + A->R[2][k] * (pa[2] - A->c[2]);
+      sg[k] = lc[k] >= A->h[k] - tol ? 1 : (lc[k] <= -A->h[k] + tol ? -1 : 0);
+    }
+    for (int pass = 0; pass < 6 && !done; pass++) {
+      const int m = (sg[0] == 0) + (sg[1] == 0) + (sg[2] == 0);
+      if (m == 3) return; /* not on the surface: keep GJK's witnesses */
+      if (m == 2) {       /* face */
+        const int k = sg[0] ? 0 : (sg[1] ? 1 : 2);
+        real nf[3], mn[3];
+        for (int i = 0; i < 3; i++) { nf[i] = sg[k] * A->R[i][k]; mn[i] = -nf[i]; }
+        ell_support(e, mn, b);
+        real bc[3] = {b[0] - A->c[0], b[1] - A->c[1], b[2] - A->c[2]};
+        const real dd = dot3(nf, bc) - A->h[k];
+        for (int i = 0; i < 3; i++) a[i] = b[i] - dd * nf[i];
+        int moved = 0;
+        for (int j = 0; j < 3; j++) {
+          if (j == k) continue;
+          const real lj = A->R[0][j] * (a[0] - A->c[0]) + A->R[1][j] * (a[1] - A->c[1]) + A->R[2][j] * (a[2] - A->c[2]);
+          if (lj > A->h[j] || lj < -A->h[j]) { sg[j] = lj > 0 ? 1 : -1; moved = 1; }
+        }
+        if (moved) continue;
+        face = 1;
+        *dist = dd;
+        done = 1;
+        break;
+      }
+      real a0[3] = {A->c[0], A->c[1], A->c[2]};
+      int jf = -1;
+      for (int k = 0; k < 3; k++) {
+        if (sg[k] == 0) { jf = k; continue; }
+        for (int i = 0; i < 3; i++) a0[i] += sg[k] * A->h[k] * A->R[i][k];
+      }
+      if (m == 1) { /* edge along axis jf */
+        real u[3] = {A->R[0][jf], A->R[1][jf], A->R[2][jf]}, t = lc[jf], l = lam;
+        edge_newton(e2, a0, u, &t, &l, N);
+        if (!(isfinite(t) && isfinite(l))) return;
+        if (t > A->h[jf] || t < -A->h[jf]) { sg[jf] = t > 0 ? 1 : -1; continue; }
+        lam = l;
+        for (int i = 0; i < 3; i++) a[i] = a0[i] + t * u[i];
+      } else { /* vertex */
+        for (int i = 0; i < 3; i++) a[i] = a0[i];
+        lam = vtx_newton(e2, a, lam, N);
+      }
+      /* optimal only if b - a (from A to the egg, along -a_i q_i) leaves A through every clamped face: an axis
+       * it does not leave through is freed */
+      real sv[3];
+      for (int i = 0; i < 3; i++) sv[i] = -a[i] / (e2[i] + lam);
+      const real sl = sqrt(dot3(sv, sv));
+      int freed = 0;
+      for (int k = 0; k < 3; k++) {
+        if (sg[k] == 0) continue;
+        const real comp = sg[k] * (A->R[0][k] * sv[0] + A->R[1][k] * sv[1] + A->R[2][k] * sv[2]);
+        if (comp < -1e-6 * sl) { sg[k] = 0; freed = 1; lc[k] = 0; }
+      }
+      if (freed) {
+        for (int k = 0; k < 3; k++) /* the free coordinates restart from the current point */
+          if (sg[k] == 0) lc[k] = A->R[0][k] * (a[0] - A->c[0]) + A->R[1][k] * (a[1] - A->c[1]) + A->R[2][k] * (a[2] - A->c[2]);
+        continue;
+      }
+      done = 1;
+    }
+    if (!done) return;
+  }
+  if (!face) {
+    real sv[3];
+    for (int i = 0; i < 3; i++) {
+      const real q = 1 / (e2[i] + lam);
+      b[i] = e2[i] * a[i] * q;
+      sv[i] = lam * a[i] * q;
+    }
+    *dist = sqrt(dot3(sv, sv));
+  }
+  if (!(isfinite(a[0]) && isfinite(a[1]) && isfinite(a[2]) && isfinite(b[0]) && isfinite(b[1]) && isfinite(b[2]) &&
+        isfinite(*dist)))
+    return;
+  for (int i = 0; i < 3; i++) { pa[i] = a[i]; pb[i] = b[i]; }
+}
+
 static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, real* pt, real* nrm,
                         real* d) {
   real pa[3], pb[3], dist, x[3];
@@ -1182,6 +1347,7 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
     return;
   }
   if (g && dist > 1e-9) {
+    cvx_polish(A, e, pa, pb, &dist);
     /* the normal is the egg's surface normal at its witness point (the gradient of the implicit
      * function): better conditioned than (pa - pb) / dist when the gap is small */
     real gr[3] = {pb[0] / (e[0] * e[0]), pb[1] / (e[1] * e[1]), pb[2] / (e[2] * e[2])};

@@ -206,7 +206,88 @@ def test_egg_gjk_distance_matches_dense_samples():
         # the normal points from the egg towards the geom: the contact point moved along it leaves the egg
         out = pt + n * (abs(d) + 1e-3)
         assert ((out / e) ** 2).sum() > 1
+        # the polished witnesses (cvx_polish) are the exact closest pair: pb on the egg with the normal its surface
+        # normal, pa on the core, and each the other's nearest point (pa = pb + n (d + core radius))
+        mg = r if r > 0 else min(1e-3, 0.5 * hb.min())
+        pb = pt - n * (0.5 * d)
+        pa = pb + n * (d + mg)
+        assert abs(((pb / e) ** 2).sum() - 1) < 1e-9, i
+        gr = pb / e ** 2
+        np.testing.assert_allclose(n, gr / np.linalg.norm(gr), atol=1e-9)
+        if r > 0:
+            u = p1 - p0
+            t = np.clip((pb - p0) @ u / (u @ u), 0, 1)
+            near = p0 + t * u
+        else:
+            near = c + R @ np.clip(R.T @ (pb - c), -(hb - mg), hb - mg)
+        np.testing.assert_allclose(pa, near, atol=1e-9, err_msg=str(i))
     assert seen >= 40
+
+
+def _egg_surface_frame(rng, e):
+    d = rng.normal(size=3)
+    d /= np.linalg.norm(d)
+    s = d / np.sqrt(((d / e) ** 2).sum())    # a point of the egg's surface and its outward normal
+    n = s / e ** 2
+    return s, n / np.linalg.norm(n)
+
+
+def _exact_pair_error(pt, n, d, e, core_r, nearest_on_core):
+    """max violation of the closest-pair conditions: pb on the egg, n its normal at pb, pa = pb + n (d + r) the
+    core's point nearest pb"""
+    pb = pt - n * (0.5 * d)
+    pa = pb + n * (d + core_r)
+    gr = pb / e ** 2
+    return max(abs(((pb / e) ** 2).sum() - 1), np.abs(n - gr / np.linalg.norm(gr)).max(),
+               np.abs(pa - nearest_on_core(pb)).max())
+
+
+def test_egg_polish_gives_the_exact_closest_pair():
+    """cvx_polish at contact gaps (0 - 12 mm): segments nearly tangent to the egg (their interior and their ends)
+    and boxes facing it with a face, an edge or a vertex -- the returned witnesses are the exact closest pair (the
+    GJK stop rule alone leaves ~1e-4 of direction error)."""
+    e = np.array([0.03, 0.03, 0.04])
+    rng = np.random.default_rng(7)
+    kinds = {"seg interior": 0, "seg end": 0, "box face": 0, "box edge": 0, "box vertex": 0}
+    for i in range(600):
+        s, n = _egg_surface_frame(rng, e)
+        gap = rng.uniform(0.0005, 0.012)
+        if i % 2 == 0:
+            tdir = np.cross(n, rng.normal(size=3))
+            tdir /= np.linalg.norm(tdir)
+            tdir = tdir + n * rng.uniform(-0.3, 0.3)
+            L = rng.uniform(0.02, 0.05)
+            off = rng.uniform(-0.9, 0.9) * L
+            c = s + n * (gap + 0.004)
+            p0, p1 = c - tdir * (0.5 * L + off), c + tdir * (0.5 * L - off)
+            if (((p0 + (p1 - p0) * np.linspace(0, 1, 200)[:, None]) / e) ** 2).sum(1).min() < 1:
+                continue
+            pt, nn, d = O.ellipsoid_contact(0, np.r_[p0, p1], 0.004, e)
+            u = p1 - p0
+
+            def near(p, p0=p0, u=u):
+                return p0 + np.clip((p - p0) @ u / (u @ u), 0, 1) * u
+            err = _exact_pair_error(pt, nn, d, e, 0.004, near)
+            t = np.clip((pt + nn * (0.5 * d + 0.004) - p0) @ u / (u @ u), 0, 1)
+            kinds["seg end" if t in (0.0, 1.0) else "seg interior"] += 1
+        else:
+            q = rng.normal(size=4)
+            R = _rot(q / np.linalg.norm(q))
+            hb = rng.uniform(0.004, 0.02, 3)
+            mg = min(1e-3, 0.5 * hb.min())
+            c = s + n * (gap + mg + np.abs(R.T @ n) @ (hb - mg))
+            pt, nn, d = O.ellipsoid_contact(1, np.r_[c, R.ravel(), hb], 0.0, e)
+            if d + mg <= 0:
+                continue
+
+            def near(p, c=c, R=R, h=hb - mg):
+                return c + R @ np.clip(R.T @ (p - c), -h, h)
+            err = _exact_pair_error(pt, nn, d, e, mg, near)
+            loc = R.T @ (pt + nn * (0.5 * d + mg) - c)
+            k = int((np.abs(np.abs(loc) - (hb - mg)) < 1e-9).sum())
+            kinds[{1: "box face", 2: "box edge", 3: "box vertex"}[k]] += 1
+        assert err < 1e-9, (i, err)
+    assert min(kinds.values()) >= 10, kinds
 
 
 def test_egg_mpr_penetration_is_a_separating_translation():
