@@ -177,7 +177,7 @@ struct TeamLDS {
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + kPgsPrefetch - 1) / kPgsPrefetch * kPgsPrefetch;
   static constexpr int RB = OBJ ? 6 : (kRBLoco <= T ? kRBLoco : 6);
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
-  // (not for the egg instance, whose fp64 narrowphase already spills: 7.46 vs 7.71 M env-steps/s measured)
+  // (not for the egg instance: with its fp32 narrowphase staged, 12.20 vs 12.42 M env-steps/s measured)
   static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (kJYRegs < MR ? kJYRegs : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
@@ -241,7 +241,7 @@ struct TeamLDS {
   // free object (OBJ): staged root row, obs staging.  The object part of a contact row, [(p - c) x d; d],
   // is recomputed from the contact list where it is needed (the 2.9 KB per team saved lets 6 blocks
   // share a CU: block 12.5 -> 13.8 M env-steps/s); the egg instance keeps the rows in LDS, whose code
-  // the compiler schedules better around the fp64 narrowphase (5.7 vs 3.6-3.9 M env-steps/s measured)
+  // the compiler schedules better around the narrowphase (fp64: 5.7 vs 3.6-3.9 M env-steps/s; fp32 staged: 12.42 vs 12.07 M)
   static constexpr int OROWS = OBJ == MG_GT_ELLIPSOID ? 3 * MC : 1;
   float rwo[OROWS][6];
   float oroot[OBJ ? 13 : 1];
@@ -1457,6 +1457,65 @@ struct Team {
     }
   }
 
+  // The egg's narrowphase, staged right after fk() (fp32, convex.hpp): its candidates are the geoms that pass
+  // collide()'s broadphase (bounding sphere against the egg's; sphere / capsule / box geoms, one candidate each,
+  // geom order), evaluated where only the joint state is live -- fk()'s register outputs are reloaded from their
+  // LDS copies afterwards (reload_tree) -- so the narrowphase's working set does not spill the tree state the
+  // ABA and the rows need.  The results wait in storage that is dead until build_rows(): point -> ct1[f],
+  // normal -> ct2[f], gap -> lmeta[f] (bits), geom -> lmeta[MN - 1 + f], count -> nrows; collide() emits them
+  // in its object pass, in the same order as the unstaged candidates.
+  __device__ __forceinline__ void egg_stage() {
+    if constexpr (OBJ == MG_GT_ELLIPSOID) {
+      static_assert(MG <= MC && MG <= MN - 1 && MG <= T, "the egg's staged candidates must fit one team pass");
+      const float ro = obj_radius(), off = p->contact_offset;
+      const int G = mt->ng;
+      bool ok = false;
+      if (tl < G) {
+        const int gt = mt->gtype[tl];
+        if ((mt->gfil[tl] & MG_COLLIDE_OBJECT) && (gt == MG_GT_SPHERE || gt == MG_GT_CAPSULE || gt == MG_GT_BOX)) {
+          V3 c;
+          M3 Rg;
+          geom_world(tl, &c, &Rg);
+          const V3 dc = c - op;
+          const float reach = mt->gf[tl][15] + ro + off;
+          ok = dot(dc, dc) <= reach * reach;
+        }
+      }
+      constexpr unsigned long long tmask = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
+      const unsigned long long live = (__ballot(ok) >> tb) & tmask;
+      const int NC = __popcll(live);
+      if (tl < NC) {
+        unsigned long long mm = live;
+        for (int k = 0; k < tl; k++) mm &= mm - 1;
+        const int g = __builtin_ctzll(mm);
+        V3 c, pt, nrm;
+        M3 Rg;
+        float d;
+        geom_world(g, &c, &Rg);
+        obj_candidate_convex(g, 0, c, Rg, &pt, &nrm, &d);
+        s->ct1[tl][0] = pt.x; s->ct1[tl][1] = pt.y; s->ct1[tl][2] = pt.z;
+        s->ct2[tl][0] = nrm.x; s->ct2[tl][1] = nrm.y; s->ct2[tl][2] = nrm.z;
+        s->lmeta[tl] = __float_as_int(d);
+        s->lmeta[MN - 1 + tl] = g;
+      }
+      if (tl == 0) s->nrows = NC;
+    }
+  }
+  // fk()'s register outputs (R, x, V; S on joint lanes) again, from the copies it stored in the LDS
+  __device__ __forceinline__ void reload_tree() {
+    asm volatile("" ::: "memory");
+    R = M3{};
+    x = v3(0, 0, 0);
+    V = S = szero();
+    if (node >= 0) {
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) R.m[a][b] = s->R[node][3 * a + b];
+      x = ld3(s->x[node]);
+      V = sv(ld3(s->V[node]), ld3(s->V[node] + 3));
+    }
+    if (node > 0) S = sv(ld3(s->S[node]), ld3(s->S[node] + 3));
+  }
+
   __device__ __forceinline__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
     s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
     s->cn[slot][0] = n.x; s->cn[slot][1] = n.y; s->cn[slot][2] = n.z;
@@ -1762,6 +1821,26 @@ struct Team {
       // the survivors' candidates in geom order: lane per geom, a team scan of the counts places each geom's
       // run, and the geom writes (geom, candidate index) for its run into a map behind the pair list, so a
       // candidate's lane finds its pair with one LDS read (instead of walking the live mask)
+      if constexpr (OBJ == MG_GT_ELLIPSOID) {  // the egg: the candidates egg_stage() computed, in geom order
+        const int ne = s->nrows;
+        int cnt = 0, g = 0;
+        V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
+        float d = 0.0f;
+        if (tl < ne) {
+          pt = ld3(s->ct1[tl]);
+          nrm = ld3(s->ct2[tl]);
+          d = __int_as_float(s->lmeta[tl]);
+          g = s->lmeta[MN - 1 + tl];
+          cnt = d < off ? 1 : 0;
+        }
+        const int incl = team_incl_scan<T>(cnt);
+        const int tot = __shfl(incl, tb + T - 1);
+        if (cnt) {
+          const int slot = base + incl - 1;
+          if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
+        }
+        base += tot;
+      } else {
       static_assert(MN * 27 >= MG * GW + MP + (17 * MG + 1) / 2, "the candidate map must fit behind the pair list");
       uint16_t* cmap = reinterpret_cast<uint16_t*>(plist + MP);
       int NC = 0;
@@ -1797,6 +1876,7 @@ struct Team {
           if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
         }
         base += tot;
+      }
       }
     }
     if (tl == 0) s->ncon = base < cap ? base : cap;
@@ -1893,6 +1973,10 @@ struct Team {
     ph_mark(15);
     hull_stage();
     fk();
+    if constexpr (OBJ == MG_GT_ELLIPSOID) {
+      egg_stage();
+      reload_tree();
+    }
     set_axis();
     ph_mark(0);
     if (OBJ) tendons();
