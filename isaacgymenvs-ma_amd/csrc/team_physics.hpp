@@ -1193,22 +1193,9 @@ struct Team {
     const V3 hb = osize();
     const int ty = mt->gtype[g];
     const float* gs = mt->gf[g] + 12;
-    if (ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE) {
-      const float r = gs[0], hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
-      const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
-      const V3 al = mulT(oR, (c - ax) - op), bl = mulT(oR, (c + ax) - op), u = bl - al;
-      const float t = seg_box_t(al, u, hb);
-      const V3 P = al + u * t;
-      V3 nb, cb;
-      const float d = point_box(P, hb, &nb, &cb) - r;
-      *pt = mul(oR, ((P - nb * r) + cb) * 0.5f) + op;
-      *nrm = mul(oR, nb);
-      *dist = d;
-      return true;
-    }
+    const bool round = ty == MG_GT_SPHERE || ty == MG_GT_CAPSULE;
     const V3 hg = v3(gs[0], gs[1], gs[2]);
-    const int v = q & 7;
-    if (q == 16) {  // edge against edge, in the object frame
+    if (!round && q == 16) {  // edge against edge, in the object frame
       M3 Rt;
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) Rt.m[a][b] = oR.m[b][a];
@@ -1220,21 +1207,39 @@ struct Team {
       *dist = de;
       return true;
     }
-    if (q < 8) {
+    // every other candidate is one point against one box: the segment's closest point (sphere / capsule) or a
+    // geom vertex against the object box, an object vertex against the geom box.  The three set up the query
+    // (point P in the box's frame, the box, the frame's rotation / origin, radius, normal sign) and share one
+    // point_box and the output transform, so a pass whose lanes mix them runs point_box once, not three times.
+    V3 P, hx, cf;
+    M3 Rf;
+    float r = 0.0f, sgn = 1.0f;
+    const int v = q & 7;
+    if (round) {
+      const float hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
+      const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
+      const V3 al = mulT(oR, (c - ax) - op), bl = mulT(oR, (c + ax) - op), u = bl - al;
+      P = al + u * seg_box_t(al, u, hb);
+      r = gs[0];
+    } else if (q < 8) {
       const V3 l = v3((v & 1 ? 1.f : -1.f) * hg.x, (v & 2 ? 1.f : -1.f) * hg.y, (v & 4 ? 1.f : -1.f) * hg.z);
-      const V3 pl = mulT(oR, (c + mul(Rg, l)) - op);
-      V3 nb, cb;
-      *dist = point_box(pl, hb, &nb, &cb);
-      *pt = mul(oR, (pl + cb) * 0.5f) + op;
-      *nrm = mul(oR, nb);
+      P = mulT(oR, (c + mul(Rg, l)) - op);
     } else {
       const V3 l = v3((v & 1 ? 1.f : -1.f) * hb.x, (v & 2 ? 1.f : -1.f) * hb.y, (v & 4 ? 1.f : -1.f) * hb.z);
-      const V3 pl = mulT(Rg, (mul(oR, l) + op) - c);
-      V3 nb, cb;
-      *dist = point_box(pl, hg, &nb, &cb);
-      *pt = mul(Rg, (pl + cb) * 0.5f) + c;
-      *nrm = mul(Rg, nb) * -1.0f;
+      P = mulT(Rg, (mul(oR, l) + op) - c);
+      sgn = -1.0f;
     }
+    const bool geom_box = !round && q >= 8;
+    hx = geom_box ? hg : hb;
+    cf = geom_box ? c : op;
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int b = 0; b < 3; b++) Rf.m[a][b] = geom_box ? Rg.m[a][b] : oR.m[a][b];
+    V3 nb, cb;
+    *dist = point_box(P, hx, &nb, &cb) - r;
+    *pt = mul(Rf, ((P - nb * r) + cb) * 0.5f) + cf;
+    *nrm = mul(Rf, nb) * sgn;
     return true;
   }
 
