@@ -1639,19 +1639,15 @@ struct Team {
       const int pi = p0 + tl;
       int ok = 0;
       if (pi < P) {
-        V3 a0, a1, b0, b1;
-        float ra, rb;
-        const bool sa = geom_segment(mt->pairs[pi][0], &a0, &a1, &ra), sb = geom_segment(mt->pairs[pi][1], &b0, &b1, &rb);
-        if (sa && sb) {
-          V3 ca = (a0 + a1) * 0.5f, cb = (b0 + b1) * 0.5f, dc = ca - cb;
-          float ha = sqrtf(dot(a1 - a0, a1 - a0)) * 0.5f, hb = sqrtf(dot(b1 - b0, b1 - b0)) * 0.5f;
-          float reach = ha + hb + ra + rb + poff;
-          ok = dot(dc, dc) <= reach * reach ? 1 : 0;
-        } else if (sa != sb) {  // a box (bounding radius about its centre) and a sphere / capsule
-          const int gx = mt->pairs[pi][sa ? 1 : 0];
-          const V3 p0 = sa ? a0 : b0, p1 = sa ? a1 : b1;
-          const V3 dc = (p0 + p1) * 0.5f - ld3(gw_tile() + GW * gx);
-          const float reach = mt->gf[gx][15] + sqrtf(dot(p1 - p0, p1 - p0)) * 0.5f + (sa ? ra : rb) + poff;
+        // the two geoms' bounding spheres (staged centre, the tile's bounding radius: capsule half length +
+        // radius, sphere radius, box half diagonal: the same bound as the cores' spheres); pairs with no segment
+        // side have no narrowphase
+        const int ga = mt->pairs[pi][0], gb = mt->pairs[pi][1];
+        const int ta = mt->gtype[ga], tb2 = mt->gtype[gb];
+        const bool sa = ta == MG_GT_SPHERE || ta == MG_GT_CAPSULE, sb = tb2 == MG_GT_SPHERE || tb2 == MG_GT_CAPSULE;
+        if (sa || sb) {  // (the non-segment side of a mixed pair is a box: the narrowphase below)
+          const V3 dc = ld3(gw_tile() + GW * ga) - ld3(gw_tile() + GW * gb);
+          const float reach = mt->gf[ga][15] + mt->gf[gb][15] + poff;
           ok = dot(dc, dc) <= reach * reach ? 1 : 0;
         }
       }
