@@ -1176,7 +1176,7 @@ static int cvx_finite(const real* p, const real* n, real d) {
  * to the egg only by R / (R + gap) per round: measured, no use.)  The kernel (csrc/convex.hpp) runs the same
  * steps in fp32 with CVX_NEWTON iterations per solve; here each solve runs CVX_NEWTON_ORACLE. */
 #ifdef ORC_FP32
-#define CVX_NEWTON_ORACLE 3
+#define CVX_NEWTON_ORACLE 4
 #else
 #define CVX_NEWTON_ORACLE 12
 #endif
@@ -1253,7 +1253,18 @@ static void cvx_polish(const cvx_shape* A, const real* e, real* pa, real* pb, re
     }
     for (int pass = 0; pass < 6 && !done; pass++) {
       const int m = (sg[0] == 0) + (sg[1] == 0) + (sg[2] == 0);
-      if (m == 3) return; /* not on the surface: keep GJK's witnesses */
+      if (m == 3) { /* GJK's witness inside the box (an early stop on a simplex across it): start from the face
+                     * whose outward normal is nearest the direction to the egg's witness */
+        real dv[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]}, best = -1;
+        int kb = 0;
+        for (int k = 0; k < 3; k++) {
+          const real dk = A->R[0][k] * dv[0] + A->R[1][k] * dv[1] + A->R[2][k] * dv[2];
+          if (fabs(dk) > best) { best = fabs(dk); kb = k; }
+        }
+        const real dk = A->R[0][kb] * dv[0] + A->R[1][kb] * dv[1] + A->R[2][kb] * dv[2];
+        sg[kb] = dk >= 0 ? 1 : -1;
+        continue;
+      }
       if (m == 2) {       /* face */
         const int k = sg[0] ? 0 : (sg[1] ? 1 : 2);
         real nf[3], mn[3];
