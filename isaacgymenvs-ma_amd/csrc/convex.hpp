@@ -5,8 +5,8 @@
 //   * everything in the object frame (ellipsoid of semi-axes e centred at the origin);
 //   * shape A is a hand geom's core: a segment (sphere / capsule, radius added afterwards) or a box;
 //   * GJK distance on A - B: closest point of the simplex by Voronoi-region tests (Ericson 5.1.2,
-//     5.1.5, 5.1.6), stop on |v|^2 - v.w <= GJK_REL |v|^2 + 1e-24 (kernel 1e-3, oracle 1e-8: the polish below
-//     makes the result independent of it), a repeated support point, no progress
+//     5.1.5, 5.1.6), stop on |v|^2 - v.w <= GJK_REL |v|^2 + 1e-24 (kernel 0.1, oracle 1e-8: the polish below
+//     makes the result independent of it; the kernel's GJK only has to find the feature), a repeated support point, no progress
 //     or 64 iterations; exit early once a separating plane is farther than the contact offset (such a
 //     candidate is no contact, so most broadphase survivors cost one or two support calls);
 //   * GJK's witnesses polished to the exact closest pair (cvx_polish): GJK converges linearly against the curved
@@ -29,9 +29,9 @@
 namespace mg {
 
 // GJK stop / no-progress thresholds relative to |v|^2 (fp32)
-constexpr float GJK_REL = 1e-3f;  // loose: the polish resolves the pair (the oracle's 1e-8 + polish give the same)
+constexpr float GJK_REL = 1e-1f;  // loose on purpose: the polish resolves the pair
 constexpr float GJK_STALL = 1e-7f;
-constexpr int CVX_NEWTON = 4;  // Newton iterations per polish solve
+constexpr int CVX_NEWTON = 6;  // Newton iterations per polish solve
 constexpr float CVX_MARGIN = 1e-3f;  // rounding of box cores against the egg (m)
 
 struct CvxShape {
@@ -236,7 +236,7 @@ __device__ __forceinline__ int cvx_gjk(const CvxShape& A, V3 e, float cut, V3& p
 // Exact closest points from GJK's witnesses (oracle cvx_polish, whose comment has the derivation): Newton on the egg
 // point's multiplier lam (b_i = e_i^2 a_i q_i, q_i = 1 / (e_i^2 + lam); a - b = lam a_i q_i) for a vertex of A
 // (unknown lam) or an edge a0 + t u (unknowns t, lam), the closed form for a box face, and an active set over the
-// box's clamped axes.  CVX_NEWTON iterations per solve from GJK's start (quadratic convergence from the ~3e-2 of
+// box's clamped axes.  CVX_NEWTON iterations per solve from GJK's start (quadratic convergence from the ~0.3 rad of
 // direction error its loose stop leaves).
 __device__ __forceinline__ float vtx_newton(V3 e2, V3 a, float lam) {
   const V3 t0 = v3(e2.x * a.x * a.x, e2.y * a.y * a.y, e2.z * a.z * a.z);

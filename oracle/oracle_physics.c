@@ -1176,7 +1176,7 @@ static int cvx_finite(const real* p, const real* n, real d) {
  * to the egg only by R / (R + gap) per round: measured, no use.)  The kernel (csrc/convex.hpp) runs the same
  * steps in fp32 with CVX_NEWTON iterations per solve; here each solve runs CVX_NEWTON_ORACLE. */
 #ifdef ORC_FP32
-#define CVX_NEWTON_ORACLE 4
+#define CVX_NEWTON_ORACLE 6
 #else
 #define CVX_NEWTON_ORACLE 12
 #endif
