@@ -177,7 +177,7 @@ struct TeamLDS {
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + kPgsPrefetch - 1) / kPgsPrefetch * kPgsPrefetch;
   static constexpr int RB = OBJ ? 6 : (kRBLoco <= T ? kRBLoco : 6);
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
-  // (not for the egg instance: with its fp32 narrowphase staged, 12.20 vs 12.42 M env-steps/s measured)
+  // (not for the egg instance: 17.16 vs 17.73 M env-steps/s and 450 vs 409 MB per launch, measured on its fp32 build)
   static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (kJYRegs < MR ? kJYRegs : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
@@ -241,7 +241,7 @@ struct TeamLDS {
   // free object (OBJ): staged root row, obs staging.  The object part of a contact row, [(p - c) x d; d],
   // is recomputed from the contact list where it is needed (the 2.9 KB per team saved lets 6 blocks
   // share a CU: block 12.5 -> 13.8 M env-steps/s); the egg instance keeps the rows in LDS, whose code
-  // the compiler schedules better around the narrowphase (fp64: 5.7 vs 3.6-3.9 M env-steps/s; fp32 staged: 12.42 vs 12.07 M)
+  // the compiler schedules better around the narrowphase (fp64: 5.7 vs 3.6-3.9 M env-steps/s; fp32: 17.73 vs 17.21 M)
   static constexpr int OROWS = OBJ == MG_GT_ELLIPSOID ? 3 * MC : 1;
   float rwo[OROWS][6];
   float oroot[OBJ ? 13 : 1];
