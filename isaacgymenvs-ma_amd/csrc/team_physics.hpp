@@ -411,7 +411,7 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
     if (fabsf(uv[k]) < 1e-12f) {
       if (av[k] < -hv[k] || av[k] > hv[k]) hit = false;
     } else {
-      const float iu = 1.0f / uv[k];
+      const float iu = prcp(uv[k]);
       ta = (-hv[k] - av[k]) * iu;
       tb = (hv[k] - av[k]) * iu;
       t0 = fmaxf(t0, fminf(ta, tb));
@@ -503,12 +503,13 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
       const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
       const float ln = sqrtf(R.m[i1][j] * R.m[i1][j] + R.m[i2][j] * R.m[i2][j]);
       if (ln < 1e-6f) continue;
-      const float near = fmaxf(fmaxf(fabsf(R.m[i1][j]), fabsf(R.m[i2][j])), fmaxf(fabsf(R.m[i][j1]), fabsf(R.m[i][j2]))) / ln;
+      const float il = prcp(ln);
+      const float near = fmaxf(fmaxf(fabsf(R.m[i1][j]), fabsf(R.m[i2][j])), fmaxf(fabsf(R.m[i][j1]), fabsf(R.m[i][j2]))) * il;
       if (near > 0.98f) continue;
       const float tl = cv[i2] * R.m[i1][j] - cv[i1] * R.m[i2][j];
       const float rb = hbv[i1] * fabsf(R.m[i2][j]) + hbv[i2] * fabsf(R.m[i1][j]);
       const float ra = hgv[j1] * fabsf(R.m[i][j2]) + hgv[j2] * fabsf(R.m[i][j1]);
-      const float sep = (fabsf(tl) - ra - rb) / ln;
+      const float sep = (fabsf(tl) - ra - rb) * il;
       if (sep > best) {
         const float sg = tl < 0.0f ? -1.0f : 1.0f;
         best = sep; bi = i; bj = j;
@@ -543,7 +544,8 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
   const V3 PA = v3(pa[0], pa[1], pa[2]), PB = v3(pb[0], pb[1], pb[2]), w0 = PA - PB;
   const float b = dot(ua, ub), dd = dot(ua, w0), e = dot(ub, w0), den = 1.0f - b * b;
   if (den < 1e-12f) return false;
-  const float sa = (b * e - dd) / den, tb = (e - b * dd) / den;
+  const float iden = prcp(den);
+  const float sa = (b * e - dd) * iden, tb = (e - b * dd) * iden;
   if (fabsf(sa) > hga || fabsf(tb) > hbb) return false;
   *pt = ((PA + ua * sa) + (PB + ub * tb)) * 0.5f;
   *nrm = v3(L[0], L[1], L[2]);
@@ -891,7 +893,7 @@ struct Team {
   __device__ __forceinline__ V3 obj_inv_inertia(V3 x) const {
     const V3 I = oinertia();
     V3 b = mulT(oR, x);
-    return mul(oR, v3(b.x / I.x, b.y / I.y, b.z / I.z));
+    return mul(oR, v3(b.x * prcp(I.x), b.y * prcp(I.y), b.z * prcp(I.z)));  // 1-ulp reciprocals, as the physics
   }
   __device__ __forceinline__ void obj_free() {
     if (!OBJ) return;
@@ -925,13 +927,13 @@ struct Team {
     const int k = tl - ob0;
     if constexpr (L::OROWS > 1) {
       const float* J = s->rwo[r];
-      if (k >= 3) return J[k] / omass();
+      if (k >= 3) return J[k] * prcp(omass());
       const V3 y = obj_inv_inertia(v3(J[0], J[1], J[2]));
       return k == 0 ? y.x : k == 1 ? y.y : y.z;
     }
     V3 wo, d;
     obj_jrow(r, &wo, &d);
-    if (k >= 3) return (k == 3 ? d.x : (k == 4 ? d.y : d.z)) / omass();
+    if (k >= 3) return (k == 3 ? d.x : (k == 4 ? d.y : d.z)) * prcp(omass());
     const V3 y = obj_inv_inertia(wo);
     return k == 0 ? y.x : k == 1 ? y.y : y.z;
   }
@@ -1893,23 +1895,24 @@ struct Team {
       sv_ = tv = 0;
     } else if (a <= eps) {
       sv_ = 0;
-      tv = fminf(fmaxf(f / e, 0.0f), 1.0f);
+      tv = fminf(fmaxf(f * prcp(e), 0.0f), 1.0f);
     } else {
       float c = dot(d1, r);
       if (e <= eps) {
         tv = 0;
-        sv_ = fminf(fmaxf(-c / a, 0.0f), 1.0f);
+        sv_ = fminf(fmaxf(-c * prcp(a), 0.0f), 1.0f);
       } else {
         float b = dot(d1, d2), den = a * e - b * b;
-        sv_ = den > eps ? (b * f - c * e) / den : 0.0f;
+        const float ia = prcp(a), ie = prcp(e);
+        sv_ = den > eps ? (b * f - c * e) * prcp(den) : 0.0f;
         sv_ = fminf(fmaxf(sv_, 0.0f), 1.0f);
-        tv = (b * sv_ + f) / e;
+        tv = (b * sv_ + f) * ie;
         if (tv < 0) {
           tv = 0;
-          sv_ = fminf(fmaxf(-c / a, 0.0f), 1.0f);
+          sv_ = fminf(fmaxf(-c * ia, 0.0f), 1.0f);
         } else if (tv > 1) {
           tv = 1;
-          sv_ = fminf(fmaxf((b - c) / a, 0.0f), 1.0f);
+          sv_ = fminf(fmaxf((b - c) * ia, 0.0f), 1.0f);
         }
       }
     }
