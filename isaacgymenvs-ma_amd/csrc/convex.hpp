@@ -58,13 +58,13 @@ __device__ __forceinline__ V3 ell_support(V3 e, V3 d) {
   const V3 q = v3(e.x * e.x * d.x, e.y * e.y * d.y, e.z * e.z * d.z);
   const float n = sqrtf(q.x * d.x + q.y * d.y + q.z * d.z);
   if (n < 1e-30f) return v3(0, 0, 0);
-  return q * (1.0f / n);
+  return q * prcp(n);
 }
 
 __device__ __forceinline__ void cvx_seg(V3 a, V3 b, float* lam) {
   const V3 ab = b - a;
   const float den = dot(ab, ab);
-  float t = den > 0.0f ? -dot(a, ab) / den : 0.0f;
+  float t = den > 0.0f ? -dot(a, ab) * prcp(den) : 0.0f;
   t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
   lam[0] = 1.0f - t;
   lam[1] = t;
@@ -81,27 +81,28 @@ __device__ __forceinline__ void cvx_tri(V3 a, V3 b, V3 c, float* lam) {
   // the edge cases divide by a length that is 0 only for coincident vertices (an MPR portal whose support
   // points repeat): the vertex itself is then the answer, not 0 / 0 (the oracle's cvx_tri likewise)
   if (vc <= 0.0f && d1 >= 0.0f && e3 <= 0.0f) {
-    const float v = (d1 - e3) > 0.0f ? d1 / (d1 - e3) : 0.0f;
+    const float v = (d1 - e3) > 0.0f ? d1 * prcp(d1 - e3) : 0.0f;
     lam[0] = 1.0f - v; lam[1] = v; return;
   }
   const float d5 = -dot(ab, c), d6 = -dot(ac, c);
   if (d6 >= 0.0f && d5 <= d6) { lam[2] = 1.0f; return; }
   const float vb = d5 * d2 - d1 * d6;
   if (vb <= 0.0f && d2 >= 0.0f && d6 <= 0.0f) {
-    const float w = (d2 - d6) > 0.0f ? d2 / (d2 - d6) : 0.0f;
+    const float w = (d2 - d6) > 0.0f ? d2 * prcp(d2 - d6) : 0.0f;
     lam[0] = 1.0f - w; lam[2] = w; return;
   }
   const float va = e3 * d6 - d5 * d4;
   if (va <= 0.0f && (d4 - e3) >= 0.0f && (d5 - d6) >= 0.0f) {
     const float den2 = (d4 - e3) + (d5 - d6);
-    const float w = den2 > 0.0f ? (d4 - e3) / den2 : 0.0f;
+    const float w = den2 > 0.0f ? (d4 - e3) * prcp(den2) : 0.0f;
     lam[1] = 1.0f - w;
     lam[2] = w;
     return;
   }
   const float den = va + vb + vc;
   if (!(den > 0.0f)) { cvx_seg(a, b, lam); lam[2] = 0.0f; return; }
-  const float v = vb / den, w = vc / den;
+  const float iden = prcp(den);
+  const float v = vb * iden, w = vc * iden;
   lam[0] = 1.0f - v - w;
   lam[1] = v;
   lam[2] = w;
@@ -244,7 +245,7 @@ __device__ __forceinline__ float vtx_newton(V3 e2, V3 a, float lam) {
     const float qx = prcp(e2.x + lam), qy = prcp(e2.y + lam), qz = prcp(e2.z + lam);
     const float tx = t0.x * qx * qx, ty = t0.y * qy * qy, tz = t0.z * qz * qz;
     const float F = (tx + ty + tz) - 1.0f, dF = -2.0f * (tx * qx + ty * qy + tz * qz);
-    const float ln = dF < 0.0f ? lam - F / dF : lam;
+    const float ln = dF < 0.0f ? lam - F * prcp(dF) : lam;
     lam = ln > 0.0f ? ln : 0.0f;
   }
   return lam;
@@ -262,7 +263,7 @@ __device__ __forceinline__ void edge_newton(V3 e2, V3 a0, V3 u, float& t, float&
     const float F2t = lam * (u.x * u.x * q.x + u.y * u.y * q.y + u.z * u.z * q.z);
     const float det = F1t * F2l - F1l * F2t;
     if (!(det > 0.0f)) break;
-    const float id = 1.0f / det;
+    const float id = prcp(det);
     t += (F1l * F2 - F1 * F2l) * id;
     const float ln = lam + (F2t * F1 - F1t * F2) * id;
     lam = ln > 0.0f ? ln : 0.0f;
@@ -386,7 +387,7 @@ __device__ __forceinline__ float cvx_polish(const CvxShape& A, V3 e, V3& pa, V3&
   if (!ok) return dist;
   float d = fd;
   if (!face) {
-    const V3 q = v3(1.0f / (e2.x + lam), 1.0f / (e2.y + lam), 1.0f / (e2.z + lam));
+    const V3 q = v3(prcp(e2.x + lam), prcp(e2.y + lam), prcp(e2.z + lam));
     b = v3(e2.x * a.x * q.x, e2.y * a.y * q.y, e2.z * a.z * q.z);
     const V3 sv = v3(a.x * q.x, a.y * q.y, a.z * q.z) * lam;
     d = sqrtf(dot(sv, sv));

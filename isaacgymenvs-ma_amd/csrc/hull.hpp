@@ -60,14 +60,14 @@ __device__ __forceinline__ V3 hcore_support(const HullCore& B, V3 d) {
 
 __device__ __forceinline__ V3 hunit(V3 a) {
   const float l = sqrtf(dot(a, a));
-  return l > 0.0f ? a * (1.0f / l) : a;
+  return l > 0.0f ? a * prcp(l) : a;
 }
 
 // closest point of segment / triangle to the origin as barycentric weights (Ericson 5.1.2 / 5.1.5), as convex.hpp
 __device__ __forceinline__ void hseg(V3 a, V3 b, float* lam) {
   const V3 ab = b - a;
   const float den = dot(ab, ab);
-  float t = den > 0.0f ? -dot(a, ab) / den : 0.0f;
+  float t = den > 0.0f ? -dot(a, ab) * prcp(den) : 0.0f;
   t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
   lam[0] = 1.0f - t;
   lam[1] = t;
@@ -81,25 +81,26 @@ __device__ __forceinline__ void htri(V3 a, V3 b, V3 c, float* lam) {
   if (e3 >= 0.0f && d4 <= e3) { lam[1] = 1.0f; return; }
   const float vc = d1 * d4 - e3 * d2;
   if (vc <= 0.0f && d1 >= 0.0f && e3 <= 0.0f) {
-    const float v = (d1 - e3) > 0.0f ? d1 / (d1 - e3) : 0.0f;
+    const float v = (d1 - e3) > 0.0f ? d1 * prcp(d1 - e3) : 0.0f;
     lam[0] = 1.0f - v; lam[1] = v; return;
   }
   const float d5 = -dot(ab, c), d6 = -dot(ac, c);
   if (d6 >= 0.0f && d5 <= d6) { lam[2] = 1.0f; return; }
   const float vb = d5 * d2 - d1 * d6;
   if (vb <= 0.0f && d2 >= 0.0f && d6 <= 0.0f) {
-    const float w = (d2 - d6) > 0.0f ? d2 / (d2 - d6) : 0.0f;
+    const float w = (d2 - d6) > 0.0f ? d2 * prcp(d2 - d6) : 0.0f;
     lam[0] = 1.0f - w; lam[2] = w; return;
   }
   const float va = e3 * d6 - d5 * d4;
   if (va <= 0.0f && (d4 - e3) >= 0.0f && (d5 - d6) >= 0.0f) {
     const float den2 = (d4 - e3) + (d5 - d6);
-    const float w = den2 > 0.0f ? (d4 - e3) / den2 : 0.0f;
+    const float w = den2 > 0.0f ? (d4 - e3) * prcp(den2) : 0.0f;
     lam[1] = 1.0f - w; lam[2] = w; return;
   }
   const float den = va + vb + vc;
   if (!(den > 0.0f)) { hseg(a, b, lam); lam[2] = 0.0f; return; }
-  const float v = vb / den, w = vc / den;
+  const float iden = prcp(den);
+  const float v = vb * iden, w = vc * iden;
   lam[0] = 1.0f - v - w; lam[1] = v; lam[2] = w;
 }
 // closest point of the simplex W[0..n-1] to the origin, compacted in place (W and the hull points P); true if
