@@ -362,7 +362,7 @@ __device__ __forceinline__ float point_box(V3 p, V3 hb, V3* nb, V3* cb) {
   V3 q = v3(fminf(fmaxf(p.x, -hb.x), hb.x), fminf(fmaxf(p.y, -hb.y), hb.y), fminf(fmaxf(p.z, -hb.z), hb.z));
   if (q.x != p.x || q.y != p.y || q.z != p.z) {
     V3 d = p - q;
-    float l = sqrtf(dot(d, d));
+    float l = psqrt(dot(d, d));
     *nb = d * prcp(l);
     *cb = q;
     return l;
@@ -471,7 +471,7 @@ __device__ __forceinline__ float point_hull(const mg_model* m, V3 pl, int* f) {
 __device__ __forceinline__ bool hull_box_near(V3 c, const M3& Rg, V3 hg, V3 w, float r, float off) {
   const V3 l = mulT(Rg, w - c);
   const float ex = fmaxf(fabsf(l.x) - hg.x, 0.0f), ey = fmaxf(fabsf(l.y) - hg.y, 0.0f), ez = fmaxf(fabsf(l.z) - hg.z, 0.0f);
-  return sqrtf(ex * ex + ey * ey + ez * ez) - r < off;
+  return psqrt(ex * ex + ey * ey + ez * ez) - r < off;
 }
 
 // box-box edge-edge contact in the object box's frame (oracle box_box_edge): hand box centre c, axes = the
@@ -501,7 +501,7 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
 #pragma unroll
     for (int j = 0; j < 3; j++) {
       const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
-      const float ln = sqrtf(R.m[i1][j] * R.m[i1][j] + R.m[i2][j] * R.m[i2][j]);
+      const float ln = psqrt(R.m[i1][j] * R.m[i1][j] + R.m[i2][j] * R.m[i2][j]);
       if (ln < 1e-6f) continue;
       const float il = prcp(ln);
       const float near = fmaxf(fmaxf(fabsf(R.m[i1][j]), fabsf(R.m[i2][j])), fmaxf(fabsf(R.m[i][j1]), fabsf(R.m[i][j2]))) * il;
@@ -1676,7 +1676,7 @@ struct Team {
           float ss, tt;
           closest_seg_seg_t(a0, a1, b0, b1, &ss, &tt);
           V3 pa = a0 + (a1 - a0) * ss, pb = b0 + (b1 - b0) * tt, dv = pa - pb;
-          float dist = sqrtf(dot(dv, dv));
+          float dist = psqrt(dot(dv, dv));
           d = dist - ra - rb;
           if (d < poff && dist > 1e-9f) {
             nrm = dv * prcp(dist);
