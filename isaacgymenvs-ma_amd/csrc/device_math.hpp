@@ -49,8 +49,8 @@ __host__ __device__ __forceinline__ M3 quat_to_mat(float x, float y, float z, fl
   R.m[2][0] = 2 * (x * z - y * w); R.m[2][1] = 2 * (y * z + x * w); R.m[2][2] = 1 - 2 * (x * x + y * y);
   return R;
 }
-__device__ __forceinline__ M3 axis_angle(V3 a, float ang) {
-  float s = sinf(ang), c = cosf(ang);
+// rotation by angle ang about unit axis a, from the angle's sine and cosine
+__device__ __forceinline__ M3 axis_angle_sc(V3 a, float s, float c) {
   float t = 1 - c;
   M3 R;
   R.m[0][0] = t * a.x * a.x + c; R.m[0][1] = t * a.x * a.y - s * a.z; R.m[0][2] = t * a.x * a.z + s * a.y;
@@ -58,6 +58,7 @@ __device__ __forceinline__ M3 axis_angle(V3 a, float ang) {
   R.m[2][0] = t * a.x * a.z - s * a.y; R.m[2][1] = t * a.y * a.z + s * a.x; R.m[2][2] = t * a.z * a.z + c;
   return R;
 }
+__device__ __forceinline__ M3 axis_angle(V3 a, float ang) { return axis_angle_sc(a, sinf(ang), cosf(ang)); }
 __device__ __forceinline__ void mat_to_quat(const M3& R, float* q) {
   float tr = R.m[0][0] + R.m[1][1] + R.m[2][2];
   if (tr > 0) {

@@ -701,12 +701,21 @@ struct Team {
         for (int k = 0; k < 6; k++) s->V[0][k] = 0.0f;
     }
     if (freeb && tl < 6) s->V[0][tl] = nu;
-    // (q, qd) per node in the union storage (free here: the ABA's child slots are written after)
+    // (q, qd) and (sin q, cos q) per node in the union storage (free here: the ABA's child slots are written
+    // after): each lane evaluates its own joint's sine and cosine once, its descendants read them
     float* qv = &s->u.slot[0][0];
-    static_assert(sizeof(s->u.slot) >= sizeof(float) * 2 * MN, "joint states must fit the union storage");
+    float* sc = qv + 2 * MN;
+    static_assert(sizeof(s->u.slot) >= sizeof(float) * 4 * MN, "joint states must fit the union storage");
+    float sn = 0.0f, cs = 1.0f;
     if (node > 0) {
       qv[2 * node] = qj;
       qv[2 * node + 1] = nu;
+      if (mt->jtype[node] == MG_JT_HINGE) {
+        sn = sinf(qj);
+        cs = cosf(qj);
+      }
+      sc[2 * node] = sn;
+      sc[2 * node + 1] = cs;
     }
     wsync();
     if (node >= 0) {
@@ -728,7 +737,7 @@ struct Team {
         const V3 ax = ld3(nf + 12);
         const float qk = k == node ? qj : qv[2 * k], vk = k == node ? nu : qv[2 * k + 1];
         if (mt->jtype[k] == MG_JT_HINGE) {
-          R = mul(Rp0, axis_angle(ax, qk));
+          R = mul(Rp0, axis_angle_sc(ax, k == node ? sn : sc[2 * k], k == node ? cs : sc[2 * k + 1]));
           x = x + tp;
           const V3 sw = mul(R, ax);
           S = sv(sw, cross(x - x0, sw));
@@ -2265,7 +2274,7 @@ struct Team {
         bb[j] = gb >= 0 ? mt->gbody[gb] : -1;
         const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
         f[j] = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) *
-               (1.0f / h);
+               prcp(h);
         pc[j] = ld3(s->cp[c]);
       }
     }
@@ -2304,6 +2313,7 @@ struct Team {
   }
   __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out) {
     fk();  // post-step pose for the sensor body frames
+    const float ih = prcp(h);  // impulses -> forces
     const int NS = m->num_sensors;
     if constexpr (T >= 32 && !OBJ) {
       if (sens_out && NS > 0) sensors_by_team_sums(sens_out, NS);
@@ -2322,7 +2332,7 @@ struct Team {
         else if (cside(c, 3) >= 0 && mt->gbody[cside(c, 3)] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
         const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
-        V3 f = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) * (sg / h);
+        V3 f = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) * (sg * ih);
         F = F + f;
         Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
       }
@@ -2342,8 +2352,8 @@ struct Team {
       for (int r = 3 * s->ncon; r < s->nrows; r++) {
         const int meta = s->lmeta[r - 3 * s->ncon];
         if ((meta >> 4) != node) continue;
-        if ((meta & 3) == 2) t += s->u.sv.rows[r].lam / h;
-        if ((meta & 3) == 3) t -= s->u.sv.rows[r].lam / h;
+        if ((meta & 3) == 2) t += s->u.sv.rows[r].lam * ih;
+        if ((meta & 3) == 3) t -= s->u.sv.rows[r].lam * ih;
       }
       dforce_out[node - 1] = t;
     }
