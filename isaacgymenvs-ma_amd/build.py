@@ -78,8 +78,9 @@ def build(force=False, verbose=False, timing=False, variant=None, defines=(), ex
         # instance TUs: no MachineLICM.  The work-queue kernels' per-item body sits in a loop, and the pass hoists
         # values out of it into registers held across all items (Humanoid: 48 spilled VGPRs vs 25 without it;
         # measured +3 % ShadowHand, +2 % egg, +1 % Humanoid, Ant unchanged)
-        # and no interprocedural register allocation: the egg's narrowphase is a real call, and with IPRA
-        # the caller kept values in registers the callee clobbers (wrong object states; csrc/convex.hpp)
+        # and no interprocedural register allocation: with IPRA a real call in these kernels (the egg narrowphase
+        # was one in round 3) returned into a caller that kept values in registers the callee clobbers (wrong
+        # object states).  Every phase is inlined now; the flag stays as a guard for any call left
         inst = [] if i < 0 else [f"-DMG_INST={i}", "-mllvm", "-disable-machine-licm", "-mllvm", "-enable-ipra=false"]
         cmds.append([hipcc] + flags + inst + ["-c", "-o", o, src])
         objs.append(o)
