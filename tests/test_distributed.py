@@ -220,11 +220,11 @@ def _packed_worker(rank, world, port, mode, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["root", "all"])
-def test_packed_gather_double_buffers_two_steps(mode):
+@pytest.mark.parametrize("mode,world", [("root", 2), ("all", 2), ("root", 4), ("all", 4)])
+def test_packed_gather_double_buffers_two_steps(mode, world):
     """PackedGather (the overlapped gather of the kernel-packed rows): with two steps in flight, each
-    slot holds its own step's rows from every rank, equal to the single-process rollout."""
-    world = 2
+    slot holds its own step's rows from every rank, equal to the single-process rollout.  World 4: the root
+    posts three receives in one batch (bench.py's default gather on a multi-GPU node is this root mode)."""
     gathered = _spawn(_packed_worker, world, mode)
     n_total = N_PER_RANK * world
     single = rollout("Ant", n_total, 0, n_total, slice(0, n_total))
