@@ -105,11 +105,12 @@ def _worker_args(rank, world, port, task, mode, q):
     _worker(rank, world, port, task, q, mode)
 
 
-@pytest.mark.parametrize("task,mode", [("Ant", "all"), ("Cartpole", "all"), ("Ant", "root"), ("MAAnt", "root")])
-def test_sharded_rollout_equals_single_process(task, mode):
+@pytest.mark.parametrize("task,mode,world", [("Ant", "all", 2), ("Cartpole", "all", 2), ("Ant", "root", 2),
+                                             ("MAAnt", "root", 2), ("MAAnt", "root", 4)])
+def test_sharded_rollout_equals_single_process(task, mode, world):
     """MAAnt: reset noise is keyed by the global actor id env_offset * A + a, so rank 1's agents draw
-    what they draw in one process (the round-1 key env_offset + a collided across ranks)."""
-    world = 2
+    what they draw in one process (the round-1 key env_offset + a collided across ranks); world 4 checks the
+    offsets of ranks past the first two."""
     gathered = _spawn(_worker_args, world, task, mode)
     n_total = N_PER_RANK * world
     single = rollout(task, n_total, 0, n_total, slice(0, n_total))
