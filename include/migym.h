@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_VERSION 5
+#define MG_VERSION 6
 
 #define MG_MAX_NODES 40
 #define MG_MAX_BODIES 40
@@ -141,6 +141,16 @@ typedef struct mg_model {
   int32_t hull_num_verts, hull_num_planes;
   float hull_vert[MG_MAX_HULL_VERTS][3];
   float hull_plane[MG_MAX_HULL_PLANES][4];
+  /* Link velocity damping and cap of the articulation (gym AssetOptions.angular_damping /
+   * max_angular_velocity; gym defaults 0.5 / 64: ant.py:152, humanoid.py:153-154, shadow_hand.py:240,
+   * cartpole.py:86-87 keeps the defaults).  Damping acts on every link as the implicit couple
+   * -c I_link w (a free link's w decays by 1/(1 + h c) per substep); the cap clamps every link's |w|
+   * after the solve.  obj_max_ang_vel: the free object's cap (its damping is
+   * obj_ang_damping).  A cap <= 0 disables it. */
+  float link_ang_damping;
+  float link_max_ang_vel;
+  float obj_max_ang_vel;
+  int32_t pad_model;
 } mg_model;
 
 /* Simulation parameters (cfg['sim'] of the task YAML: Ant.yaml:42-61). */

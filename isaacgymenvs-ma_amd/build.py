@@ -78,14 +78,22 @@ def build(force=False, verbose=False, timing=False, variant=None, defines=(), ex
         # instance TUs: no MachineLICM.  The work-queue kernels' per-item body sits in a loop, and the pass hoists
         # values out of it into registers held across all items (Humanoid: 48 spilled VGPRs vs 25 without it;
         # measured +3 % ShadowHand, +2 % egg, +1 % Humanoid, Ant unchanged)
-        # and no interprocedural register allocation: with IPRA a real call in these kernels (the egg narrowphase
-        # was one in round 3) returned into a caller that kept values in registers the callee clobbers (wrong
-        # object states).  Every phase is inlined now; the flag stays as a guard for any call left
+        # and no interprocedural register allocation (a guard only: a real call in these kernels miscompiled in
+        # round 3 with IPRA on -- wrong object states -- and, with the cause not pinned down, with IPRA off too:
+        # an illegal address and a 93 % parity build).  Every phase is force-inlined, and
+        # codeobj.check_no_calls below fails the build if any call is left in the device code
         inst = [] if i < 0 else [f"-DMG_INST={i}", "-mllvm", "-disable-machine-licm", "-mllvm", "-enable-ipra=false"]
         cmds.append([hipcc] + flags + inst + ["-c", "-o", o, src])
         objs.append(o)
     _run_parallel(cmds, verbose)
     subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs)
+    sys.path.insert(0, HERE)
+    import codeobj
+    try:
+        codeobj.check_no_calls(out + ".tmp", ARCH)
+    except Exception:
+        os.remove(out + ".tmp")
+        raise
     os.replace(out + ".tmp", out)
     return out
 

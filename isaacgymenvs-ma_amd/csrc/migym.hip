@@ -540,6 +540,13 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
       if (model->geom_type[g] == MG_GT_CONVEX && (model->geom_filter[g] & MG_COLLIDE_OBJECT) &&
           (model->geom_node[g] != 0 || !model->fixed_base))
         return fail(MG_EINVAL, "mg_sim_create: a convex-mesh geom against the object must be on the fixed root");
+  {  // one convex-mesh geom may collide with the object: the LDS tile stages one hull (build_tile's hullg)
+    int ncvx = 0;
+    for (int g = 0; g < model->num_geoms; g++)
+      ncvx += model->geom_type[g] == MG_GT_CONVEX && (model->geom_filter[g] & MG_COLLIDE_OBJECT);
+    if (model->obj_type && ncvx > 1)
+      return fail(MG_EINVAL, "mg_sim_create: at most one convex-mesh geom may collide with the object");
+  }
   if (hipSetDevice(device) != hipSuccess) return fail(MG_EDEVICE, "mg_sim_create: hipSetDevice failed");
   mg_sim* s = new (std::nothrow) mg_sim();
   if (!s) return fail(MG_ENOMEM, "mg_sim_create: out of host memory");

@@ -121,9 +121,12 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model
   }
   if (tid == 0) {
     t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; t->hnv = m->hull_num_verts;
+    // the convex-mesh geom that collides with the object (mg_sim_create allows one), else the lowest one
     t->hullg = -1;
     for (int g = ng - 1; g >= 0; g--)
       if (m->geom_type[g] == MG_GT_CONVEX) t->hullg = g;
+    for (int g = ng - 1; g >= 0; g--)
+      if (m->geom_type[g] == MG_GT_CONVEX && (m->geom_filter[g] & MG_COLLIDE_OBJECT)) t->hullg = g;
     t->hctr[0] = t->hctr[1] = t->hctr[2] = t->hctr[3] = 0.0f;
     if (OC > 1 && m->hull_num_verts > 0) {
       float cx = 0.0f, cy = 0.0f, cz = 0.0f;
@@ -282,7 +285,7 @@ struct DrTile {
 };
 // copy one env_props row (global) into the team's DrTile, team-cooperative
 template <int T, int MN, int MG>
-__device__ void load_dr(DrTile<MN, MG>* d, const float* row, const mg_model* m, int tl) {
+__device__ __forceinline__ void load_dr(DrTile<MN, MG>* d, const float* row, const mg_model* m, int tl) {
   const int nn = m->num_nodes, ng = m->num_geoms, nt = m->num_tendons;
   for (int k = tl; k < 8 * nn; k += T) d->node[k >> 3][k & 7] = row[k];
   const float* g = row + 8 * nn;
@@ -791,6 +794,15 @@ struct Team {
       SV IV = mul(IA, V);
       V3 mg = ld3(p->gravity) * (mass * gscale());
       pA = crf(V, IV) - sv(cross(cc, mg), mg);
+      // link angular damping (gym AssetOptions.angular_damping, mg_model.link_ang_damping): the couple
+      // -c I_w w, implicit: + c I_w w in the bias, + h c I_w in the link's rotational block, so a free
+      // link's w decays by 1/(1 + h c) per substep and the test solves see the same M~
+      const float cd = m->link_ang_damping;
+      if (cd != 0.0f) {
+        pA.a = pA.a + symmul(Iw, V.a) * cd;
+        const float hcd = h * cd;
+        for (int k = 0; k < 6; k++) IA.a[k] += hcd * Iw[k];
+      }
       c = node == 0 ? szero() : crm(V, S * nu);
     }
     for (int lev = maxdepth; lev >= 1; lev--) {
@@ -1455,7 +1467,9 @@ struct Team {
           }
           lb = team_max_dpp<T>(lb);
           lb -= B.kind == 1 ? sqrtf(dot(os, os)) : rB;
-          if (lb < off) {
+          // the bound is fp32 on another path than the candidates' own distances (and the oracle has no such
+          // cull): a 1 um guard band keeps a candidate just under the offset from being dropped by rounding
+          if (lb < off + 1e-6f) {
             nx = hull_core_contacts<T>(mt->hv, mt->hnv, ld3(mt->hctr), m->hull_plane, np, tl, tb, B, rB, off, res);
             near = true;
           }
@@ -2177,6 +2191,7 @@ struct Team {
     wsync();
 #undef MG_JSET
     ph_mark(6);
+    clamp_ang_vel();
     integrate();
     ph_mark(7);
   }
@@ -2193,6 +2208,62 @@ struct Team {
     IA = Sym6{};
     Dinv = u = 0.0f;
     for (int k = 0; k < 6; k++) Sl[k] = 0.0f;
+  }
+
+  // gym AssetOptions.max_angular_velocity (humanoid.py:154; gym default 64, the object's too): after the solve
+  // every link's |w| <= W.  Root first (w scaled to W, its COM velocity kept); then level by level each hinge's
+  // rate is clamped to { t : |w_parent + a t| <= W } (a = its unit world axis, s->S from this substep's fk),
+  // which holds t = 0 because the parent is clamped already; slides carry the parent's w.  Same rule as the
+  // oracle's clamp_ang_vel.  A team bound |w_root| + sum |qd| <= W (no link can reach the cap) skips the pass.
+  __device__ __forceinline__ void clamp_ang_vel() {
+    const float W = m->link_max_ang_vel;
+    if (W > 0.0f) {
+      const V3 w0 = freeb ? v3(__shfl(nu, tb), __shfl(nu, tb + 1), __shfl(nu, tb + 2)) : v3(0, 0, 0);
+      const bool hinge = node > 0 && mt->jtype[node] == MG_JT_HINGE;
+      const float n0 = sqrtf(dot(w0, w0));
+      const float bound = n0 + team_sum<T>(hinge ? fabsf(nu) : 0.0f, tb);
+      if (__ballot(bound > W) != 0ull) {  // wave-uniform
+        V3 wr = w0;
+        if (freeb && n0 > W) {
+          wr = w0 * (W / n0);
+          if (tl < 3) {
+            nu = tl == 0 ? wr.x : (tl == 1 ? wr.y : wr.z);
+          } else if (tl < 6) {
+            M3 Rr;
+            for (int a = 0; a < 3; a++)
+              for (int b = 0; b < 3; b++) Rr.m[a][b] = s->R[0][3 * a + b];
+            const V3 dv = cross(w0 - wr, mul(Rr, ld3(m->body_com[0])));
+            nu += tl == 3 ? dv.x : (tl == 4 ? dv.y : dv.z);
+          }
+        }
+        V3 om = wr;
+        const V3 ax = node > 0 ? ld3(s->S[node]) : v3(0, 0, 0);
+        const int pl = tb + (par > 0 ? col_of(par) : 0);
+        for (int lev = 1; lev <= maxdepth; lev++) {
+          const V3 wl = v3(__shfl(om.x, pl), __shfl(om.y, pl), __shfl(om.z, pl));
+          if (node > 0 && depth == lev) {
+            const V3 wp = par > 0 ? wl : wr;
+            if (hinge) {
+              V3 w = wp + ax * nu;
+              if (dot(w, w) > W * W) {
+                const float b = dot(ax, wp);
+                const float sq = sqrtf(fmaxf(b * b - dot(wp, wp) + W * W, 0.0f));
+                nu = fminf(fmaxf(nu, -b - sq), -b + sq);
+                w = wp + ax * nu;
+              }
+              om = w;
+            } else {
+              om = wp;
+            }
+          }
+        }
+      }
+    }
+    if (OBJ && m->obj_max_ang_vel > 0.0f) {
+      const V3 w = v3(__shfl(nu, tb + ob0), __shfl(nu, tb + ob0 + 1), __shfl(nu, tb + ob0 + 2));
+      const float n = sqrtf(dot(w, w));
+      if (objl && tl - ob0 < 3 && n > m->obj_max_ang_vel) nu *= m->obj_max_ang_vel / n;
+    }
   }
 
   __device__ __forceinline__ void integrate() {

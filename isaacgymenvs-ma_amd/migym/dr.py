@@ -448,16 +448,22 @@ class DomainRandomizationMixin:
         parameters, the randomized sim params and the extern samples.  None without randomization."""
         if self._dr is None:
             return None
+        # only tensors, numbers, strings and containers of them: rl_games saves env_state with torch.save, and
+        # torch.load(weights_only=True) (the default) refuses functions and numpy arrays
         noise = {}
         for name, p in self.dr_randomizations.items():
             lam = p.get("noise_lambda")
-            noise[name] = {k: v for k, v in p.items() if k != "noise_lambda"}
+            noise[name] = {k: v for k, v in p.items() if k not in ("noise_lambda", "op")}
+            if "op" in p:
+                noise[name]["op_type"] = "additive" if p["op"] is operator.add else "scaling"
             if lam is not None:
                 noise[name]["_lambda"] = (lam.calls, lam.refresh, None if lam.corr is None else lam.corr.clone())
         return {"calls": self._dr["calls"], "first_randomization": self.first_randomization, "noise": noise,
                 "gravity": tuple(float(x) for x in self.sim_params.gravity),
-                "rest_offset": float(self.sim_params.rest_offset), "og_gravity": self._og_sim_params["gravity"],
-                "extern_actor_params": {k: np.array(v, copy=True) for k, v in self.extern_actor_params.items()}}
+                "rest_offset": float(self.sim_params.rest_offset),
+                "og_gravity": tuple(float(x) for x in self._og_sim_params["gravity"]),
+                "extern_actor_params": {int(k): torch.from_numpy(np.array(v, copy=True))
+                                        for k, v in self.extern_actor_params.items()}}
 
     def _dr_set_state(self, st):
         if st is None or self._dr is None:
@@ -467,6 +473,8 @@ class DomainRandomizationMixin:
         for name, p in st["noise"].items():
             p = dict(p)
             calls, refresh, corr = p.pop("_lambda", (0, True, None))
+            if "op_type" in p:
+                p["op"] = operator.add if p.pop("op_type") == "additive" else operator.mul
             lam = self.dr_randomizations.get(name, {}).get("noise_lambda") or \
                 NoiseLambda(self, name, 1 if name == "actions" else 2)
             lam.calls, lam.refresh = calls, refresh
@@ -479,7 +487,8 @@ class DomainRandomizationMixin:
         sp.rest_offset = st["rest_offset"]
         self._og_sim_params["gravity"] = st["og_gravity"]
         _abi.check(self._lib.mg_sim_set_params(self.sim, _abi.C.byref(sp)), self._lib)
-        self.extern_actor_params = {k: np.array(v, copy=True) for k, v in st["extern_actor_params"].items()}
+        self.extern_actor_params = {int(k): (v.numpy() if torch.is_tensor(v) else np.asarray(v)).copy()
+                                    for k, v in st["extern_actor_params"].items()}
 
     def _dr_any_reset(self) -> bool:
         return (not self.dr_exact_trigger) or bool(self.reset_buf.any())

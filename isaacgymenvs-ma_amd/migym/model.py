@@ -202,6 +202,9 @@ class ModelSpec:
     obj: Optional[Dict] = None     # free object sharing the env: {type, size, mass, inertia, lin_damping, ...}
     pair_mjcf: int = 0             # 1: the pairs are explicit MJCF <pair>s (condim 1: frictionless; margin 0)
     hull: Optional[Dict] = None    # the convex-mesh geom: {geom, verts [[x,y,z]], planes [[nx,ny,nz,d]]}, geom frame
+    # gym AssetOptions of the articulation's links (ASSET_OPTIONS; gym defaults until a task sets them)
+    angular_damping: float = 0.5
+    max_angular_velocity: float = 64.0
 
     @property
     def num_dofs(self):
@@ -816,6 +819,7 @@ def _model_dtype():
         ("obj_lin_damping", f4), ("obj_ang_damping", f4), ("obj_gravity", f4),
         ("hull_num_verts", i4), ("hull_num_planes", i4),
         ("hull_vert", f4, (MAX_HULL_VERTS, 3)), ("hull_plane", f4, (MAX_HULL_PLANES, 4)),
+        ("link_ang_damping", f4), ("link_max_ang_vel", f4), ("obj_max_ang_vel", f4), ("pad_model", i4),
     ])
 
 
@@ -901,15 +905,35 @@ def pack_model(spec: ModelSpec) -> np.ndarray:
         m["hull_num_planes"] = len(h["planes"])
         m["hull_vert"][:len(h["verts"])] = h["verts"]
         m["hull_plane"][:len(h["planes"])] = h["planes"]
+    m["link_ang_damping"] = spec.angular_damping
+    m["link_max_ang_vel"] = spec.max_angular_velocity
+    m["obj_max_ang_vel"] = spec.obj.get("max_ang_vel", GYM_MAX_ANGULAR_VELOCITY) if spec.obj else 0.0
     return m
 
 
 ASSET_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets")
 
 
+GYM_ANGULAR_DAMPING = 0.5          # gymapi.AssetOptions defaults (Isaac Gym Preview 4)
+GYM_MAX_ANGULAR_VELOCITY = 64.0
+# The link options each task's create_sim sets on its articulation asset; the rest keep gym's defaults.
+ASSET_OPTIONS = {
+    "ant": {"angular_damping": 0.0},                                       # ant.py:152
+    "humanoid": {"angular_damping": 0.01, "max_angular_velocity": 100.0},  # humanoid.py:153-154
+    "shadow_hand": {"angular_damping": 0.01},                              # shadow_hand.py:240
+    "cartpole": {},                                                        # cartpole.py:86-87 (defaults)
+}
+
+
 def load_builtin(name) -> ModelSpec:
-    """Load one of the shipped model tables (generated by tools/build_models.py)."""
-    return ModelSpec.from_json(os.path.join(ASSET_DIR, name + ".json"))
+    """Load one of the shipped model tables (generated by tools/build_models.py), with the task's
+    asset options (ASSET_OPTIONS) on gym's defaults."""
+    spec = ModelSpec.from_json(os.path.join(ASSET_DIR, name + ".json"))
+    spec.angular_damping = GYM_ANGULAR_DAMPING
+    spec.max_angular_velocity = GYM_MAX_ANGULAR_VELOCITY
+    for k, v in ASSET_OPTIONS.get(name, {}).items():
+        setattr(spec, k, v)
+    return spec
 
 
 def hand_object(kind: str) -> Dict:

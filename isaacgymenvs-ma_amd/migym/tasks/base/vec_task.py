@@ -351,7 +351,8 @@ class VecTask(DomainRandomizationMixin, Env):
 
     def reset_idx(self, env_ids, goal_env_ids=None):
         """reset_idx (ant.py:252-279, humanoid.py:251-278, cartpole.py:122-136, shadow_hand.py:586-668):
-        the listed envs (actor rows for MA layouts) get their reset state written now, by one device launch
+        the listed envs (MA layouts: agent ids, kept only where every agent of the env is listed -- the AND
+        filter below; a partial agent list resets nothing) get their reset state written now, by one device launch
         (``mg_reset_idx``): DOF noise, root rows and potentials, or ShadowHand's goal, object, hand DOFs and
         PD targets; progress / reset (/ successes) cleared.  A caller reading ``root_states`` right after
         sees the reset state, as with the reference.  Inside ``step`` the fused kernel applies

@@ -166,6 +166,7 @@ typedef struct {
   real R[MAXN][3][3], x[MAXN][3];
   real S[MAXN][6];
   real I[MAXN][6][6];
+  real Iw[MAXN][3][3]; /* rotational inertia about the COM, world axes (link damping) */
   real V[MAXN][6];
   real o[3];
   real oR[3][3], op[3]; /* free object pose */
@@ -268,6 +269,7 @@ static void forward_kinematics(const mg_model* m, const astate* s, kin* k) {
     for (int a = 0; a < 3; a++)
       for (int b = 0; b < 3; b++) Rt[a][b] = k->R[i][b][a];
     matmul3(T, Rt, Iw);
+    memcpy(k->Iw[i], Iw, sizeof(Iw));
     real cc = dot3(c, c);
     real cx[3][3] = {{0, -c[2], c[1]}, {c[2], 0, -c[0]}, {-c[1], c[0], 0}};
     for (int a = 0; a < 3; a++)
@@ -329,11 +331,17 @@ static void tendon_forces(const mg_model* m, const astate* s, real* tau /* per n
   }
 }
 
-/* joint-space inertia (CRBA) incl. implicit diagonal, h = substep */
-static void mass_matrix(const mg_model* m, const kin* k, real h, real* M, const real* diag, int ld) {
+/* joint-space inertia (CRBA) incl. implicit diagonal, h = substep.  hc = h x link angular damping: the
+ * implicit part of the damping couple -c I_w w on every link, M~ += h c sum_i Ja_i^T I_w,i Ja_i (added to
+ * the links' rotational blocks before the composite pass) */
+static void mass_matrix(const mg_model* m, const kin* k, real h, real* M, const real* diag, int ld, real hc) {
   int nv = ld, nn = m->num_nodes;
   real Ic[MAXN][6][6];
   memcpy(Ic, k->I, sizeof(real) * 36 * nn);
+  if (hc != 0.0)
+    for (int i = 0; i < nn; i++)
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Ic[i][a][b] += hc * k->Iw[i][a][b];
   for (int i = nn - 1; i >= 1; i--) {
     int p = m->parent[i];
     for (int a = 0; a < 6; a++)
@@ -361,8 +369,8 @@ static void mass_matrix(const mg_model* m, const kin* k, real h, real* M, const 
   }
 }
 
-/* bias forces C(q,v) incl. gravity (RNEA with qdd = 0) */
-static void bias_forces(const mg_model* m, const kin* k, const astate* s, const real* g, real* C) {
+/* bias forces C(q,v) incl. gravity (RNEA with qdd = 0) and the link damping couples c I_w w (cd = c) */
+static void bias_forces(const mg_model* m, const kin* k, const astate* s, const real* g, real* C, real cd) {
   int nn = m->num_nodes, nv = nv_of(m); /* C has at least nv entries */
   real A[MAXN][6], f[MAXN][6];
   for (int c = 0; c < 6; c++) A[0][c] = 0;
@@ -384,6 +392,11 @@ static void bias_forces(const mg_model* m, const kin* k, const astate* s, const 
     for (int a = 0; a < 3; a++) { c[a] = k->x[i][a] + cw[a] - k->o[a]; mg[a] = mass * g[a]; }
     cross3(c, mg, n);
     for (int a = 0; a < 3; a++) { f[i][a] = IA[a] + vIV[a] - n[a]; f[i][3 + a] = IA[3 + a] + vIV[3 + a] - mg[a]; }
+    if (cd != 0.0) {
+      real Iww[3];
+      matvec3((real(*)[3])k->Iw[i], k->V[i], Iww);
+      for (int a = 0; a < 3; a++) f[i][a] += cd * Iww[a];
+    }
   }
   for (int i = nn - 1; i >= 1; i--)
     for (int c = 0; c < 6; c++) f[m->parent[i]][c] += f[i][c];
@@ -2095,6 +2108,60 @@ static void jac_row(const mg_model* m, const kin* k, int nodeA, int nodeB, const
   }
 }
 
+/* gym AssetOptions.max_angular_velocity (humanoid.py:154; gym default 64, the object's too): after the
+ * solve every link's angular velocity is held to |w| <= W.  The root first: w scaled to W, its COM
+ * velocity kept.  Then in tree order (parents first) a hinge's rate qd is clamped to the interval
+ * { t : |w_parent + a t| <= W } (a = the unit world axis): a link's w moves only along its own axis in
+ * joint space, and that interval holds qd = 0 because the parent is already clamped.  A body made of
+ * several hinge nodes is clamped node by node.  Slides carry the parent's w.  The free object: |w| <= W. */
+static void clamp_ang_vel(const mg_model* m, const kin* k, real* nu) {
+  const real W = m->link_max_ang_vel;
+  real om[MAXN][3];
+  if (W > 0.0) {
+    om[0][0] = om[0][1] = om[0][2] = 0.0;
+    if (!m->fixed_base) {
+      real w[3] = {nu[0], nu[1], nu[2]};
+      real n = sqrt(dot3(w, w));
+      if (n > W) {
+        real sc = W / n, wn[3], dw[3], cw[3], dv[3];
+        real c[3] = {m->body_com[0][0], m->body_com[0][1], m->body_com[0][2]};
+        matvec3((real(*)[3])k->R[0], c, cw);
+        for (int a = 0; a < 3; a++) { wn[a] = w[a] * sc; dw[a] = w[a] - wn[a]; }
+        cross3(dw, cw, dv);
+        for (int a = 0; a < 3; a++) { nu[a] = wn[a]; nu[3 + a] += dv[a]; }
+      }
+      for (int a = 0; a < 3; a++) om[0][a] = nu[a];
+    }
+    for (int i = 1; i < m->num_nodes; i++) {
+      const real* wp = om[m->parent[i]];
+      if (m->jtype[i] == MG_JT_HINGE) {
+        const real* ax = k->S[i];
+        const int ci = dof_col(m, i);
+        real q = nu[ci], w[3];
+        for (int a = 0; a < 3; a++) w[a] = wp[a] + ax[a] * q;
+        if (dot3(w, w) > W * W) {
+          real b = dot3(ax, wp), disc = b * b - dot3(wp, wp) + W * W;
+          real sq = sqrt(disc > 0.0 ? disc : 0.0), lo = -b - sq, hi = -b + sq;
+          q = q < lo ? lo : (q > hi ? hi : q);
+          nu[ci] = q;
+          for (int a = 0; a < 3; a++) w[a] = wp[a] + ax[a] * q;
+        }
+        for (int a = 0; a < 3; a++) om[i][a] = w[a];
+      } else {
+        for (int a = 0; a < 3; a++) om[i][a] = wp[a];
+      }
+    }
+  }
+  if (m->obj_type && m->obj_max_ang_vel > 0.0) {
+    const int nv = nv_of(m);
+    real n = sqrt(nu[nv] * nu[nv] + nu[nv + 1] * nu[nv + 1] + nu[nv + 2] * nu[nv + 2]);
+    if (n > m->obj_max_ang_vel) {
+      real sc = m->obj_max_ang_vel / n;
+      for (int a = 0; a < 3; a++) nu[nv + a] *= sc;
+    }
+  }
+}
+
 /* ---------------------------------------------------------------- one substep */
 typedef struct {
   real h;
@@ -2122,8 +2189,8 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     kk[i] = t.k; bb[i] = t.b; ref[i] = t.ref; tadd[i] = t.tadd; s->sat[i] = t.sat;
     diag[i] = m->armature[i] + h * t.b + h * h * t.k;
   }
-  mass_matrix(m, &k, h, M, diag, nvt);
-  bias_forces(m, &k, s, g, C);
+  mass_matrix(m, &k, h, M, diag, nvt, h * m->link_ang_damping);
+  bias_forces(m, &k, s, g, C, m->link_ang_damping);
   real nu[MAXV], rhs[MAXV];
   for (int c = 0; c < 6 && !m->fixed_base; c++) nu[c] = s->nu0[c];
   for (int i = 1; i < nn; i++) nu[dof_col(m, i)] = s->qd[i];
@@ -2238,6 +2305,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       for (int c = 0; c < nvt; c++) nu[c] += Y[r][c] * dl;
     }
   }
+  clamp_ang_vel(m, &k, nu);
   /* integrate */
   if (!m->fixed_base) {
     real w[3] = {nu[0], nu[1], nu[2]}, vo[3] = {nu[3], nu[4], nu[5]};
@@ -2496,7 +2564,7 @@ int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root
   kin k;
   load_state(m, root13, dof2, &s);
   forward_kinematics(m, &s, &k);
-  mass_matrix(m, &k, p->dt / p->substeps, M_out, 0, nv_of(m));
+  mass_matrix(m, &k, p->dt / p->substeps, M_out, 0, nv_of(m), 0.0);
   return nv_of(m);
 }
 
@@ -2508,8 +2576,8 @@ int orc_free_acceleration(const mg_model* m, const mg_sim_params* p, const float
   forward_kinematics(m, &s, &k);
   int nv = nv_of(m);
   real h = p->dt / p->substeps, M[MAXV * MAXV], C[MAXV], g[3] = {p->gravity[0], p->gravity[1], p->gravity[2]};
-  mass_matrix(m, &k, h, M, 0, nv);
-  bias_forces(m, &k, &s, g, C);
+  mass_matrix(m, &k, h, M, 0, nv, h * m->link_ang_damping);
+  bias_forces(m, &k, &s, g, C, m->link_ang_damping);
   if (cholesky(M, nv) != 0) return -1;
   for (int c = 0; c < nv; c++) qacc_out[c] = -C[c];
   for (int i = 1; i < m->num_nodes; i++)

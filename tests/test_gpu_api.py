@@ -194,6 +194,12 @@ def test_env_state_round_trip_with_randomization():
         env.step(actions(env, k))
     state = env.get_env_state()
     assert "domain_randomization" in state
+    # the state survives a checkpoint: torch.save, then torch.load with the safe (weights_only) loader
+    import io
+    buf = io.BytesIO()
+    torch.save(state, buf)
+    buf.seek(0)
+    state = torch.load(buf, weights_only=True)
     ref = []
     for k in range(5, 12):
         obs, rew, reset, _ = env.step(actions(env, k))

@@ -224,16 +224,22 @@ def random_states(spec, tp, n, rng, z_range, contact_frac=0.5):
     return root, dof
 
 
-@pytest.mark.parametrize("task,n,z", [("Ant", 512, (0.25, 0.7)), ("Humanoid", 256, (0.6, 1.4)),
-                                      ("Cartpole", 256, (2.0, 2.0))])
-def test_physics_step_matches_oracle(lib, task, n, z):
+@pytest.mark.parametrize("task,n,z,fast", [("Ant", 512, (0.25, 0.7), 0), ("Humanoid", 256, (0.6, 1.4), 0),
+                                           ("Cartpole", 256, (2.0, 2.0), 0), ("Ant", 256, (4.0, 5.0), 1),
+                                           ("Humanoid", 256, (4.0, 5.0), 1), ("Cartpole", 256, (2.0, 2.0), 1)])
+def test_physics_step_matches_oracle(lib, task, n, z, fast):
+    """one gym.simulate from random states; fast = 1: joint rates ~N(0, 40) and root spins ~N(0, 40) in the
+    air, so that the link angular-velocity cap (max_angular_velocity) and the link damping act in most envs"""
     spec, sp, tp = setup(task)
-    rng = np.random.default_rng(7)
+    rng = np.random.default_rng(7 + fast)
     root, dof = random_states(spec, tp, n, rng, z)
     if task == "Cartpole":
         root[:, :] = 0
         root[:, 2] = 2.0
         root[:, 6] = 1.0
+    if fast:
+        dof[:, :, 1] *= 40.0
+        root[:, 10:13] *= 80.0
     act = (rng.uniform(-1, 1, (n, spec.num_dofs)) * (15.0 if task == "Ant" else 50.0)).astype(np.float32)
     ns = max(len(spec.sensors), 1)
     sens_h = np.zeros((n, ns * 6), np.float32)
@@ -253,7 +259,10 @@ def test_physics_step_matches_oracle(lib, task, n, z):
     torch.cuda.synchronize()
     lib.mg_sim_destroy(h)
     rg, dg = r_d.cpu().numpy(), d_d.cpu().numpy()
-    test = f"test_physics_step_matches_oracle[{task}]"
+    test = f"test_physics_step_matches_oracle[{task}{'-fast' if fast else ''}]"
+    if fast:   # the cap acted: some link ends at |w| = W (root spin or a joint rate above it)
+        W = float(mnp["link_max_ang_vel"])
+        assert (np.abs(d_h[..., 1]).max() > 0.5 * W) and (np.abs(dof[..., 1]).max() > W)
     for name, a, b in (("root pose", rg[:, 0:7], r_h[:, 0:7]), ("dof pos", dg[..., 0], d_h[..., 0]),
                        ("root twist", rg[:, 7:13], r_h[:, 7:13]), ("dof vel", dg[..., 1], d_h[..., 1])):
         PS.record(test, name, a, b)
@@ -269,6 +278,50 @@ def test_physics_step_matches_oracle(lib, task, n, z):
     fg = f_d.cpu().numpy()
     PS.record(test, "dof force", fg, dfor_h)
     np.testing.assert_allclose(fg, dfor_h, atol=1e-2 * max(1.0, np.abs(dfor_h).max()))
+
+
+def test_free_link_damping_and_cap_on_device(lib):
+    """k_simulate on one free rigid link (spherical inertia, gravity off): w decays by 1 / (1 + h c) per substep
+    (gym AssetOptions.angular_damping), and a spin past max_angular_velocity ends at W with v_com kept"""
+    node = M.Node(name="link", parent=-1, jtype=M.JT_FREE, t=[0, 0, 0], r0=[0, 0, 0, 1], axis=[0, 0, 1], body=0,
+                  mass=1.0, inertia=[0.02, 0.02, 0.02, 0.0, 0.0, 0.0])
+    body = M.Body(name="link", node=0, pos=[0, 0, 0], quat=[0, 0, 0, 1], parent_body=-1, mass=1.0)
+    spec = M.ModelSpec(name="link", fixed_base=0, nodes=[node], bodies=[body], geoms=[], pairs=[], actuators=[],
+                       dof_names=[], angular_damping=0.5, max_angular_velocity=10.0)
+    mnp = M.pack_model(spec)
+    sp = taskdefs.sim_params(configs.task_config("Ant", 1), 1)
+    for i in range(3):
+        sp.gravity[i] = 0.0
+    n = 64
+    root = np.zeros((n, 13), np.float32)
+    root[:, 2] = 1.0
+    root[:, 6] = 1.0
+    root[:, 7:10] = (0.3, -0.2, 0.1)
+    rng = np.random.default_rng(0)
+    root[:, 10:13] = rng.normal(0, 1.0, (n, 3)) * np.where(np.arange(n) < n // 2, 2.0, 30.0)[:, None]
+    r_d, d_d = T(root), torch.zeros((n, 1, 2), device=DEV)  # no DOFs (a non-empty buffer to bind)
+    h = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(h)), lib)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state = P(r_d), P(d_d)
+    _abi.check(lib.mg_sim_bind(h, C.byref(v)), lib)
+    _abi.check(lib.mg_sim_simulate(h, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(h)
+    rg = r_d.cpu().numpy()
+    hh = sp.dt / sp.substeps
+    # exact decay while below the cap (first half: |w| <= ~8 < W)
+    w0 = root[:, 10:13].astype(np.float64)
+    slow = np.linalg.norm(w0, axis=1) < 10.0
+    want = w0 / (1.0 + hh * 0.5) ** sp.substeps
+    np.testing.assert_allclose(rg[slow, 10:13], want[slow], rtol=2e-6, atol=1e-7)
+    wn = np.linalg.norm(rg[:, 10:13].astype(np.float64), axis=1)
+    assert np.all(wn <= 10.0 * (1 + 1e-6)) and np.all(np.abs(wn[~slow] - 10.0) < 1e-5 * 10.0), wn
+    np.testing.assert_allclose(rg[:, 7:10], root[:, 7:10], atol=1e-7)
+    # and the oracle agrees on every env
+    r_h = root.copy()
+    O.simulate(mnp, sp, r_h, np.zeros((n, 0, 2), np.float32))
+    np.testing.assert_allclose(rg, r_h, atol=1e-6, rtol=1e-6)
 
 
 def _explained_over_steps(spec, sp, tp, mnp, pre_states, bad, sens=None):

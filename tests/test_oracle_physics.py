@@ -163,6 +163,7 @@ def test_cartpole_pendulum_energy():
         spec, mnp, sp, tp = setup("Cartpole")
         mnp["damping"][:] = 0
         mnp["armature"][:] = 0
+        mnp["link_ang_damping"] = 0   # gym's default link damping 0.5 would drain the pendulum
         sp.dt = dt
         root = np.zeros((1, 13), np.float32)
         root[0, 2] = 2.0
@@ -240,3 +241,116 @@ def test_fp32_restatement_tracks_fp64_checker():
             h.env_step(mnp, sp, tp, 0, t, 4, fp32=fp32)
         obs.append(h.obs.copy())
     np.testing.assert_allclose(obs[1], obs[0], atol=2e-3, rtol=2e-3)
+
+
+# ------------------------------------------------------------------ link damping and the angular velocity cap
+def free_link_spec(c, W, inertia=(0.02, 0.02, 0.02)):
+    """one free rigid body (spherical inertia: no gyroscopic torque), no geoms"""
+    node = M.Node(name="link", parent=-1, jtype=M.JT_FREE, t=[0, 0, 0], r0=[0, 0, 0, 1], axis=[0, 0, 1], body=0,
+                  mass=1.0, inertia=list(inertia) + [0.0, 0.0, 0.0])
+    body = M.Body(name="link", node=0, pos=[0, 0, 0], quat=[0, 0, 0, 1], parent_body=-1, mass=1.0)
+    return M.ModelSpec(name="link", fixed_base=0, nodes=[node], bodies=[body], geoms=[], pairs=[], actuators=[],
+                       dof_names=[], angular_damping=c, max_angular_velocity=W)
+
+
+def test_asset_options_follow_the_tasks():
+    """gym AssetOptions per task (ant.py:152, humanoid.py:153-154, shadow_hand.py:240; Cartpole and the hand
+    objects keep gym's defaults 0.5 / 64)"""
+    want = {"ant": (0.0, 64.0), "humanoid": (0.01, 100.0), "shadow_hand": (0.01, 64.0), "cartpole": (0.5, 64.0)}
+    for name, (c, W) in want.items():
+        m = M.pack_model(M.load_builtin(name))
+        assert m["link_ang_damping"] == np.float32(c) and m["link_max_ang_vel"] == np.float32(W), name
+    m = M.pack_model(taskdefs.hand_spec("block"))
+    assert m["obj_ang_damping"] == np.float32(0.5) and m["obj_max_ang_vel"] == np.float32(64.0)
+
+
+def test_free_link_angular_damping_decays_per_substep():
+    """a spinning free link (no gravity, spherical inertia): w -> w / (1 + h c) per substep, v untouched"""
+    c = 0.5
+    spec = free_link_spec(c, 0.0)
+    mnp = M.pack_model(spec)
+    sp = taskdefs.sim_params(configs.task_config("Ant", 1), 0)
+    for i in range(3):
+        sp.gravity[i] = 0.0
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = 1.0
+    root[0, 6] = 1.0
+    root[0, 7:10] = (0.3, -0.2, 0.1)
+    root[0, 10:13] = (3.0, -2.0, 1.0)
+    w0, v0 = root[0, 10:13].astype(np.float64), root[0, 7:10].copy()
+    h = sp.dt / sp.substeps
+    steps = 5
+    for _ in range(steps):
+        O.simulate(mnp, sp, root, np.zeros((1, 0, 2), np.float32))
+    want = w0 / (1.0 + h * c) ** (steps * sp.substeps)
+    np.testing.assert_allclose(root[0, 10:13], want, rtol=1e-6)
+    np.testing.assert_allclose(root[0, 7:10], v0, atol=1e-7)
+    # c = 0: no decay
+    mnp["link_ang_damping"] = 0.0
+    root[0, 10:13] = (3.0, -2.0, 1.0)
+    O.simulate(mnp, sp, root, np.zeros((1, 0, 2), np.float32))
+    np.testing.assert_allclose(root[0, 10:13], (3.0, -2.0, 1.0), rtol=1e-7)
+
+
+def test_free_link_angular_velocity_is_capped_keeping_com_velocity():
+    spec = free_link_spec(0.0, 10.0)
+    spec.nodes[0].com = [0.1, 0.0, 0.0]          # COM off the origin: the cap keeps v_com, not v_o
+    spec.bodies[0].com = [0.1, 0.0, 0.0]
+    mnp = M.pack_model(spec)
+    sp = taskdefs.sim_params(configs.task_config("Ant", 1), 0)
+    for i in range(3):
+        sp.gravity[i] = 0.0
+    sp.substeps = 1
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = 1.0
+    root[0, 6] = 1.0
+    root[0, 7:10] = (0.5, 0.0, 0.0)
+    root[0, 10:13] = (0.0, 0.0, 25.0)   # about z through the origin: no gyroscopic term for I = diag(.02) + m c c
+    O.simulate(mnp, sp, root, np.zeros((1, 0, 2), np.float32))
+    assert abs(np.linalg.norm(root[0, 10:13]) - 10.0) < 1e-5, root[0, 10:13]
+    np.testing.assert_allclose(root[0, 10:13], (0.0, 0.0, 10.0), atol=1e-5)
+
+
+@pytest.mark.parametrize("task,DOF,rate", [("Cartpole", 1, 200.0), ("Humanoid", 14, 400.0), ("Ant", 1, 300.0)])
+def test_link_angular_velocity_cap(task, DOF, rate):
+    """one hinge spun far past the cap (gravity and contacts off): every link's |w| ends at <= W (Cartpole's
+    pole exactly at gym's default 64; a free base's links within the axes' motion over the step)"""
+    spec, mnp, sp, tp = setup(task, gravity=(0.0, 0.0, 0.0), max_contacts=0)
+    sp.limit_margin = -1.0
+    sp.substeps = 1   # the clamp is the last velocity update of a substep
+    W = float(mnp["link_max_ang_vel"])
+    nd = spec.num_dofs
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = 5.0
+    root[0, 6] = 1.0
+    dof = np.zeros((1, nd, 2), np.float32)
+    dof[0, :, 0] = np.array(tp.initial_dof_pos[:nd])
+    dof[0, DOF, 1] = rate
+    root0, dof0 = root.copy(), dof.copy()
+    O.simulate(mnp, sp, root, dof)
+    # the links' w in the frame the clamp acts in: the step's start pose with the new velocities
+    mix_r, mix_d = root0[0].copy(), dof0[0].copy()
+    mix_r[7:13] = root[0, 7:13]
+    mix_d[:, 1] = dof[0, :, 1]
+    rb = O.rigid_body_states(mnp, mix_r, mix_d, len(spec.bodies))
+    wn = np.linalg.norm(rb[:, 10:13].astype(np.float64), axis=1)
+    if task == "Cartpole":
+        assert abs(abs(dof[0, 1, 1]) - W) < 1e-4 * W, dof[0, :, 1]
+    assert wn.max() <= W * (1 + 1e-6), (wn, W)
+    assert wn.max() >= W * (1 - 1e-6), (wn, W)       # the cap is what stopped it
+    # below the cap the clamp changes nothing: an uncapped model gives the same step bit for bit
+    root2 = np.zeros((1, 13), np.float32)
+    root2[0, 2] = 5.0
+    root2[0, 6] = 1.0
+    dof2 = np.zeros((1, nd, 2), np.float32)
+    dof2[0, :, 0] = np.array(tp.initial_dof_pos[:nd])
+    dof2[0, DOF, 1] = 0.2 * W
+    outs = []
+    for cap in (W, 0.0):
+        mm = mnp.copy()
+        mm["link_max_ang_vel"] = cap
+        r, d = root2.copy(), dof2.copy()
+        O.simulate(mm, sp, r, d)
+        outs.append((r, d))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
