@@ -401,7 +401,7 @@ __device__ __forceinline__ void seg_box_cx(float& a, float& b) {
   a = lo;
   b = hi;
 }
-__device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
+__device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb, bool* inside) {
   const float av[3] = {a.x, a.y, a.z}, uv[3] = {u.x, u.y, u.z}, hv[3] = {hb.x, hb.y, hb.z};
   float t0 = 0.0f, t1 = 1.0f;
   bool hit = true;
@@ -423,7 +423,8 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
     bp[1 + 2 * k] = (ta > 0.0f && ta < 1.0f) ? ta : 1.0f;
     bp[2 + 2 * k] = (tb > 0.0f && tb < 1.0f) ? tb : 1.0f;
   }
-  if (hit && t0 <= t1) return 0.5f * (t0 + t1);
+  *inside = hit && t0 <= t1;
+  if (*inside) return 0.5f * (t0 + t1);
   float* c = bp + 1;  // the six crossings
   seg_box_cx(c[0], c[5]); seg_box_cx(c[1], c[3]); seg_box_cx(c[2], c[4]);
   seg_box_cx(c[1], c[2]); seg_box_cx(c[3], c[4]);
@@ -452,6 +453,52 @@ __device__ __forceinline__ float seg_box_t(V3 a, V3 u, V3 hb) {
     if (f < best_f) { best_f = f; best_t = t; }
   }
   return best_t;
+}
+
+// A segment a + t u whose core has entered a box (seg_box_t's inside case; oracle seg_box_sat): the face of least
+// push-out of the whole segment -- SAT over the box's face axes, delta(k, s) = hb_k - min(s a_k, s (a_k + u_k)),
+// ties in x+ x- y+ y- z+ z- order -- and the segment end deepest behind it (*t = 0 or 1).  The inside portion's
+// midpoint lies on a thin box's mid-plane by construction when the segment pierces it (the reference's pen reset
+// pose through the palm), where fp32 and fp64 picked opposite faces; the whole segment's extents decide robustly.
+__device__ __forceinline__ int seg_box_sat(V3 a, V3 u, V3 hb, float* t) {
+  const float av[3] = {a.x, a.y, a.z}, ev[3] = {a.x + u.x, a.y + u.y, a.z + u.z}, hv[3] = {hb.x, hb.y, hb.z};
+  int best = 0;
+  float bd = 3.0e38f;
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    const int k = f >> 1;
+    const float sg = (f & 1) ? -1.0f : 1.0f;
+    const float dl = hv[k] - fminf(sg * av[k], sg * ev[k]);
+    if (dl < bd) { bd = dl; best = f; }
+  }
+  const int k = best >> 1;
+  const float sg = (best & 1) ? -1.0f : 1.0f;
+  const float a0 = k == 0 ? a.x : (k == 1 ? a.y : a.z), a1 = k == 0 ? ev[0] : (k == 1 ? ev[1] : ev[2]);
+  *t = sg * a0 <= sg * a1 ? 0.0f : 1.0f;
+  return best;
+}
+// signed distance of P (box frame) along face f's outward normal from that face's plane (negative behind it);
+// nb = the normal, cb = P moved onto the plane (oracle box_face_point)
+__device__ __forceinline__ float box_face_point(V3 P, V3 hb, int f, V3* nb, V3* cb) {
+  const int k = f >> 1;
+  const float sg = (f & 1) ? -1.0f : 1.0f;
+  *nb = v3(k == 0 ? sg : 0.0f, k == 1 ? sg : 0.0f, k == 2 ? sg : 0.0f);
+  const float pk = k == 0 ? P.x : (k == 1 ? P.y : P.z), hk = k == 0 ? hb.x : (k == 1 ? hb.y : hb.z);
+  *cb = v3(k == 0 ? sg * hk : P.x, k == 1 ? sg * hk : P.y, k == 2 ? sg * hk : P.z);
+  return sg * pk - hk;
+}
+// the segment's contact point against a box (P, box frame) with its normal / surface point: the closest point
+// outside, the seg_box_sat face inside; returns the signed distance of the core
+__device__ __forceinline__ float seg_box_point(V3 a, V3 u, V3 hb, V3* P, V3* nb, V3* cb) {
+  bool inside;
+  float t = seg_box_t(a, u, hb, &inside);
+  if (inside) {
+    const int f = seg_box_sat(a, u, hb, &t);
+    *P = a + u * t;
+    return box_face_point(*P, hb, f, nb, cb);
+  }
+  *P = a + u * t;
+  return point_box(*P, hb, nb, cb);
 }
 
 // ---- the convex-mesh geom (MG_GT_CONVEX; oracle point_hull / hull_box_near): the model's hull tables are read
@@ -1242,8 +1289,19 @@ struct Team {
       const float hl = ty == MG_GT_CAPSULE ? gs[1] : 0.0f;
       const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * hl;
       const V3 al = mulT(oR, (c - ax) - op), bl = mulT(oR, (c + ax) - op), u = bl - al;
-      P = al + u * seg_box_t(al, u, hb);
       r = gs[0];
+      bool inside;
+      float t = seg_box_t(al, u, hb, &inside);
+      if (inside) {  // the core inside the cube: the seg_box_sat face (its own point, normal and depth)
+        const int f = seg_box_sat(al, u, hb, &t);
+        P = al + u * t;
+        V3 nb, cb;
+        *dist = box_face_point(P, hb, f, &nb, &cb) - r;
+        *pt = mul(oR, ((P - nb * r) + cb) * 0.5f) + op;
+        *nrm = mul(oR, nb);
+        return true;
+      }
+      P = al + u * t;
     } else if (q < 8) {
       const V3 l = v3((v & 1 ? 1.f : -1.f) * hg.x, (v & 2 ? 1.f : -1.f) * hg.y, (v & 4 ? 1.f : -1.f) * hg.z);
       P = mulT(oR, (c + mul(Rg, l)) - op);
@@ -1395,12 +1453,16 @@ struct Team {
     }
     const V3 hg = v3(gs[0], gs[1], gs[2]);
     const V3 P0 = mulT(Rg, p0 - c), u = mulT(Rg, p1 - p0);
-    const float ts = seg_box_t(P0, u, hg);
+    bool inside;
+    float ts = seg_box_t(P0, u, hg, &inside);
+    // the core inside the box: every candidate against the seg_box_sat face (q = 0 its deepest end, the other
+    // end by its own depth behind that face)
+    const int face = inside ? seg_box_sat(P0, u, hg, &ts) : -1;
     if ((q == 1 && ts < 0.01f) || (q == 2 && ts > 0.99f)) return false;
     const float t = q == 0 ? ts : (q == 1 ? 0.0f : 1.0f);
     const V3 P = P0 + u * t;
     V3 nb, cb;
-    *dist = point_box(P, hg, &nb, &cb) - ro;
+    *dist = (inside ? box_face_point(P, hg, face, &nb, &cb) : point_box(P, hg, &nb, &cb)) - ro;
     *pt = mul(Rg, ((P - nb * ro) + cb) * 0.5f) + c;
     *nrm = mul(Rg, nb) * -1.0f;
     return true;
@@ -1715,9 +1777,8 @@ struct Team {
           const V3 hg = v3(gs[0], gs[1], gs[2]);
           const float r = sa ? ra : rb;
           const V3 al = mulT(Rx, (sa ? a0 : b0) - cx), u = mulT(Rx, (sa ? a1 : b1) - cx) - al;
-          const V3 P = al + u * seg_box_t(al, u, hg);
-          V3 nb, cbx;
-          d = point_box(P, hg, &nb, &cbx) - r;
+          V3 P, nb, cbx;
+          d = seg_box_point(al, u, hg, &P, &nb, &cbx) - r;
           if (d < poff) {
             pt = mul(Rx, ((P - nb * r) + cbx) * 0.5f) + cx;
             nrm = mul(Rx, nb) * (sa ? 1.0f : -1.0f);  // from B to A; nb points from the box to the segment

@@ -61,6 +61,10 @@ int orc_box_box_edge(const double* shape, const double* hb, double off, double* 
 /* the convex-mesh geom's plane distance of n geom-frame points: out = (distance, face) per point */
 int orc_hull_distance(const mg_model* m, const double* pl, int32_t n, double* out);
 int orc_hull_core_contact(const mg_model* m, const double* shape, double rB, double off, double* out);
+/* parity-test support: bit mask of the physics discontinuities env e's gym.simulate passes near (delta m / rad
+ * of a contact / pair / limit threshold with the row in use; drives within df of saturation; seg_box_sat ties) */
+int orc_step_flips(const mg_model* m, const mg_sim_params* p, const mg_state_views* v, int32_t e, double delta,
+                   double df);
 /* world poses of the gym rigid bodies (n_bodies x 13, velocity at body COM) */
 int orc_rigid_body_states(const mg_model* m, const float* root13, const float* dof2, float* out);
 

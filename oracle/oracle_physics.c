@@ -56,6 +56,11 @@ typedef double real;
 #define CVX_MARGIN 1e-3 /* rounding of box cores against the egg (m) */
 #define BOX_BLEND 1e-3  /* point_box: the band (m) over which an interior point's normal blends faces */
 #define MPR_EPS 1e-12 /* origin-side tests */
+/* the explicit MJCF pairs' contact threshold (0: MuJoCo margin 0); moved only by orc_step_flips */
+static __thread double orc_pair_offset = 0.0;
+/* orc_step_flips: seg_box_sat reports a tie of its two least push-out faces within orc_tie_delta */
+static __thread double orc_tie_delta = -1.0;
+static __thread int orc_tie_hit = 0;
 
 typedef real v3[3];
 
@@ -609,6 +614,39 @@ static real seg_box_t(const real* a, const real* u, const real* hb, int* inside)
   return best_t;
 }
 
+/* A segment a + t u whose core has entered a box (seg_box_t's inside case): the contact is taken against the
+ * face of least push-out of the WHOLE segment -- SAT over the box's face axes, delta(k, s) = hb_k - min(s a_k,
+ * s (a_k + u_k)) for the face of outward normal s e_k, ties in x+ x- y+ y- z+ z- order -- at the segment end
+ * deepest behind it.  The inside portion's midpoint (the rule before round 4) lies on a thin box's mid-plane by
+ * construction when the segment pierces it (the reference's pen reset pose through the palm, shadow_hand.py:
+ * 313-314, 625-629), so the face it was pushed through flipped with rounding; the whole segment's extents
+ * decide robustly.  Returns the face (2 k + (s < 0)); *t = the deepest end (0 or 1). */
+static int seg_box_sat(const real* a, const real* u, const real* hb, real* t) {
+  int best = 0;
+  real bd = 1e300, bd2 = 1e300;
+  for (int f = 0; f < 6; f++) {
+    const int k = f >> 1;
+    const real sg = (f & 1) ? -1.0 : 1.0, e0 = sg * a[k], e1 = sg * (a[k] + u[k]);
+    const real dl = hb[k] - (e0 < e1 ? e0 : e1);
+    if (dl < bd) { bd2 = bd; bd = dl; best = f; }
+    else if (dl < bd2) bd2 = dl;
+  }
+  if (bd2 - bd < orc_tie_delta) orc_tie_hit = 1;
+  const int k = best >> 1;
+  const real sg = (best & 1) ? -1.0 : 1.0;
+  *t = sg * a[k] <= sg * (a[k] + u[k]) ? 0.0 : 1.0;
+  return best;
+}
+/* signed distance of point P (box frame) along face f's outward normal from that face's plane (negative behind
+ * it); nb = the normal, cb = P moved onto the plane */
+static real box_face_point(const real* P, const real* hb, int f, real* nb, real* cb) {
+  const int k = f >> 1;
+  const real sg = (f & 1) ? -1.0 : 1.0;
+  for (int a = 0; a < 3; a++) { nb[a] = a == k ? sg : 0.0; cb[a] = P[a]; }
+  cb[k] = sg * hb[k];
+  return sg * P[k] - hb[k];
+}
+
 static void to_obj(const kin* k, const real* pw, real* pl) {
   real d[3] = {pw[0] - k->op[0], pw[1] - k->op[1], pw[2] - k->op[2]};
   mattvec3((real(*)[3])k->oR, d, pl);
@@ -744,8 +782,9 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
     for (int a = 0; a < 3; a++) u[a] = bl[a] - al[a];
     int inside;
     real t = seg_box_t(al, u, hb, &inside), P[3], nb[3], cb[3];
+    const int face = inside ? seg_box_sat(al, u, hb, &t) : -1;
     for (int a = 0; a < 3; a++) P[a] = al[a] + t * u[a];
-    real sd = point_box(P, hb, nb, cb), d = sd - r;
+    real sd = inside ? box_face_point(P, hb, face, nb, cb) : point_box(P, hb, nb, cb), d = sd - r;
     if (d < off) {
       real pm[3], pw[3], nw[3];
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - r * nb[a]) + cb[a]);
@@ -1940,13 +1979,16 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
   mattvec3(R, d0, P0);
   mattvec3(R, du, u);
   int inside;
-  const real ts = seg_box_t(P0, u, hg, &inside);
+  real ts = seg_box_t(P0, u, hg, &inside);
+  /* the core inside the box: every candidate against the face seg_box_sat picks (q = 0 its deepest end, the
+   * other end by its own depth behind that face) */
+  const int face = inside ? seg_box_sat(P0, u, hg, &ts) : -1;
   for (int q = 0; q < 3; q++) {
     if ((q == 1 && ts < 0.01) || (q == 2 && ts > 0.99)) continue;
     const real t = q == 0 ? ts : (q == 1 ? 0.0 : 1.0);
     real P[3], nb[3], cb[3], pm[3];
     for (int a = 0; a < 3; a++) P[a] = P0[a] + t * u[a];
-    const real d = point_box(P, hg, nb, cb) - ro;
+    const real d = (inside ? box_face_point(P, hg, face, nb, cb) : point_box(P, hg, nb, cb)) - ro;
     if (d < off) {
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - nb[a] * ro) + cb[a]);
       matvec3(R, pm, pw);
@@ -2017,7 +2059,8 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
     from_obj_pt(k, sl, e);
     n = sphere_plane(out, n, cap, OBJ_NODE, -2, e, 0.0, off);
   }
-  const real poff = m->pair_mjcf ? 0.0 : off; /* explicit MJCF pairs: in contact from zero distance (margin 0) */
+  /* explicit MJCF pairs: in contact from zero distance (margin 0); orc_step_flips moves that threshold too */
+  const real poff = m->pair_mjcf ? orc_pair_offset : off;
   for (int pi = 0; pi < m->num_pairs; pi++) {
     int ga = m->pair[pi][0], gb = m->pair[pi][1];
     real a0[3], a1[3], b0[3], b1[3], ra, rb;
@@ -2034,9 +2077,10 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
       mattvec3(R, d0, al);
       mattvec3(R, du, u);
       int inside;
-      const real t = seg_box_t(al, u, hg, &inside);
+      real t = seg_box_t(al, u, hg, &inside);
+      const int face = inside ? seg_box_sat(al, u, hg, &t) : -1;
       for (int a = 0; a < 3; a++) P[a] = al[a] + t * u[a];
-      const real d = point_box(P, hg, nb, cb) - r;
+      const real d = (inside ? box_face_point(P, hg, face, nb, cb) : point_box(P, hg, nb, cb)) - r;
       if (d < poff) {
         for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - nb[a] * r) + cb[a]);
         matvec3(R, pm, pw);
@@ -2168,6 +2212,7 @@ typedef struct {
   contact con[MAXC];
   int ncon;
   real lam[MAXR];
+  real lmax[MAXR];    /* the largest |impulse| a row held at any visit of the sweeps */
   int nrows;
   int row_kind[MAXR]; /* 0 normal, 1 friction, 2 limit-lower, 3 limit-upper */
   int row_ref[MAXR];  /* contact index or node */
@@ -2277,6 +2322,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     for (int c = 0; c < nvt; c++) w += J[r][c] * Y[r][c];
     W[r] = w;
     so->lam[r] = 0;
+    so->lmax[r] = 0;
   }
   for (int it = 0; it < p->pos_iters; it++) {
     for (int r = 0; r < nr; r++) {
@@ -2302,6 +2348,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       }
       real dl = lnew - so->lam[r];
       so->lam[r] = lnew;
+      if (fabs(lnew) > so->lmax[r]) so->lmax[r] = fabs(lnew);
       for (int c = 0; c < nvt; c++) nu[c] += Y[r][c] * dl;
     }
   }
@@ -2558,6 +2605,86 @@ int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* ro
 }
 
 #ifndef ORC_FP32 /* fp64 inspection hooks of the checker (KATs); not in the fp32 timing build */
+/* The discontinuities of the build's physics that env `e`'s gym.simulate (state views as orc_simulate_views)
+ * passes near, substep by substep (tests/parity_stats.py): an fp32 and an fp64 step of the same state may part
+ * ways there, and nowhere else.  Each substep is solved once more with the thresholds moved out by `delta` (the
+ * contact offset, the MJCF pairs' zero distance, the joint-limit margin), and the state advances by the normal
+ * substep.  Bits:
+ *   1  a contact within delta of its threshold that the solve uses (its normal impulse leaves 0 at some visit;
+ *      a row whose impulse stays 0 changes nothing, so its presence or absence is no discontinuity)
+ *   2  a joint-limit row within delta of the margin that the solve uses (the same rule)
+ *   4  a PD drive whose explicit force is within df (relative) of its effort limit (implicit <-> saturated)
+ *   8  a segment core inside a box whose two least push-out faces are within delta (seg_box_sat's tie) */
+int orc_step_flips(const mg_model* m0, const mg_sim_params* p, const mg_state_views* v, int32_t e, double delta,
+                   double df) {
+  const mg_model* m = m0;
+  int nd = m0->num_dofs, rows = m0->obj_type ? 3 : 1, nb = m0->num_bodies + (m0->obj_type ? 2 : 0);
+  (void)nb;
+  float* root = v->root_states + (size_t)13 * rows * e;
+  float* dof = v->dof_state + (size_t)2 * nd * e;
+  const float* act = v->dof_actuation ? v->dof_actuation + (size_t)nd * e : 0;
+  const float* tgt = v->dof_targets ? v->dof_targets + (size_t)nd * e : 0;
+  const float* of = (m0->obj_type && v->rb_forces) ? v->rb_forces + ((size_t)(m0->num_bodies + 2) * e + m0->num_bodies) * 3 : 0;
+  const float* props = v->env_props ? v->env_props + (size_t)v->env_props_stride * e : 0;
+  astate s;
+  memset(&s, 0, sizeof(s));
+  mg_model* mdr = NULL;
+  real gmu[MG_MAX_GEOMS + 1];
+  if (props) {
+    mdr = (mg_model*)malloc(sizeof(mg_model));
+    apply_env_props(m0, props, mdr, gmu);
+    m = mdr;
+    s.gmu = gmu;
+  }
+  load_state(m, root, dof, &s);
+  s.tgt = tgt;
+  if (m->obj_type) load_object(&s, root + 13);
+  if (of)
+    for (int a = 0; a < 3; a++) s.of[a] = of[a];
+  s.of_local = v->rb_force_space == MG_LOCAL_SPACE;
+  real tau[MAXN];
+  for (int i = 0; i < m->num_dofs; i++) tau[i] = act ? act[i] : 0.0;
+  substep_out* so = (substep_out*)calloc(1, sizeof(substep_out));
+  mg_sim_params pw = *p;
+  pw.contact_offset = (float)(p->contact_offset + delta);
+  pw.limit_margin = (float)(p->limit_margin + delta);
+  int flags = 0;
+  for (int st = 0; st < p->substeps; st++) {
+    /* drives near saturation at this substep's state */
+    for (int i = 1; i < m->num_nodes; i++) {
+      if (m->drive_kp[i] <= 0.0) continue;
+      const real fe = m->drive_kp[i] * ((tgt ? tgt[i - 1] : 0.0) - s.qj[i]) - m->damping[i] * s.qd[i];
+      const real lim = m->effort_limit[i];
+      if (fabs(fabs(fe) - lim) < df * (lim > 1e-6 ? lim : 1e-6)) flags |= 4;
+    }
+    /* the solve with the thresholds moved out (its collide also reports seg_box_sat ties) */
+    astate sw = s;
+    orc_pair_offset = delta;
+    orc_tie_delta = delta;
+    orc_tie_hit = 0;
+    substep(m, &pw, &sw, tau, so);
+    orc_pair_offset = 0.0;
+    orc_tie_delta = -1.0;
+    if (orc_tie_hit) flags |= 8;
+    const real eps = 1e-9;
+    for (int c = 0; c < so->ncon; c++) {
+      const contact* ct = &so->con[c];
+      const int pair = m->pair_mjcf && ct->nodeB >= 0;
+      const real thr = pair ? 0.0 : p->contact_offset;
+      if (fabs(ct->d - thr) < delta && so->lmax[3 * c] > eps) flags |= 1;
+    }
+    for (int r = 3 * so->ncon; r < so->nrows; r++) {
+      const int i = so->row_ref[r];
+      const real d = so->row_kind[r] == 2 ? s.qj[i] - m->lower[i] : m->upper[i] - s.qj[i];
+      if (fabs(d - p->limit_margin) < delta && so->lmax[r] > eps) flags |= 2;
+    }
+    substep(m, p, &s, tau, so);
+  }
+  free(so);
+  free(mdr);
+  return flags;
+}
+
 int orc_mass_matrix(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2,
                     real* M_out) {
   astate s;

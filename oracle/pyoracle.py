@@ -64,6 +64,8 @@ def lib():
         l.orc_box_box_edge.argtypes = [P, P, C.c_double, P]
         l.orc_hull_distance.argtypes = [P, P, C.c_int32, P]
         l.orc_hull_core_contact.argtypes = [P, P, C.c_double, C.c_double, P]
+        l.orc_step_flips.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.StateViews), C.c_int32, C.c_double,
+                                     C.c_double]
         l.orc_dr_apply.argtypes = [C.POINTER(_abi.DrApplyArgs)]
         l.orc_dr_noise.argtypes = [C.POINTER(_abi.DrNoiseArgs)]
         _lib = l
@@ -156,6 +158,15 @@ def ellipsoid_contact(kind, shape, radius, e):
     out = np.zeros(7)
     lib().orc_ellipsoid_contact(int(kind), p(sh), float(radius), p(ev), p(out))
     return out[0:3], out[3:6], out[6]
+
+
+def step_flips(model_np, sp, host, delta=1e-4, df=1e-2):
+    """per env of a HostEnv / HandHostEnv holding a step's physics input (after pre-physics): the bit mask of
+    orc_step_flips (1 contact threshold in use, 2 limit threshold in use, 4 drive near saturation, 8 seg_box_sat
+    tie) over the substeps of one gym.simulate"""
+    v = host.views()
+    return np.array([lib().orc_step_flips(model_np.ctypes.data, C.byref(sp), C.byref(v), e, delta, df)
+                     for e in range(host.n)], np.int32)
 
 
 def rigid_body_states(model_np, root13, dof2, nbodies):
@@ -307,6 +318,7 @@ class HandHostEnv:
         # running-mean partial sums left for a cross-rank all-reduce (defer_finalize)
         self.scratch = np.zeros(2, np.uint64)
         self.defer_finalize = 0
+        self.env_props = None   # (n, stride) domain-randomized properties, or None
 
     def views(self):
         v = _abi.StateViews()
@@ -314,6 +326,8 @@ class HandHostEnv:
         v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), p(self.rbs)
         v.dof_targets = p(self.targets)
         v.rb_forces, v.rb_force_space = p(self.rb_forces), _abi.MG_LOCAL_SPACE
+        if self.env_props is not None:
+            v.env_props, v.env_props_stride = p(self.env_props), self.env_props.shape[1]
         return v
 
     def buffers(self, seed=0, step=0, env_offset=0):

@@ -1,21 +1,26 @@
 """Helpers of the GPU-vs-oracle physics tests (test infrastructure): error statistics, and the
 discontinuities of the build's physics that let an fp32 (GPU) and an fp64 (oracle) step of the same state
-part ways:
+part ways.
 
-  * contact threshold: a candidate whose gap lies within `delta` of contact_offset is a contact on one side
-    and not on the other (detected by regenerating the oracle's contacts with the offset moved by +-delta; the hand's explicit
-    MJCF pairs switch on at distance 0, and their threshold is moved by +-delta the same way);
-  * joint-limit rows: a DOF within `dq` of the limit margin (limit_margin 0.1 rad from a limit);
-  * PD drive saturation (hand tasks): an explicit drive force within `df` of its effort limit;
-  * deep penetration (a contact deeper than 5 mm, reachable only where a reset places the object into hand
-    geometry): the normal of a point inside a box is its nearest face's, a discontinuous function of position.
+The tests compare one physics step, or fused steps teacher-forced step by step (both sides restarted from the
+oracle's state every step, so a step's rounding difference cannot grow chaotically over the next).  An env-step
+whose GPU and oracle results disagree is accepted only when the oracle's orc_step_flips puts that step, in one of
+its substeps, at a discontinuity:
 
-  * any other state where the oracle itself is sensitive: replayed alone from step 1 with positions
-    perturbed by 1e-6, the oracle moves by at least a quarter of the GPU-vs-oracle difference
-    (oracle_sensitive; e.g. a separating-axis tie between a face and an edge axis, a friction-cone clamp).
+  * a contact within STEP_DELTA of its threshold (contact_offset; 0 for the hand's explicit MJCF pairs) whose row
+    the solve uses: present on one side and absent on the other, it changes the result only if its impulse leaves
+    zero at some PGS visit (a row whose impulse stays zero changes nothing);
+  * a joint-limit row within STEP_DELTA of the limit margin, used by the solve (the same rule);
+  * a PD drive whose explicit force is within STEP_DF (relative) of its effort limit (implicit <-> saturated);
+  * a capsule core inside a box whose two least push-out faces tie (seg_box_sat);
 
-An env whose GPU and oracle results disagree is accepted only when one of these holds for it.  Set
-MIGYM_PARITY_REPORT=<path> to collect the max / 99.9th-percentile errors of every check into a JSON file.
+or where the oracle is itself sensitive (one step of the env alone with positions moved by 1e-6 moves its
+observation by >= 1/4 of the GPU-vs-oracle gap).  The fraction of ALL env-steps these predicates exempt is
+recorded and capped (REACH_CAP), so a test cannot pass by exempting the contact-rich envs wholesale.
+
+The older per-state predicates (contact_flips, limit_flips, drive_flips, deep_contacts) remain for the
+diagnostic tools.  Set MIGYM_PARITY_REPORT=<path> to collect the error statistics and exemptions of every check
+into a JSON file.
 """
 import copy
 import json
@@ -113,6 +118,84 @@ def drive_flips(q, qd, targets, kp, damping, effort, df=1e-2):
     lim = np.asarray(effort)
     near = (np.asarray(kp) > 0) & (np.abs(np.abs(fe) - lim) < df * np.maximum(lim, 1e-6))
     return near.reshape(len(q), -1).any(axis=1)
+
+
+# thresholds of the per-step predicates (orc_step_flips): a teacher-forced step starts the GPU and the oracle
+# from the same state, so the two stay within fp32 rounding (~1e-6 m) of each other through its substeps
+STEP_DELTA = 1e-5    # m / rad from a contact, pair or joint-limit threshold (with the row in use)
+STEP_DF = 2e-4       # relative distance of a PD drive's explicit force from its effort limit
+# at most this fraction of the env-steps of a test may be exempt (flagged) at all: beyond it the predicates would
+# excuse too much for the test to see a bug in contact-rich envs ("What's weak" 2)
+REACH_CAP = 0.05
+SENS_CAP = 0.01      # and at most this fraction by the oracle-sensitivity fallback
+
+
+def step_flags(mnp, sp, host, delta=STEP_DELTA, df=STEP_DF):
+    """per env: orc_step_flips of the physics input `host` holds (a HostEnv with act_eff / a HandHostEnv after
+    pre_physics, optionally with env_props): bit 1 contact threshold in use, 2 limit threshold in use, 4 drive
+    near saturation, 8 seg_box_sat tie"""
+    return O.step_flips(mnp, sp, host, delta, df)
+
+
+def loco_physics_input(h, mnp, sp, tp, seed, step):
+    """a HostEnv copy holding step `step`'s physics input: the state as the step starts (the locomotion resets
+    run in post_physics) and the actuation pre_physics computes from h.actions"""
+    g, tmp = copy.deepcopy(h), copy.deepcopy(h)
+    tmp.env_step(mnp, sp, tp, seed=seed, step=step, threads=1)
+    g.act_eff[:] = tmp.act_eff
+    return g
+
+
+def hand_physics_input(h, mnp, tp, seed, step):
+    """a HandHostEnv copy after pre_physics of step `step` (goal / env resets, PD targets, object forces)"""
+    g = copy.deepcopy(h)
+    g.pre_physics(mnp, tp, seed=seed, step=step)
+    return g
+
+
+def assert_steps_explained(test, bad, flags, sens=None, reach_cap=REACH_CAP, sens_cap=SENS_CAP):
+    """bad, flags: (steps, envs).  Every disagreeing env-step must be flagged by orc_step_flips at that step (or,
+    through `sens(t, i)`, sit where the oracle itself is sensitive); the flags' reach (the fraction of ALL env-steps
+    they would exempt) and the sensitivity fallback's use are recorded and capped"""
+    bad = np.asarray(bad, bool)
+    flagged = np.asarray(flags) != 0
+    why = flagged.copy()
+    nsens = 0
+    if sens is not None:
+        for t, i in zip(*np.nonzero(bad & ~why)):
+            if sens(int(t), int(i)):
+                why[t, i] = True
+                nsens += 1
+    total = bad.size
+    rec = {"env_steps": int(total), "disagreeing": int(bad.sum()), "flagged_reach": float(flagged.mean()),
+           "explained_by_flags": int((bad & flagged).sum()), "explained_by_sensitivity": nsens,
+           "bits": {str(b): float(((np.asarray(flags) & b) != 0).mean()) for b in (1, 2, 4, 8)}}
+    _REPORT.setdefault(test, {})["exemptions"] = rec
+    unexplained = np.argwhere(bad & ~why)
+    assert unexplained.size == 0, (f"{test}: {len(unexplained)} of {int(bad.sum())} disagreeing env-steps are not at a "
+                                   f"discontinuity (step, env): {unexplained[:10].tolist()}")
+    assert flagged.mean() <= reach_cap, f"{test}: the predicates exempt {flagged.mean():.3f} of the env-steps (cap {reach_cap})"
+    assert nsens <= sens_cap * total, f"{test}: {nsens} env-steps excused by oracle sensitivity (cap {sens_cap} x {total})"
+    return rec
+
+
+def oracle_sensitive_step(mnp, sp, tp, pre, action, i, gpu_out, oracle_out, seed, step, hand, eps=1e-6, ratio=0.25):
+    """one teacher-forced step of env i alone from `pre` (its state before the step), once as recorded and once
+    with positions moved by eps: True if the final observation moves by >= ratio x the GPU-vs-oracle gap"""
+    runs = []
+    for pert in (0.0, eps):
+        g = env_slice(pre, i)
+        if hand:
+            g.root[:, 1, 0:3] += pert
+        else:
+            g.root[:, 0:3] += pert
+        g.dof[..., 0] += pert
+        g.actions[:] = action[i:i + 1]
+        g.env_step(mnp, sp, tp, seed=seed, step=step, threads=1, env_offset=i)
+        runs.append(g.obs[0].astype(np.float64).copy())
+    moved = np.abs(runs[1] - runs[0]).max()
+    gap = np.abs(np.asarray(gpu_out, np.float64) - np.asarray(oracle_out, np.float64)).max()
+    return moved >= ratio * gap
 
 
 def assert_explained(bad, explained, what):

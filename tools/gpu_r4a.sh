@@ -1,6 +1,6 @@
 set -o pipefail
 cd /root/repo
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r4a_gpu.log 2>&1
+MIGYM_PARITY_REPORT=gpurun_out/parity_r4a.json timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r4a_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 tail -40 gpurun_out/r4a_gpu.log
