@@ -62,8 +62,8 @@ extern "C" {
 #define MG_MAX_SENSORS 8
 #define MG_MAX_TENDONS 8
 #define MG_MAX_HAND_DOFS 32
-#define MG_MAX_HULL_VERTS 64    /* the convex-mesh geom's hull (mg_model.hull_*) */
-#define MG_MAX_HULL_PLANES 128
+#define MG_MAX_HULL_VERTS 160   /* the convex-mesh geom's hull (mg_model.hull_*) */
+#define MG_MAX_HULL_PLANES 320
 
 enum { MG_JT_FREE = 0, MG_JT_FIXED = 1, MG_JT_HINGE = 2, MG_JT_SLIDE = 3 };
 enum { MG_GT_PLANE = 0, MG_GT_SPHERE = 1, MG_GT_CAPSULE = 2, MG_GT_BOX = 3, MG_GT_CYLINDER = 4, MG_GT_ELLIPSOID = 5,

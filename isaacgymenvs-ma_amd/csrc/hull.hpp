@@ -343,8 +343,7 @@ __device__ __forceinline__ int hull_face_clip(const HullQ& H, int f, V3 p0, V3 u
   const V3 q0 = p0 - nf * s0, qu = u - nf * su;
   float lo = 0.0f, hi = 1.0f;
   bool empty = false;
-#pragma unroll
-  for (int k = 0; k < (MG_MAX_HULL_PLANES + T - 1) / T; k++) {
+  for (int k = 0; k * T < H.np; k++) {
     const int i = k * T + H.tl;
     if (i >= H.np || i == f) continue;
     const float4 q = *reinterpret_cast<const float4*>(H.pl[i]);
@@ -412,20 +411,14 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
   // the hull's features at pa: the planes through it (the first two in index order), one ballot per T planes
   int kA = 0, fa0 = 0, fa1 = 0;
   const unsigned long long tm = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
-  constexpr int KP = (MG_MAX_HULL_PLANES + T - 1) / T;
-  bool on[KP];
-#pragma unroll
-  for (int k = 0; k < KP; k++) {  // the loads first (one batch), then the ballots in plane order
+  for (int k = 0; k * T < np; k++) {  // one ballot per T planes, in plane order
     const int f = k * T + tl;
-    on[k] = false;
+    bool on = false;
     if (f < np) {
       const float4 q = *reinterpret_cast<const float4*>(pl[f]);
-      on[k] = fabsf(q.x * pa.x + q.y * pa.y + q.z * pa.z - q.w) < HULL_FEAT_EPS;
+      on = fabsf(q.x * pa.x + q.y * pa.y + q.z * pa.z - q.w) < HULL_FEAT_EPS;
     }
-  }
-#pragma unroll
-  for (int k = 0; k < KP; k++) {
-    unsigned long long bits = (__ballot(on[k]) >> tb) & tm;
+    unsigned long long bits = (__ballot(on) >> tb) & tm;
     while (bits) {
       const int i = k * T + __builtin_ctzll(bits);
       bits &= bits - 1;

@@ -42,7 +42,7 @@ static __device__ unsigned long long* g_phase_buf;
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
 struct Shape {
   static constexpr int E1 = 64 / T;  // teams (actors) per wave
-  static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>);
+  static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OBJ)>);
   static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T>) +
                                         (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
   static constexpr int per_cu(int w) {
@@ -398,7 +398,7 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // one work item of k_hand_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
 __device__ __forceinline__ void hand_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, 16 * MG>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
@@ -646,9 +646,9 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
   constexpr int E = SH::E, W = SH::W;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
-  __shared__ mg::ModelTile<MN, MG, MP, 16 * MG> tile;
+  __shared__ mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
-  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, 16 * MG>*>(timg));
+  mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {  // as k_env_step
     if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
@@ -702,7 +702,7 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
 
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int BuildTile<T, MN, MC, MG, MP, OBJ>::run(mg_sim* sim) {
-  using MT = mg::ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>;   // the kernels' tile type (Team::MT)
+  using MT = mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OBJ)>;   // the kernels' tile type (Team::MT)
   MT* img = new (std::nothrow) MT();
   if (!img) return fail(MG_ENOMEM, "mg_sim_create: out of host memory (model tile)");
   mg::build_tile(img, &sim->host_model);

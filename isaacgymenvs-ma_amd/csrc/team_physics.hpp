@@ -48,7 +48,11 @@ namespace mg {
 // every per-node / per-geom constant is an LDS read (~64 cycles) instead of a dependent global load.
 // Rows padded to odd strides.  The image is built once on the host (build_tile, at mg_sim_create) and
 // each block copies it with 16-byte loads; the W waves of a block share one copy.
-template <int MN, int MG, int MP, int OC = 1>  // OC > 1: the free-object (hand) instances
+// vertices of the convex hull the LDS model tile holds: the block / pen instances, whose exact hull candidates
+// (hull.hpp) read them in every GJK support; the egg tests the hull's planes only (global memory)
+constexpr int tile_hull_verts(int obj) { return (obj == MG_GT_BOX || obj == MG_GT_CAPSULE) ? MG_MAX_HULL_VERTS : 1; }
+
+template <int MN, int MG, int MP, int HV = 1>  // HV: hull vertex capacity of the tile (tile_hull_verts)
 struct alignas(16) ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
@@ -63,15 +67,15 @@ struct alignas(16) ModelTile {
   int nn, ng, np;
   int hnv;            // vertices of the convex-mesh geom's hull (mg_model.hull_*), 0 if none
   int hullg;          // the convex-mesh geom (-1 if none)
-  // hand instances: the hull's vertices and their centroid for the exact hull candidates (hull.hpp), read by
-  // every GJK support; its planes stay in global memory (one pass per call)
-  float hv[OC > 1 ? MG_MAX_HULL_VERTS : 1][3];
+  // block / pen instances: the hull's vertices and their centroid for the exact hull candidates (hull.hpp), read
+  // by every GJK support; its planes stay in global memory (one pass per call)
+  float hv[HV][3];
   float hctr[4];
 };
 
 // host: the finished tile image of model m (child masks, rest rotations as matrices, geom frames)
-template <int MN, int MG, int MP, int OC>
-__host__ __device__ void build_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model* m, int tid = 0, int nt = 1) {
+template <int MN, int MG, int MP, int HV>
+__host__ __device__ void build_tile(ModelTile<MN, MG, MP, HV>* t, const mg_model* m, int tid = 0, int nt = 1) {
   const int nn = m->num_nodes < MN ? m->num_nodes : MN, ng = m->num_geoms < MG ? m->num_geoms : MG;
   const int np = m->num_pairs < MP ? m->num_pairs : MP;
   for (int i = tid; i < nn; i += nt) {
@@ -128,7 +132,7 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, OC>* t, const mg_model
     for (int g = ng - 1; g >= 0; g--)
       if (m->geom_type[g] == MG_GT_CONVEX && (m->geom_filter[g] & MG_COLLIDE_OBJECT)) t->hullg = g;
     t->hctr[0] = t->hctr[1] = t->hctr[2] = t->hctr[3] = 0.0f;
-    if (OC > 1 && m->hull_num_verts > 0) {
+    if (HV > 1 && m->hull_num_verts > 0 && m->hull_num_verts <= HV) {
       float cx = 0.0f, cy = 0.0f, cz = 0.0f;
       for (int v = 0; v < m->hull_num_verts; v++) {
         for (int k = 0; k < 3; k++) t->hv[v][k] = m->hull_vert[v][k];
@@ -609,7 +613,7 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
 template <int T, int MN, int MC, int MG, int MP, int OBJ = 0>  // OBJ: the free object's type (0: none)
 struct Team {
   using L = TeamLDS<T, MN, MC, OBJ>;
-  using MT = ModelTile<MN, MG, MP, OBJ ? 16 * MG : 1>;
+  using MT = ModelTile<MN, MG, MP, tile_hull_verts(OBJ)>;
   static constexpr int MR = L::MR;
   L* s;
   const MT* mt;
@@ -1517,8 +1521,8 @@ struct Team {
           // planes of the nearer end (max_f min_t <= min_t max_f); at or beyond the offset there is no contact
           float lb = -3.0e38f;
           const int np = m->hull_num_planes;
-#pragma unroll
-          for (int k = 0; k < (MG_MAX_HULL_PLANES + T - 1) / T; k++) {  // one batch of loads, then the reduction
+#pragma unroll 4
+          for (int k = 0; k < (MG_MAX_HULL_PLANES + T - 1) / T; k++) {  // batches of loads, then the reduction
             const int f = tl + k * T;
             if (f < np) {
               const float4 q = *reinterpret_cast<const float4*>(m->hull_plane[f]);

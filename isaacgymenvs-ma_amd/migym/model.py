@@ -45,8 +45,8 @@ MAX_GEOMS = 48
 MAX_PAIRS = 192
 MAX_SENSORS = 8
 MAX_TENDONS = 8
-MAX_HULL_VERTS = 64
-MAX_HULL_PLANES = 128
+MAX_HULL_VERTS = 160
+MAX_HULL_PLANES = 320
 COLLIDE_GROUND, COLLIDE_OBJECT = 1, 2
 
 JT_FREE, JT_FIXED, JT_HINGE, JT_SLIDE = 0, 1, 2, 3
@@ -925,15 +925,19 @@ ASSET_OPTIONS = {
 }
 
 
-def load_builtin(name) -> ModelSpec:
-    """Load one of the shipped model tables (generated by tools/build_models.py), with the task's
-    asset options (ASSET_OPTIONS) on gym's defaults."""
-    spec = ModelSpec.from_json(os.path.join(ASSET_DIR, name + ".json"))
+def apply_asset_options(spec: ModelSpec, name: str) -> ModelSpec:
+    """the task's link options (ASSET_OPTIONS) on gym's defaults; tools/build_models.py writes them into the
+    shipped tables"""
     spec.angular_damping = GYM_ANGULAR_DAMPING
     spec.max_angular_velocity = GYM_MAX_ANGULAR_VELOCITY
     for k, v in ASSET_OPTIONS.get(name, {}).items():
         setattr(spec, k, v)
     return spec
+
+
+def load_builtin(name) -> ModelSpec:
+    """Load one of the shipped model tables (generated by tools/build_models.py, asset options included)."""
+    return ModelSpec.from_json(os.path.join(ASSET_DIR, name + ".json"))
 
 
 def hand_object(kind: str) -> Dict:

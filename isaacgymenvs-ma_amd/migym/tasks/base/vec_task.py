@@ -112,8 +112,9 @@ class VecTask(DomainRandomizationMixin, Env):
         self.cfg = config
         super().__init__(config, rl_device, sim_device, graphics_device_id, headless)
         if self.device == "cpu":
-            raise RuntimeError("migym simulates on the MI355X only: use pipeline='gpu' and sim_device='cuda:N' "
-                               "(the reference's CPU PhysX pipeline has no counterpart on this path)")
+            raise RuntimeError("migym simulates on the MI355X: for the CPU pipeline (use_gpu_pipeline=False or "
+                               "sim_device='cpu') create the task through migym.make / isaacgymenvs.make, which runs "
+                               "the HIP step and exposes host-side views (migym/host_pipeline.py)")
         if not torch.cuda.is_available():
             raise RuntimeError("migym needs a HIP device (torch.cuda.is_available() is False)")
         self.virtual_screen_capture = virtual_screen_capture

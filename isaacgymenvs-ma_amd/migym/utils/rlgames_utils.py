@@ -51,9 +51,21 @@ def get_rlgames_env_creator(seed, task_config, task_name, sim_device, rl_device,
             cfg["world_size"] = world
             cfg["env_offset"] = global_rank * int(cfg["env"]["numEnvs"])
         cfg["seed"] = seed
+        # the CPU pipeline (vec_task.py:78-90: use_gpu_pipeline False, or a non-GPU sim_device): the HIP step on the
+        # GPU with host-side views of every tensor (migym/host_pipeline.py)
+        dev_type, _, dev_id = str(sim_device).partition(":")
+        host = not cfg.get("sim", {}).get("use_gpu_pipeline", True) or dev_type.lower() not in ("cuda", "gpu")
+        if host:
+            if dev_type.lower() not in ("cuda", "gpu"):
+                print("GPU Pipeline can only be used with GPU simulation. Forcing CPU Pipeline.")
+            cfg["sim"] = dict(cfg["sim"], use_gpu_pipeline=True)
+            sim_device = f"cuda:{int(dev_id) if dev_id and dev_type.lower() in ('cuda', 'gpu') else 0}"
         env = isaacgym_task_map[task_name](cfg=cfg, rl_device=rl_device, sim_device=sim_device,
                                            graphics_device_id=graphics_device_id, headless=headless,
                                            virtual_screen_capture=virtual_screen_capture, force_render=force_render)
+        if host:
+            from ..host_pipeline import HostPipeline
+            env = HostPipeline(env)
         if post_create_hook is not None:
             post_create_hook()
         return env

@@ -212,3 +212,37 @@ def test_env_state_round_trip_with_randomization():
         assert torch.equal(obs["obs"], o) and torch.equal(rew, r) and torch.equal(reset, d)
         assert torch.equal(env.env_props, p)
     env.close()
+
+
+@pytest.mark.parametrize("task,n,how", [("Ant", 256, "sim_device"), ("ShadowHand", 64, "pipeline")])
+def test_cpu_pipeline_host_views(task, n, how):
+    """use_gpu_pipeline=False / sim_device='cpu' (vec_task.py:78-90): env.device is 'cpu' and every tensor the task
+    exposes is a host tensor, the HIP step runs underneath (the same numbers as the GPU pipeline, bit for bit), views
+    keep their base (dof_pos on dof_state), and host-side edits of the buffers take effect on the next step."""
+    g = make(task, n)
+    if how == "sim_device":
+        c = migym.make(seed=3, task=task, num_envs=n, sim_device="cpu", rl_device=DEV, headless=True)
+    else:
+        cfg = configs.task_config(task, n, sim_device=DEV, pipeline="cpu")
+        assert cfg["sim"]["use_gpu_pipeline"] is False
+        c = migym.make(seed=3, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                       cfg={"task": cfg})
+    assert c.device == "cpu" and c.unwrapped.device.startswith("cuda")
+    for name in ("root_states", "dof_state", "obs_buf", "rew_buf", "reset_buf", "progress_buf"):
+        assert getattr(c, name).device.type == "cpu", name
+    assert c.dof_pos.untyped_storage().data_ptr() == c.dof_state.untyped_storage().data_ptr()
+    for k in range(3):
+        og, rg, dg, _ = g.step(actions(g, k))
+        oc, rc, dc, _ = c.step(actions(g, k).cpu())
+        assert torch.equal(oc["obs"], og["obs"]) and torch.equal(rc, rg) and torch.equal(dc, dg)
+        assert torch.equal(c.root_states, g.root_states.cpu()) and torch.equal(c.dof_pos, g.dof_pos.cpu())
+        assert torch.equal(c.progress_buf, g.progress_buf.cpu())
+    # a host-side edit: force resets of the first envs on both
+    c.reset_buf[:5] = 1
+    g.reset_buf[:5] = 1
+    og, _, _, _ = g.step(actions(g, 9))
+    oc, _, _, _ = c.step(actions(g, 9).cpu())
+    assert torch.equal(oc["obs"], og["obs"]) and torch.equal(c.progress_buf, g.progress_buf.cpu())
+    assert bool((c.progress_buf[:5] <= 1).all())
+    g.close()
+    c.close()

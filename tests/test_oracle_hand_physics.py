@@ -405,7 +405,7 @@ def _forearm_frame(mnp, h, spec):
 
 
 def test_forearm_hull_tables():
-    """The forearm's convex mesh (shared_asset.xml:15) is a hull of 64 vertices with outward planes: every
+    """The forearm's convex mesh (shared_asset.xml:15) is a hull of 160 vertices with outward planes: every
     kept vertex lies on or inside every plane, the centre is inside, points beyond the bounding box are
     outside, and the plane distance never exceeds the true distance to the kept vertices' hull."""
     spec = M.load_builtin("shadow_hand")
@@ -413,7 +413,7 @@ def test_forearm_hull_tables():
     assert spec.geoms[spec.hull["geom"]].gtype == M.GT_CONVEX and spec.geoms[spec.hull["geom"]].name == "robot0:C_forearm"
     v = np.array(spec.hull["verts"])
     d, _ = O.hull_distance(mnp, v)
-    assert d.max() < 1e-6 and len(v) == 64
+    assert d.max() < 1e-6 and len(v) == 160
     d0, _ = O.hull_distance(mnp, np.zeros((1, 3)))
     assert d0[0] < -0.03
     hb = np.array(spec.geoms[spec.hull["geom"]].size)
@@ -521,11 +521,18 @@ def test_hull_exact_pen_across_face():
     mnp = M.pack_model(spec)
     _, V, P, on = _hull_edges(spec)
     ro, hl = 0.008, 0.1
+    checked = 0
     for f in range(0, len(P), 7):
         n = P[f, :3]
         ctr = V[on[:, f]].mean(0)
         t = np.cross(n, [0.3, 0.2, 0.9])
         t /= np.linalg.norm(t)
+        # faces whose plane the pen's ends overhang by centimetres (the end-sphere candidates far from contact)
+        e0, e1 = ctr + n * ro - t * hl, ctr + n * ro + t * hl
+        ends, _ = O.hull_distance(mnp, np.stack([e0, e1]))
+        if not (ends - ro > 0.022).all():
+            continue
+        checked += 1
         for gap in (0.001, 0.0, -0.002):
             p0, p1 = ctr + n * (ro + gap) - t * hl, ctr + n * (ro + gap) + t * hl
             ends, _ = O.hull_distance(mnp, np.stack([p0, p1]))
@@ -553,6 +560,7 @@ def test_hull_exact_pen_across_face():
                     continue
                 assert len(r2) in count, (f, deg, r2)
                 assert min(x[2] for x in r2) < gap and all(x[1] @ -n > np.cos(np.radians(15)) for x in r2), r2
+    assert checked >= 10, checked
 
 
 
@@ -625,3 +633,39 @@ def test_flexed_fingers_meet_through_the_explicit_pairs():
         res[pairs] = (np.abs(h.dof[0, rf, 0] - tgt[rf]).max(), len(con))
     assert res[True][0] > 0.02 and res[True][1] >= 1, res
     assert res[False][0] < 0.02 and res[False][1] == 0, res
+
+
+def test_egg_mpr_depth_against_the_minimum_translation():
+    """A6, MPR vs EPA (documented difference): for a capsule core overlapping the egg, MPR's depth
+    is the refined portal's point nearest the origin, a separating translation (>= the minimum translation
+    distance, MTD) but not always the minimum one.  Against the exact MTD (brute force: the minimum over unit
+    directions of h_segment(d) + h_egg(-d), a 4000-direction sweep refined by Nelder-Mead) over 120 random overlaps
+    up to 4 cm deep: never below it, median within 6 %, and never more than 1.9x (the bound this build ships;
+    EPA would close it, the deep case being reachable only from reset poses)."""
+    from scipy.optimize import minimize
+    e = np.array([0.03, 0.03, 0.04])
+    hE = lambda d: np.sqrt(((e * d) ** 2).sum())
+    n = 4000
+    i = np.arange(n) + 0.5
+    phi, th = np.arccos(1 - 2 * i / n), np.pi * (1 + 5 ** 0.5) * i
+    D = np.stack([np.cos(th) * np.sin(phi), np.sin(th) * np.sin(phi), np.cos(phi)], 1)
+    rng = np.random.default_rng(0)
+    ratios = []
+    while len(ratios) < 120:
+        c = rng.normal(0, 0.02, 3)
+        u = rng.normal(size=3)
+        u /= np.linalg.norm(u)
+        hl = rng.uniform(0.005, 0.04)
+        p0, p1 = c - u * hl, c + u * hl
+        f = lambda d: max(p0 @ d, p1 @ d) / np.linalg.norm(d) + hE(-d / np.linalg.norm(d))
+        vals = np.maximum(D @ p0, D @ p1) + np.sqrt(((e * D) ** 2).sum(1))
+        k = int(vals.argmin())
+        mtd = min(vals[k], minimize(f, D[k], method="Nelder-Mead", options=dict(xatol=1e-10, fatol=1e-12)).fun)
+        if mtd < 1e-4:
+            continue   # separated or grazing
+        _, _, d = O.ellipsoid_contact(0, np.r_[p0, p1], 0.008, e)
+        depth = -(d + 0.008)
+        assert depth >= mtd - 2e-7, (depth, mtd)   # MPR's portal tolerance (MPR_TOL 1e-7 m)
+        ratios.append(depth / mtd)
+    r = np.array(ratios)
+    assert np.median(r) <= 1.06 and r.max() <= 1.9, (np.median(r), r.max())

@@ -14,9 +14,10 @@ them from migym/assets/*.json.
              tendon limit_stiffness 30 / damping 0.1 on the four T_*J1c tendons, fingertip force
              sensors; the object keeps gym's default AssetOptions: angular_damping 0.5, gravity on).
             The forearm's convex collision mesh (forearm_electric_cvx.stl, 455 hull vertices) is
-            imported as a convex hull of 64 of its vertices (greedy: the 26 axis / diagonal extremes,
+            imported as a convex hull of 160 of its vertices (greedy: the 26 axis / diagonal extremes,
             then repeatedly the vertex farthest outside the current hull; every dropped vertex lies
-            within 1.9 mm of the kept hull) with its face planes (coplanar facets merged).
+            within 0.46 mm of the kept hull; PhysX cooks such meshes to <= 255 vertices) with its face
+            planes (coplanar facets merged).
   hand_objects.json  the free object of each ShadowHand objectType (shadow_hand.py:86-100):
             block = urdf/objects/cube_multicolor.urdf, egg = mjcf/open_ai_assets/hand/egg.xml
             (ellipsoid), pen = mjcf/open_ai_assets/hand/pen.xml (capsule along the body z); mass and
@@ -51,7 +52,7 @@ def stl_vertices(path, scale=(1.0, 1.0, 1.0)):
     return np.unique(v * np.asarray(scale), axis=0)
 
 
-def reduced_hull(v, max_verts=64, tol=1e-5):
+def reduced_hull(v, max_verts=160, tol=1e-5):
     """a convex hull of at most max_verts of the points v: the extremes along the 26 axis / diagonal
     directions, then greedily the point farthest outside the current hull.  Returns (kept vertices,
     merged outward face planes [n, d] with n.x <= d inside, largest distance of a dropped point
@@ -131,14 +132,18 @@ def hand_objects(hand):
 def main():
     out = M.ASSET_DIR
     ant = M.load_mjcf(os.path.join(REF, "assets/mjcf/nv_ant.xml"), "ant")
+    M.apply_asset_options(ant, "ant")
     ant.sensors = [i for i, b in enumerate(ant.bodies) if "foot" in b.name]
     ant.to_json(os.path.join(out, "ant.json"))
     hum = M.load_mjcf(os.path.join(REF, "assets/mjcf/nv_humanoid.xml"), "humanoid", self_collision=True)
     hum.sensors = [hum.body_index("right_foot"), hum.body_index("left_foot")]
+    M.apply_asset_options(hum, "humanoid")
     hum.to_json(os.path.join(out, "humanoid.json"))
     cp = M.load_urdf(os.path.join(REF, "assets/urdf/cartpole.urdf"), "cartpole", fix_base=True)
+    M.apply_asset_options(cp, "cartpole")
     cp.to_json(os.path.join(out, "cartpole.json"))
     sh = shadow_hand()
+    M.apply_asset_options(sh, "shadow_hand")
     sh.to_json(os.path.join(out, "shadow_hand.json"))
     objs = hand_objects(sh)
     with open(os.path.join(out, "hand_objects.json"), "w") as f:
