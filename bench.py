@@ -127,6 +127,18 @@ def baseline_config0(dev, steps=1000, n=256):
     torch.cuda.synchronize()
     gpu_s = time.perf_counter() - t0
     env.close()
+    # the configuration as BASELINE.json names it: pipeline=cpu, sim_device=cpu, through make() -- the HIP step
+    # underneath with host-side views of every task tensor (migym/host_pipeline.py), host actions in, host
+    # outputs (rl_device cpu) out, the mirrors' transfers included
+    cenv = migym.make(seed=0, task="Cartpole", num_envs=n, sim_device="cpu", rl_device="cpu", headless=True)
+    for i in range(10):
+        cenv.step(host[i % 8])
+    t0 = time.perf_counter()
+    for i in range(steps):
+        cenv.step(host[i % 8])
+    cpu_pipe_s = time.perf_counter() - t0
+    assert cenv.device == "cpu" and cenv.obs_buf.device.type == "cpu"
+    cenv.close()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
     from migym import configs, model as M, taskdefs
@@ -149,6 +161,9 @@ def baseline_config0(dev, steps=1000, n=256):
     return {"workload": f"Cartpole {n} envs x {steps} random-action steps (BASELINE.json configs[0])",
             "gpu": {"seconds": gpu_s, "env_steps_per_s": n * steps / gpu_s, "device": dev,
                     "note": "fused HIP step, host action copy per step included"},
+            "cpu_pipeline": {"seconds": cpu_pipe_s, "env_steps_per_s": n * steps / cpu_pipe_s,
+                             "note": "make(sim_device='cpu', rl_device='cpu'): env.device 'cpu', host tensors, the "
+                                     "HIP step on the GPU underneath (host_pipeline.py), mirror transfers included"},
             "cpu_port": {f"{nt}_cores": {"seconds": s, "env_steps_per_s": n * steps / s} for nt, s in cpu.items()},
             "cpu_kind": "port (oracle fp32 restatement; the reference's PhysX CPU pipeline is not runnable here)"}
 
@@ -163,7 +178,7 @@ def pmc_traffic(task, n, kern_ms, object_type="block"):
     None when no pass was recorded for this workload."""
     path = None
     tag = task if (task != "ShadowHand" or object_type == "block") else f"{task}-{object_type}"   # per kernel instance
-    for rnd in ("r03", "r02", "r01"):   # the newest round's passes of this workload
+    for rnd in ("r04", "r03", "r02", "r01"):   # the newest round's passes of this workload
         cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_{n}.json")
         if os.path.exists(cand):
             path = cand

@@ -17,6 +17,21 @@ struct mg_sim {
   int32_t device;
   mg_state_views views;
   bool bound;
+  // work ordering of the fused step (MIGYM_ORDER_EVERY = K > 0, read at mg_sim_create): every K-th mg_env_step
+  // first sorts the envs by their last step's constraint-row count, descending (k_order), and the step kernels
+  // take their envs in that order -- teams of similar cost share a wave (the wave runs its slowest team's rows)
+  // and the heavy envs start first.  Envs are independent, so every result is the same bit for bit.
+  int order_every;
+  long long order_steps;
+  bool order_valid;
+  int* d_order;        // (n / A) env slots -> env
+  unsigned char* d_cost; // (n) the last step's row count per actor (saturated at 255)
+};
+
+// the step kernels' ordering arguments (nullptr order: slot = env)
+struct MgOrder {
+  const int* order;
+  unsigned char* cost;
 };
 
 namespace mgi {

@@ -567,18 +567,30 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   // the LDS model tile of the instance that will run this model, prebuilt once on the host; a model no
   // instance fits is still created (its launches report MG_ECAPACITY)
   s->d_tile = nullptr;
+  // work ordering (MIGYM_ORDER_EVERY = K: every K-th env step sorts the envs by their last row count, k_order)
+  s->order_every = 0;
+  s->order_steps = 0;
+  s->order_valid = false;
+  s->d_order = nullptr;
+  s->d_cost = nullptr;
+  if (const char* e = getenv("MIGYM_ORDER_EVERY")) s->order_every = atoi(e);
+  if (s->order_every > 0) {
+    const int A = params->agents > 1 ? params->agents : 1;
+    if (hipMalloc(&s->d_order, sizeof(int) * (size_t)((num_envs + A - 1) / A)) != hipSuccess ||
+        hipMalloc(&s->d_cost, (size_t)num_envs) != hipSuccess || hipMemset(s->d_cost, 0, (size_t)num_envs) != hipSuccess) {
+      mg_sim_destroy(s);
+      return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(work order) failed");
+    }
+  }
   // the step kernels' work-queue counters: zero here, and zeroed again by the last wave of every launch
   if (hipMalloc(&s->d_wq, 2 * sizeof(unsigned)) != hipSuccess || hipMemset(s->d_wq, 0, 2 * sizeof(unsigned)) != hipSuccess) {
-    (void)hipFree(s->d_model);
-    delete s;
+    mg_sim_destroy(s);
     return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(work queue) failed");
   }
   if (mgi::team_size(s->host_model, s->params.max_contacts) > 0) {
     const int rc = mgi::dispatch<mgi::BuildTile>(s->host_model, s->params.max_contacts, s);
     if (rc) {
-      (void)hipFree(s->d_model);
-      (void)hipFree(s->d_wq);
-      delete s;
+      mg_sim_destroy(s);
       return rc;
     }
   }
@@ -661,9 +673,11 @@ int mg_dr_noise(const mg_dr_noise_args* a, void* stream) {
 
 int mg_sim_destroy(mg_sim* sim) {
   if (!sim) return MG_OK;
-  (void)hipFree(sim->d_model);
+  if (sim->d_model) (void)hipFree(sim->d_model);
   if (sim->d_tile) (void)hipFree(sim->d_tile);
-  (void)hipFree(sim->d_wq);
+  if (sim->d_wq) (void)hipFree(sim->d_wq);
+  if (sim->d_order) (void)hipFree(sim->d_order);
+  if (sim->d_cost) (void)hipFree(sim->d_cost);
   delete sim;
   return MG_OK;
 }
@@ -792,6 +806,33 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
   return check_launch("mg_post_physics");
 }
 
+// Work ordering (sim->order_every): a counting sort of the envs by their last step's row count, descending
+// (the largest first), one workgroup.  An env of A agents takes its agents' largest count.  Ties land in
+// atomic order: which env a team runs never changes its results, only which envs share a wave.
+__global__ __launch_bounds__(1024) void k_order(const unsigned char* __restrict__ cost, int* __restrict__ order, int nenv,
+                                                int A) {
+  __shared__ int cnt[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;
+  __syncthreads();
+  auto key = [&](int e) {
+    int k = 0;
+    for (int j = 0; j < A; j++) k = max(k, (int)cost[(size_t)e * A + j]);
+    return 255 - k;  // descending
+  };
+  for (int e = threadIdx.x; e < nenv; e += blockDim.x) atomicAdd(&cnt[key(e)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int i = 0; i < 256; i++) {
+      const int c = cnt[i];
+      cnt[i] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nenv; e += blockDim.x) order[atomicAdd(&cnt[key(e)], 1)] = e;
+}
+
 static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
                     void* stream) {
   if (!sim || !sim->bound || !tp || !tb || !tb->actions || !tb->obs || !tb->rew || !tb->reset || !tb->progress ||
@@ -823,6 +864,14 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   }
   if (tp->num_actions > 64 || tp->num_obs > 256 || tp->num_states > 256)
     return fail(MG_EINVAL, "mg_env_step: num_actions > 64, num_obs > 256 or num_states > 256");
+  if (sim->order_every > 0 && !rp) {
+    if (sim->order_steps > 0 && sim->order_steps % sim->order_every == 0) {
+      const int A = tp->num_agents > 1 ? tp->num_agents : 1;
+      hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, (hipStream_t)stream, sim->d_cost, sim->d_order, sim->n / A, A);
+      sim->order_valid = true;
+    }
+    sim->order_steps++;
+  }
   int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
                                           (const mg_sim*)sim, tp, tb, rp);
   if (rc) return rc;

@@ -161,17 +161,28 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
 // are latency-bound; occupancy is the lever — DESIGN.md §3)
 // RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
 // post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
+// the actor a team slot works on: the slot itself, or under a work ordering (MgOrder, sim->order_every) the
+// slot's env in k_order's permutation (envs of A agents stay whole and aligned: the AND filter and the "others"
+// block exchange within the env's A consecutive teams of one wave)
+__device__ __forceinline__ int ordered_actor(const MgOrder& ord, int slot, int n, int A) {
+  if (slot >= n) return n - 1;
+  if (!ord.order) return slot;
+  const int a1 = A > 1 ? A : 1;
+  return ord.order[slot / a1] * a1 + slot % a1;
+}
+
 // one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
 __device__ __forceinline__ void env_step_item(
     const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
-    const mg_task_buffers& tb, int n, const mg_replay& rp, int item) {
+    const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
   const int team = threadIdx.x / T;
   const int wt = (threadIdx.x & 63) / T;  // team index within the wave (ballot / shuffle positions)
-  const int a = item * SH::E1 + wt;
-  const bool valid = a < n;
+  const int slot = item * SH::E1 + wt;
+  const bool valid = slot < n;
+  const int a = ordered_actor(ord, slot, n, tp.num_agents);
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
   mg::TeamLDS<T, MN, MC>& L = lds[team].v;
@@ -353,6 +364,7 @@ __device__ __forceinline__ void env_step_item(
     if (v.dof_force)
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
+  if (valid && ord.cost && t.tl == 0) ord.cost[a] = (unsigned char)(L.nrows < 255 ? L.nrows : 255);
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
 }
@@ -360,7 +372,7 @@ __device__ __forceinline__ void env_step_item(
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
 __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
-    mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq) {
+    mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
   constexpr int E = SH::E, W = SH::W;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
@@ -370,14 +382,14 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {
     // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
-    if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
+    if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
   } else {
     // multi-wave blocks: the work queue (wq_next), the grid being the resident capacity
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
       const int z = opaque_zero();
       env_step_item<T, MN, MC, MG, MP, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
-                                               (&rp)[z], item);
+                                               (&rp)[z], item, (&ord)[z]);
     }
     wq_done(wq, gwv);
   }
@@ -400,11 +412,12 @@ template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
 __device__ __forceinline__ void hand_step_item(
     const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
-    const mg_task_buffers& tb, int n, const mg_replay& rp, int item) {
+    const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
   const int team = threadIdx.x / T;
-  const int e = item * SH::E1 + (int)(threadIdx.x & 63) / T;
-  const bool valid = e < n;
+  const int slot = item * SH::E1 + (int)(threadIdx.x & 63) / T;
+  const bool valid = slot < n;
+  const int e = ordered_actor(ord, slot, n, 1);
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
@@ -635,6 +648,7 @@ __device__ __forceinline__ void hand_step_item(
       }
     }
   }
+  if (valid && ord.cost && t.tl == 0) ord.cost[e] = (unsigned char)(L.nrows < 255 ? L.nrows : 255);
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
 }
@@ -642,7 +656,7 @@ __device__ __forceinline__ void hand_step_item(
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
 __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
-    mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq) {
+    mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
   constexpr int E = SH::E, W = SH::W;
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
@@ -651,13 +665,13 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {  // as k_env_step
-    if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x);
+    if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
   } else {
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
       const int z = opaque_zero();
       hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z],
-                                                    (&tb)[z], n, (&rp)[z], item);
+                                                    (&tb)[z], n, (&rp)[z], item, (&ord)[z]);
     }
     wq_done(wq, gwv);
   }
@@ -672,7 +686,7 @@ static void launch(K kern, hipStream_t s, int n, A... args) {
 // launch of a step kernel: multi-wave blocks get min(blocks of the whole batch, resident blocks) blocks (the
 // work queue; occupancy query cached per kernel and device), one-wave blocks one block per item
 template <class SH, class K, class... A>
-static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
+static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A... args) {
   struct Entry { const void* k; int dev, blocks; };
   static Entry cache[32];  // (kernel, device) -> resident blocks
   const void* kp = reinterpret_cast<const void*>(kern);
@@ -691,12 +705,13 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, A... args) {
   }
   const int items = (sim->n + SH::E1 - 1) / SH::E1;
   const int need = (items + SH::W - 1) / SH::W;
+  const MgOrder ord{(ordered && sim->order_valid) ? sim->d_order : nullptr, ordered ? sim->d_cost : nullptr};
   if (SH::W == 1) {  // the kernels' one-wave-block path: the static grid, one block per item
-    hipLaunchKernelGGL(kern, dim3(need), dim3(SH::kThreads), 0, s, args..., sim->d_wq);
+    hipLaunchKernelGGL(kern, dim3(need), dim3(SH::kThreads), 0, s, args..., sim->d_wq, ord);
     return MG_OK;
   }
   const int blocks = need < resident ? need : resident;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), 0, s, args..., sim->d_wq);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), 0, s, args..., sim->d_wq, ord);
   return MG_OK;
 }
 
@@ -754,23 +769,23 @@ int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, co
     mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
     mg::h_fill_maps(&tpm);
     if (rp)
-      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>, s, sim,
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>, s, sim, false,
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>, s, sim,
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>, s, sim, true,
                                                    sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else
-      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>, s, sim,
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>, s, sim, true,
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
   } else {
     if (rp)
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim, false, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim, true, sim->d_model,
                                                  ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim, true, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
   }
   return MG_OK;
