@@ -35,6 +35,7 @@ constexpr float HULL_MARGIN = 1e-3f;                      // rounding of the cub
 constexpr float HULL_FEAT_EPS = 1e-6f;                    // a witness lies on a plane within this (m)
 constexpr float HULL_SIN_PARALLEL = 0.0871557427f;        // sin 5 deg
 constexpr float HULL_SIN_ON_FACE = 0.0348994967f;         // sin 2 deg
+constexpr float HULL_COS_COPLANAR = 0.99996192306f;       // cos 0.5 deg: planes this close to parallel are one face
 constexpr float HULL_CLIP_EPS = 1e-9f;                    // slack of the face clipping (m)
 constexpr float HULL_MPR_TOL = 1e-7f, HULL_MPR_EPS = 1e-12f;
 
@@ -408,8 +409,11 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
   // no contact can be made at or beyond the offset: a face-clip gap is at least the distance, and the cube's
   // sharp edge is at most (sqrt2 - 1) of its rounding nearer than the rounded core
   if (!(d - (B.kind == 1 ? 0.41422f * rB : 0.0f) < off)) return 0;
-  // the hull's features at pa: the planes through it (the first two in index order), one ballot per T planes
+  // the hull's features at pa: the planes through it (the first two in index order), one ballot per T planes; a plane
+  // within 0.5 deg of one already kept is the same face (qhull's triangulation of the curved forearm mesh: a
+  // witness on such a seam lies on two planes without being on an edge; oracle hull_core_contacts)
   int kA = 0, fa0 = 0, fa1 = 0;
+  float fd0 = 0.0f, fd1 = 0.0f;
   const unsigned long long tm = T >= 64 ? ~0ull : ((1ull << T) - 1ull);
   for (int k = 0; k * T < np; k++) {  // one ballot per T planes, in plane order
     const int f = k * T + tl;
@@ -422,8 +426,18 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
     while (bits) {
       const int i = k * T + __builtin_ctzll(bits);
       bits &= bits - 1;
-      if (kA == 0) fa0 = i;
-      else if (kA == 1) fa1 = i;
+      const V3 ni = ld3(pl[i]);
+      const float di = fabsf(dot(ni, pa) - pl[i][3]);
+      if (kA >= 1 && dot(ni, ld3(pl[fa0])) > HULL_COS_COPLANAR) {  // the same face: keep the plane pa is nearer to
+        if (di < fd0) { fa0 = i; fd0 = di; }
+        continue;
+      }
+      if (kA >= 2 && dot(ni, ld3(pl[fa1])) > HULL_COS_COPLANAR) {
+        if (di < fd1) { fa1 = i; fd1 = di; }
+        continue;
+      }
+      if (kA == 0) { fa0 = i; fd0 = di; }
+      else if (kA == 1) { fa1 = i; fd1 = di; }
       kA++;
     }
   }

@@ -61,6 +61,23 @@ static __thread double orc_pair_offset = 0.0;
 /* orc_step_flips: seg_box_sat reports a tie of its two least push-out faces within orc_tie_delta */
 static __thread double orc_tie_delta = -1.0;
 static __thread int orc_tie_hit = 0;
+/* orc_step_flips: a narrowphase decision within its tolerance band of the threshold (bit 16), and the contact
+ * being pushed has an ill-conditioned normal (bit 32: the direction of a core distance below NORMAL_ILL that
+ * the geometry does not pin -- an end point or a box edge / corner at the closest point) */
+static __thread int orc_amb_hit = 0;
+static __thread int orc_ill_next = 0;
+static __thread int orc_pb_ill = 0;   /* the last point_box: outside, two or more axes clamped, nearer than NORMAL_ILL */
+static __thread int orc_cvx_ill = 0;  /* the last cvx_contact: an MPR depth below NORMAL_ILL */
+static __thread int orc_hull_ill = 0; /* the last hull_core_contacts: a GJK distance below NORMAL_ILL */
+#define NORMAL_ILL 5e-4
+/* orc_step_flips bit 64: the angular-velocity cap clipped a hinge rate to an interval end whose fp32 value is
+ * ill-conditioned: disc = b^2 - |w_p|^2 + W^2 carries the rounding of W^2-sized terms (~2 eps32 W^2), so the end
+ * point -b +- sqrt(disc) is off by ~eps32 W^2 / sq; flagged when that exceeds CAP_ILL_TOL (rad/s) */
+static __thread int orc_cap_hit = 0;
+#define CAP_ILL_TOL 1e-3
+static void amb_band(double x, double thr, double lo, double hi) {
+  if (orc_tie_delta >= 0.0 && x > thr * lo && x < thr * hi) orc_amb_hit = 1;
+}
 
 typedef real v3[3];
 
@@ -180,6 +197,7 @@ typedef struct {
 typedef struct {
   int nodeA, nodeB, geomA, geomB;
   real p[3], n[3], d;
+  int ill;   /* ill-conditioned normal (orc_step_flips bit 32) */
 } contact;
 
 static int nv_of(const mg_model* m) { return (m->fixed_base ? 0 : 6) + m->num_dofs; }
@@ -457,6 +475,8 @@ static int push_contact(contact* out, int n, int cap, int nodeA, int gA, int nod
   c->nodeA = nodeA; c->geomA = gA; c->nodeB = nodeB; c->geomB = gB;
   for (int a = 0; a < 3; a++) { c->p[a] = p[a]; c->n[a] = nrm[a]; }
   c->d = d;
+  c->ill = orc_ill_next;
+  orc_ill_next = 0;
   return n + 1;
 }
 
@@ -521,13 +541,15 @@ static int geom_segment(const mg_model* m, const kin* k, int g, real* a, real* b
 static real point_box(const real* pl, const real* hb, real* nb, real* cb) {
   real q[3];
   int out = 0;
+  orc_pb_ill = 0;
   for (int a = 0; a < 3; a++) {
     q[a] = pl[a] < -hb[a] ? -hb[a] : (pl[a] > hb[a] ? hb[a] : pl[a]);
-    if (q[a] != pl[a]) out = 1;
+    if (q[a] != pl[a]) out++;
   }
   if (out) {
     real d[3] = {pl[0] - q[0], pl[1] - q[1], pl[2] - q[2]};
     real l = sqrt(dot3(d, d));
+    orc_pb_ill = out >= 2 && l < NORMAL_ILL;
     for (int a = 0; a < 3; a++) { nb[a] = d[a] / l; cb[a] = q[a]; }
     return l;
   }
@@ -790,6 +812,7 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * ((P[a] - r * nb[a]) + cb[a]);
       from_obj_pt(k, pm, pw);
       from_obj_dir(k, nb, nw);
+      orc_ill_next = !inside && orc_pb_ill;
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
     }
     return n;
@@ -809,6 +832,7 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
         for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
         from_obj_pt(k, pm, pw);
         from_obj_dir(k, nb, nw);
+        orc_ill_next = orc_pb_ill;
         n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
       }
     }
@@ -848,6 +872,7 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
       for (int a = 0; a < 3; a++) pm[a] = 0.5 * (pl[a] + cb[a]);
       from_obj_pt(k, pm, pw);
       from_obj_dir(k, nb, nw);
+      orc_ill_next = orc_pb_ill;
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
     }
   }
@@ -865,6 +890,7 @@ static int geom_object(const mg_model* m, const kin* k, int g, real off, contact
       for (int a = 0; a < 3; a++) pw[a] += c[a];
       matvec3(R, nb, nw);
       for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+      orc_ill_next = orc_pb_ill;
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
     }
   }
@@ -1402,6 +1428,7 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
     rA += mg;
   }
   real sp[3];
+  orc_cvx_ill = 0;
   const int g = cvx_core_point(A, e, sp) ? 0 : cvx_gjk(A, e, rA + cut, pa, pb, &dist); /* overlap: MPR */
   if (g == 2) { /* farther than rA + cut: only the (lower-bound) distance is meaningful */
     *d = dist - rA;
@@ -1427,6 +1454,7 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
         pt[a] = pa[a] - 0.5 * x[a] - nrm[a] * rA * 0.5;
       }
       *d = -l - rA;
+      orc_cvx_ill = l < NORMAL_ILL;
       if (cvx_finite(pt, nrm, *d)) return;
     }
   }
@@ -1471,6 +1499,7 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
 #define HULL_SIN_PARALLEL 0.0871557427476582  /* sin 5 deg: edges closer to parallel are no edge-edge contact */
 #define HULL_SIN_ON_FACE 0.0348994967025010   /* sin 2 deg: an edge closer to a face's plane lies on the face */
 #define HULL_CLIP_EPS 1e-9     /* slack of the face clipping (m) */
+#define HULL_COS_COPLANAR 0.9999619230641713  /* cos 0.5 deg: planes this close to parallel are one face */
 static void hull_support(const real (*hv)[3], int nv, const cvx_shape* B, const real* d, real* w) {
   real best = -1e300;
   int bi = 0;
@@ -1654,9 +1683,11 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   else v3cp(cb, B->c);
   v3sub(ctr, cb, v0);
   const int gk = hull_gjk(hv, nv, v0, B, rB + off, pa, pb, &dist);
+  orc_hull_ill = 0;
   if (gk == 2) return 0;
   if (gk == 1) {
     if (!(dist > 1e-9)) return 0;
+    orc_hull_ill = dist < NORMAL_ILL;
     for (int a = 0; a < 3; a++) {
       nrm[a] = (pa[a] - pb[a]) / dist;
       pt[a] = 0.5 * (pa[a] + pb[a] + nrm[a] * rB);
@@ -1677,13 +1708,29 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   /* no contact can be made at or beyond the offset: a face-clip gap is at least the distance, and the cube's
    * sharp edge is at most (sqrt2 - 1) of its rounding nearer than the rounded core */
   if (!(d - (B->kind == 1 ? 0.41422 * rB : 0.0) < off)) return 0;
-  /* the hull's features at pa: the planes through it (the first two kept) */
+  /* the hull's features at pa: the planes through it (the first two kept).  A plane within 0.5 deg of one already
+   * kept is the same face (the one pa lies nearer to is kept): qhull triangulates the curved forearm mesh into
+   * facets a fraction of a degree apart, and a witness on such a seam lies on two planes without being on an edge */
   int kA = 0, fa[2] = {0, 0};
-  for (int i = 0; i < np; i++)
-    if (fabs(pl[i][0] * pa[0] + pl[i][1] * pa[1] + pl[i][2] * pa[2] - pl[i][3]) < HULL_FEAT_EPS) {
-      if (kA < 2) fa[kA] = i;
+  real fd[2] = {0, 0};
+  for (int i = 0; i < np; i++) {
+    const real di = fabs(pl[i][0] * pa[0] + pl[i][1] * pa[1] + pl[i][2] * pa[2] - pl[i][3]);
+    amb_band(di, HULL_FEAT_EPS, 0.5, 2.0);
+    if (di < HULL_FEAT_EPS) {
+      int same = -1;
+      for (int j = 0; j < (kA < 2 ? kA : 2); j++) {
+        const real c = pl[i][0] * pl[fa[j]][0] + pl[i][1] * pl[fa[j]][1] + pl[i][2] * pl[fa[j]][2];
+        amb_band(1.0 - c, 1.0 - HULL_COS_COPLANAR, 0.9, 1.1);
+        if (same < 0 && c > HULL_COS_COPLANAR) same = j;
+      }
+      if (same >= 0) {
+        if (di < fd[same]) { fa[same] = i; fd[same] = di; }
+        continue;
+      }
+      if (kA < 2) { fa[kA] = i; fd[kA] = di; }
       kA++;
     }
+  }
   if (kA == 0 || kA >= 3) return 0; /* a hull vertex (or a witness off the surface) */
   /* the core's feature at pb: the edge direction ub (0 for a box face / vertex or a segment end) */
   real ub[3] = {0, 0, 0}, u[3];
@@ -1694,6 +1741,8 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
     real dp[3];
     v3sub(pb, B->p0, dp);
     const real t = uu > 0 ? dot3(dp, u) / uu : 0.0;
+    amb_band(t * sqrt(uu), HULL_FEAT_EPS, 0.5, 2.0);
+    amb_band((1.0 - t) * sqrt(uu), HULL_FEAT_EPS, 0.5, 2.0);
     if (!(t * sqrt(uu) > HULL_FEAT_EPS && (1.0 - t) * sqrt(uu) > HULL_FEAT_EPS)) return 0; /* an end */
     v3cp(ub, u);
     kB = 2;
@@ -1704,6 +1753,7 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
     kB = 0;
     int free_ax = -1;
     for (int k = 0; k < 3; k++) {
+      amb_band(B->h[k] - fabs(l[k]), HULL_FEAT_EPS, 0.5, 2.0);
       if (fabs(l[k]) > B->h[k] - HULL_FEAT_EPS) kB++;
       else free_ax = k;
     }
@@ -1717,6 +1767,7 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   for (int i = 0; i < kA; i++) { /* the parallel face best aligned with the contact normal */
     const real nn[3] = {pl[fa[i]][0], pl[fa[i]][1], pl[fa[i]][2]};
     const real al = -dot3(nn, nrm);
+    amb_band(fabs(dot3(nn, ub)), HULL_SIN_ON_FACE * lub, 0.98, 1.02);
     if (fabs(dot3(nn, ub)) < HULL_SIN_ON_FACE * lub && al > falign) { face = fa[i]; falign = al; }
   }
   if (face >= 0 || kA == 1) {
@@ -1728,10 +1779,12 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   real ua[3], cx[3];
   cross3(n1, n2, ua);
   cross3(ua, ub, cx);
+  amb_band(sqrt(dot3(cx, cx)), HULL_SIN_PARALLEL * sqrt(dot3(ua, ua) * dot3(ub, ub)), 0.98, 1.02);
   if (!(dot3(cx, cx) > HULL_SIN_PARALLEL * HULL_SIN_PARALLEL * dot3(ua, ua) * dot3(ub, ub))) return 0;
   if (B->kind == 1) /* the hull edge lying on a face of the box: the hull edge's ends are vertex candidates */
     for (int k = 0; k < 3; k++) {
       const real col[3] = {B->R[0][k], B->R[1][k], B->R[2][k]};
+      amb_band(fabs(dot3(col, ua)), HULL_SIN_ON_FACE * sqrt(dot3(ua, ua)), 0.98, 1.02);
       if (fabs(dot3(col, ub)) < 0.5 && fabs(dot3(col, ua)) < HULL_SIN_ON_FACE * sqrt(dot3(ua, ua))) {
         /* col is a face normal of the box adjacent to its witness edge */
         real dl[3], l[3];
@@ -1813,6 +1866,7 @@ static int hull_object_exact(const mg_model* m, const kin* k, int g, const real*
     matvec3(R, res + 7 * i, pw);
     for (int a = 0; a < 3; a++) pw[a] += c[a];
     matvec3(R, res + 7 * i + 3, nw);
+    orc_ill_next = orc_hull_ill;
     n = push_contact(out, n, cap, m->geom_node[g], g, OBJ_NODE, -2, pw, nw, res[7 * i + 6]);
   }
   return n;
@@ -1894,6 +1948,7 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
           nw[a] = dv[a] / dist;
           pw[a] = 0.5 * (w[a] + (q[a] + nw[a] * ro));
         }
+        orc_ill_next = dist < NORMAL_ILL;   /* a hull vertex against the segment: a point */
         n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
       }
     }
@@ -1943,6 +1998,7 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
     if (d < off) {
       from_obj_pt(k, pl, pw);
       from_obj_dir(k, nl, nw);
+      orc_ill_next = orc_cvx_ill;
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
     }
     return n;
@@ -1967,6 +2023,7 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
         nw[a] = dv[a] / dist;
         pw[a] = 0.5 * ((pa[a] - nw[a] * r) + (pb[a] + nw[a] * ro));
       }
+      orc_ill_next = dist < NORMAL_ILL;
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
     }
     return n;
@@ -1995,6 +2052,7 @@ static int geom_object_convex(const mg_model* m, const kin* k, int g, real off, 
       for (int a = 0; a < 3; a++) pw[a] += c[a];
       matvec3(R, nb, nw);
       for (int a = 0; a < 3; a++) nw[a] = -nw[a];
+      orc_ill_next = !inside && orc_pb_ill;
       n = push_contact(out, n, cap, nd, g, OBJ_NODE, -2, pw, nw, d);
     }
   }
@@ -2086,6 +2144,7 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
         matvec3(R, pm, pw);
         matvec3(R, nb, nw);
         for (int a = 0; a < 3; a++) { pw[a] += c[a]; nw[a] = sa ? nw[a] : -nw[a]; } /* normal from B to A */
+        orc_ill_next = !inside && orc_pb_ill;
         n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pw, nw, d);
       }
       continue;
@@ -2103,6 +2162,7 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
     if (d < poff && dist > 1e-9) {
       real nrm[3] = {dv[0] / dist, dv[1] / dist, dv[2] / dist}, pt[3];
       for (int a = 0; a < 3; a++) pt[a] = 0.5 * (pa[a] - ra * nrm[a] + pb[a] + rb * nrm[a]);
+      orc_ill_next = dist < NORMAL_ILL;
       n = push_contact(out, n, cap, m->geom_node[ga], ga, m->geom_node[gb], gb, pt, nrm, d);
     }
   }
@@ -2186,6 +2246,7 @@ static void clamp_ang_vel(const mg_model* m, const kin* k, real* nu) {
         if (dot3(w, w) > W * W) {
           real b = dot3(ax, wp), disc = b * b - dot3(wp, wp) + W * W;
           real sq = sqrt(disc > 0.0 ? disc : 0.0), lo = -b - sq, hi = -b + sq;
+          if (1.1920929e-7 * W * W > CAP_ILL_TOL * sq) orc_cap_hit = 1;
           q = q < lo ? lo : (q > hi ? hi : q);
           nu[ci] = q;
           for (int a = 0; a < 3; a++) w[a] = wp[a] + ax[a] * q;
@@ -2604,6 +2665,27 @@ int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* ro
   return orc_simulate_views(m, p, n, &v, threads);
 }
 
+/* contacts of one actor with both geoms: (nodeA, geomA, nodeB, geomB, p(3), n(3), d) records of 11 reals (real is
+ * float in the fp32 build: diagnostics of fp32-vs-fp64 partings, tools/pair_diag.py) */
+int orc_contacts_full(const mg_model* m, const mg_sim_params* p, const float* root13, const float* dof2, real* out,
+                      int32_t cap) {
+  astate s;
+  kin k;
+  memset(&s, 0, sizeof(s));
+  load_state(m, root13, dof2, &s);
+  if (m->obj_type) load_object(&s, root13 + 13);
+  forward_kinematics(m, &s, &k);
+  contact con[MAXC];
+  int nc = collide(m, p, &k, con, cap < MAXC ? cap : MAXC);
+  for (int i = 0; i < nc; i++) {
+    real* o = out + 11 * i;
+    o[0] = con[i].nodeA; o[1] = con[i].geomA; o[2] = con[i].nodeB; o[3] = con[i].geomB;
+    for (int a = 0; a < 3; a++) { o[4 + a] = con[i].p[a]; o[7 + a] = con[i].n[a]; }
+    o[10] = con[i].d;
+  }
+  return nc;
+}
+
 #ifndef ORC_FP32 /* fp64 inspection hooks of the checker (KATs); not in the fp32 timing build */
 /* The discontinuities of the build's physics that env `e`'s gym.simulate (state views as orc_simulate_views)
  * passes near, substep by substep (tests/parity_stats.py): an fp32 and an fp64 step of the same state may part
@@ -2614,7 +2696,13 @@ int orc_simulate(const mg_model* m, const mg_sim_params* p, int32_t n, float* ro
  *      a row whose impulse stays 0 changes nothing, so its presence or absence is no discontinuity)
  *   2  a joint-limit row within delta of the margin that the solve uses (the same rule)
  *   4  a PD drive whose explicit force is within df (relative) of its effort limit (implicit <-> saturated)
- *   8  a segment core inside a box whose two least push-out faces are within delta (seg_box_sat's tie) */
+ *   8  a segment core inside a box whose two least push-out faces are within delta (seg_box_sat's tie)
+ *  16  a narrowphase decision near its threshold: a hull witness 0.5-2 um from a plane, a segment end or a box
+ *      face (HULL_FEAT_EPS 1 um decides the features), an edge within 2 % of the parallel / on-face angles
+ *  32  a contact in use whose normal is ill-conditioned: the direction of a core distance below NORMAL_ILL
+ *      (0.5 mm) that the geometry does not pin (an end point, a box edge or corner at the closest point; an
+ *      MPR or hull-GJK depth), so that a 1e-7 m difference of the state turns it by ~1e-4 rad
+ *  64  the angular-velocity cap clipped a hinge rate to an ill-conditioned interval end (clamp_ang_vel) */
 int orc_step_flips(const mg_model* m0, const mg_sim_params* p, const mg_state_views* v, int32_t e, double delta,
                    double df) {
   const mg_model* m = m0;
@@ -2662,16 +2750,21 @@ int orc_step_flips(const mg_model* m0, const mg_sim_params* p, const mg_state_vi
     orc_pair_offset = delta;
     orc_tie_delta = delta;
     orc_tie_hit = 0;
+    orc_amb_hit = 0;
+    orc_cap_hit = 0;
     substep(m, &pw, &sw, tau, so);
     orc_pair_offset = 0.0;
     orc_tie_delta = -1.0;
     if (orc_tie_hit) flags |= 8;
+    if (orc_amb_hit) flags |= 16;
+    if (orc_cap_hit) flags |= 64;
     const real eps = 1e-9;
     for (int c = 0; c < so->ncon; c++) {
       const contact* ct = &so->con[c];
       const int pair = m->pair_mjcf && ct->nodeB >= 0;
       const real thr = pair ? 0.0 : p->contact_offset;
       if (fabs(ct->d - thr) < delta && so->lmax[3 * c] > eps) flags |= 1;
+      if (ct->ill && so->lmax[3 * c] > eps) flags |= 32;
     }
     for (int r = 3 * so->ncon; r < so->nrows; r++) {
       const int i = so->row_ref[r];

@@ -133,7 +133,9 @@ SENS_CAP = 0.01      # and at most this fraction by the oracle-sensitivity fallb
 def step_flags(mnp, sp, host, delta=STEP_DELTA, df=STEP_DF):
     """per env: orc_step_flips of the physics input `host` holds (a HostEnv with act_eff / a HandHostEnv after
     pre_physics, optionally with env_props): bit 1 contact threshold in use, 2 limit threshold in use, 4 drive
-    near saturation, 8 seg_box_sat tie"""
+    near saturation, 8 seg_box_sat tie, 16 a narrowphase decision within its ambiguity band, 32 an
+    ill-conditioned contact normal (core distance / MPR depth below 0.5 mm), 64 the angular-velocity cap clipped a
+    hinge rate to an ill-conditioned interval end"""
     return O.step_flips(mnp, sp, host, delta, df)
 
 
@@ -169,7 +171,7 @@ def assert_steps_explained(test, bad, flags, sens=None, reach_cap=REACH_CAP, sen
     total = bad.size
     rec = {"env_steps": int(total), "disagreeing": int(bad.sum()), "flagged_reach": float(flagged.mean()),
            "explained_by_flags": int((bad & flagged).sum()), "explained_by_sensitivity": nsens,
-           "bits": {str(b): float(((np.asarray(flags) & b) != 0).mean()) for b in (1, 2, 4, 8)}}
+           "bits": {str(b): float(((np.asarray(flags) & b) != 0).mean()) for b in (1, 2, 4, 8, 16, 32, 64)}}
     _REPORT.setdefault(test, {})["exemptions"] = rec
     unexplained = np.argwhere(bad & ~why)
     assert unexplained.size == 0, (f"{test}: {len(unexplained)} of {int(bad.sum())} disagreeing env-steps are not at a "

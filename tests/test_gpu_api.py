@@ -230,12 +230,13 @@ def test_cpu_pipeline_host_views(task, n, how):
     assert c.device == "cpu" and c.unwrapped.device.startswith("cuda")
     for name in ("root_states", "dof_state", "obs_buf", "rew_buf", "reset_buf", "progress_buf"):
         assert getattr(c, name).device.type == "cpu", name
-    assert c.dof_pos.untyped_storage().data_ptr() == c.dof_state.untyped_storage().data_ptr()
+    pos = "shadow_hand_dof_pos" if task == "ShadowHand" else "dof_pos"
+    assert getattr(c, pos).untyped_storage().data_ptr() == c.dof_state.untyped_storage().data_ptr()
     for k in range(3):
         og, rg, dg, _ = g.step(actions(g, k))
         oc, rc, dc, _ = c.step(actions(g, k).cpu())
         assert torch.equal(oc["obs"], og["obs"]) and torch.equal(rc, rg) and torch.equal(dc, dg)
-        assert torch.equal(c.root_states, g.root_states.cpu()) and torch.equal(c.dof_pos, g.dof_pos.cpu())
+        assert torch.equal(c.root_states, g.root_states.cpu()) and torch.equal(getattr(c, pos), getattr(g, pos).cpu())
         assert torch.equal(c.progress_buf, g.progress_buf.cpu())
     # a host-side edit: force resets of the first envs on both
     c.reset_buf[:5] = 1

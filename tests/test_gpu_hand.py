@@ -170,7 +170,7 @@ def hand_states(spec, tp, n, rng, dz=0.07, pen=False):
     return h
 
 
-def _physics_vs_oracle(lib, spec, sp, h, rng, n):
+def _physics_vs_oracle(lib, spec, sp, h, rng, n, reach_cap=PS.REACH_CAP):
     """one simulate of the states h on the GPU and in the oracle; asserts determinism and per-env agreement"""
     # applied object forces (LOCAL_SPACE) on half of the envs
     h.rb_forces[: n // 2, len(spec.bodies)] = rng.normal(0, 0.3, (n // 2, 3))
@@ -211,7 +211,7 @@ def _physics_vs_oracle(lib, spec, sp, h, rng, n):
         PS.record(test, name, a, b, envs_outside=int(eb.sum()), atol=atol, rtol=rtol)
         bad |= eb
     flags = PS.step_flags(mnp, sp, h0)   # h0: the targets and object forces this simulate used
-    PS.assert_steps_explained(test, bad[None], flags[None])
+    PS.assert_steps_explained(test, bad[None], flags[None], reach_cap=reach_cap)
     return mnp, h0
 
 
@@ -333,7 +333,9 @@ def test_hand_physics_hull_exact_matches_oracle(lib, kind):
             ob[i, 0:3] = c + R @ ctr
             ob[i, 3:7] = Rotation.from_matrix(R @ Rl).as_quat()
     ob[:, 7:13] = rng.normal(0, 0.05, (n, 6))
-    mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n)
+    # these placements sit on the hull's features by construction (an edge across an edge, a segment across a
+    # face next to its ridges), so the feature-decision band (bit 16) reaches more of them than of random states
+    mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n, reach_cap=0.10)
     node = spec.geoms[spec.hull["geom"]].node
     touching = 0
     for i in range(n):
