@@ -11,8 +11,8 @@
 #define MG_INSTANCES(X)                                                                                     \
   X(8, 4, 8, 4, 0, 0) X(16, 9, 16, 16, 0, 0) X(16, 16, 24, 24, 32, 0) X(32, 24, 32, 24, 160, 0)            \
   X(32, 32, 48, 48, 192, 0) X(64, 40, 48, 48, 192, 0) X(32, 25, 24, 24, 24, MG_GT_BOX)                      \
-  X(32, 25, 24, 24, 24, MG_GT_CAPSULE) X(32, 25, 24, 24, 24, MG_GT_ELLIPSOID) X(64, 25, 24, 24, 24, MG_GT_BOX)
-#define MG_NUM_INST 10
+  X(32, 25, 24, 24, 24, MG_GT_CAPSULE) X(32, 25, 24, 24, 24, MG_GT_ELLIPSOID)
+#define MG_NUM_INST 9
 
 namespace mgi {
 struct InstDesc {
@@ -47,18 +47,9 @@ inline int model_lanes(const mg_model& m) {
   const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs + (m.obj_type ? 6 : 0);
   return nv > m.num_sensors ? nv : m.num_sensors;
 }
-// the narrowest team the dispatcher may pick (MIGYM_MIN_TEAM, host environment, read once): an A/B knob for
-// wider teams on small shards (one env over more lanes); 0 = the smallest instance that fits
-inline int min_team() {
-  static const int v = [] {
-    const char* e = getenv("MIGYM_MIN_TEAM");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
 #define MG_FITS(T, MN, MC, MG, MP, OBJ)                                                              \
   (m.num_nodes <= MN && max_contacts <= MC && model_lanes(m) <= T && (m.fixed_base || T >= 6) &&   \
-   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ) && T >= min_team())
+   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ))
 
 // team size the dispatcher picks for a model (0: none fits)
 inline int team_size(const mg_model& m, int max_contacts) {

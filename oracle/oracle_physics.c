@@ -64,7 +64,8 @@ static __thread int orc_tie_hit = 0;
 /* orc_step_flips: a narrowphase decision within its tolerance band of the threshold (bit 16), and the contact
  * being pushed has an ill-conditioned normal (bit 32: the direction of a core distance below NORMAL_ILL that
  * the geometry does not pin -- an end point or a box edge / corner at the closest point) */
-static __thread int orc_amb_hit = 0;
+static __thread int orc_amb_hit = 0;  /* bit 16 for the whole step (an ambiguous decision that made no contact) */
+static __thread int orc_amb_pend = 0; /* an ambiguous decision in the current geom-object candidate set */
 static __thread int orc_ill_next = 0;
 static __thread int orc_pb_ill = 0;   /* the last point_box: outside, two or more axes clamped, nearer than NORMAL_ILL */
 static __thread int orc_cvx_ill = 0;  /* the last cvx_contact: an MPR depth below NORMAL_ILL */
@@ -75,9 +76,8 @@ static __thread int orc_hull_ill = 0; /* the last hull_core_contacts: a GJK dist
  * point -b +- sqrt(disc) is off by ~eps32 W^2 / sq; flagged when that exceeds CAP_ILL_TOL (rad/s) */
 static __thread int orc_cap_hit = 0;
 #define CAP_ILL_TOL 1e-3
-static void amb_band(double x, double thr, double lo, double hi) {
-  if (orc_tie_delta >= 0.0 && x > thr * lo && x < thr * hi) orc_amb_hit = 1;
-}
+/* the hull narrowphase's decision thresholds, scaled by orc_step_flips' variants (1 = the build's) */
+static __thread struct { double fe, ang, cop; int seam, face; } orc_hv = {1.0, 1.0, 1.0, 0, -1};
 
 typedef real v3[3];
 
@@ -198,6 +198,7 @@ typedef struct {
   int nodeA, nodeB, geomA, geomB;
   real p[3], n[3], d;
   int ill;   /* ill-conditioned normal (orc_step_flips bit 32) */
+  int amb;   /* made by a geom-object candidate set with a decision in its ambiguity band (bit 16) */
 } contact;
 
 static int nv_of(const mg_model* m) { return (m->fixed_base ? 0 : 6) + m->num_dofs; }
@@ -476,6 +477,7 @@ static int push_contact(contact* out, int n, int cap, int nodeA, int gA, int nod
   for (int a = 0; a < 3; a++) { c->p[a] = p[a]; c->n[a] = nrm[a]; }
   c->d = d;
   c->ill = orc_ill_next;
+  c->amb = 0;
   orc_ill_next = 0;
   return n + 1;
 }
@@ -1673,8 +1675,10 @@ static int hull_face_clip(const float (*pl)[4], int np, int f, const real* p0, c
 }
 /* the exact candidates in the hull's geom frame: core B (+ radius rB); up to 2 contacts (point, normal from the
  * object to the hull, gap) written to out[7 * i], their count returned */
-static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4], int np, const cvx_shape* B, real rB,
+static int hull_core_contacts_at(const real (*hv)[3], int nv, const float (*pl)[4], int np, const cvx_shape* B, real rB,
                               real off, real* out) {
+  const real FE = HULL_FEAT_EPS * orc_hv.fe, SOF = HULL_SIN_ON_FACE * orc_hv.ang, SPA = HULL_SIN_PARALLEL * orc_hv.ang;
+  const real COP = 1.0 - (1.0 - HULL_COS_COPLANAR) * orc_hv.cop;
   real ctr[3] = {0, 0, 0}, cb[3], v0[3], pa[3], pb[3], x[3], dist, nrm[3], pt[3], d;
   for (int v = 0; v < nv; v++)
     for (int a = 0; a < 3; a++) ctr[a] += hv[v][a];
@@ -1715,16 +1719,18 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   real fd[2] = {0, 0};
   for (int i = 0; i < np; i++) {
     const real di = fabs(pl[i][0] * pa[0] + pl[i][1] * pa[1] + pl[i][2] * pa[2] - pl[i][3]);
-    amb_band(di, HULL_FEAT_EPS, 0.5, 2.0);
-    if (di < HULL_FEAT_EPS) {
+    if (di < FE) {
       int same = -1;
       for (int j = 0; j < (kA < 2 ? kA : 2); j++) {
         const real c = pl[i][0] * pl[fa[j]][0] + pl[i][1] * pl[fa[j]][1] + pl[i][2] * pl[fa[j]][2];
-        amb_band(1.0 - c, 1.0 - HULL_COS_COPLANAR, 0.9, 1.1);
-        if (same < 0 && c > HULL_COS_COPLANAR) same = j;
+        if (same < 0 && c > COP) same = j;
       }
       if (same >= 0) {
-        if (di < fd[same]) { fa[same] = i; fd[same] = di; }
+        /* the nearer of the two is the face that clips the segment (orc_hv.seam 1 / 2: the later / the earlier
+         * plane whatever the distances -- a segment parallel to the seam's facets has its witness on the seam,
+         * where fp32 and fp64 GJK can land on either side) */
+        const int take = orc_hv.seam == 1 ? 1 : (orc_hv.seam == 2 ? 0 : di < fd[same]);
+        if (take) { fa[same] = i; fd[same] = di; }
         continue;
       }
       if (kA < 2) { fa[kA] = i; fd[kA] = di; }
@@ -1741,9 +1747,7 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
     real dp[3];
     v3sub(pb, B->p0, dp);
     const real t = uu > 0 ? dot3(dp, u) / uu : 0.0;
-    amb_band(t * sqrt(uu), HULL_FEAT_EPS, 0.5, 2.0);
-    amb_band((1.0 - t) * sqrt(uu), HULL_FEAT_EPS, 0.5, 2.0);
-    if (!(t * sqrt(uu) > HULL_FEAT_EPS && (1.0 - t) * sqrt(uu) > HULL_FEAT_EPS)) return 0; /* an end */
+    if (!(t * sqrt(uu) > FE && (1.0 - t) * sqrt(uu) > FE)) return 0; /* an end */
     v3cp(ub, u);
     kB = 2;
   } else {
@@ -1753,8 +1757,7 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
     kB = 0;
     int free_ax = -1;
     for (int k = 0; k < 3; k++) {
-      amb_band(B->h[k] - fabs(l[k]), HULL_FEAT_EPS, 0.5, 2.0);
-      if (fabs(l[k]) > B->h[k] - HULL_FEAT_EPS) kB++;
+      if (fabs(l[k]) > B->h[k] - FE) kB++;
       else free_ax = k;
     }
     if (kB != 2) return 0; /* a face of the box (an edge of the hull lying on it) or a corner */
@@ -1767,11 +1770,11 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   for (int i = 0; i < kA; i++) { /* the parallel face best aligned with the contact normal */
     const real nn[3] = {pl[fa[i]][0], pl[fa[i]][1], pl[fa[i]][2]};
     const real al = -dot3(nn, nrm);
-    amb_band(fabs(dot3(nn, ub)), HULL_SIN_ON_FACE * lub, 0.98, 1.02);
-    if (fabs(dot3(nn, ub)) < HULL_SIN_ON_FACE * lub && al > falign) { face = fa[i]; falign = al; }
+    if (fabs(dot3(nn, ub)) < SOF * lub && al > falign) { face = fa[i]; falign = al; }
   }
   if (face >= 0 || kA == 1) {
     if (B->kind != 0) return 0; /* a box edge on a hull face: its ends are vertex-face candidates */
+    orc_hv.face = face >= 0 ? face : fa[0];
     return hull_face_clip(pl, np, face >= 0 ? face : fa[0], B->p0, u, rB, off, out);
   }
   /* edge against edge: the hull edge's direction, the core edge not near parallel to it nor to the box's faces */
@@ -1779,18 +1782,16 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   real ua[3], cx[3];
   cross3(n1, n2, ua);
   cross3(ua, ub, cx);
-  amb_band(sqrt(dot3(cx, cx)), HULL_SIN_PARALLEL * sqrt(dot3(ua, ua) * dot3(ub, ub)), 0.98, 1.02);
-  if (!(dot3(cx, cx) > HULL_SIN_PARALLEL * HULL_SIN_PARALLEL * dot3(ua, ua) * dot3(ub, ub))) return 0;
+  if (!(dot3(cx, cx) > SPA * SPA * dot3(ua, ua) * dot3(ub, ub))) return 0;
   if (B->kind == 1) /* the hull edge lying on a face of the box: the hull edge's ends are vertex candidates */
     for (int k = 0; k < 3; k++) {
       const real col[3] = {B->R[0][k], B->R[1][k], B->R[2][k]};
-      amb_band(fabs(dot3(col, ua)), HULL_SIN_ON_FACE * sqrt(dot3(ua, ua)), 0.98, 1.02);
-      if (fabs(dot3(col, ub)) < 0.5 && fabs(dot3(col, ua)) < HULL_SIN_ON_FACE * sqrt(dot3(ua, ua))) {
+      if (fabs(dot3(col, ub)) < 0.5 && fabs(dot3(col, ua)) < SOF * sqrt(dot3(ua, ua))) {
         /* col is a face normal of the box adjacent to its witness edge */
         real dl[3], l[3];
         v3sub(pb, B->c, dl);
         mattvec3((real(*)[3])B->R, dl, l);
-        if (fabs(l[k]) > B->h[k] - HULL_FEAT_EPS) return 0;
+        if (fabs(l[k]) > B->h[k] - FE) return 0;
       }
     }
   if (B->kind == 1) {
@@ -1801,7 +1802,7 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
     mattvec3((real(*)[3])B->R, dl, l);
     v3cp(q, pb);
     for (int k = 0; k < 3; k++) {
-      if (!(fabs(l[k]) > B->h[k] - HULL_FEAT_EPS)) continue;
+      if (!(fabs(l[k]) > B->h[k] - FE)) continue;
       const real sg = l[k] < 0 ? -rB : rB;
       for (int a = 0; a < 3; a++) q[a] += sg * B->R[a][k];
     }
@@ -1824,6 +1825,45 @@ static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4],
   v3cp(out + 3, nrm);
   out[6] = d;
   return 1;
+}
+/* hull_core_contacts_at with the build's thresholds.  Under orc_step_flips it also runs with every decision
+ * threshold moved within its band -- HULL_FEAT_EPS x0.5 / x2, the parallel / on-face angles and the coplanar
+ * angle x0.98 / x1.02, either facet of a near-coplanar seam -- and marks the pair (orc_amb_pend, bit 16) when any
+ * of them changes the contacts: the decision is then one an fp32 witness can take either way */
+static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4], int np, const cvx_shape* B, real rB,
+                              real off, real* out) {
+  orc_hv.face = -1;
+  const int nc = hull_core_contacts_at(hv, nv, pl, np, B, rB, off, out);
+  if (orc_tie_delta < 0.0) return nc;
+  const int ill = orc_hull_ill, f = orc_hv.face;
+  if (f >= 0 && nc > 0) {
+    /* the face case: another facet within the coplanar angle whose clip reaches as deep (within HULL_FEAT_EPS) is
+     * one the witness could have landed on (a segment lying across near-coplanar facets) */
+    real g0 = out[6];
+    for (int i = 1; i < nc; i++) g0 = fmin(g0, out[7 * i + 6]);
+    for (int i = 0; i < np && !orc_amb_pend; i++) {
+      if (i == f || pl[i][0] * pl[f][0] + pl[i][1] * pl[f][1] + pl[i][2] * pl[f][2] <= HULL_COS_COPLANAR) continue;
+      real o2[14], u[3];
+      v3sub(B->p1, B->p0, u);
+      const int n2 = hull_face_clip(pl, np, i, B->p0, u, rB, off, o2);
+      for (int j = 0; j < n2; j++)
+        if (fabs(o2[7 * j + 6] - g0) < HULL_FEAT_EPS) orc_amb_pend = 1;
+    }
+  }
+  static const double var[8][4] = {{0.5, 1, 1, 0}, {2, 1, 1, 0}, {1, 0.98, 1, 0}, {1, 1.02, 1, 0},
+                                   {1, 1, 0.98, 0}, {1, 1, 1.02, 0}, {1, 1, 1, 1}, {1, 1, 1, 2}};
+  for (int k = 0; k < 8 && !orc_amb_pend; k++) {
+    real o2[14];
+    orc_hv.fe = var[k][0]; orc_hv.ang = var[k][1]; orc_hv.cop = var[k][2]; orc_hv.seam = (int)var[k][3];
+    const int n2 = hull_core_contacts_at(hv, nv, pl, np, B, rB, off, o2);
+    int same = n2 == nc;
+    for (int i = 0; same && i < 7 * nc; i++) same = fabs(o2[i] - out[i]) <= 1e-12;
+    if (!same) orc_amb_pend = 1;
+  }
+  orc_hv.fe = orc_hv.ang = orc_hv.cop = 1.0;
+  orc_hv.seam = 0;
+  orc_hull_ill = ill;
+  return nc;
 }
 /* the object's core in the hull's geom frame (centre c, axes R) */
 static void hull_object_core(const mg_model* m, const kin* k, const real* c, real R[3][3], cvx_shape* B, real* rB) {
@@ -2171,8 +2211,19 @@ static int collide(const mg_model* m, const mg_sim_params* p, const kin* k, cont
     for (int pass = 0; pass < 2; pass++)
       for (int g = 0; g < m->num_geoms; g++)
         if ((m->geom_filter[g] & MG_COLLIDE_OBJECT) && ((m->geom_type[g] == MG_GT_CONVEX) == (pass == 0)))
+        {
+          /* an ambiguous narrowphase decision marks the contacts of this geom-object pair (bit 16 when the solve
+           * uses one of them); one that left the pair without any contact marks the step */
+          const int n0 = n;
+          orc_amb_pend = 0;
           n = m->obj_type == MG_GT_BOX ? geom_object(m, k, g, off, out, n, cap)
                                        : geom_object_convex(m, k, g, off, out, n, cap);
+          if (orc_amb_pend) {
+            for (int i = n0; i < n; i++) out[i].amb = 1;
+            if (n == n0) orc_amb_hit = 1;
+          }
+          orc_amb_pend = 0;
+        }
   return n;
 }
 
@@ -2698,7 +2749,8 @@ int orc_contacts_full(const mg_model* m, const mg_sim_params* p, const float* ro
  *   4  a PD drive whose explicit force is within df (relative) of its effort limit (implicit <-> saturated)
  *   8  a segment core inside a box whose two least push-out faces are within delta (seg_box_sat's tie)
  *  16  a narrowphase decision near its threshold: a hull witness 0.5-2 um from a plane, a segment end or a box
- *      face (HULL_FEAT_EPS 1 um decides the features), an edge within 2 % of the parallel / on-face angles
+ *      face (HULL_FEAT_EPS 1 um decides the features), an edge within 2 % of the parallel / on-face angles --
+ *      when the solve uses a contact of that geom-object pair, or the decision left the pair without any
  *  32  a contact in use whose normal is ill-conditioned: the direction of a core distance below NORMAL_ILL
  *      (0.5 mm) that the geometry does not pin (an end point, a box edge or corner at the closest point; an
  *      MPR or hull-GJK depth), so that a 1e-7 m difference of the state turns it by ~1e-4 rad
@@ -2765,6 +2817,7 @@ int orc_step_flips(const mg_model* m0, const mg_sim_params* p, const mg_state_vi
       const real thr = pair ? 0.0 : p->contact_offset;
       if (fabs(ct->d - thr) < delta && so->lmax[3 * c] > eps) flags |= 1;
       if (ct->ill && so->lmax[3 * c] > eps) flags |= 32;
+      if (ct->amb && so->lmax[3 * c] > eps) flags |= 16;
     }
     for (int r = 3 * so->ncon; r < so->nrows; r++) {
       const int i = so->row_ref[r];
