@@ -417,8 +417,9 @@ size_t mg_state_views_sizeof(void);
 size_t mg_dr_desc_sizeof(void);
 size_t mg_dr_apply_args_sizeof(void);
 size_t mg_dr_noise_args_sizeof(void);
-/* profiling aid (phase-timing build only, see isaacgymenvs-ma_amd/build.py --timing) */
-int mg_debug_phase_cycles(uint64_t* out16, int32_t reset);
+/* profiling aid (phase-timing build only, see isaacgymenvs-ma_amd/build.py --timing): MG_NUM_PHASES counters */
+#define MG_NUM_PHASES 24
+int mg_debug_phase_cycles(uint64_t* out, int32_t reset);
 
 int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
                   mg_sim** out);

@@ -490,33 +490,33 @@ size_t mg_dr_noise_args_sizeof(void) { return sizeof(mg_dr_noise_args); }
 // build only; returns MG_EINVAL otherwise).  Phases: 0 FK, 1 ABA (+tendons), 2 collide (+object
 // free step), 3 rows, 4 row Jacobians / W, 5 test solves, 6 PGS, 7 integrate, 8 outputs, 9 task layer +
 // write-back, 13 constraint rows (count), 14 load + pre-physics, 15 substep entry.
-int mg_debug_phase_cycles(uint64_t* out16, int32_t reset) {
+int mg_debug_phase_cycles(uint64_t* out, int32_t reset) {
 #ifdef MG_PHASE_TIMING
   constexpr int kPhaseCap = 1 << 16;  // blocks tracked (step_kernels.hpp)
   static unsigned long long* buf = nullptr;
-  const size_t bytes = (size_t)kPhaseCap * 16 * sizeof(unsigned long long);
+  const size_t bytes = (size_t)kPhaseCap * MG_NUM_PHASES * sizeof(unsigned long long);
   if (!buf) {  // first call: allocate + zero the per-wave rows and publish them to the kernels
     if (hipMalloc(&buf, bytes) != hipSuccess || hipMemset(buf, 0, bytes) != hipSuccess)
       return fail(MG_EDEVICE, "mg_debug_phase_cycles: buffer setup failed");
     if (int rc = publish_all(buf, std::make_integer_sequence<int, MG_NUM_INST>{})) return rc;
     if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
-    if (out16) memset(out16, 0, 16 * sizeof(uint64_t));
+    if (out) memset(out, 0, MG_NUM_PHASES * sizeof(uint64_t));
     return MG_OK;
   }
   if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
-  if (out16) {
-    std::vector<unsigned long long> h((size_t)kPhaseCap * 16);
+  if (out) {
+    std::vector<unsigned long long> h((size_t)kPhaseCap * MG_NUM_PHASES);
     if (hipMemcpy(h.data(), buf, bytes, hipMemcpyDeviceToHost) != hipSuccess)
       return fail(MG_EDEVICE, "mg_debug_phase_cycles: copy failed");
-    for (int i = 0; i < 16; i++) out16[i] = 0;
+    for (int i = 0; i < MG_NUM_PHASES; i++) out[i] = 0;
     for (size_t w = 0; w < (size_t)kPhaseCap; w++)
-      for (int i = 0; i < 16; i++) out16[i] += h[16 * w + i];
+      for (int i = 0; i < MG_NUM_PHASES; i++) out[i] += h[MG_NUM_PHASES * w + i];
   }
   if (reset && hipMemset(buf, 0, bytes) != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: reset failed");
   if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_debug_phase_cycles: sync failed");
   return MG_OK;
 #else
-  (void)out16;
+  (void)out;
   (void)reset;
   return fail(MG_EINVAL, "mg_debug_phase_cycles: library built without MG_PHASE_TIMING");
 #endif

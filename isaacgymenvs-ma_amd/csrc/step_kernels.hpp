@@ -15,7 +15,7 @@
 
 namespace mgi {
 #ifdef MG_PHASE_TIMING
-// per-wave accumulators (one row of 16 per block; plain read-modify-writes by the block's own wave,
+// per-wave accumulators (one row of MG_NUM_PHASES per block; plain read-modify-writes by the block's own wave,
 // so the profiling build adds no atomic traffic that would slow the solver's memory path)
 constexpr int kPhaseCap = 1 << 16;  // waves tracked
 // one copy per instance translation unit (each is its own code object): phase_buf_publish<I> sets it
@@ -23,11 +23,11 @@ static __device__ unsigned long long* g_phase_buf;
 #define MG_PHASE_FLUSH(t, item)                                                        \
   {                                                                                    \
     const unsigned gw_ = (unsigned)(item), l_ = threadIdx.x & 63;                      \
-    if (g_phase_buf && gw_ < kPhaseCap && l_ < 16) {                                   \
+    if (g_phase_buf && gw_ < kPhaseCap && l_ < MG_NUM_PHASES) {                        \
       unsigned int v_ = 0;                                                             \
-      for (int i_ = 0; i_ < 16; i_++)                                                  \
+      for (int i_ = 0; i_ < MG_NUM_PHASES; i_++)                                       \
         if ((int)l_ == i_) v_ = (t).ph[i_];                                            \
-      g_phase_buf[16 * (size_t)gw_ + l_] += v_;                                        \
+      g_phase_buf[MG_NUM_PHASES * (size_t)gw_ + l_] += v_;                             \
     }                                                                                  \
   }
 #else

@@ -643,10 +643,10 @@ struct Team {
 #ifdef MG_PHASE_TIMING
   // shader-clock cycles per solver phase (profiling build only, see build.py --timing); wave-uniform
   // 32-bit accumulators so they stay in SGPRs and do not disturb the vector register budget
-  unsigned int ph[16];
+  unsigned int ph[MG_NUM_PHASES];
   unsigned long long tmark;
   __device__ __forceinline__ void ph_start() {
-    for (int i = 0; i < 16; i++) ph[i] = 0u;
+    for (int i = 0; i < MG_NUM_PHASES; i++) ph[i] = 0u;
     tmark = __builtin_amdgcn_s_memtime();
   }
   __device__ __forceinline__ void ph_mark(int i) {
@@ -856,6 +856,7 @@ struct Team {
       }
       c = node == 0 ? szero() : crm(V, S * nu);
     }
+    ph_mark(16);
     for (int lev = maxdepth; lev >= 1; lev--) {
       if (node > 0 && depth == lev) {
         U = mul(IA, S);
@@ -901,6 +902,7 @@ struct Team {
         }
       }
     }
+    ph_mark(17);
     if (tl == 0) {
       if (freeb) {
         chol6(IA, s->L0);
@@ -925,6 +927,7 @@ struct Team {
       s->u.sv.ts.aba.acc[0][tl] = a;
     }
     wsync();
+    ph_mark(18);
     float qdd = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {

@@ -18,7 +18,9 @@ os.environ.setdefault("MIGYM_LIB", os.path.join(ROOT, "isaacgymenvs-ma_amd", "mi
                                                 "libmigym_timing.so"))
 
 NAMES = {0: "fk", 1: "aba", 2: "collide", 3: "rows", 4: "row_jacobians", 5: "rows_finish", 6: "pgs",
-         7: "integrate", 8: "outputs", 9: "task+writeback", 10: "ts_walks", 11: "ts_root", 12: "ts_forward", 13: "rows_count", 14: "load+pre", 15: "substep_entry"}
+         7: "integrate", 8: "outputs", 9: "task+writeback", 10: "ts_walks", 11: "ts_root", 12: "ts_forward", 13: "rows_count", 14: "load+pre", 15: "substep_entry",
+         16: "aba.setup", 17: "aba.backward", 18: "aba.root"}   # slot 1 "aba": the forward pass after the marks 16-18
+NPHASE = 24
 
 
 def main():
@@ -47,7 +49,7 @@ def main():
     acts = [torch.rand((env.num_actors, env.num_actions), device="cuda:0", generator=g) * 2 - 1 for _ in range(4)]
     for i in range(args.warmup):
         env.step(acts[i % 4])
-    out = np.zeros(16, np.uint64)
+    out = np.zeros(NPHASE, np.uint64)
     timing = lib.mg_debug_phase_cycles(out.ctypes.data, 1) == 0  # production build: wall clock only
     torch.cuda.synchronize()
     import time
