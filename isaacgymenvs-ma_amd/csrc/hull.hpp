@@ -471,7 +471,27 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
   }
   if (face >= 0 || kA == 1) {
     if (B.kind != 0) return 0;
-    return hull_face_clip<T>(H, face >= 0 ? face : fa0, B.p0, u, rB, off, out);
+    // the face that clips: among the planes within the coplanar angle of the witness's face, the one highest at
+    // the segment's midpoint (the facet under it; ties to the lowest index).  A segment parallel to near-coplanar
+    // facets has its witness anywhere along them; the midpoint does not move with it (oracle hull_core_contacts_at)
+    const int f0 = face >= 0 ? face : fa0;
+    const V3 n0 = ld3(pl[f0]), mid = B.p0 + u * 0.5f;
+    float bv = -1e30f;
+    int fc = f0;
+    for (int k = 0; k * T < np; k++) {
+      const int i = k * T + tl;
+      if (i < np) {
+        const float4 q = *reinterpret_cast<const float4*>(pl[i]);
+        if (q.x * n0.x + q.y * n0.y + q.z * n0.z > HULL_COS_COPLANAR) {
+          const float v = q.x * mid.x + q.y * mid.y + q.z * mid.z - q.w;
+          if (v > bv) { bv = v; fc = i; }
+        }
+      }
+    }
+    // team argmax of (bv, -fc): the highest plane, the lowest index among equal ones
+    const float tb_v = team_max_dpp<T>(bv);
+    fc = team_min_dpp_i<T>(bv == tb_v ? fc : 0x7fffffff);
+    return hull_face_clip<T>(H, fc, B.p0, u, rB, off, out);
   }
   // edge against edge
   const V3 ua = cross(ld3(pl[fa0]), ld3(pl[fa1])), cx3 = cross(ua, ub);

@@ -77,7 +77,7 @@ static __thread int orc_hull_ill = 0; /* the last hull_core_contacts: a GJK dist
 static __thread int orc_cap_hit = 0;
 #define CAP_ILL_TOL 1e-3
 /* the hull narrowphase's decision thresholds, scaled by orc_step_flips' variants (1 = the build's) */
-static __thread struct { double fe, ang, cop; int seam, face; } orc_hv = {1.0, 1.0, 1.0, 0, -1};
+static __thread struct { double fe, ang, cop; int seam, face; double marg; } orc_hv = {1.0, 1.0, 1.0, 0, -1, 0.0};
 
 typedef real v3[3];
 
@@ -1774,8 +1774,23 @@ static int hull_core_contacts_at(const real (*hv)[3], int nv, const float (*pl)[
   }
   if (face >= 0 || kA == 1) {
     if (B->kind != 0) return 0; /* a box edge on a hull face: its ends are vertex-face candidates */
-    orc_hv.face = face >= 0 ? face : fa[0];
-    return hull_face_clip(pl, np, face >= 0 ? face : fa[0], B->p0, u, rB, off, out);
+    /* the face that clips: among the planes within the coplanar angle of the witness's face, the one highest at
+     * the segment's midpoint (on a convex hull: the facet under it).  A segment lying parallel to near-coplanar
+     * facets has its witness anywhere along them -- fp32 and fp64 GJK end on different facets -- and its
+     * midpoint does not move with the witness */
+    const int f0 = face >= 0 ? face : fa[0];
+    real mid[3], bv = -1e30, sv = -1e30;
+    int fc = f0;
+    for (int a = 0; a < 3; a++) mid[a] = B->p0[a] + 0.5 * u[a];
+    for (int i = 0; i < np; i++) {
+      if (pl[i][0] * pl[f0][0] + pl[i][1] * pl[f0][1] + pl[i][2] * pl[f0][2] <= COP) continue;
+      const real v = pl[i][0] * mid[0] + pl[i][1] * mid[1] + pl[i][2] * mid[2] - pl[i][3];
+      if (v > bv) { sv = bv; bv = v; fc = i; }
+      else if (v > sv) sv = v;
+    }
+    orc_hv.face = fc;
+    orc_hv.marg = bv - sv;
+    return hull_face_clip(pl, np, fc, B->p0, u, rB, off, out);
   }
   /* edge against edge: the hull edge's direction, the core edge not near parallel to it nor to the box's faces */
   const real n1[3] = {pl[fa[0]][0], pl[fa[0]][1], pl[fa[0]][2]}, n2[3] = {pl[fa[1]][0], pl[fa[1]][1], pl[fa[1]][2]};
@@ -1829,27 +1844,16 @@ static int hull_core_contacts_at(const real (*hv)[3], int nv, const float (*pl)[
 /* hull_core_contacts_at with the build's thresholds.  Under orc_step_flips it also runs with every decision
  * threshold moved within its band -- HULL_FEAT_EPS x0.5 / x2, the parallel / on-face angles and the coplanar
  * angle x0.98 / x1.02, either facet of a near-coplanar seam -- and marks the pair (orc_amb_pend, bit 16) when any
- * of them changes the contacts: the decision is then one an fp32 witness can take either way */
+ * of them changes the contacts, or when the face case's clipping facet is a near tie at the segment's midpoint:
+ * the decision is then one fp32 can take either way */
 static int hull_core_contacts(const real (*hv)[3], int nv, const float (*pl)[4], int np, const cvx_shape* B, real rB,
                               real off, real* out) {
   orc_hv.face = -1;
   const int nc = hull_core_contacts_at(hv, nv, pl, np, B, rB, off, out);
   if (orc_tie_delta < 0.0) return nc;
-  const int ill = orc_hull_ill, f = orc_hv.face;
-  if (f >= 0 && nc > 0) {
-    /* the face case: another facet within the coplanar angle whose clip reaches as deep (within HULL_FEAT_EPS) is
-     * one the witness could have landed on (a segment lying across near-coplanar facets) */
-    real g0 = out[6];
-    for (int i = 1; i < nc; i++) g0 = fmin(g0, out[7 * i + 6]);
-    for (int i = 0; i < np && !orc_amb_pend; i++) {
-      if (i == f || pl[i][0] * pl[f][0] + pl[i][1] * pl[f][1] + pl[i][2] * pl[f][2] <= HULL_COS_COPLANAR) continue;
-      real o2[14], u[3];
-      v3sub(B->p1, B->p0, u);
-      const int n2 = hull_face_clip(pl, np, i, B->p0, u, rB, off, o2);
-      for (int j = 0; j < n2; j++)
-        if (fabs(o2[7 * j + 6] - g0) < HULL_FEAT_EPS) orc_amb_pend = 1;
-    }
-  }
+  const int ill = orc_hull_ill, f = orc_hv.face;   /* orc_hv.marg: that face's margin (below) */
+  /* the face case: the midpoint within HULL_FEAT_EPS of the seam between the two highest facets */
+  if (f >= 0 && nc > 0 && orc_hv.marg < HULL_FEAT_EPS) orc_amb_pend = 1;
   static const double var[8][4] = {{0.5, 1, 1, 0}, {2, 1, 1, 0}, {1, 0.98, 1, 0}, {1, 1.02, 1, 0},
                                    {1, 1, 0.98, 0}, {1, 1, 1.02, 0}, {1, 1, 1, 1}, {1, 1, 1, 2}};
   for (int k = 0; k < 8 && !orc_amb_pend; k++) {
