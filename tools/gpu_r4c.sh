@@ -10,3 +10,5 @@ for spec in Humanoid:32768 Ant:65536 ShadowHand:16384; do
     > gpurun_out/phase/${t}_$n.txt 2>&1 || { echo "phase $t rc=$?"; tail -5 gpurun_out/phase/${t}_$n.txt; exit 1; }
   cat gpurun_out/phase/${t}_$n.txt | tail -20
 done
+# same-box A/B of the variant libraries (migym/_lib/var/*.so) against the default build
+VAR_SPECS="Humanoid:32768 ShadowHand:16384 Ant:65536" STEPS=${STEPS:-200} bash tools/gpu_variants.sh
