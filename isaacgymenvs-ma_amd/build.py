@@ -65,6 +65,12 @@ def build(force=False, verbose=False, timing=False, variant=None, defines=(), ex
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wno-unused-result"]
+    # no packed FP32 (v_pk_fma_f32 / v_pk_mul_f32): the packed forms need their operands in aligned register
+    # pairs, and the moves and pair pressure that costs outweigh the halved instruction count in these latency-
+    # bound kernels.  Spilled VGPRs: Humanoid 19 -> 2, ShadowHand block 52 -> 33, pen 49 -> 38, egg 57 -> 14;
+    # same-box A/B: Ant +3.8 % (16,384 envs +4.5 %), Humanoid +4.7 %, ShadowHand +3.2 % (profiles/r04).
+    # (-Xclang reaches the host compile too, where the AMDGPU feature name is ignored)
+    flags += ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
     if timing:
         flags.append("-DMG_PHASE_TIMING")
     flags += ["-D" + d for d in defines]

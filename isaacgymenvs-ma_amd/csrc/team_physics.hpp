@@ -172,7 +172,13 @@ constexpr float kBoxBlend = 1e-3f;  // point_box: the band (m) over which an int
 constexpr int kPgsPrefetch = 4;
 // rows whose (J, Y) columns stay in registers; the rest live in private (scratch) arrays (same-box A/B vs 16:
 // Ant +0.8 %, Humanoid +0.8 %, ShadowHand +0.6 %; 8 and 20 slower).  The egg keeps every row in scratch.
-constexpr int kJYRegs = 12;
+#ifndef MG_KJY
+#define MG_KJY 12
+#endif
+#ifndef MG_KJY_EGG
+#define MG_KJY_EGG 0
+#endif
+constexpr int kJYRegs = MG_KJY;
 // test-solve columns per batch (a multiple of 3): 12 for the 16- and 32-lane locomotion teams (12 walkers
 // instead of 6 halve the batches per substep: Ant +0.7 %, MA-Ant +1.0 %; 15 columns -3.5 %, 9 or 18 for
 // 32-lane teams -5 % / -34 %); hand teams and Cartpole keep 6
@@ -185,7 +191,7 @@ struct TeamLDS {
   static constexpr int RB = OBJ ? 6 : (kRBLoco <= T ? kRBLoco : 6);
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
   // (not for the egg instance: 17.16 vs 17.73 M env-steps/s and 450 vs 409 MB per launch, measured on its fp32 build)
-  static constexpr int KR = OBJ == MG_GT_ELLIPSOID ? 0 : (kJYRegs < MR ? kJYRegs : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
+  static constexpr int KR = ((OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : kJYRegs) < MR ? (OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : kJYRegs) : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
@@ -721,9 +727,6 @@ struct Team {
     }
     if (tl == 0) s->anc[0] = 1ull;
     maxdepth = wave_max<T>(depth);
-#ifdef MG_CHAIN_ABA
-    chain_init();
-#endif
     h = p->dt / (float)p->substeps;
     nu = 0.0f;
     qj = 0.0f;
@@ -860,9 +863,6 @@ struct Team {
       c = node == 0 ? szero() : crm(V, S * nu);
     }
     ph_mark(16);
-#ifdef MG_CHAIN_ABA
-    aba_backward_chains();
-#else
     for (int lev = maxdepth; lev >= 1; lev--) {
       if (node > 0 && depth == lev) {
         U = mul(IA, S);
@@ -908,7 +908,6 @@ struct Team {
         }
       }
     }
-#endif
     ph_mark(17);
     if (tl == 0) {
       if (freeb) {
@@ -935,9 +934,6 @@ struct Team {
     }
     wsync();
     ph_mark(18);
-#ifdef MG_CHAIN_ABA
-    const float qdd = aba_forward_chains();
-#else
     float qdd = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
@@ -949,164 +945,12 @@ struct Team {
       }
       wsync();
     }
-#endif
     // nu* = nu + h * acc
     if (tl < nv) {
       float a = (freeb && tl < 6) ? s->u.sv.ts.aba.acc[0][tl] : qdd;
       nu += h * a;
     }
   }
-
-#ifdef MG_CHAIN_ABA
-  // ---------------------------------------------------------------- ABA over chains (super-levels)
-  // A chain is a maximal path of nodes each of which but the last has exactly one child (Humanoid: a hip's
-  // three hinges, knee and ankle; ShadowHand: a finger; Ant: hip + ankle).  Its last node (the bottom: a leaf or
-  // a branching node) owns the chain: the backward pass runs up the chain and the forward pass down it on the
-  // bottom's lane, so a wave syncs once per chain level (Humanoid 9 tree levels -> 2, ShadowHand 7 -> 2, Ant
-  // 2 -> 1) instead of once per tree level.  The other members publish their own terms in setup: body inertia
-  // and bias (slot), c (V row, dead after setup), the drive's t and D terms (U row, written over by U).
-  int cbot, sdep, smax, ctop;
-  float tdrv, Dx;   // own drive terms (t and D - S.U), every node lane
-  __device__ __forceinline__ int nchild(int k) const { return __builtin_popcountll(mt->children[k]); }
-  __device__ __forceinline__ void chain_init() {
-    cbot = node > 0 && nchild(node) != 1;
-    sdep = 0;
-    ctop = node;
-    if (node > 0) {
-      for (int k = node; k > 0; k = mt->parent[k]) sdep += nchild(k) != 1 ? 1 : 0;
-      while (mt->parent[ctop] > 0 && nchild(mt->parent[ctop]) == 1) ctop = mt->parent[ctop];
-    }
-    smax = wave_max<T>(cbot ? sdep : 0);
-  }
-  // own drive terms (as the level loop computed them) and the members' published terms
-  __device__ __forceinline__ void chain_setup() {
-    if (node > 0) {
-      const float* np = nprop(node);  // [mass, arm, damp, stiff, lower, upper, kp, effort]
-      float kk = np[3], bb = np[2], ref = 0.0f, tadd = 0.0f;
-      sat = 0;
-      if (np[6] > 0.0f) {
-        const float fe = np[6] * (tgt - qj) - np[2] * nu;
-        if (fabsf(fe) > np[7]) {
-          kk = 0.0f; bb = 0.0f; tadd = fe > 0.0f ? np[7] : -np[7]; sat = 1;
-        } else {
-          kk = np[6]; ref = tgt;
-        }
-      }
-      Dx = np[1] + h * bb + h * h * kk;
-      tdrv = tau + tadd + ttend - bb * nu - kk * (qj - ref + h * nu);
-      if (!cbot) {
-        float* sl = s->u.slot[node];
-        for (int k = 0; k < 6; k++) { sl[k] = IA.a[k]; sl[15 + k] = IA.c[k]; }
-        for (int k = 0; k < 9; k++) sl[6 + k] = IA.b[k];
-        sl[21] = pA.a.x; sl[22] = pA.a.y; sl[23] = pA.a.z;
-        sl[24] = pA.l.x; sl[25] = pA.l.y; sl[26] = pA.l.z;
-        float* cv = s->V[node];
-        cv[0] = c.a.x; cv[1] = c.a.y; cv[2] = c.a.z; cv[3] = c.l.x; cv[4] = c.l.y; cv[5] = c.l.z;
-        s->U[node][0] = tdrv;
-        s->U[node][1] = Dx;
-      }
-    }
-  }
-  // the per-node u values for the forward pass, in the contact point storage (dead until collide)
-  __device__ __forceinline__ float* ubuf() const {
-    static_assert(sizeof(s->cp) >= sizeof(float) * MN, "u values must fit the contact point storage");
-    return &s->cp[0][0];
-  }
-  __device__ __forceinline__ void aba_backward_chains() {
-    chain_setup();
-    wsync();
-    float* ub = ubuf();
-    for (int lev = smax; lev >= 1; lev--) {
-      if (cbot && sdep == lev) {
-        int k = node;
-        Sym6 IAk = IA;
-        SV pAk = pA, ck = c, Sk = S;
-        float tk = tdrv, Dxk = Dx;
-        while (true) {
-          const SV Uk = mul(IAk, Sk);
-          const float Dk = prcp(dot(Sk, Uk) + Dxk);
-          const float uk = tk - dot(Sk, pAk);
-          if (k == node) { U = Uk; Dinv = Dk; u = uk; }
-          Sym6 Ia = IAk;
-          rank1_sub(Ia, Uk, Dk);
-          const SV pa = pAk + mul(Ia, ck) + Uk * (uk * Dk);
-          s->U[k][0] = Uk.a.x; s->U[k][1] = Uk.a.y; s->U[k][2] = Uk.a.z;
-          s->U[k][3] = Uk.l.x; s->U[k][4] = Uk.l.y; s->U[k][5] = Uk.l.z;
-          s->Dinv[k] = Dk;
-          ub[k] = uk;
-          float* sl = s->u.slot[k];
-          if (k == ctop) {
-            for (int q = 0; q < 6; q++) { sl[q] = Ia.a[q]; sl[15 + q] = Ia.c[q]; }
-            for (int q = 0; q < 9; q++) sl[6 + q] = Ia.b[q];
-            sl[21] = pa.a.x; sl[22] = pa.a.y; sl[23] = pa.a.z;
-            sl[24] = pa.l.x; sl[25] = pa.l.y; sl[26] = pa.l.z;
-            break;
-          }
-          // the next member up: its own body terms plus this articulated projection
-          k = mt->parent[k];
-          sl = s->u.slot[k];
-          for (int q = 0; q < 6; q++) { IAk.a[q] = sl[q] + Ia.a[q]; IAk.c[q] = sl[15 + q] + Ia.c[q]; }
-          for (int q = 0; q < 9; q++) IAk.b[q] = sl[6 + q] + Ia.b[q];
-          pAk = sv(v3(sl[21], sl[22], sl[23]), v3(sl[24], sl[25], sl[26])) + pa;
-          ck = sv(ld3(s->V[k]), ld3(s->V[k] + 3));
-          Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3));
-          tk = s->U[k][0];
-          Dxk = s->U[k][1];
-        }
-      }
-      wsync();
-      if (node >= 0 && (node == 0 ? lev == 1 : (cbot && sdep == lev - 1))) {
-        unsigned long long ch = mt->children[node];
-        while (ch) {
-          const int k = __builtin_ctzll(ch);
-          ch &= ch - 1;
-          const float* sl = s->u.slot[k];
-          for (int q = 0; q < 6; q++) { IA.a[q] += sl[q]; IA.c[q] += sl[15 + q]; }
-          for (int q = 0; q < 9; q++) IA.b[q] += sl[6 + q];
-          pA = pA + sv(v3(sl[21], sl[22], sl[23]), v3(sl[24], sl[25], sl[26]));
-        }
-      }
-    }
-    // the members' own factors back in their lanes (test solves, root coupling)
-    if (node > 0 && !cbot) {
-      U = sv(ld3(s->U[node]), ld3(s->U[node] + 3));
-      Dinv = s->Dinv[node];
-    }
-  }
-  __device__ __forceinline__ float aba_forward_chains() {
-    const float* ub = ubuf();
-    auto& acc = s->u.sv.ts.aba.acc;
-    float qdd = 0.0f;
-    for (int lev = 1; lev <= smax; lev++) {
-      if (cbot && sdep == lev) {
-        int k = ctop;
-        SV ap = sv(ld3(acc[mt->parent[k]]), ld3(acc[mt->parent[k]] + 3));
-        while (true) {
-          const bool own = k == node;
-          const SV ck = own ? c : sv(ld3(s->V[k]), ld3(s->V[k] + 3));
-          const SV Uk = own ? U : sv(ld3(s->U[k]), ld3(s->U[k] + 3));
-          const SV Sk = own ? S : sv(ld3(s->S[k]), ld3(s->S[k] + 3));
-          const float Dk = own ? Dinv : s->Dinv[k];
-          ap = ap + ck;
-          const float qk = (ub[k] - dot(Uk, ap)) * Dk;
-          const SV a = ap + Sk * qk;
-          if (own) {
-            qdd = qk;
-            acc[node][0] = a.a.x; acc[node][1] = a.a.y; acc[node][2] = a.a.z;
-            acc[node][3] = a.l.x; acc[node][4] = a.l.y; acc[node][5] = a.l.z;
-            break;
-          }
-          acc[k][0] = qk;  // a member's qdd (its acc row is nobody else's)
-          ap = a;
-          k = __builtin_ctzll(mt->children[k]);
-        }
-      }
-      wsync();
-    }
-    if (node > 0 && !cbot) qdd = acc[node][0];
-    return qdd;
-  }
-#endif
 
   // ---------------------------------------------------------------- fixed tendons (explicit soft limits)
   __device__ __forceinline__ void tendons() {
@@ -1206,11 +1050,12 @@ struct Team {
           fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
         }
         float* ut = ts.ut[tl];
-#ifdef MG_WALK_MERGED
-        // Both sides of a contact at once: below their lowest common ancestor the two paths are walked in one
-        // loop (two independent chains per step), and from there to the root the map pv -> pv + U D (t - S.pv)
-        // being linear, the sum of the two forces is walked once (a limit row: one path, no second side)
-        {
+        // 32-lane locomotion teams (Humanoid: 35 % of the contacts are self contacts with two tree sides): both
+        // sides of a contact at once.  Below their lowest common ancestor the two paths are walked in one loop
+        // (two independent chains per step), and from there to the root, the map pv -> pv + U D (t - S.pv) being
+        // linear, the sum of the two forces is walked once; a limit row has one path.  Same-box A/B: Humanoid
+        // +1.9 %; Ant -1.3 % and ShadowHand -0.6 % (few two-sided contacts), which keep the side-by-side walks.
+        if constexpr (T >= 32 && !OBJ) {
           const bool two = kind < 2 && nodeA > 0 && nodeB > 0;
           int ka = kind >= 2 ? (jn > 0 ? jn : -1) : nodeA, kb = two ? nodeB : -1;
           SV pa = kind >= 2 ? szero() : fw * -1.0f, pb = fw;
@@ -1251,11 +1096,8 @@ struct Team {
             pv = pv + Uk * (uk * s->Dinv[k]);
           }
           if (ka > 0 || two) proot = proot + pv;
-        }
-        for (int side = 3; side < 3; side++) {
-#else
+        } else {
         for (int side = 0; side < 3; side++) {
-#endif
           int k0;
           SV pv;
           float tq = 0.0f;
@@ -1292,6 +1134,7 @@ struct Team {
             k = kn; Sk = Sn; Uk = Un; Dk = Dn;
           }
           proot = proot + pv;
+        }
         }
       }
       float* pr = ts.proot[tl];
