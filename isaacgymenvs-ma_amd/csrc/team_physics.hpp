@@ -1772,6 +1772,7 @@ struct Team {
       }
       base += tot;
     }
+    ph_mark(19);
     // self-collision pairs, pair order preserved (Humanoid: every non-adjacent pair; ShadowHand: the MJCF's
     // explicit <contact><pair>s).  Pass 1, lane per pair: the bounding-sphere test of the two cores; the
     // survivors' indices are compacted (team scan) into a list in the union storage behind the geom frames.
@@ -1855,6 +1856,7 @@ struct Team {
       }
       base += tot;
     }
+    ph_mark(20);
     if constexpr (OBJ != 0) {
       // articulation geoms vs the object: one lane per (geom, candidate) in geom order (the oracle's
       // emission order); a candidate whose geom's bounding sphere cannot come within the contact
@@ -1966,6 +1968,7 @@ struct Team {
           base += nx;
         }
       }
+      ph_mark(21);
       // the survivors' candidates in geom order: lane per geom, a team scan of the counts places each geom's
       // run, and the geom writes (geom, candidate index) for its run into a map behind the pair list, so a
       // candidate's lane finds its pair with one LDS read (instead of walking the live mask)

@@ -19,7 +19,8 @@ os.environ.setdefault("MIGYM_LIB", os.path.join(ROOT, "isaacgymenvs-ma_amd", "mi
 
 NAMES = {0: "fk", 1: "aba", 2: "collide", 3: "rows", 4: "row_jacobians", 5: "rows_finish", 6: "pgs",
          7: "integrate", 8: "outputs", 9: "task+writeback", 10: "ts_walks", 11: "ts_root", 12: "ts_forward", 13: "rows_count", 14: "load+pre", 15: "substep_entry",
-         16: "aba.setup", 17: "aba.backward", 18: "aba.root"}   # slot 1 "aba": the forward pass after the marks 16-18
+         16: "aba.setup", 17: "aba.backward", 18: "aba.root",   # slot 1 "aba": the forward pass after the marks 16-18
+         19: "collide.ground", 20: "collide.pairs", 21: "collide.hull"}   # slot 2 "collide": the object candidates
 NPHASE = 24
 
 
