@@ -130,7 +130,9 @@ def baseline_config0(dev, steps=1000, n=256):
     # the configuration as BASELINE.json names it: pipeline=cpu, sim_device=cpu, through make() -- the HIP step
     # underneath with host-side views of every task tensor (migym/host_pipeline.py), host actions in, host
     # outputs (rl_device cpu) out, the mirrors' transfers included
-    cenv = migym.make(seed=0, task="Cartpole", num_envs=n, sim_device="cpu", rl_device="cpu", headless=True)
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):  # VecTask's "Forcing CPU Pipeline" notice: stdout carries one JSON line
+        cenv = migym.make(seed=0, task="Cartpole", num_envs=n, sim_device="cpu", rl_device="cpu", headless=True)
     for i in range(10):
         cenv.step(host[i % 8])
     t0 = time.perf_counter()

@@ -9,7 +9,8 @@ import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "isaacgymenvs-ma_amd/csrc/migym.hip"
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-c", "--cuda-device-only",
-       "-Rpass-analysis=kernel-resource-usage", "-o", "/dev/null", src] + sys.argv[2:]
+       "-Rpass-analysis=kernel-resource-usage", "-o", "/dev/null", src,
+       "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"] + sys.argv[2:]   # build.py's flags
 if src.endswith("inst.hip"):  # the instance TUs' build flags (build.py)
     cmd += ["-mllvm", "-disable-machine-licm", "-mllvm", "-enable-ipra=false"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
