@@ -67,6 +67,7 @@ struct alignas(16) ModelTile {
   int nn, ng, np;
   int hnv;            // vertices of the convex-mesh geom's hull (mg_model.hull_*), 0 if none
   int hullg;          // the convex-mesh geom (-1 if none)
+  int ground_round;   // every ground-colliding geom is a sphere or a capsule (one-pass ground contacts)
   // block / pen instances: the hull's vertices and their centroid for the exact hull candidates (hull.hpp), read
   // by every GJK support; its planes stay in global memory (one pass per call)
   float hv[HV][3];
@@ -125,6 +126,10 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, HV>* t, const mg_model
   }
   if (tid == 0) {
     t->nn = nn; t->ng = ng; t->np = np; t->nten = nten; t->hnv = m->hull_num_verts;
+    t->ground_round = 1;
+    for (int g = 0; g < ng; g++)
+      if ((m->geom_filter[g] & MG_COLLIDE_GROUND) && m->geom_type[g] != MG_GT_SPHERE && m->geom_type[g] != MG_GT_CAPSULE)
+        t->ground_round = 0;
     // the convex-mesh geom that collides with the object (mg_sim_create allows one), else the lowest one
     t->hullg = -1;
     for (int g = ng - 1; g >= 0; g--)
@@ -340,6 +345,23 @@ __device__ __forceinline__ int team_incl_scan(int v) {
     if (tl >= d) v += o;
   }
   return v;
+}
+// the same inclusive scan for 0 <= v < 2^NB (contact-candidate flags and counts) and the team's total: one ballot
+// per bit plane, a lane-mask popcount (v_mbcnt) and the plane's bit count, no cross-lane permutes (same-box A/B
+// against the permute scan: Humanoid +2.0 %, ShadowHand pen +1.4 %, block +1.0 %, Ant +0.9 %)
+template <int T, int NB>
+__device__ __forceinline__ int team_scan_bits(int v, int& tot) {
+  const int tl = threadIdx.x % T, tb = (threadIdx.x & 63) - tl;
+  const unsigned long long tm = (T >= 64 ? ~0ull : ((1ull << T) - 1ull)) << tb;
+  int ex = 0;
+  tot = 0;
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    const unsigned long long bl = __ballot((v >> b) & 1) & tm;
+    ex += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bl >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bl, 0u)) << b;
+    tot += __builtin_popcountll(bl) << b;
+  }
+  return ex + v;
 }
 // team argmax of (v, i): the largest v, the smallest i among equal v (a serial loop's first maximum)
 template <int T>
@@ -1696,6 +1718,42 @@ struct Team {
     wsync();
     // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
     // pass 1 counts, a team scan places them, pass 2 recomputes and writes (no private arrays).
+    // spheres and capsules only (the locomotion models): at most two candidates per geom, kept in registers,
+    // one pass (same-box A/B against the two passes: Ant +2.3 %, Ant 16,384 +1.9 %, MA-Ant +2.4 %, Humanoid +1.2 %)
+    if (mt->ground_round) {
+      for (int g0 = 0; g0 < G; g0 += T) {
+        const int g = g0 + tl;
+        V3 e0 = v3(0, 0, 0), e1 = v3(0, 0, 0);
+        float r = 0.0f, d0 = 1e30f, d1 = 1e30f;
+        if (g < G && (mt->gfil[g] & MG_COLLIDE_GROUND)) {
+          V3 c;
+          M3 Rg;
+          geom_staged(g, &c, &Rg);
+          if (c.z - mt->gf[g][15] < off) {
+            const float* gs = mt->gf[g] + 12;
+            r = gs[0];
+            if (mt->gtype[g] == MG_GT_CAPSULE) {
+              const V3 ax = v3(Rg.m[0][2], Rg.m[1][2], Rg.m[2][2]) * gs[1];
+              e0 = c - ax;
+              e1 = c + ax;
+              d1 = e1.z - r;
+            } else {
+              e0 = c;
+            }
+            d0 = e0.z - r;
+          }
+        }
+        const bool k0 = d0 < off, k1 = d1 < off;
+        const int cnt = (k0 ? 1 : 0) + (k1 ? 1 : 0);
+        int scan_tot;
+        const int incl = team_scan_bits<T, 2>(cnt, scan_tot);
+        const int slot0 = base + incl - cnt;
+        base += scan_tot;
+        if (k0 && slot0 < cap) put_contact(slot0, v3(e0.x, e0.y, e0.z - r), v3(0, 0, 1), d0, mt->gnode[g], g, -1, -1);
+        const int s1 = slot0 + (k0 ? 1 : 0);
+        if (k1 && s1 < cap) put_contact(s1, v3(e1.x, e1.y, e1.z - r), v3(0, 0, 1), d1, mt->gnode[g], g, -1, -1);
+      }
+    } else
     for (int g0 = 0; g0 < G; g0 += T) {
       const int g = g0 + tl;
       V3 c = v3(0, 0, 0);
@@ -1766,8 +1824,8 @@ struct Team {
       }
       const float d = e.z - r;
       cnt = cnt && d < off ? 1 : 0;
-      const int incl = team_incl_scan<T>(cnt);
-      const int tot = __shfl(incl, tb + T - 1);
+      int tot;
+      const int incl = team_scan_bits<T, 1>(cnt, tot);
       if (cnt) {
         const int slot = base + incl - 1;
         if (slot < cap) put_contact(slot, v3(e.x, e.y, e.z - r), v3(0, 0, 1), d, OBJ_NODE, -2, -1, -1);
@@ -1802,9 +1860,10 @@ struct Team {
           ok = dot(dc, dc) <= reach * reach ? 1 : 0;
         }
       }
-      const int incl = team_incl_scan<T>(ok);
+      int scan_tot;
+      const int incl = team_scan_bits<T, 1>(ok, scan_tot);
       if (ok) plist[npc + incl - 1] = pi;
-      npc += __shfl(incl, tb + T - 1);
+      npc += scan_tot;
     }
     wsync();
     const int npw = __builtin_amdgcn_readfirstlane(wave_max<T>(npc));  // wave-uniform trip count
@@ -1850,8 +1909,8 @@ struct Team {
           }
         }
       }
-      const int incl = team_incl_scan<T>(cnt);
-      const int tot = __shfl(incl, tb + T - 1);
+      int tot;
+      const int incl = team_scan_bits<T, 1>(cnt, tot);
       if (cnt) {
         const int slot = base + incl - 1;
         if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[ga], ga, mt->gnode[gb], gb);
@@ -1910,8 +1969,8 @@ struct Team {
             V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
             float d = 0.0f;
             if (q < nhv) cnt = hull_vertex_candidate(q, c, Rg, &pt, &nrm, &d) && d < off ? 1 : 0;
-            const int incl = team_incl_scan<T>(cnt);
-            const int tot = __shfl(incl, tb + T - 1);
+            int tot;
+            const int incl = team_scan_bits<T, 1>(cnt, tot);
             if (cnt) {
               const int slot = base + incl - 1;
               if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
@@ -1955,8 +2014,8 @@ struct Team {
           nrm = mul(Rg, ng) * -1.0f;
           cnt = d < off ? 1 : 0;
         }
-        const int incl = team_incl_scan<T>(cnt);
-        const int tot = __shfl(incl, tb + T - 1);
+        int tot;
+        const int incl = team_scan_bits<T, 1>(cnt, tot);
         if (cnt) {
           const int slot = base + incl - 1;
           if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
@@ -1986,8 +2045,8 @@ struct Team {
           g = s->lmeta[MN - 1 + tl];
           cnt = d < off ? 1 : 0;
         }
-        const int incl = team_incl_scan<T>(cnt);
-        const int tot = __shfl(incl, tb + T - 1);
+        int tot;
+        const int incl = team_scan_bits<T, 1>(cnt, tot);
         if (cnt) {
           const int slot = base + incl - 1;
           if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
@@ -2022,8 +2081,8 @@ struct Team {
           else ok = obj_candidate_convex(g, q, c, Rg, &pt, &nrm, &d);
           cnt = ok && d < off ? 1 : 0;
         }
-        const int incl = team_incl_scan<T>(cnt);
-        const int tot = __shfl(incl, tb + T - 1);
+        int tot;
+        const int incl = team_scan_bits<T, 1>(cnt, tot);
         if (cnt) {
           const int slot = base + incl - 1;
           if (slot < cap) put_contact(slot, pt, nrm, d, mt->gnode[g], g, OBJ_NODE, -2);
@@ -2107,8 +2166,8 @@ struct Team {
       hi = du < p->limit_margin;
       cnt = (lo ? 1 : 0) + (hi ? 1 : 0);
     }
-    const int incl = team_incl_scan<T>(cnt);
-    const int tot = __shfl(incl, tb + T - 1);
+    int tot;
+    const int incl = team_scan_bits<T, 2>(cnt, tot);
     int li = incl - cnt;
     for (int side = 0; side < 2; side++) {
       bool on = side == 0 ? lo : hi;
