@@ -336,17 +336,7 @@ __device__ __forceinline__ float team_sum(float v, int) {
   if (T >= 64) v += __shfl_xor(v, 32);
   return v;
 }
-template <int T>
-__device__ __forceinline__ int team_incl_scan(int v) {
-  const int tl = threadIdx.x % T;
-#pragma unroll
-  for (int d = 1; d < T; d <<= 1) {
-    int o = __shfl_up(v, d, T);
-    if (tl >= d) v += o;
-  }
-  return v;
-}
-// the same inclusive scan for 0 <= v < 2^NB (contact-candidate flags and counts) and the team's total: one ballot
+// the inclusive scan over the team's lanes of 0 <= v < 2^NB (contact-candidate flags and counts) and the team's total: one ballot
 // per bit plane, a lane-mask popcount (v_mbcnt) and the plane's bit count, no cross-lane permutes (same-box A/B
 // against the permute scan: Humanoid +2.0 %, ShadowHand pen +1.4 %, block +1.0 %, Ant +0.9 %)
 template <int T, int NB>
@@ -366,12 +356,39 @@ __device__ __forceinline__ int team_scan_bits(int v, int& tot) {
 // team argmax of (v, i): the largest v, the smallest i among equal v (a serial loop's first maximum)
 template <int T>
 __device__ __forceinline__ void team_argmax(float& v, int& i) {
-#pragma unroll
-  for (int d = 1; d < T; d <<= 1) {
-    const float ov = __shfl_xor(v, d, T);
-    const int oi = __shfl_xor(i, d, T);
+  // DPP butterfly (as team_sum): the pair with the larger v, on ties the smaller i, at every step (same-box A/B,
+  // with the ballot forms of the wave maxima and the remaining scans: ShadowHand +1.7 %, pen +1.4 %)
+  auto step = [&](float ov, int oi) {
     if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  };
+  step(__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)),
+       __builtin_amdgcn_update_dpp(0, i, 0xB1, 0xF, 0xF, false));
+  step(__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)),
+       __builtin_amdgcn_update_dpp(0, i, 0x4E, 0xF, 0xF, false));
+  if (T >= 8)
+    step(__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)),
+         __builtin_amdgcn_update_dpp(0, i, 0x141, 0xF, 0xF, false));
+  if (T >= 16)
+    step(__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)),
+         __builtin_amdgcn_update_dpp(0, i, 0x140, 0xF, 0xF, false));
+  if (T >= 32) {
+    const auto rv = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const auto ri = __builtin_amdgcn_permlane16_swap((unsigned)i, (unsigned)i, false, false);
+    step(__uint_as_float((threadIdx.x & 16) ? rv[0] : rv[1]), (int)((threadIdx.x & 16) ? ri[0] : ri[1]));
   }
+  if (T >= 64) step(__shfl_xor(v, 32), __shfl_xor(i, 32));
+}
+// the wave's maximum of 0 <= v < 2^NB, wave-uniform: a bitwise search with one ballot per bit
+static_assert(MG_MAX_HULL_PLANES < 512 && MG_MAX_HULL_VERTS < 512, "candidate counts are scanned in 9 bit planes");
+template <int NB>
+__device__ __forceinline__ int wave_max_bits(int v) {
+  int m = 0;
+#pragma unroll
+  for (int b = NB - 1; b >= 0; b--) {
+    const int c = m | (1 << b);
+    if (__ballot(v >= c) != 0ull) m = c;
+  }
+  return m;
 }
 template <int T>
 __device__ __forceinline__ int wave_max(int v) {
@@ -1769,9 +1786,10 @@ struct Team {
       for (int pass = 0; pass < 2; pass++) {
         int k = 0, slot0 = 0;
         if (pass == 1) {
-          const int incl = team_incl_scan<T>(cnt);
+          int tot;
+          const int incl = team_scan_bits<T, 9>(cnt, tot);  // a geom's candidates: <= 8, a hull's vertices <= 160
           slot0 = base + incl - cnt;
-          base += __shfl(incl, tb + T - 1);
+          base += tot;
         }
         const int nc = ty == MG_GT_SPHERE ? 1 : (ty == MG_GT_CAPSULE ? 2 : (ty == MG_GT_BOX ? 8 : (ty == MG_GT_CONVEX ? mt->hnv : 0)));
         for (int q = 0; q < nc; q++) {
@@ -1866,7 +1884,8 @@ struct Team {
       npc += scan_tot;
     }
     wsync();
-    const int npw = __builtin_amdgcn_readfirstlane(wave_max<T>(npc));  // wave-uniform trip count
+    static_assert(MP < 256, "wave_max_bits<8>");
+    const int npw = wave_max_bits<8>(npc);  // wave-uniform trip count
     for (int c0 = 0; c0 < npw; c0 += T) {
       const int ci = c0 + tl;
       int cnt = 0;
@@ -2059,9 +2078,10 @@ struct Team {
       for (int g0 = 0; g0 < G; g0 += T) {
         const int g = g0 + tl;
         const int n = (g < G && ((live >> g) & 1ull)) ? ocand_count(mt->gtype[g]) : 0;
-        const int incl = team_incl_scan<T>(n);
+        int tot;
+        const int incl = team_scan_bits<T, 9>(n, tot);  // a geom's object candidates (the hull's planes: <= 320)
         for (int q = 0; q < n; q++) cmap[NC + incl - n + q] = (uint16_t)(g | (q << 8));
-        NC += __shfl(incl, tb + T - 1);
+        NC += tot;
       }
       wsync();
       for (int f0 = 0; f0 < NC; f0 += T) {
@@ -2203,7 +2223,8 @@ struct Team {
     build_rows();
     ph_mark(3);
     const int nrows = s->nrows;
-    const int wave_rows = __builtin_amdgcn_readfirstlane(wave_max<T>(nrows));
+    static_assert(MR < 256, "wave_max_bits<8>");
+    const int wave_rows = wave_max_bits<8>(nrows);
 #ifdef MG_PHASE_TIMING
     ph[13] += wave_rows;
 #endif
