@@ -180,6 +180,9 @@ constexpr int kPgsPrefetch = 4;
 #ifndef MG_KJY
 #define MG_KJY 12
 #endif
+#ifndef MG_KJY_LOCO32
+#define MG_KJY_LOCO32 16
+#endif
 #ifndef MG_KJY_EGG
 #define MG_KJY_EGG 0
 #endif
@@ -196,7 +199,8 @@ struct TeamLDS {
   static constexpr int RB = OBJ ? 6 : (kRBLoco <= T ? kRBLoco : 6);
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
   // (not for the egg instance: 17.16 vs 17.73 M env-steps/s and 450 vs 409 MB per launch, measured on its fp32 build)
-  static constexpr int KR = ((OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : kJYRegs) < MR ? (OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : kJYRegs) : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
+  static constexpr int KR0 = OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : ((T >= 32 && !OBJ) ? MG_KJY_LOCO32 : kJYRegs);
+  static constexpr int KR = (KR0 < MR ? KR0 : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
