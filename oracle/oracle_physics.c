@@ -1233,6 +1233,115 @@ static int cvx_mpr(const cvx_shape* A, const real* e, real* x, real* pa) {
   return 1;
 }
 
+/* Exact penetration of a segment core [p0, p1] (or a point) overlapping the ellipsoid e (the minimum
+ * translation): depth = min over unit n of max_k (h_E(n) - n.p_k), the translation of the core along n that
+ * separates it.  The minimum is a vertex one -- the distance from an end inside the ellipsoid to the surface,
+ * valid when the other end is not deeper along that normal -- or, when neither is, the edge one on the great
+ * circle n.u = 0: the distance from the core's shadow point to the boundary of the ellipsoid's shadow ellipse in
+ * the plane normal to u.  Each is the nearest-boundary-point problem of an interior point: b_i = s_i q_i / (s_i +
+ * lam) with the root lam in (-min s_i, 0] of sum_i s_i q_i^2 / (s_i + lam)^2 = 1 (s = squared semi-axes), by
+ * Newton's method from lam = 0 (the function is convex and decreasing there: one step lands left of the root,
+ * the rest climb to it).  MPR's portal normal is a facet of a polytope approximation (a 1e-7 m change of the
+ * state turned it by 1e-2 rad for a capsule 1 cm deep); this solution moves smoothly with the state away from
+ * the medial axis, where orc_cvx_ill marks it.  The kernel (convex.hpp mpr64::seg_mtd) runs the same in fp64. */
+static real ell_root(int k, const real* s2, const real* q, real* smin_out) {
+  real smin = s2[0];
+  for (int i = 1; i < k; i++) smin = fmin(smin, s2[i]);
+  real lam = 0.0;
+  for (int it = 0; it < 64; it++) {
+    real f = -1.0, fp = 0.0;
+    for (int i = 0; i < k; i++) {
+      const real den = s2[i] + lam, r = s2[i] * q[i] * q[i] / (den * den);
+      f += r;
+      fp -= 2.0 * r / den;
+    }
+    if (!(fp < 0.0)) break;
+    real nl = lam - f / fp;
+    if (!(nl > -smin)) nl = 0.5 * (lam - smin); /* keep clear of the pole */
+    if (nl > 0.0) nl = 0.0;
+    const real dl = fabs(nl - lam);
+    lam = nl;
+    if (dl <= 1e-14 * smin) break;
+  }
+  *smin_out = smin;
+  return lam;
+}
+/* the vertex solution of an end p inside e: outward normal n, depth */
+static int mtd_vertex(const real* e, const real* p, real* n, real* depth, int* ill) {
+  const real s2[3] = {e[0] * e[0], e[1] * e[1], e[2] * e[2]};
+  if (!(p[0] * p[0] / s2[0] + p[1] * p[1] / s2[1] + p[2] * p[2] / s2[2] < 1.0)) return 0;
+  real smin;
+  const real lam = ell_root(3, s2, p, &smin);
+  real g[3];
+  for (int i = 0; i < 3; i++) g[i] = p[i] / (s2[i] + lam);
+  const real gl = sqrt(dot3(g, g));
+  if (!(gl > 0.0) || !isfinite(gl)) return 0;
+  for (int i = 0; i < 3; i++) n[i] = g[i] / gl;
+  *depth = -lam * gl;
+  *ill = (smin + lam) < 1e-3 * smin;
+  return 1;
+}
+static int seg_mtd(const cvx_shape* A, const real* e, real* n, real* depth, real* pa) {
+  real u[3], n0[3], n1[3], d0 = 0, d1 = 0;
+  int i0 = 0, i1 = 0;
+  v3sub(A->p1, A->p0, u);
+  const real uu = dot3(u, u);
+  const int v0 = mtd_vertex(e, A->p0, n0, &d0, &i0), v1 = uu > 0.0 && mtd_vertex(e, A->p1, n1, &d1, &i1);
+  const int ok0 = v0 && (uu == 0.0 || dot3(n0, u) >= 0.0); /* p1 not deeper along n0 */
+  const int ok1 = v1 && dot3(n1, u) <= 0.0;
+  if (ok0 && (!ok1 || d0 <= d1)) {
+    v3cp(n, n0); *depth = d0; v3cp(pa, A->p0); orc_cvx_ill = i0;
+    return 1;
+  }
+  if (ok1) {
+    v3cp(n, n1); *depth = d1; v3cp(pa, A->p1); orc_cvx_ill = i1;
+    return 1;
+  }
+  if (!(uu > 0.0)) return 0;
+  /* the edge: the plane normal to u, basis (w1, w2); the shadow ellipse's matrix S = P diag(s) P^T */
+  real uh[3] = {u[0], u[1], u[2]}, a[3] = {0, 0, 0}, w1[3], w2[3];
+  v3unit(uh);
+  const int ax = fabs(uh[0]) <= fabs(uh[1]) ? (fabs(uh[0]) <= fabs(uh[2]) ? 0 : 2) : (fabs(uh[1]) <= fabs(uh[2]) ? 1 : 2);
+  a[ax] = 1.0;
+  cross3(uh, a, w1);
+  v3unit(w1);
+  cross3(uh, w1, w2);
+  const real s2[3] = {e[0] * e[0], e[1] * e[1], e[2] * e[2]};
+  real S00 = 0, S01 = 0, S11 = 0;
+  for (int i = 0; i < 3; i++) {
+    S00 += w1[i] * w1[i] * s2[i];
+    S01 += w1[i] * w2[i] * s2[i];
+    S11 += w2[i] * w2[i] * s2[i];
+  }
+  const real tr = 0.5 * (S00 + S11), df = 0.5 * (S00 - S11), rad = sqrt(df * df + S01 * S01);
+  const real l2[2] = {tr + rad, tr - rad};
+  real c0 = 1.0, c1 = 0.0; /* eigenvector of l2[0] in (w1, w2) */
+  if (rad > 1e-30) {
+    const real x = S01, y = l2[0] - S00, yl = sqrt(x * x + y * y);
+    if (yl > 1e-30) { c0 = x / yl; c1 = y / yl; }
+    else if (df < 0) { c0 = 0.0; c1 = 1.0; }
+  }
+  const real q0 = dot3(w1, A->p0), q1 = dot3(w2, A->p0);
+  const real q[2] = {c0 * q0 + c1 * q1, -c1 * q0 + c0 * q1};
+  if (!(l2[1] > 0.0) || !(q[0] * q[0] / l2[0] + q[1] * q[1] / l2[1] < 1.0)) return 0;
+  real smin;
+  const real lam = ell_root(2, l2, q, &smin);
+  const real g0 = q[0] / (l2[0] + lam), g1 = q[1] / (l2[1] + lam), gl = sqrt(g0 * g0 + g1 * g1);
+  if (!(gl > 0.0) || !isfinite(gl)) return 0;
+  const real m0 = (c0 * g0 - c1 * g1) / gl, m1 = (c1 * g0 + c0 * g1) / gl; /* back in (w1, w2) */
+  for (int i = 0; i < 3; i++) n[i] = m0 * w1[i] + m1 * w2[i];
+  *depth = -lam * gl;
+  /* the core's point: the segment point nearest the ellipsoid's support point along n */
+  real b[3], db[3];
+  ell_support(e, n, b);
+  v3sub(b, A->p0, db);
+  real t = dot3(db, u) / uu;
+  t = t < 0 ? 0 : (t > 1 ? 1 : t);
+  for (int i = 0; i < 3; i++) pa[i] = A->p0[i] + t * u[i];
+  orc_cvx_ill = (smin + lam) < 1e-3 * smin;
+  return 1;
+}
+
 /* one contact between core A (+ radius rA) and the ellipsoid e, object frame: GJK when the cores are
  * apart, MPR penetration when they overlap, the centre direction if MPR degenerates.  Normal from the
  * object to A. */
@@ -1447,6 +1556,10 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
     for (int a = 0; a < 3; a++) nrm[a] = gl2 > 1e-30 ? gr[a] / sqrt(gl2) : (pa[a] - pb[a]) / dist;
     for (int a = 0; a < 3; a++) pt[a] = 0.5 * ((pa[a] - nrm[a] * rA) + pb[a]);
     *d = dist - rA;
+    if (cvx_finite(pt, nrm, *d)) return;
+  } else if (A->kind == 0 && seg_mtd(A, e, nrm, &dist, pa)) { /* a segment core: the exact penetration */
+    for (int a = 0; a < 3; a++) pt[a] = pa[a] + 0.5 * dist * nrm[a] - 0.5 * rA * nrm[a];
+    *d = -dist - rA;
     if (cvx_finite(pt, nrm, *d)) return;
   } else if (cvx_mpr(A, e, x, pa)) {
     real l = sqrt(dot3(x, x));
