@@ -17,8 +17,8 @@ struct mg_sim {
   int32_t device;
   mg_state_views views;
   bool bound;
-  // work ordering of the fused step (K = 8 for the 32-lane instances, else off; MIGYM_ORDER_EVERY = K overrides
-  // at mg_sim_create): every K-th mg_env_step
+  // work ordering of the fused step (32-lane instances: K = 1 from 16,384 envs, 8 below; else off;
+  // MIGYM_ORDER_EVERY = K overrides at mg_sim_create): every K-th mg_env_step
   // first sorts the envs by their last step's constraint-row count, descending (k_order), and the step kernels
   // take their envs in that order -- teams of similar cost share a wave (the wave runs its slowest team's rows)
   // and the heavy envs start first.  Envs are independent, so every result is the same bit for bit.

@@ -573,9 +573,12 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   s->order_valid = false;
   s->d_order = nullptr;
   s->d_cost = nullptr;
-  // default: on for the 32-lane instances (ShadowHand, Humanoid: two teams per wave, +4% measured), off for the
-  // narrower ones (Ant's four 16-lane teams: no gain); MIGYM_ORDER_EVERY overrides (0: off)
-  s->order_every = mgi::team_size(s->host_model, s->params.max_contacts) >= 32 ? 8 : 0;
+  // default: on for the 32-lane instances (ShadowHand, Humanoid: two teams per wave), off for the narrower ones
+  // (Ant's four 16-lane teams: no gain); every step from 16,384 envs up (the last step's row counts are the best
+  // guess of this one's: Humanoid 32,768 K = 8 35.4 -> K = 1 36.5 M, ShadowHand 16,384 18.9 -> 19.4 M), every 8th
+  // below (ShadowHand 4,096: the sort's own launch outweighs the fresher order, 12.4 vs 12.2 M); MIGYM_ORDER_EVERY
+  // overrides (0: off)
+  s->order_every = mgi::team_size(s->host_model, s->params.max_contacts) >= 32 ? (num_envs >= 16384 ? 1 : 8) : 0;
   if (const char* e = getenv("MIGYM_ORDER_EVERY")) s->order_every = atoi(e);
   if (s->order_every > 0) {
     const int A = params->agents > 1 ? params->agents : 1;
