@@ -578,86 +578,85 @@ __device__ __forceinline__ bool cvx_mpr(const CvxShape& A, D3 e, D3& x, D3& pa) 
   return true;
 }
 
+}  // namespace mpr64
+
 // Exact penetration of a segment core overlapping the ellipsoid (the minimum translation), as the oracle's
-// seg_mtd: the vertex solutions (an end inside: the distance to the surface, valid when the other end is not
-// deeper along its normal) or the edge one (the shadow point's distance to the shadow ellipse's boundary in the
-// plane normal to u), each the nearest-boundary-point root lam in (-min s, 0] by Newton's method from 0.
-__device__ __forceinline__ creal ell_root(int k, const creal* s2, const creal* q) {
-  creal smin = s2[0];
-  for (int i = 1; i < k; i++) smin = fmin(smin, s2[i]);
-  creal lam = 0.0;
-  for (int it = 0; it < 64; it++) {
-    creal f = -1.0, fp = 0.0;
+// seg_mtd, in fp32: the vertex solutions (an end inside: its distance to the surface, valid when the other end is
+// not deeper along that normal; the first valid one is the minimum) or the edge one (the shadow point's distance to
+// the shadow ellipse's boundary in the plane normal to u), each the nearest-boundary-point root lam in (-min s, 0]
+// by Newton's method from 0.  A smooth function of the state (no portal decisions, unlike MPR), so fp32 suffices;
+// fp64 raised the egg kernel's spills (14 -> 29) and its traffic (309 -> 350 MB per launch).
+__device__ __forceinline__ float ell_root(int k, const float* s2, const float* q) {
+  float smin = s2[0];
+  for (int i = 1; i < k; i++) smin = fminf(smin, s2[i]);
+  float lam = 0.0f;
+  for (int it = 0; it < 32; it++) {
+    float f = -1.0f, fp = 0.0f;
     for (int i = 0; i < k; i++) {
-      const creal den = s2[i] + lam, r = s2[i] * q[i] * q[i] / (den * den);
+      const float den = s2[i] + lam, r = s2[i] * q[i] * q[i] / (den * den);
       f += r;
-      fp -= 2.0 * r / den;
+      fp -= 2.0f * r / den;
     }
-    if (!(fp < 0.0)) break;
-    creal nl = lam - f / fp;
-    if (!(nl > -smin)) nl = 0.5 * (lam - smin);
-    if (nl > 0.0) nl = 0.0;
-    const creal dl = fabs(nl - lam);
+    if (!(fp < 0.0f)) break;
+    float nl = lam - f / fp;
+    if (!(nl > -smin)) nl = 0.5f * (lam - smin);
+    if (nl > 0.0f) nl = 0.0f;
+    const float dl = fabsf(nl - lam);
     lam = nl;
-    if (dl <= 1e-14 * smin) break;
+    if (dl <= 1e-7f * smin) break;
   }
   return lam;
 }
-__device__ __forceinline__ bool mtd_vertex(D3 e, D3 p, D3& n, creal& depth) {
-  const creal s2[3] = {e.x * e.x, e.y * e.y, e.z * e.z};
-  if (!(p.x * p.x / s2[0] + p.y * p.y / s2[1] + p.z * p.z / s2[2] < 1.0)) return false;
-  const creal q[3] = {p.x, p.y, p.z};
-  const creal lam = ell_root(3, s2, q);
-  const D3 g = d3(p.x / (s2[0] + lam), p.y / (s2[1] + lam), p.z / (s2[2] + lam));
-  const creal gl = sqrt(dot(g, g));
-  if (!(gl > 0.0) || !isfinite(gl)) return false;
-  n = g * (1.0 / gl);
+__device__ __forceinline__ bool mtd_vertex(V3 e, V3 p, V3& n, float& depth) {
+  const float s2[3] = {e.x * e.x, e.y * e.y, e.z * e.z};
+  if (!(p.x * p.x / s2[0] + p.y * p.y / s2[1] + p.z * p.z / s2[2] < 1.0f)) return false;
+  const float q[3] = {p.x, p.y, p.z};
+  const float lam = ell_root(3, s2, q);
+  const V3 g = v3(p.x / (s2[0] + lam), p.y / (s2[1] + lam), p.z / (s2[2] + lam));
+  const float gl = sqrtf(dot(g, g));
+  if (!(gl > 0.0f) || !isfinite(gl)) return false;
+  n = g * (1.0f / gl);
   depth = -lam * gl;
   return true;
 }
-__device__ __forceinline__ bool seg_mtd(const CvxShape& A, D3 e, D3& n, creal& depth, D3& pa) {
-  const D3 u = A.p1 - A.p0;
-  const creal uu = dot(u, u);
-  D3 n0, n1;
-  creal d0 = 0.0, d1 = 0.0;
-  const bool v0 = mtd_vertex(e, A.p0, n0, d0), v1 = uu > 0.0 && mtd_vertex(e, A.p1, n1, d1);
-  const bool ok0 = v0 && (uu == 0.0 || dot(n0, u) >= 0.0), ok1 = v1 && dot(n1, u) <= 0.0;
-  if (ok0 && (!ok1 || d0 <= d1)) { n = n0; depth = d0; pa = A.p0; return true; }
-  if (ok1) { n = n1; depth = d1; pa = A.p1; return true; }
-  if (!(uu > 0.0)) return false;
-  const D3 uh = unit3(u);
-  const int ax = fabs(uh.x) <= fabs(uh.y) ? (fabs(uh.x) <= fabs(uh.z) ? 0 : 2) : (fabs(uh.y) <= fabs(uh.z) ? 1 : 2);
-  const D3 w1 = unit3(cross(uh, d3(ax == 0 ? 1.0 : 0.0, ax == 1 ? 1.0 : 0.0, ax == 2 ? 1.0 : 0.0)));
-  const D3 w2 = cross(uh, w1);
-  const creal sx = e.x * e.x, sy = e.y * e.y, sz = e.z * e.z;
-  const creal S00 = w1.x * w1.x * sx + w1.y * w1.y * sy + w1.z * w1.z * sz;
-  const creal S01 = w1.x * w2.x * sx + w1.y * w2.y * sy + w1.z * w2.z * sz;
-  const creal S11 = w2.x * w2.x * sx + w2.y * w2.y * sy + w2.z * w2.z * sz;
-  const creal tr = 0.5 * (S00 + S11), df = 0.5 * (S00 - S11), rad = sqrt(df * df + S01 * S01);
-  const creal l2[2] = {tr + rad, tr - rad};
-  creal c0 = 1.0, c1 = 0.0;
-  if (rad > 1e-30) {
-    const creal x = S01, y = l2[0] - S00, yl = sqrt(x * x + y * y);
-    if (yl > 1e-30) { c0 = x / yl; c1 = y / yl; }
-    else if (df < 0.0) { c0 = 0.0; c1 = 1.0; }
+__device__ __forceinline__ bool seg_mtd(const CvxShape& A, V3 e, V3& n, float& depth, V3& pa) {
+  const V3 u = A.p1 - A.p0;
+  const float uu = dot(u, u);
+  if (mtd_vertex(e, A.p0, n, depth) && (uu == 0.0f || dot(n, u) >= 0.0f)) { pa = A.p0; return true; }
+  if (!(uu > 0.0f)) return false;
+  if (mtd_vertex(e, A.p1, n, depth) && dot(n, u) <= 0.0f) { pa = A.p1; return true; }
+  const V3 uh = u * (1.0f / sqrtf(uu));
+  const int ax = fabsf(uh.x) <= fabsf(uh.y) ? (fabsf(uh.x) <= fabsf(uh.z) ? 0 : 2) : (fabsf(uh.y) <= fabsf(uh.z) ? 1 : 2);
+  V3 w1 = cross(uh, v3(ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f));
+  w1 = w1 * (1.0f / sqrtf(dot(w1, w1)));
+  const V3 w2 = cross(uh, w1);
+  const float sx = e.x * e.x, sy = e.y * e.y, sz = e.z * e.z;
+  const float S00 = w1.x * w1.x * sx + w1.y * w1.y * sy + w1.z * w1.z * sz;
+  const float S01 = w1.x * w2.x * sx + w1.y * w2.y * sy + w1.z * w2.z * sz;
+  const float S11 = w2.x * w2.x * sx + w2.y * w2.y * sy + w2.z * w2.z * sz;
+  const float tr = 0.5f * (S00 + S11), df = 0.5f * (S00 - S11), rad = sqrtf(df * df + S01 * S01);
+  const float l2[2] = {tr + rad, tr - rad};
+  float c0 = 1.0f, c1 = 0.0f;
+  if (rad > 1e-30f) {
+    const float x = S01, y = l2[0] - S00, yl = sqrtf(x * x + y * y);
+    if (yl > 1e-30f) { c0 = x / yl; c1 = y / yl; }
+    else if (df < 0.0f) { c0 = 0.0f; c1 = 1.0f; }
   }
-  const creal q0 = dot(w1, A.p0), q1 = dot(w2, A.p0);
-  const creal q[2] = {c0 * q0 + c1 * q1, -c1 * q0 + c0 * q1};
-  if (!(l2[1] > 0.0) || !(q[0] * q[0] / l2[0] + q[1] * q[1] / l2[1] < 1.0)) return false;
-  const creal lam = ell_root(2, l2, q);
-  const creal g0 = q[0] / (l2[0] + lam), g1 = q[1] / (l2[1] + lam), gl = sqrt(g0 * g0 + g1 * g1);
-  if (!(gl > 0.0) || !isfinite(gl)) return false;
-  const creal m0 = (c0 * g0 - c1 * g1) / gl, m1 = (c1 * g0 + c0 * g1) / gl;
+  const float q0 = dot(w1, A.p0), q1 = dot(w2, A.p0);
+  const float q[2] = {c0 * q0 + c1 * q1, -c1 * q0 + c0 * q1};
+  if (!(l2[1] > 0.0f) || !(q[0] * q[0] / l2[0] + q[1] * q[1] / l2[1] < 1.0f)) return false;
+  const float lam = ell_root(2, l2, q);
+  const float g0 = q[0] / (l2[0] + lam), g1 = q[1] / (l2[1] + lam), gl = sqrtf(g0 * g0 + g1 * g1);
+  if (!(gl > 0.0f) || !isfinite(gl)) return false;
+  const float m0 = (c0 * g0 - c1 * g1) / gl, m1 = (c1 * g0 + c0 * g1) / gl;
   n = w1 * m0 + w2 * m1;
   depth = -lam * gl;
-  const D3 b = ell_support(e, n);
-  creal t = dot(b - A.p0, u) / uu;
-  t = t < 0.0 ? 0.0 : (t > 1.0 ? 1.0 : t);
+  const V3 b = ell_support(e, n);
+  float t = dot(b - A.p0, u) / uu;
+  t = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
   pa = A.p0 + u * t;
   return true;
 }
-
-}  // namespace mpr64
 
 __device__ __forceinline__ bool cvx_finite(V3 p, V3 n, float d) {
   return isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(n.x) && isfinite(n.y) && isfinite(n.z) &&
@@ -700,6 +699,15 @@ __device__ __forceinline__ CvxHit cvx_contact_body(CvxShape A, float rA, V3 e, f
     o.pt = ((pa - o.nrm * rA) + pb) * 0.5f;
     o.d = dist - rA;
     if (cvx_finite(o.pt, o.nrm, o.d)) return o;
+  } else if (A.kind == 0) {  // a segment core: the exact penetration
+    V3 nd, pa2;
+    float dep;
+    if (seg_mtd(A, e, nd, dep, pa2)) {
+      o.nrm = nd;
+      o.pt = pa2 + nd * (0.5f * dep) - nd * (0.5f * rA);
+      o.d = -dep - rA;
+      if (cvx_finite(o.pt, o.nrm, o.d)) return o;
+    }
   } else {
     mpr64::CvxShape A64;
     A64.kind = A.kind;
@@ -711,14 +719,8 @@ __device__ __forceinline__ CvxHit cvx_contact_body(CvxShape A, float rA, V3 e, f
     for (int i = 0; i < 3; i++)
 #pragma unroll
       for (int k = 0; k < 3; k++) A64.R[i][k] = A.R[i][k];
-    mpr64::D3 x, pa, nd;
-    double dep;
-    if (A.kind == 0 && mpr64::seg_mtd(A64, mpr64::d3(e), nd, dep, pa)) {  // a segment core: the exact penetration
-      o.nrm = mpr64::f3(nd);
-      o.pt = mpr64::f3(pa + nd * (0.5 * dep) - nd * (0.5 * rA));
-      o.d = (float)(-dep - rA);
-      if (cvx_finite(o.pt, o.nrm, o.d)) return o;
-    } else if (mpr64::cvx_mpr(A64, mpr64::d3(e), x, pa)) {
+    mpr64::D3 x, pa;
+    if (mpr64::cvx_mpr(A64, mpr64::d3(e), x, pa)) {
       const double l = sqrt(mpr64::dot(x, x));
       if (l > 1e-9) {
         const mpr64::D3 nd = x * (-1.0 / l);

@@ -1243,7 +1243,8 @@ static int cvx_mpr(const cvx_shape* A, const real* e, real* x, real* pa) {
  * Newton's method from lam = 0 (the function is convex and decreasing there: one step lands left of the root,
  * the rest climb to it).  MPR's portal normal is a facet of a polytope approximation (a 1e-7 m change of the
  * state turned it by 1e-2 rad for a capsule 1 cm deep); this solution moves smoothly with the state away from
- * the medial axis, where orc_cvx_ill marks it.  The kernel (convex.hpp mpr64::seg_mtd) runs the same in fp64. */
+ * the medial axis, where orc_cvx_ill marks it.  The kernel (convex.hpp seg_mtd) runs the same in fp32: the result
+ * is a smooth function of the state, with no portal decisions for fp32 to take differently. */
 static real ell_root(int k, const real* s2, const real* q, real* smin_out) {
   real smin = s2[0];
   for (int i = 1; i < k; i++) smin = fmin(smin, s2[i]);
@@ -1282,22 +1283,21 @@ static int mtd_vertex(const real* e, const real* p, real* n, real* depth, int* i
   return 1;
 }
 static int seg_mtd(const cvx_shape* A, const real* e, real* n, real* depth, real* pa) {
-  real u[3], n0[3], n1[3], d0 = 0, d1 = 0;
-  int i0 = 0, i1 = 0;
+  real u[3];
+  int ill = 0;
   v3sub(A->p1, A->p0, u);
   const real uu = dot3(u, u);
-  const int v0 = mtd_vertex(e, A->p0, n0, &d0, &i0), v1 = uu > 0.0 && mtd_vertex(e, A->p1, n1, &d1, &i1);
-  const int ok0 = v0 && (uu == 0.0 || dot3(n0, u) >= 0.0); /* p1 not deeper along n0 */
-  const int ok1 = v1 && dot3(n1, u) <= 0.0;
-  if (ok0 && (!ok1 || d0 <= d1)) {
-    v3cp(n, n0); *depth = d0; v3cp(pa, A->p0); orc_cvx_ill = i0;
-    return 1;
-  }
-  if (ok1) {
-    v3cp(n, n1); *depth = d1; v3cp(pa, A->p1); orc_cvx_ill = i1;
+  /* a valid vertex solution (the other end not deeper along its normal) is the minimum -- both valid: equal
+   * depths -- so the first valid one is taken */
+  if (mtd_vertex(e, A->p0, n, depth, &ill) && (uu == 0.0 || dot3(n, u) >= 0.0)) {
+    v3cp(pa, A->p0); orc_cvx_ill = ill;
     return 1;
   }
   if (!(uu > 0.0)) return 0;
+  if (mtd_vertex(e, A->p1, n, depth, &ill) && dot3(n, u) <= 0.0) {
+    v3cp(pa, A->p1); orc_cvx_ill = ill;
+    return 1;
+  }
   /* the edge: the plane normal to u, basis (w1, w2); the shadow ellipse's matrix S = P diag(s) P^T */
   real uh[3] = {u[0], u[1], u[2]}, a[3] = {0, 0, 0}, w1[3], w2[3];
   v3unit(uh);
@@ -1557,10 +1557,12 @@ static void cvx_contact(const cvx_shape* A0, real rA, const real* e, real cut, r
     for (int a = 0; a < 3; a++) pt[a] = 0.5 * ((pa[a] - nrm[a] * rA) + pb[a]);
     *d = dist - rA;
     if (cvx_finite(pt, nrm, *d)) return;
-  } else if (A->kind == 0 && seg_mtd(A, e, nrm, &dist, pa)) { /* a segment core: the exact penetration */
-    for (int a = 0; a < 3; a++) pt[a] = pa[a] + 0.5 * dist * nrm[a] - 0.5 * rA * nrm[a];
-    *d = -dist - rA;
-    if (cvx_finite(pt, nrm, *d)) return;
+  } else if (A->kind == 0) { /* a segment core: the exact penetration (no MPR fallback, as the kernel) */
+    if (seg_mtd(A, e, nrm, &dist, pa)) {
+      for (int a = 0; a < 3; a++) pt[a] = pa[a] + 0.5 * dist * nrm[a] - 0.5 * rA * nrm[a];
+      *d = -dist - rA;
+      if (cvx_finite(pt, nrm, *d)) return;
+    }
   } else if (cvx_mpr(A, e, x, pa)) {
     real l = sqrt(dot3(x, x));
     if (l > 1e-9) {
