@@ -636,12 +636,11 @@ __device__ __forceinline__ bool seg_mtd(const CvxShape& A, V3 e, V3& n, float& d
   const float S11 = w2.x * w2.x * sx + w2.y * w2.y * sy + w2.z * w2.z * sz;
   const float tr = 0.5f * (S00 + S11), df = 0.5f * (S00 - S11), rad = sqrtf(df * df + S01 * S01);
   const float l2[2] = {tr + rad, tr - rad};
-  float c0 = 1.0f, c1 = 0.0f;
+  float c0 = 1.0f, c1 = 0.0f;  // eigenvector of l2[0] from the row without cancellation (the oracle's note)
   if (rad > 1e-30f) {
-    const float x = S01, y = l2[0] - S00, yl = sqrtf(x * x + y * y);
+    const float x = df >= 0.0f ? df + rad : S01, y = df >= 0.0f ? S01 : rad - df, yl = sqrtf(x * x + y * y);
     if (yl > 1e-30f) { c0 = x / yl; c1 = y / yl; }
-    else if (df < 0.0f) { c0 = 0.0f; c1 = 1.0f; }
-  }
+  } else if (df < 0.0f) { c0 = 0.0f; c1 = 1.0f; }
   const float q0 = dot(w1, A.p0), q1 = dot(w2, A.p0);
   const float q[2] = {c0 * q0 + c1 * q1, -c1 * q0 + c0 * q1};
   if (!(l2[1] > 0.0f) || !(q[0] * q[0] / l2[0] + q[1] * q[1] / l2[1] < 1.0f)) return false;

@@ -1315,12 +1315,13 @@ static int seg_mtd(const cvx_shape* A, const real* e, real* n, real* depth, real
   }
   const real tr = 0.5 * (S00 + S11), df = 0.5 * (S00 - S11), rad = sqrt(df * df + S01 * S01);
   const real l2[2] = {tr + rad, tr - rad};
-  real c0 = 1.0, c1 = 0.0; /* eigenvector of l2[0] in (w1, w2) */
+  real c0 = 1.0, c1 = 0.0; /* eigenvector of l2[0] in (w1, w2), from the row without cancellation: (df + rad, S01)
+                              * for df >= 0, (S01, rad - df) otherwise (l2[0] - S00 = rad - df loses all of it in fp32
+                              * when S01 is small and df > 0) */
   if (rad > 1e-30) {
-    const real x = S01, y = l2[0] - S00, yl = sqrt(x * x + y * y);
+    const real x = df >= 0 ? df + rad : S01, y = df >= 0 ? S01 : rad - df, yl = sqrt(x * x + y * y);
     if (yl > 1e-30) { c0 = x / yl; c1 = y / yl; }
-    else if (df < 0) { c0 = 0.0; c1 = 1.0; }
-  }
+  } else if (df < 0) { c0 = 0.0; c1 = 1.0; }
   const real q0 = dot3(w1, A->p0), q1 = dot3(w2, A->p0);
   const real q[2] = {c0 * q0 + c1 * q1, -c1 * q0 + c0 * q1};
   if (!(l2[1] > 0.0) || !(q[0] * q[0] / l2[0] + q[1] * q[1] / l2[1] < 1.0)) return 0;
