@@ -83,6 +83,9 @@ def lib_f32():
         l.orc_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
                                    C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32, C.c_int32]
         l.orc_hand_env_step.argtypes = l.orc_env_step.argtypes
+        l.orc_simulate.argtypes = [P, C.POINTER(_abi.SimParams), C.c_int32, P, P, P, P, P, C.c_int32]
+        l.orc_simulate_views.argtypes = [P, C.POINTER(_abi.SimParams), C.c_int32, C.POINTER(_abi.StateViews),
+                                         C.c_int32]
         _lib32 = l
     return _lib32
 
@@ -99,9 +102,9 @@ def p(a):
     return None if a is None else a.ctypes.data
 
 
-def simulate(model_np, sp, root, dof, act=None, sensors=None, dof_force=None, threads=0):
+def simulate(model_np, sp, root, dof, act=None, sensors=None, dof_force=None, threads=0, fp32=False):
     n = root.shape[0]
-    lib().orc_simulate(model_np.ctypes.data, C.byref(sp), n, p(root), p(dof), p(act), p(sensors), p(dof_force),
+    (lib_f32() if fp32 else lib()).orc_simulate(model_np.ctypes.data, C.byref(sp), n, p(root), p(dof), p(act), p(sensors), p(dof_force),
                        threads)
 
 
@@ -356,9 +359,9 @@ class HandHostEnv:
         v, b = self.views(), self.buffers(seed, step, env_offset)
         lib().orc_hand_post_physics(model_np.ctypes.data, C.byref(tp), C.byref(v), C.byref(b), self.n)
 
-    def simulate(self, model_np, sp, threads=0):
+    def simulate(self, model_np, sp, threads=0, fp32=False):
         v = self.views()
-        lib().orc_simulate_views(model_np.ctypes.data, C.byref(sp), self.n, C.byref(v), threads)
+        (lib_f32() if fp32 else lib()).orc_simulate_views(model_np.ctypes.data, C.byref(sp), self.n, C.byref(v), threads)
 
     def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0, fp32=False):
         v, b = self.views(), self.buffers(seed, step, env_offset)

@@ -130,6 +130,63 @@ REACH_CAP = 0.05
 SENS_CAP = 0.01      # and at most this fraction by the oracle-sensitivity fallback
 
 
+def spin_bad(ra, da, rb, db, root0, dof0, dt, atol_p=2e-4, atol_v=2e-3, rtol_v=2e-3, k_spin=1e-4):
+    """per env of the fast-spin stress states (tests/test_gpu_parity.py, fast = 1): result a vs the checker's b
+    (root states (n, 13), dof states (n, ndof, 2)) from the same pre-step state (root0, dof0).  A velocity may
+    differ by atol_v + rtol_v |v| + k_spin x the env's largest initial rate (fp32 rounding of the spin-sized
+    Coriolis and cap terms, |w|^2 h, reaches every velocity of the env, also the ones that end near 0); a position
+    by atol_p + dt x the tolerance of its velocity (the step integrates q' = q + dt v', the quaternion with
+    |dq| <= dt |dw| / 2)"""
+    n = len(ra)
+    spin = np.maximum(np.abs(dof0[..., 1]).reshape(n, -1).max(axis=1), np.abs(root0[:, 10:13]).max(axis=1))
+    base = atol_v + k_spin * spin[:, None]
+    tv_d = base + rtol_v * np.abs(db[..., 1])
+    tv_r = base + rtol_v * np.abs(rb[:, 7:13])
+    bad = (np.abs(da[..., 1] - db[..., 1]) > tv_d).any(axis=1)
+    bad |= (np.abs(ra[:, 7:13] - rb[:, 7:13]) > tv_r).any(axis=1)
+    bad |= (np.abs(da[..., 0] - db[..., 0]) > atol_p + dt * tv_d).any(axis=1)
+    bad |= (np.abs(ra[:, 0:3] - rb[:, 0:3]) > atol_p + dt * tv_r[:, 0:3]).any(axis=1)
+    bad |= (np.abs(ra[:, 3:7] - rb[:, 3:7]) > atol_p + 0.5 * dt * tv_r[:, 3:6].max(axis=1, keepdims=True)).any(axis=1)
+    return bad
+
+
+def first_substep_drift(mnp, sp, root0, dof0, act, floor=1e-6):
+    """per env: how far apart an fp32 and an fp64 first substep put the positions (root position, joint
+    positions; max abs), measured with the oracle's fp32 build (liboracle_f32) against the checker, at least
+    `floor`: the input perturbation simulate_sensitive uses (the rest of the step starts from states this far apart)"""
+    sp1 = copy.copy(sp)
+    sp1.substeps, sp1.dt = 1, sp.dt / sp.substeps
+    out = []
+    for fp32 in (False, True):
+        r, d = np.array(root0, np.float32), np.array(dof0, np.float32)
+        O.simulate(mnp, sp1, r, d, np.ascontiguousarray(act, np.float32), threads=8, fp32=fp32)
+        out.append((r.astype(np.float64), d.astype(np.float64)))
+    (r64, d64), (r32, d32) = out
+    n = len(r64)
+    dq = np.maximum(np.abs(r32[:, 0:3] - r64[:, 0:3]).max(axis=1),
+                    np.abs(d32[..., 0] - d64[..., 0]).reshape(n, -1).max(axis=1))
+    return np.maximum(dq, floor)
+
+
+def simulate_sensitive(mnp, sp, root0, dof0, act, i, out_a, out_b, eps=1e-6, ratio=0.25):
+    """the oracle's own sensitivity at env i of a direct simulate from (root0, dof0, act): one simulate of env i
+    alone, once as given and once with its positions (root position, joint positions) moved by eps (e.g. its
+    first_substep_drift); True if its result (root states and dof states) moves by >= ratio x the gap
+    |out_a - out_b| of env i"""
+    runs = []
+    for pert in (0.0, eps):
+        r = np.array(root0[i:i + 1], np.float64)
+        d = np.array(dof0[i:i + 1], np.float64)
+        r[:, 0:3] += pert
+        d[..., 0] += pert
+        r, d = r.astype(np.float32), d.astype(np.float32)
+        O.simulate(mnp, sp, r, d, np.ascontiguousarray(act[i:i + 1], np.float32))
+        runs.append(np.concatenate([r.ravel(), d.ravel()]).astype(np.float64))
+    moved = np.abs(runs[1] - runs[0]).max()
+    gap = np.abs(np.asarray(out_a[i], np.float64).ravel() - np.asarray(out_b[i], np.float64).ravel()).max()
+    return moved >= ratio * gap
+
+
 def step_flags(mnp, sp, host, delta=STEP_DELTA, df=STEP_DF):
     """per env: orc_step_flips of the physics input `host` holds (a HostEnv with act_eff / a HandHostEnv after
     pre_physics, optionally with env_props): bit 1 contact threshold in use, 2 limit threshold in use, 4 drive

@@ -296,17 +296,13 @@ def _forearm_world(spec, h):
     return h.root[0, 0, 0:3] + Rn @ np.asarray(g.pos), Rn @ Rotation.from_quat(np.asarray(g.quat, np.float64)).as_matrix()
 
 
-@pytest.mark.parametrize("kind", ["block", "pen"])
-def test_hand_physics_hull_exact_matches_oracle(lib, kind):
-    """A6, the exact hull candidate (hull.hpp / oracle hull_core_contact): the cube with an edge across one of the
+def hull_exact_states(kind, n, rng):
+    """the exact-hull placements (hull.hpp / oracle hull_core_contact): the cube with an edge across one of the
     hull's upper edges, or the pen lying across one of its upper faces with its ends overhanging, at gaps of
-    -0.5 .. 1.5 mm, where the vertex-face candidates see nothing (test_oracle_hand_physics.py KATs).  GPU vs
-    oracle like the palm states; most envs must be in contact with the hull."""
+    -0.5 .. 1.5 mm (tests/test_step_flags.py uses them on the CPU too)"""
     from scipy.spatial.transform import Rotation
     from test_oracle_hand_physics import _cube_across_edge, _hull_edges
     spec, sp, tp = setup(kind=kind)
-    n = 256
-    rng = np.random.default_rng(13)
     h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
     h.dof[:, :, 0] = 0.0   # fingers straight and away from the forearm
     c, R = _forearm_world(spec, h)
@@ -335,6 +331,18 @@ def test_hand_physics_hull_exact_matches_oracle(lib, kind):
     ob[:, 7:13] = rng.normal(0, 0.05, (n, 6))
     # these placements sit on the hull's features by construction (an edge across an edge, a segment across a
     # face next to its ridges), so the feature-decision band (bit 16) reaches more of them than of random states
+    return spec, sp, tp, h
+
+
+@pytest.mark.parametrize("kind", ["block", "pen"])
+def test_hand_physics_hull_exact_matches_oracle(lib, kind):
+    """A6, the exact hull candidate (hull.hpp / oracle hull_core_contact): the cube with an edge across one of the
+    hull's upper edges, or the pen lying across one of its upper faces with its ends overhanging, at gaps of
+    -0.5 .. 1.5 mm, where the vertex-face candidates see nothing (test_oracle_hand_physics.py KATs).  GPU vs
+    oracle like the palm states; most envs must be in contact with the hull."""
+    n = 256
+    rng = np.random.default_rng(13)
+    spec, sp, tp, h = hull_exact_states(kind, n, rng)
     mnp, h0 = _physics_vs_oracle(lib, spec, sp, h, rng, n, reach_cap=0.10)
     node = spec.geoms[spec.hull["geom"]].node
     touching = 0

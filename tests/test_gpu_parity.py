@@ -270,17 +270,15 @@ def test_physics_step_matches_oracle(lib, task, n, z, fast):
     if fast:   # every env within tolerance unless its step clipped a rate to an ill-conditioned cap interval end
         pre = O.HostEnv(tp, spec, n)
         pre.root[:], pre.dof[:], pre.act_eff[:] = root, dof, act
-        # velocities: fp32 rounding of the spin-sized Coriolis / cap terms (|w|^2 h) adds ~1e-4 x the env's largest
-        # initial rate to the absolute error of every velocity, also of the ones that end near 0
-        spin = np.maximum(np.abs(dof[..., 1]).max(axis=1), np.abs(root[:, 10:13]).max(axis=1))
-        bad = np.zeros(n, bool)
-        for name, a, b, atol, rtol in checks:
-            at = atol + (1e-4 * spin if "vel" in name or "twist" in name else 0.0)
-            a2, b2 = a.reshape(n, -1), b.reshape(n, -1)
-            bad |= ~((np.abs(a2 - b2) <= at[:, None] + rtol * np.abs(b2)).all(axis=1)) if np.ndim(at) else PS.env_bad(a, b, atol, rtol)
+        bad = PS.spin_bad(rg, dg, r_h, d_h, root, dof, sp.dt)
         # every env spins its root above the cap, so each hinge below a clamped link has |w_p| = W and an interval
         # of half-width |a . w_p|: bit 64 reaches ~3% (Ant) / ~8% (Humanoid) of these stress states, hence 12%
-        PS.assert_steps_explained(test, bad[None], PS.step_flags(mnp, sp, pre)[None], reach_cap=0.12)
+        # and the oracle-sensitivity fallback where the dynamics are stiff (tests/test_step_flags.py)
+        og = np.concatenate([rg, dg.reshape(n, -1)], 1)
+        oh = np.concatenate([r_h, d_h.reshape(n, -1)], 1)
+        drift = PS.first_substep_drift(mnp, sp, root, dof, act)
+        sens = lambda t, i: PS.simulate_sensitive(mnp, sp, root, dof, act, i, og, oh, eps=drift[i])
+        PS.assert_steps_explained(test, bad[None], PS.step_flags(mnp, sp, pre)[None], sens=sens, reach_cap=0.12)
         return
     np.testing.assert_allclose(rg[:, 0:7], r_h[:, 0:7], atol=2e-4)
     np.testing.assert_allclose(dg[..., 0], d_h[..., 0], atol=2e-4)
