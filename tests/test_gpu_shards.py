@@ -95,3 +95,46 @@ def test_work_queue_items_equal_the_static_grid(task, obj):
             assert torch.equal(rew, w[lo:hi]), f"{task}/{obj} shard {r} step {k}: rew differ"
             assert torch.equal(reset, d[lo:hi]), f"{task}/{obj} shard {r} step {k}: reset differ"
         sh.close()
+
+
+@pytest.mark.parametrize("task,obj", [("Ant", "block"), ("Humanoid", "block"), ("MAAnt", "block"), ("Cartpole", "block"),
+                                      ("ShadowHand", "block"), ("ShadowHand", "egg"), ("ShadowHand", "pen")])
+def test_ragged_shards_equal_slices_of_one_rollout(task, obj):
+    """Ragged env counts: shards of 1, 7, 67 and 225 envs at offsets 0, 1, 8 and 75 of one 300-env rollout (none a
+    multiple of a wave's teams or of a block's waves, so every shard ends in a partly filled wave and the kernels'
+    `slot < n` masks decide which lanes write).  Every shard must be the bit-identical slice of the full rollout
+    over 6 steps with resets, and the full rollout must stay finite."""
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    steps, n = 6, 300
+    cuts = [(0, 1), (1, 8), (8, 75), (75, 300)]
+
+    def make(num, offset):
+        cfg = configs.task_config(task, num, sim_device=DEV)
+        cfg["env_offset"] = offset
+        if task == "ShadowHand":
+            cfg["env"]["objectType"] = obj
+        return migym.make(seed=7, task=task, num_envs=num, sim_device=DEV, rl_device=DEV, headless=True,
+                          cfg={"task": cfg})
+
+    full = make(n, 0)
+    A = full.num_agents
+    g = torch.Generator(device=DEV).manual_seed(9)
+    acts = [torch.rand((full.num_actors, full.num_actions), device=DEV, generator=g) * 2.4 - 1.2 for _ in range(steps)]
+    ref = []
+    for a in acts:
+        obs, rew, reset, _ = full.step(a)
+        ref.append((obs["obs"].clone(), rew.clone(), reset.clone()))
+    full.close()
+    del full
+    assert all(torch.isfinite(o).all() for o, _, _ in ref)
+    for lo_e, hi_e in cuts:
+        sh = make(hi_e - lo_e, lo_e)
+        lo, hi = lo_e * A, hi_e * A
+        for k, a in enumerate(acts):
+            obs, rew, reset, _ = sh.step(a[lo:hi].contiguous())
+            o, w, d = ref[k]
+            assert obs["obs"].shape[0] == hi - lo
+            assert torch.equal(obs["obs"], o[lo:hi]), f"{task} envs [{lo_e}, {hi_e}) step {k}: obs differ"
+            assert torch.equal(rew, w[lo:hi]), f"{task} envs [{lo_e}, {hi_e}) step {k}: rew differ"
+            assert torch.equal(reset, d[lo:hi]), f"{task} envs [{lo_e}, {hi_e}) step {k}: reset differ"
+        sh.close()
