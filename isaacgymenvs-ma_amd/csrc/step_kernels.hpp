@@ -223,7 +223,7 @@ __device__ __forceinline__ void env_step_item(
     // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
     const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
     for (int st = 0; st < nsub; st++) t.substep();
-    t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
+    t.template outputs<true>(L.u.sv.st.sens, L.u.sv.st.dforce);  // no rigid-body states here: pose-only FK
     t.stage_state();
   }
   mg::wsync();

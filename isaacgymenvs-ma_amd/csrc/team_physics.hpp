@@ -792,7 +792,10 @@ struct Team {
   // positions / velocities published once in LDS.  The operations per link are those of a level-by-level pass
   // (R = R_parent R_rest rot(axis, q), x, S, V = V_parent + S qd), so the results are bit-identical to it; the
   // deeper lanes repeat their ancestors' few dozen FMAs instead of waiting for one LDS round trip and wave
-  // barrier per level.  R, x, V, S are then stored for the later phases.
+  // barrier per level.  R, x, V, S are then stored for the later phases.  POSE: R and x only (the post-step
+  // sensor frames of the fused locomotion step, which reads no velocity or axis after it; R and x are computed
+  // by the same operations either way)
+  template <bool POSE = false>
   __device__ __forceinline__ void fk() {
     if (OBJ) oR = quat_to_mat(oq[0], oq[1], oq[2], oq[3]);
     const M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
@@ -800,10 +803,10 @@ struct Team {
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) s->R[0][3 * a + b] = Rr.m[a][b];
       s->x[0][0] = p0.x; s->x[0][1] = p0.y; s->x[0][2] = p0.z;
-      if (!freeb)
+      if (!freeb && !POSE)
         for (int k = 0; k < 6; k++) s->V[0][k] = 0.0f;
     }
-    if (freeb && tl < 6) s->V[0][tl] = nu;
+    if (freeb && tl < 6 && !POSE) s->V[0][tl] = nu;
     // (q, qd) and (sin q, cos q) per node in the union storage (free here: the ABA's child slots are written
     // after): each lane evaluates its own joint's sine and cosine once, its descendants read them
     float* qv = &s->u.slot[0][0];
@@ -825,7 +828,7 @@ struct Team {
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) R.m[a][b] = s->R[0][3 * a + b];
       x = ld3(s->x[0]);
-      V = sv(ld3(s->V[0]), ld3(s->V[0] + 3));
+      if (!POSE) V = sv(ld3(s->V[0]), ld3(s->V[0] + 3));
     }
     if (node > 0) {
       const V3 x0 = x;
@@ -842,23 +845,27 @@ struct Team {
         if (mt->jtype[k] == MG_JT_HINGE) {
           R = mul(Rp0, axis_angle_sc(ax, k == node ? sn : sc[2 * k], k == node ? cs : sc[2 * k + 1]));
           x = x + tp;
-          const V3 sw = mul(R, ax);
-          S = sv(sw, cross(x - x0, sw));
+          if (!POSE) {
+            const V3 sw = mul(R, ax);
+            S = sv(sw, cross(x - x0, sw));
+          }
         } else {
           R = Rp0;
           const V3 sw = mul(Rp0, ax);
           x = x + tp + sw * qk;
-          S = sv(v3(0, 0, 0), sw);
+          if (!POSE) S = sv(v3(0, 0, 0), sw);
         }
-        V = V + S * vk;
+        if (!POSE) V = V + S * vk;
       }
       for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) s->R[node][3 * a + b] = R.m[a][b];
       s->x[node][0] = x.x; s->x[node][1] = x.y; s->x[node][2] = x.z;
-      s->V[node][0] = V.a.x; s->V[node][1] = V.a.y; s->V[node][2] = V.a.z;
-      s->V[node][3] = V.l.x; s->V[node][4] = V.l.y; s->V[node][5] = V.l.z;
-      s->S[node][0] = S.a.x; s->S[node][1] = S.a.y; s->S[node][2] = S.a.z;
-      s->S[node][3] = S.l.x; s->S[node][4] = S.l.y; s->S[node][5] = S.l.z;
+      if (!POSE) {
+        s->V[node][0] = V.a.x; s->V[node][1] = V.a.y; s->V[node][2] = V.a.z;
+        s->V[node][3] = V.l.x; s->V[node][4] = V.l.y; s->V[node][5] = V.l.z;
+        s->S[node][0] = S.a.x; s->S[node][1] = S.a.y; s->S[node][2] = S.a.z;
+        s->S[node][3] = S.l.x; s->S[node][4] = S.l.y; s->S[node][5] = S.l.z;
+      }
     }
     wsync();
   }
@@ -2593,8 +2600,11 @@ struct Team {
       o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
     }
   }
+  // POSE: the caller reads no link velocity / axis afterwards (k_env_step; k_simulate and k_hand_step write the
+  // rigid-body states from them)
+  template <bool POSE = false>
   __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out) {
-    fk();  // post-step pose for the sensor body frames
+    fk<POSE>();  // post-step pose for the sensor body frames
     const float ih = prcp(h);  // impulses -> forces
     const int NS = m->num_sensors;
     if constexpr (T >= 32 && !OBJ) {
