@@ -223,7 +223,10 @@ __device__ __forceinline__ void env_step_item(
     // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
     const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
     for (int st = 0; st < nsub; st++) t.substep();
-    t.template outputs<true>(L.u.sv.st.sens, L.u.sv.st.dforce);  // no rigid-body states here: pose-only FK
+    // no rigid-body states here: pose-only FK; DOF forces only where something reads them (the bound view, or the
+    // Humanoid's observation: the reference's Ant and Cartpole never acquire a DOF-force tensor)
+    t.template outputs<true>(L.u.sv.st.sens,
+                             (v.dof_force || tp.task_id == MG_TASK_HUMANOID) ? L.u.sv.st.dforce : nullptr);
     t.stage_state();
   }
   mg::wsync();
