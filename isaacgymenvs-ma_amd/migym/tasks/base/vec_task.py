@@ -177,7 +177,7 @@ class VecTask(DomainRandomizationMixin, Env):
         v = _abi.StateViews()
         v.root_states, v.dof_state = _abi.ptr(self.root_states), _abi.ptr(self.dof_state)
         v.dof_actuation, v.sensors = _abi.ptr(self.dof_actuation), _abi.ptr(self.sensor_tensor)
-        # the DOF-force view only where the reference acquires one (humanoid.py:240-245); Ant and Cartpole never do
+        # the DOF-force view only where the reference acquires one (humanoid.py:85-86); Ant and Cartpole never do
         # (ant.py, cartpole.py), so the fused step skips their DOF forces and dof_force_tensor stays zero
         v.dof_force = _abi.ptr(self.dof_force_tensor) if self.task_name == "Humanoid" else None
         v.rigid_body_states = None
