@@ -168,11 +168,11 @@ def first_substep_drift(mnp, sp, root0, dof0, act, floor=1e-6):
     return np.maximum(dq, floor)
 
 
-def simulate_sensitive(mnp, sp, root0, dof0, act, i, out_a, out_b, eps=1e-6, ratio=0.25):
+def simulate_sensitive(mnp, sp, root0, dof0, act, i, out_a, out_b, eps=1e-6, ratio=0.25, log=None):
     """the oracle's own sensitivity at env i of a direct simulate from (root0, dof0, act): one simulate of env i
     alone, once as given and once with its positions (root position, joint positions) moved by eps (e.g. its
     first_substep_drift); True if its result (root states and dof states) moves by >= ratio x the gap
-    |out_a - out_b| of env i"""
+    |out_a - out_b| of env i (log: a list collecting (i, moved, gap))"""
     runs = []
     for pert in (0.0, eps):
         r = np.array(root0[i:i + 1], np.float64)
@@ -184,6 +184,8 @@ def simulate_sensitive(mnp, sp, root0, dof0, act, i, out_a, out_b, eps=1e-6, rat
         runs.append(np.concatenate([r.ravel(), d.ravel()]).astype(np.float64))
     moved = np.abs(runs[1] - runs[0]).max()
     gap = np.abs(np.asarray(out_a[i], np.float64).ravel() - np.asarray(out_b[i], np.float64).ravel()).max()
+    if log is not None:
+        log.append((i, float(moved), float(gap)))
     return moved >= ratio * gap
 
 

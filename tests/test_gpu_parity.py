@@ -224,9 +224,26 @@ def random_states(spec, tp, n, rng, z_range, contact_frac=0.5):
     return root, dof
 
 
+def _gpu_simulate(lib, mnp, sp, root, dof, act, ns):
+    """one mg_sim_simulate of the states on the device: (root, dof, sensors, dof force) after it"""
+    n = len(root)
+    r_d, d_d, a_d = T(root), T(dof), T(act)
+    s_d, f_d = torch.zeros((n, ns * 6), device=DEV), torch.zeros((n, dof.shape[1]), device=DEV)
+    h = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(h)), lib)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force = P(r_d), P(d_d), P(a_d), P(s_d), P(f_d)
+    _abi.check(lib.mg_sim_bind(h, C.byref(v)), lib)
+    _abi.check(lib.mg_sim_simulate(h, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(h)
+    return r_d.cpu().numpy(), d_d.cpu().numpy(), s_d.cpu().numpy(), f_d.cpu().numpy()
+
+
 @pytest.mark.parametrize("task,n,z,fast", [("Ant", 512, (0.25, 0.7), 0), ("Humanoid", 256, (0.6, 1.4), 0),
                                            ("Cartpole", 256, (2.0, 2.0), 0), ("Ant", 256, (4.0, 5.0), 1),
-                                           ("Humanoid", 256, (4.0, 5.0), 1), ("Cartpole", 256, (2.0, 2.0), 1)])
+                                           ("Humanoid", 256, (4.0, 5.0), 1), ("Cartpole", 256, (2.0, 2.0), 1),
+                                           ("Humanoid", 4096, (4.0, 5.0), 1)])
 def test_physics_step_matches_oracle(lib, task, n, z, fast):
     """one gym.simulate from random states; fast = 1: joint rates ~N(0, 40) and root spins ~N(0, 40) in the
     air, so that the link angular-velocity cap (max_angular_velocity) and the link damping act in most envs"""
@@ -247,18 +264,7 @@ def test_physics_step_matches_oracle(lib, task, n, z, fast):
     mnp = M.pack_model(spec)
     r_h, d_h = root.copy(), dof.copy()
     O.simulate(mnp, sp, r_h, d_h, act, sens_h, dfor_h, threads=8)
-    # device
-    r_d, d_d, a_d = T(root), T(dof), T(act)
-    s_d, f_d = torch.zeros((n, ns * 6), device=DEV), torch.zeros((n, spec.num_dofs), device=DEV)
-    h = C.c_void_p()
-    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(h)), lib)
-    v = _abi.StateViews()
-    v.root_states, v.dof_state, v.dof_actuation, v.sensors, v.dof_force = P(r_d), P(d_d), P(a_d), P(s_d), P(f_d)
-    _abi.check(lib.mg_sim_bind(h, C.byref(v)), lib)
-    _abi.check(lib.mg_sim_simulate(h, stream()), lib)
-    torch.cuda.synchronize()
-    lib.mg_sim_destroy(h)
-    rg, dg = r_d.cpu().numpy(), d_d.cpu().numpy()
+    rg, dg, sg, fg = _gpu_simulate(lib, mnp, sp, root, dof, act, ns)
     test = f"test_physics_step_matches_oracle[{task}{'-fast' if fast else ''}]"
     if fast:   # the cap acted: some link ends at |w| = W (root spin or a joint rate above it)
         W = float(mnp["link_max_ang_vel"])
@@ -276,20 +282,29 @@ def test_physics_step_matches_oracle(lib, task, n, z, fast):
         # and the oracle-sensitivity fallback where the dynamics are stiff (tests/test_step_flags.py)
         og = np.concatenate([rg, dg.reshape(n, -1)], 1)
         oh = np.concatenate([r_h, d_h.reshape(n, -1)], 1)
-        drift = PS.first_substep_drift(mnp, sp, root, dof, act)
-        sens = lambda t, i: PS.simulate_sensitive(mnp, sp, root, dof, act, i, og, oh, eps=drift[i])
-        PS.assert_steps_explained(test, bad[None], PS.step_flags(mnp, sp, pre)[None], sens=sens, reach_cap=0.12)
+        # the perturbation: how far apart the kernel's and the checker's first substep put each env's positions
+        sp1 = copy.copy(sp)
+        sp1.substeps, sp1.dt = 1, sp.dt / sp.substeps
+        r1g, d1g, _, _ = _gpu_simulate(lib, mnp, sp1, root, dof, act, ns)
+        r1h, d1h = root.copy(), dof.copy()
+        O.simulate(mnp, sp1, r1h, d1h, act, threads=8)
+        drift = np.maximum(np.maximum(np.abs(r1g[:, 0:3] - r1h[:, 0:3]).max(axis=1),
+                                      np.abs(d1g[..., 0] - d1h[..., 0]).max(axis=1)), 1e-6)
+        log = []
+        sens = lambda t, i: PS.simulate_sensitive(mnp, sp, root, dof, act, i, og, oh, eps=drift[i], log=log)
+        try:
+            PS.assert_steps_explained(test, bad[None], PS.step_flags(mnp, sp, pre)[None], sens=sens, reach_cap=0.12)
+        finally:
+            print("sensitivity fallback (env, drift, moved, gap):", [(i, drift[i], mv, gp) for i, mv, gp in log])
         return
     np.testing.assert_allclose(rg[:, 0:7], r_h[:, 0:7], atol=2e-4)
     np.testing.assert_allclose(dg[..., 0], d_h[..., 0], atol=2e-4)
     np.testing.assert_allclose(rg[:, 7:13], r_h[:, 7:13], atol=2e-3, rtol=2e-3)
     np.testing.assert_allclose(dg[..., 1], d_h[..., 1], atol=2e-3, rtol=2e-3)
-    sg = s_d.cpu().numpy()
     if len(spec.sensors):
         scale = max(1.0, np.abs(sens_h).max())
         PS.record(test, "sensors", sg, sens_h, scale=scale)
         np.testing.assert_allclose(sg, sens_h, atol=1e-2 * scale)
-    fg = f_d.cpu().numpy()
     PS.record(test, "dof force", fg, dfor_h)
     np.testing.assert_allclose(fg, dfor_h, atol=1e-2 * max(1.0, np.abs(dfor_h).max()))
 
