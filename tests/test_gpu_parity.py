@@ -265,7 +265,7 @@ def test_physics_step_matches_oracle(lib, task, n, z, fast):
     r_h, d_h = root.copy(), dof.copy()
     O.simulate(mnp, sp, r_h, d_h, act, sens_h, dfor_h, threads=8)
     rg, dg, sg, fg = _gpu_simulate(lib, mnp, sp, root, dof, act, ns)
-    test = f"test_physics_step_matches_oracle[{task}{'-fast' if fast else ''}]"
+    test = f"test_physics_step_matches_oracle[{task}{'-fast' if fast else ''}{f'-{n}' if n > 512 else ''}]"
     if fast:   # the cap acted: some link ends at |w| = W (root spin or a joint rate above it)
         W = float(mnp["link_max_ang_vel"])
         assert (np.abs(d_h[..., 1]).max() > 0.5 * W) and (np.abs(dof[..., 1]).max() > W)
