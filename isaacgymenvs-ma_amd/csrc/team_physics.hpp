@@ -710,7 +710,8 @@ struct Team {
   // drives / tendons (node lanes)
   float tgt;           // PD target of the own DOF
   float ttend;         // tendon generalized force (current substep)
-  int sat;             // drive saturated (current substep)
+  int sat;             // bit 0: drive saturated (current substep); bits 1 / 2: a lower / upper limit row, bits 3+: its
+                       // index among the limit rows (build_rows; outputs() reads the DOF force's limit impulses there)
   // domain randomization: the team's DrTile (nullptr: the model's constants)
   const float* drn;    // node rows (stride 9)
   const float* drg;    // geom friction
@@ -2200,6 +2201,7 @@ struct Team {
     int tot;
     const int incl = team_scan_bits<T, 2>(cnt, tot);
     int li = incl - cnt;
+    sat = (sat & 1) | (lo ? 2 : 0) | (hi ? 4 : 0) | (li << 3);
     for (int side = 0; side < 2; side++) {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
@@ -2637,16 +2639,15 @@ struct Team {
       float t = tau + ttend;
       if (np[6] > 0.0f) {
         const float fe = np[6] * (tgt - qj) - np[2] * nu;
-        t += sat ? (fe > 0.0f ? np[7] : -np[7]) : fe;
+        t += (sat & 1) ? (fe > 0.0f ? np[7] : -np[7]) : fe;
       } else {
         t += -np[2] * nu - np[3] * qj;
       }
-      for (int r = 3 * s->ncon; r < s->nrows; r++) {
-        const int meta = s->lmeta[r - 3 * s->ncon];
-        if ((meta >> 4) != node) continue;
-        if ((meta & 3) == 2) t += s->u.sv.rows[r].lam * ih;
-        if ((meta & 3) == 3) t -= s->u.sv.rows[r].lam * ih;
-      }
+      // the node's own limit rows of the last substep (lower, then upper: consecutive from the index build_rows
+      // kept in sat), instead of a scan over every limit row
+      const int lr = 3 * s->ncon + (sat >> 3);
+      if (sat & 2) t += s->u.sv.rows[lr].lam * ih;
+      if (sat & 4) t -= s->u.sv.rows[lr + ((sat >> 1) & 1)].lam * ih;
       dforce_out[node - 1] = t;
     }
   }
