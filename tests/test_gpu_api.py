@@ -247,3 +247,23 @@ def test_cpu_pipeline_host_views(task, n, how):
     assert bool((c.progress_buf[:5] <= 1).all())
     g.close()
     c.close()
+
+
+@pytest.mark.parametrize("task,filled", [("Ant", False), ("MAAnt", False), ("Cartpole", False), ("Humanoid", True),
+                                         ("ShadowHand", True)])
+def test_dof_force_tensor_where_the_reference_acquires_one(task, filled):
+    """dof_force_tensor is filled every step where the reference task acquires a DOF-force tensor (humanoid.py:85-86,
+    shadow_hand.py:157-159) and stays zero where it does not (ant.py, cartpole.py: the fused step skips it); the
+    Humanoid observation's DOF-force block (obs[54:75], humanoid.py:405) is the tensor times contact_force_scale"""
+    env = make(task, 64)
+    for k in range(3):
+        obs, _, _, _ = env.step(actions(env, k))
+    torch.cuda.synchronize()
+    f = env.dof_force_tensor
+    if not filled:
+        assert int(torch.count_nonzero(f)) == 0
+        return
+    assert bool(torch.isfinite(f).all()) and float(f.abs().max()) > 0.0
+    if task == "Humanoid":
+        ob = obs["obs"]
+        torch.testing.assert_close(ob[:, 54:75], f * env.task_params.contact_force_scale, rtol=1e-6, atol=1e-6)
