@@ -7,8 +7,10 @@
 One "step" = one VecTask.step of every env on every rank (controlFrequencyInv=1,
 2 physics substeps), random U(-1,1) actions generated on device before the timed
 region, inputs resident in HBM.  Envs are independent, so ranks shard them
-(weak scaling: --num-envs per GPU; the only collective is the obs/rew/reset gather to rank 0, timed).  Rank 0 prints ONE
-JSON line.  See DESIGN.md §Measurement for the roofline accounting.
+(weak scaling: --num-envs per GPU; the only collective is the obs/rew/reset gather to rank 0, timed).  The same
+line carries `strong_scaling`: BASELINE.json's fixed-total configs (MA-Ant 65,536 envs, ShadowHand 32,768, and Ant
+65,536) split over the ranks, timed the same way.  `roofline.kernel_ms` is the median of a separate untimed pass of
+launches bracketed by HIP events.  Rank 0 prints ONE JSON line.  See DESIGN.md §7 for the roofline accounting.
 """
 import argparse
 import json
@@ -211,6 +213,84 @@ def pmc_traffic(task, n, kern_ms, object_type="block"):
     return out
 
 
+# BASELINE.json's fixed-total configs (split over the ranks), plus the headline Ant total for the strong curve
+STRONG_CONFIGS = (("MAAnt", 65536, "BASELINE configs[3]: multi-agent Ant (4 agents/env), 65,536 envs total"),
+                  ("ShadowHand", 32768, "BASELINE configs[4]: ShadowHand, 32,768 envs total"),
+                  ("Ant", 65536, "Ant, 65,536 envs total (strong-scaling counterpart of the headline)"))
+
+
+def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed, what=None, total=None):
+    """One workload: make() `n` envs on this rank, W warm-up steps, K timed steps between barrier + synchronize
+    (max over ranks), then a separate kernel-duration pass (HIP events around each of --kernel-samples launches on
+    the launch stream, median; the timed region has no events, so its wall time is not diluted by them)."""
+    import torch
+    import torch.distributed as dist
+    import migym
+    mk = {}
+    if task == "ShadowHand" and object_type != "block":
+        from migym import configs
+        tcfg = configs.task_config("ShadowHand", n, sim_device=dev)
+        tcfg["env"]["objectType"] = object_type
+        mk["cfg"] = {"task": tcfg}
+    env = migym.make(seed=seed, task=task, num_envs=n, sim_device=dev, rl_device=dev, headless=True,
+                     multi_gpu=world > 1, **mk)
+    na = env.num_actions
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
+    gather = None
+    if gather_mode != "none" and world > 1:
+        from migym.dist import PackedGather
+        gather = PackedGather(env.num_actors, env.num_obs, dev, mode=gather_mode)
+        env.attach_output_gather(gather)
+    for i in range(args.warmup):
+        env.step(pool[i % 8])
+    if gather is not None:
+        gather.drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        env.step(pool[i % 8])
+    if gather is not None:
+        gather.drain()   # the last step's rows have reached the root
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # kernel-duration pass (untimed): events around each launch, on the stream it is launched on
+    ks = max(1, args.kernel_samples)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(ks)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(ks)]
+    for i in range(ks):
+        env.launch_events = (starts[i], ends[i])
+        env.step(pool[i % 8])
+    env.launch_events = None
+    if gather is not None:
+        gather.drain()
+    torch.cuda.synchronize()
+    durs = sorted(starts[i].elapsed_time(ends[i]) for i in range(ks))
+    kern_ms = durs[ks // 2] if ks % 2 else 0.5 * (durs[ks // 2 - 1] + durs[ks // 2])
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    info = {"substeps": env.sim_params.substeps, "pos_iters": env.sim_params.pos_iters, "agents": env.num_agents}
+    env.close()
+    del env, pool, gather
+    value = n * world * args.steps / elapsed
+    r = {"value": value, "unit": "env-steps/s", "ms_per_step": 1e3 * elapsed / args.steps, "kernel_ms": kern_ms,
+         "kernel_ms_sample": f"median of {ks} launches after the timed region, HIP events on the launch stream "
+                             f"(max over ranks)",
+         "gathered": gather_mode if (gather_mode != "none" and world > 1) else None, "env_info": info}
+    if what is not None:
+        r.update({"config": what, "task": task, "num_envs_total": total, "num_envs_per_gpu": n, "n_gpus": world,
+                  "agents_per_env": info["agents"], "agent_steps_per_s": value * info["agents"],
+                  "scaling": "strong"})
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,9 +305,12 @@ def main():
                          "the next step): 'root' = point-to-point sends to rank 0 (default when --gpus > 1), "
                          "'all' = one RCCL all-gather, 'none' = no gather")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--event-stride", type=int, default=8,
-                    help="HIP events around every k-th launch of the timed region (the kernel-duration sample); each "
-                         "event pair is two more queue packets between launches")
+    ap.add_argument("--kernel-samples", type=int, default=32,
+                    help="launches of the kernel-duration pass after the timed region, each between HIP events on its "
+                         "stream (roofline.kernel_ms = their median); the timed region itself carries no events")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the strong-scaling lines (BASELINE configs[3]/[4] and Ant 65,536 as fixed totals "
+                         "split over the ranks)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--object-type", default="block", choices=["block", "egg", "pen"],
                     help="ShadowHand objectType (shadow_hand.py:86-100)")
@@ -250,81 +333,46 @@ def main():
 
     import migym
     n = args.num_envs
-    mk = {}
-    if args.task == "ShadowHand" and args.object_type != "block":
-        from migym import configs
-        tcfg = configs.task_config("ShadowHand", n, sim_device=dev)
-        tcfg["env"]["objectType"] = args.object_type
-        mk["cfg"] = {"task": tcfg}
-    env = migym.make(seed=rank, task=args.task, num_envs=n, sim_device=dev, rl_device=dev, headless=True,
-                     multi_gpu=world > 1, **mk)
-    na = env.num_actions
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    pool = [torch.rand((env.num_actors, na), device=dev, generator=g) * 2 - 1 for _ in range(8)]
     gather_mode = args.gather or ("root" if world > 1 else "none")
-    gather = None
-    if gather_mode != "none" and world > 1:
-        from migym.dist import PackedGather
-        gather = PackedGather(env.num_actors, env.num_obs, dev, mode=gather_mode)
-        env.attach_output_gather(gather)
-
-    for i in range(args.warmup):
-        env.step(pool[i % 8])
-    if gather is not None:
-        gather.drain()
-    torch.cuda.synchronize()
-    # HIP events around each fused launch, on the stream it is launched on (VecTask.launch_events)
-    stride = max(1, args.event_stride)
-    sampled = list(range(0, args.steps, stride))
-    starts = {i: torch.cuda.Event(enable_timing=True) for i in sampled}
-    ends = {i: torch.cuda.Event(enable_timing=True) for i in sampled}
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        env.launch_events = (starts[i], ends[i]) if i in starts else None
-        env.step(pool[i % 8])
-    if gather is not None:
-        gather.drain()   # the last step's rows have reached the root
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    env.launch_events = None
-    kern_ms = sum(starts[i].elapsed_time(ends[i]) for i in sampled) / len(sampled)
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                         device=dev if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-    value = n * world * args.steps / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
+    head = run_workload(args.task, n, args.object_type, args, world, rank, dev, gather_mode, seed=rank)
+    # strong scaling: BASELINE.json's fixed-total multi-GPU configs, each rank stepping total / world envs of one
+    # node-size rollout (global env ids rank * n_rank ..., so the shards are slices of it), same timing rules
+    strong = []
+    if not args.no_strong:
+        for task, total, what in STRONG_CONFIGS:
+            if total % world:
+                continue
+            strong.append(run_workload(task, total // world, "block", args, world, rank, dev, gather_mode, seed=0,
+                                       what=what, total=total))
+    value = head["value"]
+    ms_per_step, kern_ms = head["ms_per_step"], head["kernel_ms"]
     if rank == 0:
         per_launch = ALGO_BYTES[args.task] * n
         achieved = per_launch / (kern_ms * 1e-3)
+        env = head["env_info"]
         out = {
             "metric": "env-steps/sec (whole node) at num_envs=65536; 1/2/4/8 MI355X scaling",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (U(-1,1) actions, device-resident)",
-            "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, {env.sim_params.substeps} substeps, "
-                                   f"PGS x{env.sim_params.pos_iters}",
+            "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, {env['substeps']} substeps, "
+                                   f"PGS x{env['pos_iters']}",
                        "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
-                       "agents_per_env": env.num_agents, "agent_steps_per_s": value * env.num_agents,
+                       "agents_per_env": env["agents"], "agent_steps_per_s": value * env["agents"],
                        "obs_gather": (f"{gather_mode}: kernel-packed [obs|rew|reset] rows, double-buffered, "
                                       f"overlapped with the next step, inside the timed region")
-                                     if gather is not None else None,
+                                     if head["gathered"] else None,
                        "parallelism": f"env-sharded x{world}",
                        **({"object_type": args.object_type} if args.task == "ShadowHand" else {})},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms, args.object_type),
                          "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",
-                         "kernel_ms": kern_ms,
-                         "kernel_ms_sample": f"HIP events on the launch stream around every {stride}th of the {args.steps} "
-                                             f"timed launches ({len(sampled)} launches)",
+                         "kernel_ms": kern_ms, "kernel_ms_sample": head["kernel_ms_sample"],
+                         "kernel_ms_le_ms_per_step": kern_ms <= ms_per_step,
                          "algo_bytes_per_env_step": ALGO_BYTES[args.task]},
         }
+        if strong:
+            out["strong_scaling"] = [{k: v for k, v in r.items() if k != "env_info"} for r in strong]
         if not args.no_cpu_baseline and world == 1:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n, args.object_type)
@@ -336,7 +384,6 @@ def main():
             except Exception as ex:  # noqa: BLE001
                 out["baseline_config0"] = {"error": repr(ex)}
         print(json.dumps(out), flush=True)
-    env.close()
     if world > 1:
         dist.destroy_process_group()
 

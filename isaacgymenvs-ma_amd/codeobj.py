@@ -17,7 +17,34 @@ import struct
 import subprocess
 import tempfile
 
-OBJDUMP = os.environ.get("MIGYM_OBJDUMP", "/opt/rocm/lib/llvm/bin/llvm-objdump")
+def _objdump():
+    """llvm-objdump of the ROCm install that builds the library: MIGYM_OBJDUMP, else <root>/lib/llvm/bin/llvm-objdump
+    with <root> from ROCM_PATH, or from the hipcc in use (HIPCC, or hipcc on PATH: <root>/bin/hipcc), else /opt/rocm"""
+    if os.environ.get("MIGYM_OBJDUMP"):
+        return os.environ["MIGYM_OBJDUMP"]
+    roots = []
+    if os.environ.get("ROCM_PATH"):
+        roots.append(os.environ["ROCM_PATH"])
+    import shutil
+    hipcc = os.environ.get("HIPCC") or shutil.which("hipcc")
+    if hipcc:
+        roots.append(os.path.dirname(os.path.dirname(os.path.realpath(hipcc))))
+    roots.append("/opt/rocm")
+    for r in roots:
+        cand = os.path.join(r, "lib", "llvm", "bin", "llvm-objdump")
+        if os.path.exists(cand):
+            return cand
+    raise FileNotFoundError("codeobj: no llvm-objdump under " + ", ".join(f"{r}/lib/llvm/bin" for r in roots) +
+                            "; set MIGYM_OBJDUMP to its path (or ROCM_PATH to the ROCm root)")
+
+
+def have_objdump():
+    try:
+        return os.path.exists(_objdump())
+    except FileNotFoundError:
+        return False
+
+
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
@@ -62,7 +89,7 @@ def calls(so, arch="gfx950"):
             f = os.path.join(td, f"co{k}.o")
             with open(f, "wb") as fh:
                 fh.write(co)
-            txt = subprocess.run([OBJDUMP, "-d", f"--mcpu={arch}", f], capture_output=True, text=True,
+            txt = subprocess.run([_objdump(), "-d", f"--mcpu={arch}", f], capture_output=True, text=True,
                                  check=True).stdout
             fn = "?"
             for line in txt.splitlines():

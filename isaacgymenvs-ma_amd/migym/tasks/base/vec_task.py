@@ -106,6 +106,9 @@ class VecTask(DomainRandomizationMixin, Env):
     # whether the task resets (and so randomizes) in pre_physics_step (ShadowHand) or post_physics_step
     dr_actor_names = {}
     dr_reset_in_pre_physics = False
+    # whether the reference task calls gym.acquire_dof_force_tensor (humanoid.py:85-86, shadow_hand.py:157-159): the
+    # DOF-force view is bound, and the fused step computes the forces, only then
+    acquires_dof_force = False
 
     def __init__(self, config, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
                  force_render=False):
@@ -177,9 +180,10 @@ class VecTask(DomainRandomizationMixin, Env):
         v = _abi.StateViews()
         v.root_states, v.dof_state = _abi.ptr(self.root_states), _abi.ptr(self.dof_state)
         v.dof_actuation, v.sensors = _abi.ptr(self.dof_actuation), _abi.ptr(self.sensor_tensor)
-        # the DOF-force view only where the reference acquires one (humanoid.py:85-86); Ant and Cartpole never do
-        # (ant.py, cartpole.py), so the fused step skips their DOF forces and dof_force_tensor stays zero
-        v.dof_force = _abi.ptr(self.dof_force_tensor) if self.task_name == "Humanoid" else None
+        # the DOF-force view only where the reference acquires one (humanoid.py:85-86: acquires_dof_force); Ant and
+        # Cartpole never do (ant.py, cartpole.py), so the fused step skips their DOF forces and dof_force_tensor
+        # stays zero
+        v.dof_force = _abi.ptr(self.dof_force_tensor) if self.acquires_dof_force else None
         v.rigid_body_states = None
         self._views = v
         _abi.check(self._lib.mg_sim_bind(self.sim, _abi.C.byref(v)), self._lib)
@@ -391,7 +395,16 @@ class VecTask(DomainRandomizationMixin, Env):
                                           n, self._stream()), self._lib)
 
     def reset_done(self):
+        """reset_done (vec_task.py:442-457): ``reset_idx`` of every env whose ``reset_buf`` is set, applied now (one
+        ``mg_reset_idx`` launch: noise, root/DOF rows, potentials; progress and reset_buf cleared), then the current
+        observations clamped -- not recomputed, so they stay the terminal ones, as in the reference -- and the done
+        ids.  The next ``step`` then simulates those envs from their reset state and does not reset them again.
+        Multi-agent layouts: the ids are agent ids and ``reset_idx``'s AND filter applies (franka_reach_MA.py:
+        616-621), so an env resets only when all its agents are done.  The ``nonzero`` is a host synchronisation,
+        as in the reference; ``step`` itself never needs one."""
         done_env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
+        if len(done_env_ids) > 0:
+            self.reset_idx(done_env_ids)
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
         if self.num_states > 0:
             self.obs_dict["states"] = self.get_state()

@@ -59,6 +59,7 @@ class Humanoid(_Locomotion):
     num_obs_default = 108
     num_act_default = 21
     dr_actor_names = {"humanoid": "articulation"}
+    acquires_dof_force = True   # humanoid.py:85-86
 
 
 class MAAnt(_Locomotion):

@@ -27,6 +27,7 @@ class ShadowHand(VecTask):
     task_name = "ShadowHand"
     dr_actor_names = {"hand": "articulation", "object": "object", "goal_object": "none"}
     dr_reset_in_pre_physics = True
+    acquires_dof_force = True   # shadow_hand.py:157-159 (bound in create_sim below)
 
     def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture=False,
                  force_render=False):

@@ -76,6 +76,8 @@ int orc_compute_reward(const mg_task_params* tp, int32_t n, const float* obs, co
                        const float* potentials, const float* prev_potentials, const int64_t* progress,
                        int64_t* reset, float* rew);
 int orc_post_physics(const mg_task_params* tp, const mg_state_views* v, const mg_task_buffers* tb, int32_t n);
+int orc_reset_idx(const mg_task_params* tp, const mg_state_views* v, const mg_task_buffers* tb, const int32_t* ids,
+                  int32_t n_ids, int32_t n);
 int orc_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp, const mg_state_views* v,
                  const mg_task_buffers* tb, int32_t n, int32_t threads);
 

@@ -328,6 +328,19 @@ int orc_post_physics(const mg_task_params* tp, const mg_state_views* v, const mg
   return 0;
 }
 
+/* reset_idx(ids) applied now (ant.py:252-279, humanoid.py:253-279, cartpole.py:144-157), the counterpart of
+   mg_reset_idx: ids < 0 or >= n are skipped (the AND-filtered multi-agent rows); the counter RNG runs on its
+   manual-reset stream (step_counter | 2^62), injected noise rows are indexed by actor. */
+int orc_reset_idx(const mg_task_params* tp, const mg_state_views* v, const mg_task_buffers* tb, const int32_t* ids,
+                  int32_t n_ids, int32_t n) {
+  if (tp->task_id == MG_TASK_SHADOW_HAND) return -1;
+  mg_task_buffers t = *tb;
+  t.step_counter = tb->step_counter | (1ull << 62);
+  for (int k = 0; k < n_ids; k++)
+    if (ids[k] >= 0 && ids[k] < n) reset_one(tp, ids[k], v, &t);
+  return 0;
+}
+
 int orc_env_step(const mg_model* m, const mg_sim_params* p, const mg_task_params* tp, const mg_state_views* v,
                  const mg_task_buffers* tb, int32_t n, int32_t threads) {
   int na = tp->num_actions, nd = m->num_dofs;

@@ -48,6 +48,8 @@ def lib():
                                        C.POINTER(_abi.TaskBuffers), C.c_int32]
         l.orc_env_step.argtypes = [P, C.POINTER(_abi.SimParams), C.POINTER(_abi.TaskParams),
                                    C.POINTER(_abi.StateViews), C.POINTER(_abi.TaskBuffers), C.c_int32, C.c_int32]
+        l.orc_reset_idx.argtypes = [C.POINTER(_abi.TaskParams), C.POINTER(_abi.StateViews),
+                                    C.POINTER(_abi.TaskBuffers), P, C.c_int32, C.c_int32]
         l.orc_simulate_views.argtypes = [P, C.POINTER(_abi.SimParams), C.c_int32, C.POINTER(_abi.StateViews),
                                          C.c_int32]
         l.orc_randomize_rotation.restype = None
@@ -274,6 +276,13 @@ class HostEnv:
         v, b = self.views(), self.buffers(seed, step, env_offset)
         (lib_f32() if fp32 else lib()).orc_env_step(model_np.ctypes.data, C.byref(sp), C.byref(tp), C.byref(v),
                                                      C.byref(b), self.n, threads)
+
+    def reset_idx(self, tp, ids, seed=0, step=0, env_offset=0):
+        """reset_idx(ids) now (orc_reset_idx; ids < 0 skipped, noise rows by actor)"""
+        ids = np.ascontiguousarray(ids, np.int32)
+        v, b = self.views(), self.buffers(seed, step, env_offset)
+        rc = lib().orc_reset_idx(C.byref(tp), C.byref(v), C.byref(b), p(ids), len(ids), self.n)
+        assert rc == 0
 
 
 class HandHostEnv:

@@ -219,7 +219,10 @@ def physics_output(g, N, nd, lo, hi, z_range, nsens):
     return root, dof, sens
 
 
-def run_locomotion(task, N=64, T=8, ep_len=5):
+def run_locomotion(task, N=64, T=8, ep_len=5, reset_done=False):
+    """reset_done=True: after every step the trace calls the reference's own ``VecTask.reset_done``
+    (vec_task.py:442-457), the rl_games AMP agent/player pattern (learning/common_agent.py:458-459,
+    common_player.py:173-174), and records its draws, the state it leaves and the observations it returns."""
     import importlib
     mod = importlib.import_module("isaacgymenvs.tasks." + task.lower())
     if task == "Ant":
@@ -258,6 +261,10 @@ def run_locomotion(task, N=64, T=8, ep_len=5):
     out = {k: [] for k in ("actions", "phys_root", "phys_dof", "phys_sensors", "phys_dof_force", "noise",
                            "reset_mask", "obs", "rew", "reset", "progress", "timeouts", "potentials",
                            "prev_potentials", "root_after", "dof_after", "reset_in", "progress_in")}
+    if reset_done:
+        for k in ("rd_mask", "rd_noise", "rd_root", "rd_dof", "rd_reset", "rd_progress", "rd_potentials",
+                  "rd_prev_potentials", "rd_obs"):
+            out[k] = []
     out["init_obs"] = env.reset()["obs"].clone()
     for t in range(T):
         actions = torch.rand(N, env.num_actions, generator=g) * 2.4 - 1.2  # exercises the ±1 clip
@@ -293,6 +300,29 @@ def run_locomotion(task, N=64, T=8, ep_len=5):
         out["dof_after"].append(env.dof_state.view(N, nd, 2).clone())
         out["reset_in"].append(reset_in)
         out["progress_in"].append(progress_in)
+        if reset_done:
+            done_in = env.reset_buf.clone()
+            rec.draws.clear()
+            rd_obs, rd_ids = env.reset_done()
+            ids = done_in.nonzero(as_tuple=False).flatten()
+            assert torch.equal(rd_ids, ids)
+            noise = torch.zeros(N, 2 * nd)
+            if len(ids) > 0:
+                noise[ids, :nd] = rec.draws[0]
+                noise[ids, nd:] = rec.draws[1]
+            else:
+                assert not rec.draws
+            mask = torch.zeros(N, dtype=torch.int64)
+            mask[ids] = 1
+            out["rd_mask"].append(mask)
+            out["rd_noise"].append(noise)
+            out["rd_root"].append(env.root_states.clone())
+            out["rd_dof"].append(env.dof_state.view(N, nd, 2).clone())
+            out["rd_reset"].append(env.reset_buf.clone())
+            out["rd_progress"].append(env.progress_buf.clone())
+            out["rd_potentials"].append(env.potentials.clone())
+            out["rd_prev_potentials"].append(env.prev_potentials.clone())
+            out["rd_obs"].append(rd_obs["obs"].clone())
     res = {k: (torch.stack(v) if isinstance(v, list) else v) for k, v in out.items()}
     res["lower"], res["upper"] = lo, hi
     res["episode_length"] = torch.tensor(ep_len)
@@ -867,13 +897,17 @@ def main():
     # one task per process: vec_task keeps a process-global sim (vec_task.py:55-64)
     if which == "all":
         import subprocess
-        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces", "shadowhand_pen", "ant_dr"):
+        for t in ("ant", "humanoid", "cartpole", "shadowhand", "shadowhand_obs", "shadowhand_forces", "shadowhand_pen", "ant_dr",
+                  "ant_reset_done", "humanoid_reset_done"):
             subprocess.check_call([sys.executable, __file__, t])
         return
     if which == "ant":
         save("trace_ant.npz", run_locomotion("Ant"))
     elif which == "humanoid":
         save("trace_humanoid.npz", run_locomotion("Humanoid"))
+    elif which in ("ant_reset_done", "humanoid_reset_done"):  # step -> reset_done -> step (vec_task.py:442-457)
+        task = "Ant" if which.startswith("ant") else "Humanoid"
+        save(f"trace_{task.lower()}_reset_done.npz", run_locomotion(task, N=64, T=7, ep_len=4, reset_done=True))
     elif which == "cartpole":
         save("trace_cartpole.npz", run_cartpole())
     elif which == "shadowhand":

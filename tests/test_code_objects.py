@@ -19,7 +19,7 @@ import codeobj  # noqa: E402
 SO = os.path.join(PKG, "migym", "_lib", "libmigym.so")
 
 
-@pytest.mark.skipif(not os.path.exists(codeobj.OBJDUMP), reason="llvm-objdump not installed")
+@pytest.mark.skipif(not codeobj.have_objdump(), reason="llvm-objdump not installed")
 def test_shipped_library_has_no_device_calls():
     assert os.path.exists(SO), "build first (__graft_entry__.build)"
     cos = codeobj.device_code_objects(SO)
@@ -27,7 +27,7 @@ def test_shipped_library_has_no_device_calls():
     assert codeobj.calls(SO) == []
 
 
-@pytest.mark.skipif(not os.path.exists(codeobj.OBJDUMP), reason="llvm-objdump not installed")
+@pytest.mark.skipif(not codeobj.have_objdump(), reason="llvm-objdump not installed")
 def test_checker_sees_a_real_call(tmp_path):
     """the checker itself: a tiny HIP library with a noinline device function is flagged"""
     import subprocess

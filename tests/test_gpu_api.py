@@ -145,6 +145,23 @@ def test_reset_idx_shadow_hand():
     assert torch.equal(root[keep], root_before[keep])
     env.step(actions(env, 5))
     assert torch.isfinite(env.obs_buf).all()
+    # reset_done (the reference's base reset_done would call the two-argument reset_idx with one
+    # argument and raise): the done envs reset now, each with its goal, the others untouched
+    done = torch.tensor([2, 9], device=DEV)
+    env.reset_buf.zero_()
+    env.reset_buf[done] = 1
+    env.progress_buf[done] = 5
+    root_before = env.root_state_tensor.view(n, 3, 13).clone()
+    obs_before = env.obs_buf.clone()
+    obs, ids = env.reset_done()
+    torch.cuda.synchronize()
+    assert torch.equal(ids, done)
+    assert (env.reset_buf == 0).all() and (env.progress_buf[done] == 0).all()
+    torch.testing.assert_close(env.cur_targets[done], dof[done, :, 0], rtol=0, atol=0)
+    keep = torch.ones(n, dtype=torch.bool, device=DEV)
+    keep[done] = False
+    assert torch.equal(root[keep], root_before[keep]) and not torch.equal(root[done], root_before[done])
+    torch.testing.assert_close(obs["obs"], torch.clamp(obs_before, -env.clip_obs, env.clip_obs), rtol=0, atol=0)
     env.close()
 
 
@@ -179,6 +196,118 @@ def test_reset_idx_multi_agent_and_filter():
             assert torch.equal(env.progress_buf[rows], prog_before[rows])
     env.step(actions(env, 7))
     assert torch.isfinite(env.obs_buf).all()
+    env.close()
+
+
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_reset_done_replays_reference_trace(task):
+    """step -> VecTask.reset_done() -> step against the reference's own reset_done (vec_task.py:442-457), traced
+    on the fake gym after every step (tests/golden/make_traces.py, reset_done=True).  The steps run the device
+    task layer over the trace's physics outputs (mg_post_physics on the env's own buffers); reset_done is the
+    build's VecTask method, with the reference's draws injected.  Asserted: the reset rows (root exact, DOF to
+    1e-7), reset_buf / progress / potentials exact, reset_done's returned obs = the terminal obs, and the next
+    step's obs / rew / resets / progress (so the reset envs are not reset a second time)."""
+    import ctypes as C
+    from migym import _abi
+    d = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", f"trace_{task.lower()}_reset_done.npz")))
+    Tn, N = d["actions"].shape[:2]
+    env = make(task, N)
+    lib, tp = env._lib, env.task_params
+    tp.max_episode_length = int(d["episode_length"])
+    nd = env.num_dof
+    T = lambda a, dt=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(DEV, dt)  # noqa: E731
+    stream = torch.cuda.current_stream().cuda_stream
+    for t in range(Tn):
+        act = T(d["actions"][t]).contiguous()
+        env.root_states.copy_(T(d["phys_root"][t]))
+        env.dof_state.copy_(T(d["phys_dof"][t]).view(N * nd, 2))
+        env.sensor_tensor.copy_(T(d["phys_sensors"][t]).view(env.sensor_tensor.shape))
+        env.dof_force_tensor.copy_(T(d["phys_dof_force"][t]))
+        noise = T(d["noise"][t]).contiguous()
+        tb = env._tb
+        tb.actions, tb.noise, tb.step_counter = act.data_ptr(), noise.data_ptr(), t
+        assert torch.equal(env.reset_buf.cpu(), torch.as_tensor(d["reset_in"][t]))
+        _abi.check(lib.mg_post_physics(None, C.byref(tp), C.byref(env._views), C.byref(tb), N, stream), lib)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(env.obs_buf.cpu().numpy(), d["obs"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(env.rew_buf.cpu().numpy(), d["rew"][t], rtol=1e-4, atol=1e-4)
+        np.testing.assert_array_equal(env.reset_buf.cpu().numpy(), d["reset"][t])
+        np.testing.assert_array_equal(env.progress_buf.cpu().numpy(), d["progress"][t])
+        # VecTask.reset_done with the reference's reset_idx draws
+        env.set_reset_noise(T(d["rd_noise"][t]))
+        obs, done = env.reset_done()
+        env.set_reset_noise(None)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(done.cpu().numpy(), np.nonzero(d["rd_mask"][t])[0])
+        np.testing.assert_array_equal(env.root_states.cpu().numpy(), d["rd_root"][t])
+        np.testing.assert_allclose(env.dof_state.view(N, nd, 2).cpu().numpy(), d["rd_dof"][t], rtol=1e-7, atol=1e-7)
+        np.testing.assert_array_equal(env.reset_buf.cpu().numpy(), d["rd_reset"][t])
+        np.testing.assert_array_equal(env.progress_buf.cpu().numpy(), d["rd_progress"][t])
+        np.testing.assert_array_equal(env.potentials.cpu().numpy(), d["rd_potentials"][t])
+        np.testing.assert_array_equal(env.prev_potentials.cpu().numpy(), d["rd_prev_potentials"][t])
+        np.testing.assert_allclose(obs["obs"].cpu().numpy(), d["rd_obs"][t], rtol=1e-4, atol=1e-4)
+    assert d["rd_mask"][1:].sum() > 0
+    env.close()
+
+
+@pytest.mark.parametrize("task,n", [("Ant", 256), ("MAAnt", 64)])
+def test_reset_done_with_physics_matches_oracle(task, n):
+    """reset_done between fused physics steps, device RNG: the done envs (for MAAnt: the envs whose agents are
+    all done, the AND filter) hold the oracle's reset state bit for bit (orc_reset_idx on the same counter-RNG
+    stream), the others keep their state; the following fused step starts the reset envs from that state, so
+    their observations match the oracle's step from the same state."""
+    import pyoracle as O
+    from migym import model as M
+    env = make(task, n)
+    A = env.num_agents
+    rows = n * A
+    for k in range(2):
+        env.step(actions(env, k))
+    torch.cuda.synchronize()
+    g = np.random.default_rng(4)
+    mask = (g.random(rows) < 0.5).astype(np.int64)
+    if A > 1:
+        mask[0:A] = 1        # env 0 fully done; env 1 partly
+        mask[A:2 * A] = [1] * (A - 1) + [0]
+    env.reset_buf.copy_(torch.as_tensor(mask, device=DEV))
+    keep_root = env.root_states.clone()
+    h = O.HostEnv(env.task_params, env.model_spec, rows)
+    h.root[:] = env.root_states.cpu().numpy()
+    h.dof[:] = env.dof_state.view(rows, env.num_dof, 2).cpu().numpy()
+    h.reset[:] = mask
+    h.progress[:] = env.progress_buf.cpu().numpy()
+    h.potentials[:] = env.potentials.cpu().numpy()
+    h.prev_potentials[:] = env.prev_potentials.cpu().numpy()
+    obs_before = env.obs_buf.clone()
+    step = env.control_steps
+    obs, done = env.reset_done()
+    torch.cuda.synchronize()
+    assert torch.equal(done.cpu(), torch.as_tensor(np.nonzero(mask)[0]))
+    assert torch.equal(obs["obs"], obs_before)    # not recomputed (vec_task.py:451)
+    full = (np.bincount(np.nonzero(mask)[0] // A, minlength=n) >= A) if A > 1 else mask.astype(bool)
+    reset_rows = np.repeat(full, A) if A > 1 else full
+    ids = np.where(reset_rows, np.arange(rows), -1)
+    h.reset_idx(env.task_params, ids, seed=env.seed, step=step)
+    np.testing.assert_array_equal(env.root_states.cpu().numpy(), h.root)
+    np.testing.assert_array_equal(env.dof_state.view(rows, env.num_dof, 2).cpu().numpy(), h.dof)
+    np.testing.assert_array_equal(env.reset_buf.cpu().numpy(), h.reset)
+    np.testing.assert_array_equal(env.progress_buf.cpu().numpy(), h.progress)
+    np.testing.assert_array_equal(env.potentials.cpu().numpy(), h.potentials)
+    assert torch.equal(env.root_states[torch.as_tensor(~reset_rows, device=DEV)],
+                       keep_root[torch.as_tensor(~reset_rows, device=DEV)])
+    assert reset_rows.any() and (~reset_rows).any()
+    if A > 1:
+        assert reset_rows[0:A].all() and not reset_rows[A:2 * A].any()
+    # the next fused step from the reset state: the reset envs' observations against the oracle's step
+    a = actions(env, 5)
+    env.step(a)
+    torch.cuda.synchronize()
+    h.actions[:] = a.cpu().numpy()
+    h.env_step(M.pack_model(env.model_spec), env.sim_params, env.task_params, seed=env.seed, step=step, threads=8)
+    np.testing.assert_array_equal(env.progress_buf.cpu().numpy(), h.progress)
+    og = env.obs_buf.cpu().numpy()[reset_rows]
+    oh = h.obs[reset_rows]
+    assert (np.abs(og - oh) <= 2e-3 + 2e-3 * np.abs(oh)).mean() > 0.99
     env.close()
 
 
@@ -245,6 +374,18 @@ def test_cpu_pipeline_host_views(task, n, how):
     oc, _, _, _ = c.step(actions(g, 9).cpu())
     assert torch.equal(oc["obs"], og["obs"]) and torch.equal(c.progress_buf, g.progress_buf.cpu())
     assert bool((c.progress_buf[:5] <= 1).all())
+    # a device-side edit between calls (through env.unwrapped) is not reverted by the untouched host mirror
+    c.unwrapped.reset_buf[5:8] = 1
+    g.reset_buf[5:8] = 1
+    og, _, dg, _ = g.step(actions(g, 10))
+    oc, _, dc, _ = c.step(actions(g, 10).cpu())
+    assert torch.equal(oc["obs"], og["obs"]) and torch.equal(dc, dg)
+    assert torch.equal(c.progress_buf, g.progress_buf.cpu()) and bool((c.progress_buf[5:8] <= 1).all())
+    # get_env_state: host tensors, with a host edit made just before it included
+    c.progress_buf[0] = 123
+    st = c.get_env_state()
+    assert all(v.device.type == "cpu" for v in st.values() if torch.is_tensor(v))
+    assert int(st["progress_buf"][0]) == 123 and int(c.unwrapped.progress_buf[0]) == 123
     g.close()
     c.close()
 

@@ -13,6 +13,8 @@ same GPU, with the same actions, and must agree bit for bit on obs, rew and rese
 (The per-rank consecutive_successes mean is reduced across ranks by the dist layer and is not part of
 obs / rew / reset.)
 """
+import os
+
 import pytest
 import torch
 
@@ -138,3 +140,52 @@ def test_ragged_shards_equal_slices_of_one_rollout(task, obj):
             assert torch.equal(rew, w[lo:hi]), f"{task} envs [{lo_e}, {hi_e}) step {k}: rew differ"
             assert torch.equal(reset, d[lo:hi]), f"{task} envs [{lo_e}, {hi_e}) step {k}: reset differ"
         sh.close()
+
+
+def _rollout_with_order(task, n, env_cfg, order_every, steps):
+    """`steps` fused steps of `task` with MIGYM_ORDER_EVERY = order_every (read at mg_sim_create), a short episode
+    so that timeouts and terminations reset envs inside the run; every step's outputs and state, cloned"""
+    old = os.environ.get("MIGYM_ORDER_EVERY")
+    os.environ["MIGYM_ORDER_EVERY"] = str(order_every)
+    try:
+        cfg = configs.task_config(task, n, sim_device=DEV)
+        cfg["env"].update(env_cfg)
+        env = migym.make(seed=17, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                         cfg={"task": cfg})
+    finally:
+        if old is None:
+            del os.environ["MIGYM_ORDER_EVERY"]
+        else:
+            os.environ["MIGYM_ORDER_EVERY"] = old
+    g = torch.Generator(device=DEV).manual_seed(23)
+    out = []
+    for _ in range(steps):
+        a = torch.rand((env.num_actors, env.num_actions), device=DEV, generator=g) * 2.4 - 1.2
+        obs, rew, reset, extras = env.step(a)
+        out.append((obs["obs"].clone(), rew.clone(), reset.clone(), env.root_states.clone(), env.dof_state.clone(),
+                    env.progress_buf.clone()))
+    resets = sum(int(o[2].sum()) for o in out[1:])
+    env.close()
+    return out, resets
+
+
+@pytest.mark.parametrize("task,n,env_cfg", [("Humanoid", 301, {}),
+                                            ("ShadowHand", 301, {"objectType": "block"}),
+                                            ("ShadowHand", 301, {"objectType": "egg"}),
+                                            ("ShadowHand", 301, {"objectType": "pen"}),
+                                            ("MAAnt", 301, {"numAgents": 2})])
+def test_work_order_changes_no_result(task, n, env_cfg):
+    """Work ordering (k_order + the ordered actor permutation) only changes which envs share a wave:
+    sorting every step (MIGYM_ORDER_EVERY=1, the first sort on the second step) and never (0) give the same
+    obs, rew, reset, root and DOF state bit for bit over 12 steps with resets, on a ragged env count (the last
+    wave partly filled).  MAAnt with 2 agents per env has the ordering forced on, so the agent alignment that the
+    AND filter and the 'others' shuffles rely on is exercised under the permutation."""
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    env_cfg = dict(env_cfg, episodeLength=7)
+    on, r_on = _rollout_with_order(task, n, env_cfg, 1, 12)
+    off, r_off = _rollout_with_order(task, n, env_cfg, 0, 12)
+    assert r_on == r_off and r_on > 0
+    names = ("obs", "rew", "reset", "root state", "dof state", "progress")
+    for k, (a, b) in enumerate(zip(on, off)):
+        for name, x, y in zip(names, a, b):
+            assert torch.equal(x, y), f"{task} {env_cfg} step {k}: {name} differ with the work order on"

@@ -118,6 +118,45 @@ def test_full_step_trace_matches_reference(task):
         np.testing.assert_array_equal(h.prev_potentials, d["prev_potentials"][t])
 
 
+@pytest.mark.parametrize("task", ["Ant", "Humanoid"])
+def test_reset_done_trace_matches_reference(task):
+    """step -> reset_done -> step: the reference's own VecTask.reset_done (vec_task.py:442-457) after every
+    physics-free step (make_traces.py run_locomotion(reset_done=True)), replayed through the oracle's post-physics
+    and reset_idx with the reference's draws injected: the reset state written, reset_buf / progress cleared, the
+    returned observations the terminal ones, and the next step simulating from the reset state without a second
+    reset."""
+    d = load(f"trace_{task.lower()}_reset_done.npz")
+    tp, spec = tparams(task)
+    tp.max_episode_length = int(d["episode_length"])
+    T, N = d["actions"].shape[:2]
+    h = O.HostEnv(tp, spec, N)
+    assert d["rd_mask"][1:].sum() > 0 and d["timeouts"].sum() > 0   # the trace exercises both kinds of done
+    for t in range(T):
+        h.actions[:] = d["actions"][t]
+        h.root[:] = d["phys_root"][t]
+        h.dof[:] = d["phys_dof"][t]
+        h.sensors[:] = d["phys_sensors"][t]
+        h.dof_force[:] = d["phys_dof_force"][t]
+        h.noise = O.f32(d["noise"][t])
+        np.testing.assert_array_equal(h.reset, d["reset_in"][t])
+        h.post_physics(tp)
+        np.testing.assert_allclose(h.obs_clamped, d["obs"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_allclose(h.rew, d["rew"][t], rtol=RTOL, atol=ATOL)
+        np.testing.assert_array_equal(h.reset, d["reset"][t])
+        # reset_done: reset_idx(reset_buf.nonzero())
+        ids = np.nonzero(h.reset)[0]
+        np.testing.assert_array_equal(ids, np.nonzero(d["rd_mask"][t])[0])
+        h.noise = O.f32(d["rd_noise"][t])
+        h.reset_idx(tp, ids)
+        np.testing.assert_array_equal(h.root, d["rd_root"][t])
+        np.testing.assert_allclose(h.dof, d["rd_dof"][t], rtol=1e-7, atol=1e-7)
+        np.testing.assert_array_equal(h.reset, d["rd_reset"][t])
+        np.testing.assert_array_equal(h.progress, d["rd_progress"][t])
+        np.testing.assert_array_equal(h.potentials, d["rd_potentials"][t])
+        np.testing.assert_array_equal(h.prev_potentials, d["rd_prev_potentials"][t])
+        np.testing.assert_allclose(h.obs_clamped, d["rd_obs"][t], rtol=RTOL, atol=ATOL)   # terminal obs, unchanged
+
+
 def test_cartpole_trace_matches_reference():
     d = load("trace_cartpole.npz")
     tp, spec = tparams("Cartpole")
