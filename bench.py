@@ -9,8 +9,8 @@ One "step" = one VecTask.step of every env on every rank (controlFrequencyInv=1,
 region, inputs resident in HBM.  Envs are independent, so ranks shard them
 (weak scaling: --num-envs per GPU; the only collective is the obs/rew/reset gather to rank 0, timed).  The same
 line carries `strong_scaling`: BASELINE.json's fixed-total configs (MA-Ant 65,536 envs, ShadowHand 32,768, and Ant
-65,536) split over the ranks, timed the same way.  `roofline.kernel_ms` is the median of a separate untimed pass of
-launches bracketed by HIP events.  Rank 0 prints ONE JSON line.  See DESIGN.md §7 for the roofline accounting.
+65,536) split over the ranks, timed the same way.  `roofline.kernel_ms` is the mean device-side span (first wave start
+to last wave end, GPU wall clock) of the timed launches themselves.  Rank 0 prints ONE JSON line.  See DESIGN.md §7 for the roofline accounting.
 """
 import argparse
 import json
@@ -250,6 +250,12 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # the device-side span of every timed launch (first wave start -> last wave end on the GPU wall clock,
+    # mg_kernel_span_begin: one plain store per wave at its start and end; same-box A/B against a build without the
+    # hooks: no difference, profiles/r05/ab_span.txt).  Launches are stream-ordered, so the spans of the timed
+    # launches sum to at most the timed wall time: kernel_ms (their mean) <= ms_per_step by construction.
+    nspan = min(args.steps, 1024)
+    env.kernel_span_begin(nspan)
     t0 = time.perf_counter()
     for i in range(args.steps):
         env.step(pool[i % 8])
@@ -259,7 +265,11 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # kernel-duration pass (untimed): events around each launch, on the stream it is launched on
+    spans = [float(x) for x in env.kernel_span_read(nspan) if x > 0]
+    env.kernel_span_begin(0)
+    span_ok = len(spans) == nspan
+    # HIP events around each of --kernel-samples further launches (untimed), for comparison: kernel + the event
+    # packets' dispatch latency; kernel_ms falls back to their median for a library built without the span hooks
     ks = max(1, args.kernel_samples)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(ks)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(ks)]
@@ -270,19 +280,26 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
     if gather is not None:
         gather.drain()
     torch.cuda.synchronize()
-    durs = sorted(starts[i].elapsed_time(ends[i]) for i in range(ks))
-    kern_ms = durs[ks // 2] if ks % 2 else 0.5 * (durs[ks // 2 - 1] + durs[ks // 2])
+    ev = sorted(starts[i].elapsed_time(ends[i]) for i in range(ks))
+    event_ms = ev[ks // 2] if ks % 2 else 0.5 * (ev[ks // 2 - 1] + ev[ks // 2])
+    if not span_ok:
+        print(f"bench.py: the span hooks recorded {len(spans)} of {nspan} launches; kernel_ms from HIP events",
+              file=sys.stderr)
+    kern_ms = sum(spans) / len(spans) if span_ok else event_ms
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, kern_ms, event_ms], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, event_ms = float(t[0]), float(t[1]), float(t[2])
     info = {"substeps": env.sim_params.substeps, "pos_iters": env.sim_params.pos_iters, "agents": env.num_agents}
     env.close()
     del env, pool, gather
     value = n * world * args.steps / elapsed
     r = {"value": value, "unit": "env-steps/s", "ms_per_step": 1e3 * elapsed / args.steps, "kernel_ms": kern_ms,
-         "kernel_ms_sample": f"median of {ks} launches after the timed region, HIP events on the launch stream "
-                             f"(max over ranks)",
+         "kernel_ms_sample": (f"mean over the {nspan} timed launches of each launch's device-side span (first wave "
+                              f"start to last wave end, GPU wall clock; max over ranks)") if span_ok else
+                             f"median of HIP events around {ks} launches (no span hooks in this library)",
+         "event_ms": event_ms,
          "gathered": gather_mode if (gather_mode != "none" and world > 1) else None, "env_info": info}
     if what is not None:
         r.update({"config": what, "task": task, "num_envs_total": total, "num_envs_per_gpu": n, "n_gpus": world,
@@ -306,8 +323,8 @@ def main():
                          "'all' = one RCCL all-gather, 'none' = no gather")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--kernel-samples", type=int, default=32,
-                    help="launches of the kernel-duration pass after the timed region, each between HIP events on its "
-                         "stream (roofline.kernel_ms = their median); the timed region itself carries no events")
+                    help="launches after the timed region bracketed by HIP events on the launch stream (event_ms, "
+                         "their median, reported beside kernel_ms: the timed launches' mean device-side span)")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the strong-scaling lines (BASELINE configs[3]/[4] and Ant 65,536 as fixed totals "
                          "split over the ranks)")
@@ -346,6 +363,8 @@ def main():
                                        what=what, total=total))
     value = head["value"]
     ms_per_step, kern_ms = head["ms_per_step"], head["kernel_ms"]
+    if kern_ms > ms_per_step and rank == 0:   # the device span cannot exceed the steady-state time per step
+        print(f"bench.py: kernel_ms {kern_ms:.4f} > ms_per_step {ms_per_step:.4f}", file=sys.stderr)
     if rank == 0:
         per_launch = ALGO_BYTES[args.task] * n
         achieved = per_launch / (kern_ms * 1e-3)
@@ -369,6 +388,9 @@ def main():
                          "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",
                          "kernel_ms": kern_ms, "kernel_ms_sample": head["kernel_ms_sample"],
                          "kernel_ms_le_ms_per_step": kern_ms <= ms_per_step,
+                         "event_ms": head["event_ms"],
+                         "event_ms_note": "HIP events around each launch of the same pass: kernel + the event "
+                                          "packets' dispatch latency, so above kernel_ms",
                          "algo_bytes_per_env_step": ALGO_BYTES[args.task]},
         }
         if strong:

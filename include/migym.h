@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_VERSION 6
+#define MG_VERSION 7
 
 #define MG_MAX_NODES 40
 #define MG_MAX_BODIES 40
@@ -492,6 +492,15 @@ typedef struct mg_replay {
 } mg_replay;
 int mg_env_step_replay(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
                        void* stream);
+
+/* Measurement aid (no reference counterpart; bench.py's roofline.kernel_ms): the device-side duration of the
+ * fused step kernel, from the first wave's start to the last wave's end on the GPU's constant wall clock
+ * (wall_clock64, hipDeviceAttributeWallClockRate), so that no launch, queue or event-packet overhead is in it.
+ * mg_kernel_span_begin(sim, cap): the next `cap` mg_env_step launches of `sim` record their span (one slot each;
+ * 0 turns recording off; the kernels run unchanged otherwise).  mg_kernel_span_read(sim, ms, cap, &n):
+ * synchronises the device and returns the recorded spans in milliseconds, in launch order. */
+int mg_kernel_span_begin(mg_sim* sim, int32_t cap);
+int mg_kernel_span_read(mg_sim* sim, double* ms, int32_t cap, int32_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -27,12 +27,17 @@ struct mg_sim {
   bool order_valid;
   int* d_order;        // (n / A) env slots -> env
   unsigned char* d_cost; // (n) the last step's row count per actor (saturated at 255)
+  // kernel spans (mg_kernel_span_begin): per recorded launch, span_stride (start, end) pairs, one per wave
+  unsigned long long* d_span;
+  int span_cap, span_next, span_stride;
+  int span_waves[1024];  // waves of each recorded launch
 };
 
 // the step kernels' ordering arguments (nullptr order: slot = env)
 struct MgOrder {
   const int* order;
   unsigned char* cost;
+  unsigned long long* clk;  // nullptr, or this launch's span slot (mg_kernel_span_begin)
 };
 
 namespace mgi {

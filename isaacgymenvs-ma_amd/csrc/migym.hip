@@ -573,6 +573,8 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   s->order_valid = false;
   s->d_order = nullptr;
   s->d_cost = nullptr;
+  s->d_span = nullptr;
+  s->span_cap = s->span_next = s->span_stride = 0;
   // default: on for the 32-lane instances (ShadowHand, Humanoid: two teams per wave), off for the narrower ones
   // (Ant's four 16-lane teams: no gain); every step from 16,384 envs up (the last step's row counts are the best
   // guess of this one's: Humanoid 32,768 K = 8 35.4 -> K = 1 36.5 M, ShadowHand 16,384 18.9 -> 19.4 M), every 8th
@@ -684,7 +686,56 @@ int mg_sim_destroy(mg_sim* sim) {
   if (sim->d_wq) (void)hipFree(sim->d_wq);
   if (sim->d_order) (void)hipFree(sim->d_order);
   if (sim->d_cost) (void)hipFree(sim->d_cost);
+  if (sim->d_span) (void)hipFree(sim->d_span);
   delete sim;
+  return MG_OK;
+}
+
+int mg_kernel_span_begin(mg_sim* sim, int32_t cap) {
+  if (!sim || cap < 0 || cap > (int32_t)(sizeof(sim->span_waves) / sizeof(sim->span_waves[0])))
+    return fail(MG_EINVAL, "mg_kernel_span_begin: bad arguments (cap 0..1024)");
+  if (sim->d_span) (void)hipFree(sim->d_span);
+  sim->d_span = nullptr;
+  sim->span_cap = sim->span_next = 0;
+  if (cap == 0) return MG_OK;
+  // a launch's waves: one per 64 / T actors (T = the instance's team size), rounded up to whole blocks (<= 8 waves)
+  const int T = mgi::team_size(sim->host_model, sim->params.max_contacts);
+  sim->span_stride = (int)(((int64_t)sim->n * (T > 0 ? T : 64) + 63) / 64) + 8;
+  const size_t bytes = sizeof(unsigned long long) * 2 * (size_t)sim->span_stride * (size_t)cap;
+  if (hipMalloc(&sim->d_span, bytes) != hipSuccess) {
+    sim->d_span = nullptr;
+    return fail(MG_ENOMEM, "mg_kernel_span_begin: hipMalloc failed");
+  }
+  // zeros: a launch that records nothing (a build without the hooks) reads back as a zero span
+  if (hipMemset(sim->d_span, 0, bytes) != hipSuccess) return fail(MG_EDEVICE, "mg_kernel_span_begin: memset failed");
+  sim->span_cap = cap;
+  return MG_OK;
+}
+
+int mg_kernel_span_read(mg_sim* sim, double* ms, int32_t cap, int32_t* n_out) {
+  if (!sim || !ms || !n_out || cap < 0) return fail(MG_EINVAL, "mg_kernel_span_read: bad arguments");
+  *n_out = 0;
+  const int n = sim->span_next < cap ? sim->span_next : cap;
+  if (!sim->d_span || n == 0) return MG_OK;
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, sim->device) != hipSuccess || khz <= 0)
+    return fail(MG_EDEVICE, "mg_kernel_span_read: wall clock rate query failed");
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_kernel_span_read: sync failed");
+  std::vector<unsigned long long> h;
+  for (int i = 0; i < n; i++) {
+    const int w = sim->span_waves[i];
+    h.resize(2 * (size_t)w);
+    if (hipMemcpy(h.data(), sim->d_span + 2 * (size_t)sim->span_stride * i, h.size() * sizeof(unsigned long long),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(MG_EDEVICE, "mg_kernel_span_read: copy failed");
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int k = 0; k < w; k++) {
+      t0 = h[2 * k] < t0 ? h[2 * k] : t0;
+      t1 = h[2 * k + 1] > t1 ? h[2 * k + 1] : t1;
+    }
+    ms[i] = t1 >= t0 ? (double)(t1 - t0) / (double)khz : -1.0;
+  }
+  *n_out = n;
   return MG_OK;
 }
 

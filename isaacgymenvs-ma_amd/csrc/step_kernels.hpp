@@ -13,6 +13,15 @@
 #include "team_physics.hpp"
 
 
+// waves per SIMD the register allocator targets (2: the 256-VGPR budget; an A/B variant may ask for 3, <= 168 VGPRs)
+#ifndef MG_WAVES_PER_EU
+#define MG_WAVES_PER_EU 2
+#endif
+// dynamic LDS added to every step-kernel launch (0; an occupancy A/B variant pads it to hold fewer waves per CU)
+#ifndef MG_LDS_PAD
+#define MG_LDS_PAD 0
+#endif
+
 namespace mgi {
 #ifdef MG_PHASE_TIMING
 // per-wave accumulators (one row of MG_NUM_PHASES per block; plain read-modify-writes by the block's own wave,
@@ -84,6 +93,20 @@ __device__ __forceinline__ int wq_next(unsigned* wq, int grid_waves) {
   if ((threadIdx.x & 63) == 0) v = atomicAdd(&wq[0], 1u);
   return grid_waves + (int)__builtin_amdgcn_readfirstlane(v);
 }
+// kernel span (mg_kernel_span_begin): lane 0 of each wave stores its start and end times (GPU wall clock) into the
+// wave's own pair of the launch's slot -- plain stores to distinct addresses, no atomics (a same-address atomic per
+// wave cost Ant 12 % in its first form); mg_kernel_span_read reduces them.  A kernel-argument branch otherwise.
+// (MG_NO_SPAN: compiled out, the A/B variant that checks the hooks cost the timed launches nothing)
+__device__ __forceinline__ void span_start(unsigned long long* clk, int wave) {
+#ifndef MG_NO_SPAN
+  if (clk && (threadIdx.x & 63) == 0) clk[2 * (size_t)wave] = (unsigned long long)wall_clock64();
+#endif
+}
+__device__ __forceinline__ void span_end(unsigned long long* clk, int wave) {
+#ifndef MG_NO_SPAN
+  if (clk && (threadIdx.x & 63) == 0) clk[2 * (size_t)wave + 1] = (unsigned long long)wall_clock64();
+#endif
+}
 __device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
   if ((threadIdx.x & 63) == 0 && atomicAdd(&wq[1], 1u) == (unsigned)grid_waves - 1u) {
     atomicExch(&wq[0], 0u);
@@ -95,7 +118,7 @@ __device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_simulate(
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_simulate(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_state_views v, int n) {
   using SH = Shape<T, MN, MC, MG, MP, OBJ, DR>;
   constexpr int E = SH::E, W = SH::W;
@@ -157,7 +180,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
 // state, the team writes it back to HBM.  Multi-agent: the agents of an env are consecutive
 // teams of one wave, so the AND-filter is a ballot over team leaders and the others-block a
 // shuffle from the other agents' leaders.
-// amdgpu_waves_per_eu(2): the register budget that lets two waves share a SIMD (the team kernels
+// amdgpu_waves_per_eu(MG_WAVES_PER_EU): the register budget that lets two waves share a SIMD (the team kernels
 // are latency-bound; occupancy is the lever — DESIGN.md §3)
 // RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
 // post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
@@ -373,7 +396,7 @@ __device__ __forceinline__ void env_step_item(
 }
 
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_env_step(
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_env_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
@@ -381,11 +404,13 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {
     // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
     if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
+    span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   } else {
     // multi-wave blocks: the work queue (wq_next), the grid being the resident capacity
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
@@ -394,6 +419,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
       env_step_item<T, MN, MC, MG, MP, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
                                                (&rp)[z], item, (&ord)[z]);
     }
+    span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
     wq_done(wq, gwv);
   }
 }
@@ -657,7 +683,7 @@ __device__ __forceinline__ void hand_step_item(
 }
 
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(2))) void k_hand_step(
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_hand_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
@@ -665,10 +691,12 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
+  span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {  // as k_env_step
     if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
+    span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   } else {
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
@@ -676,6 +704,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
       hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z],
                                                     (&tb)[z], n, (&rp)[z], item, (&ord)[z]);
     }
+    span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
     wq_done(wq, gwv);
   }
 }
@@ -698,7 +727,7 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     if (c.k == kp && c.dev == sim->device) resident = c.blocks;
   if (resident <= 0) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, SH::kThreads, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, SH::kThreads, MG_LDS_PAD) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sim->device) != hipSuccess || per_cu <= 0 ||
         cus <= 0)
       return fail(MG_EDEVICE, "mg_env_step: occupancy query failed");
@@ -708,13 +737,16 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
   }
   const int items = (sim->n + SH::E1 - 1) / SH::E1;
   const int need = (items + SH::W - 1) / SH::W;
-  const MgOrder ord{(ordered && sim->order_valid) ? sim->d_order : nullptr, ordered ? sim->d_cost : nullptr};
-  if (SH::W == 1) {  // the kernels' one-wave-block path: the static grid, one block per item
-    hipLaunchKernelGGL(kern, dim3(need), dim3(SH::kThreads), 0, s, args..., sim->d_wq, ord);
-    return MG_OK;
+  const int blocks = SH::W == 1 ? need : (need < resident ? need : resident);
+  unsigned long long* clk = nullptr;  // mg_kernel_span_begin: this launch's slot, one (start, end) pair per wave
+  if (sim->d_span && sim->span_next < sim->span_cap && blocks * SH::W <= sim->span_stride) {
+    mg_sim* ms = const_cast<mg_sim*>(sim);   // recording bookkeeping only
+    clk = ms->d_span + 2 * (size_t)ms->span_stride * ms->span_next;
+    ms->span_waves[ms->span_next++] = blocks * SH::W;
   }
-  const int blocks = need < resident ? need : resident;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), 0, s, args..., sim->d_wq, ord);
+  const MgOrder ord{(ordered && sim->order_valid) ? sim->d_order : nullptr, ordered ? sim->d_cost : nullptr, clk};
+  // one-wave blocks: the static grid, one block per item; multi-wave blocks: the resident capacity (work queue)
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), MG_LDS_PAD, s, args..., sim->d_wq, ord);
   return MG_OK;
 }
 

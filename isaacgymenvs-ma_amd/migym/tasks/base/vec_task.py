@@ -284,6 +284,18 @@ class VecTask(DomainRandomizationMixin, Env):
         elif pending_increment:
             self.randomize_buf_actors += 1
 
+    def kernel_span_begin(self, n: int):
+        """record the device-side duration (first wave start -> last wave end, GPU wall clock) of the next n fused
+        step launches (mg_kernel_span_begin; 0 stops recording).  A measurement aid: bench.py's kernel_ms"""
+        _abi.check(self._lib.mg_kernel_span_begin(self.sim, int(n)), self._lib)
+
+    def kernel_span_read(self, n: int):
+        """the recorded spans in ms, in launch order (synchronises the device)"""
+        buf = np.zeros(max(int(n), 1), np.float64)
+        got = _abi.C.c_int32(0)
+        _abi.check(self._lib.mg_kernel_span_read(self.sim, buf.ctypes.data, int(n), _abi.C.byref(got)), self._lib)
+        return buf[:got.value]
+
     def post_launch(self):
         """Device work that follows the fused launch in stream order (ShadowHand: the cross-rank
         running-mean reduction)."""

@@ -60,6 +60,39 @@ def write_report():
             json.dump(old, f, indent=1, sort_keys=True)
 
 
+# observation column groups of the locomotion tasks (ant.py:325-351 compute_ant_observations, humanoid.py:382-413):
+# [height | vel_loc | angvel_loc | yaw roll angle_to_target | up_proj heading_proj | dof pos | dof vel | ... | actions]
+OBS_GROUPS = {
+    60: {"height": [0], "vel_loc": [1, 2, 3], "angvel_loc": [4, 5, 6], "yaw/roll/angle_to_target": [7, 8, 9],
+         "up/heading proj": [10, 11], "dof pos (scaled)": list(range(12, 20)), "dof vel": list(range(20, 28)),
+         "foot force-torques": list(range(28, 52)), "actions": list(range(52, 60))},
+    108: {"height": [0], "vel_loc": [1, 2, 3], "angvel_loc": [4, 5, 6], "yaw/roll/angle_to_target": [7, 8, 9],
+          "up/heading proj": [10, 11], "dof pos (scaled)": list(range(12, 33)), "dof vel": list(range(33, 54)),
+          "dof force": list(range(54, 75)), "foot force-torques": list(range(75, 87)), "actions": list(range(87, 108))},
+}
+NORTH_STAR_RTOL = 1e-4   # BASELINE.json north_star: "obs/reward parity to CPU reference within 1e-4 rel"
+
+
+def column_stats(test, name, a, b, keep, groups, rtol=NORTH_STAR_RTOL):
+    """per column group over the env-steps in `keep` (unflagged): max |a - b|, max relative error |a - b| / |b| (over
+    |b| > 1e-3), the fraction of elements within rtol |b| alone, and the atol that rtol needs to hold everywhere
+    (max(|a - b| - rtol |b|)); recorded under test/name and returned"""
+    a = np.asarray(a, np.float64)[keep]
+    b = np.asarray(b, np.float64)[keep]
+    out = {}
+    for g, cols in groups.items():
+        x, y = a[:, cols], b[:, cols]
+        d = np.abs(x - y)
+        big = np.abs(y) > 1e-3
+        out[g] = {"max_abs": float(d.max()) if d.size else 0.0,
+                  "max_rel": float((d[big] / np.abs(y[big])).max()) if big.any() else 0.0,
+                  "frac_within_rtol": float((d <= rtol * np.abs(y)).mean()) if d.size else 1.0,
+                  "atol_needed": float(np.maximum(d - rtol * np.abs(y), 0.0).max()) if d.size else 0.0,
+                  "scale": float(np.abs(y).max()) if d.size else 0.0}
+    _REPORT.setdefault(test, {})[name] = out
+    return out
+
+
 def env_bad(a, b, atol, rtol):
     """per-env: some element outside atol + rtol |b|"""
     a = np.asarray(a).reshape(len(a), -1)
@@ -198,11 +231,11 @@ def step_flags(mnp, sp, host, delta=STEP_DELTA, df=STEP_DF):
     return O.step_flips(mnp, sp, host, delta, df)
 
 
-def loco_physics_input(h, mnp, sp, tp, seed, step):
+def loco_physics_input(h, mnp, sp, tp, seed, step, threads=1):
     """a HostEnv copy holding step `step`'s physics input: the state as the step starts (the locomotion resets
     run in post_physics) and the actuation pre_physics computes from h.actions"""
     g, tmp = copy.deepcopy(h), copy.deepcopy(h)
-    tmp.env_step(mnp, sp, tp, seed=seed, step=step, threads=1)
+    tmp.env_step(mnp, sp, tp, seed=seed, step=step, threads=threads)
     g.act_eff[:] = tmp.act_eff
     return g
 

@@ -37,7 +37,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_struct_layouts_match(lib):
     _abi.check_layout(lib)
     assert lib.mg_model_sizeof() == M.MODEL_DTYPE.itemsize
-    assert lib.mg_version() == 6
+    assert lib.mg_version() == 7
 
 
 def test_bad_arguments_fail_loudly_without_device(lib):

@@ -355,19 +355,21 @@ def test_free_link_damping_and_cap_on_device(lib):
     np.testing.assert_allclose(rg, r_h, atol=1e-6, rtol=1e-6)
 
 
-def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=None):
+def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=None, threads=8):
     """mg_env_step vs orc_env_step step by step, each step started on both sides from the oracle's state (the GPU
     buffers are reloaded from it), so one step's fp32-vs-fp64 difference cannot grow into a chaotic divergence
     over the following steps.  Per step: progress exact; every env's obs within 2e-3 + 2e-3 |x|, reward within
     5e-3 + 5e-3 |r| and the same reset, unless orc_step_flips puts that env's step at a discontinuity (or the
-    oracle is itself sensitive there); the exemptions' reach is capped (parity_stats.assert_steps_explained)."""
+    oracle is itself sensitive there); the exemptions' reach is capped (parity_stats.assert_steps_explained).
+    Returns the per-column-group statistics against north_star's 1e-4 relative over the unflagged env-steps
+    (parity_stats.column_stats; recorded in the parity report)."""
     n = h.n
     mnp = M.pack_model(spec)
     sim = C.c_void_p()
     _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
     bad = np.zeros((steps, n), bool)
     flags = np.zeros((steps, n), np.int32)
-    pres, outs = [], []
+    pres, outs, rews = [], [], []
     try:
         for t in range(steps):
             h.actions[:] = actions[t]
@@ -375,9 +377,9 @@ def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=Non
                 mutate(t, h)
             e = DevEnv(h)
             _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
-            flags[t] = PS.step_flags(mnp, sp, PS.loco_physics_input(h, mnp, sp, tp, seed, t))
+            flags[t] = PS.step_flags(mnp, sp, PS.loco_physics_input(h, mnp, sp, tp, seed, t, threads=threads))
             pres.append(copy.deepcopy(h))
-            h.env_step(mnp, sp, tp, seed=seed, step=t, threads=8)
+            h.env_step(mnp, sp, tp, seed=seed, step=t, threads=threads)
             _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=seed, step=t)), stream()), lib)
             torch.cuda.synchronize()
             np.testing.assert_array_equal(e.progress.cpu().numpy(), h.progress)
@@ -385,6 +387,7 @@ def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=Non
             bad[t] = (PS.env_bad(og, h.obs, 2e-3, 2e-3) | PS.env_bad(rg[:, None], h.rew[:, None], 5e-3, 5e-3)
                       | (e.reset.cpu().numpy() != h.reset))
             outs.append((og, h.obs.copy()))
+            rews.append((rg, h.rew.copy()))
             PS.record(test, f"obs step {t}", og, h.obs, envs_outside=int(bad[t].sum()))
     finally:
         lib.mg_sim_destroy(sim)
@@ -392,6 +395,16 @@ def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=Non
                                                  seed=seed, step=t, hand=False)
     # (a multi-agent env cannot be replayed one actor alone: no sensitivity fallback there)
     PS.assert_steps_explained(test, bad, flags, sens if tp.num_agents <= 1 else None)
+    keep = (flags == 0).ravel()
+    og = np.concatenate([o[0] for o in outs])
+    oh = np.concatenate([o[1] for o in outs])
+    groups = dict(PS.OBS_GROUPS.get(tp.num_obs, {"obs": list(range(tp.num_obs))}))
+    cols = PS.column_stats(test, "columns vs 1e-4 rel (unflagged env-steps)", og, oh, keep, groups)
+    rw = PS.column_stats(test, "reward vs 1e-4 rel (unflagged env-steps)",
+                         np.concatenate([r[0] for r in rews])[:, None], np.concatenate([r[1] for r in rews])[:, None],
+                         keep, {"reward": [0]})
+    cols.update(rw)
+    return cols
 
 
 @pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128), ("Cartpole", 256)])
@@ -402,6 +415,24 @@ def test_fused_env_step_matches_oracle(lib, task, n):
     rng = np.random.default_rng(3)
     acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(4)]
     _teacher_forced(lib, f"test_fused_env_step_matches_oracle[{task}]", spec, sp, tp, h, 4, acts, seed=5)
+
+
+@pytest.mark.parametrize("task,n", [("Ant", 16384), ("Humanoid", 32768)])
+def test_fused_parity_at_baseline_size(lib, task, n):
+    """BASELINE.json configs[1] (Ant, 16,384 envs) and configs[2] (Humanoid, 32,768 envs: the work-ordered K = 1
+    path) against the oracle at full size: the oracle first rolls every env 12 steps on from the
+    all-reset start (random actions; falls, resets and contacts spread over the batch), then 3 fused steps are
+    teacher-forced as in test_fused_env_step_matches_oracle.  The per-column-group errors against north_star's
+    1e-4 relative are recorded (MIGYM_PARITY_REPORT)."""
+    spec, sp, tp = setup(task)
+    h = O.HostEnv(tp, spec, n)
+    mnp = M.pack_model(spec)
+    rng = np.random.default_rng(31)
+    for t in range(12):
+        h.actions[:] = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+        h.env_step(mnp, sp, tp, seed=7, step=100 + t, threads=16)
+    acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(3)]
+    _teacher_forced(lib, f"test_fused_parity_at_baseline_size[{task}-{n}]", spec, sp, tp, h, 3, acts, seed=7, threads=16)
 
 
 @pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128)])
