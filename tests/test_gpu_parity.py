@@ -282,14 +282,10 @@ def test_physics_step_matches_oracle(lib, task, n, z, fast):
         # and the oracle-sensitivity fallback where the dynamics are stiff (tests/test_step_flags.py)
         og = np.concatenate([rg, dg.reshape(n, -1)], 1)
         oh = np.concatenate([r_h, d_h.reshape(n, -1)], 1)
-        # the perturbation: how far apart the kernel's and the checker's first substep put each env's positions
-        sp1 = copy.copy(sp)
-        sp1.substeps, sp1.dt = 1, sp.dt / sp.substeps
-        r1g, d1g, _, _ = _gpu_simulate(lib, mnp, sp1, root, dof, act, ns)
-        r1h, d1h = root.copy(), dof.copy()
-        O.simulate(mnp, sp1, r1h, d1h, act, threads=8)
-        drift = np.maximum(np.maximum(np.abs(r1g[:, 0:3] - r1h[:, 0:3]).max(axis=1),
-                                      np.abs(d1g[..., 0] - d1h[..., 0]).max(axis=1)), 1e-6)
+        # the perturbation: how far apart an fp32 and an fp64 first substep put each env's positions, measured with the
+        # oracle's own fp32 build against the checker (parity_stats.first_substep_drift) -- a rounding scale from an
+        # implementation independent of the kernel under test (round 4 used the kernel's own first-substep drift here)
+        drift = PS.first_substep_drift(mnp, sp, root, dof, act)
         log = []
         sens = lambda t, i: PS.simulate_sensitive(mnp, sp, root, dof, act, i, og, oh, eps=drift[i], log=log)
         try:
@@ -407,6 +403,17 @@ def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=Non
     return cols
 
 
+def assert_north_star_rtol(cols):
+    """north_star: obs / reward parity within 1e-4 relative.  Every unflagged env-step (the teacher-forced fp32 GPU step
+    against the fp64 oracle from the same state) holds |gpu - oracle| <= 1e-4 (|oracle| + S_g), S_g the magnitude of
+    its column group in the batch (max |oracle| over the group): 1e-4 relative to the element, with an absolute floor
+    of 1e-4 of the group's scale, which is what fp32 rounding inside one physics step leaves on entries near zero
+    (the solve mixes a group's magnitudes: a velocity that ends near 0 carries the rounding of the O(S_g) terms that
+    cancelled; DESIGN.md §6 gives the derivation and the measured per-group margins)"""
+    bad = {g: v for g, v in cols.items() if v["atol_needed"] > 1e-4 * max(v["scale"], 1e-30)}
+    assert not bad, f"column groups outside 1e-4 (|x| + S_g): {bad}"
+
+
 @pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128), ("Cartpole", 256)])
 def test_fused_env_step_matches_oracle(lib, task, n):
     """mg_env_step (the bench path) vs orc_env_step over 4 teacher-forced control steps, device RNG resets."""
@@ -414,7 +421,8 @@ def test_fused_env_step_matches_oracle(lib, task, n):
     h = O.HostEnv(tp, spec, n)
     rng = np.random.default_rng(3)
     acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(4)]
-    _teacher_forced(lib, f"test_fused_env_step_matches_oracle[{task}]", spec, sp, tp, h, 4, acts, seed=5)
+    cols = _teacher_forced(lib, f"test_fused_env_step_matches_oracle[{task}]", spec, sp, tp, h, 4, acts, seed=5)
+    assert_north_star_rtol(cols)
 
 
 @pytest.mark.parametrize("task,n", [("Ant", 16384), ("Humanoid", 32768)])
@@ -432,7 +440,9 @@ def test_fused_parity_at_baseline_size(lib, task, n):
         h.actions[:] = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
         h.env_step(mnp, sp, tp, seed=7, step=100 + t, threads=16)
     acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(3)]
-    _teacher_forced(lib, f"test_fused_parity_at_baseline_size[{task}-{n}]", spec, sp, tp, h, 3, acts, seed=7, threads=16)
+    cols = _teacher_forced(lib, f"test_fused_parity_at_baseline_size[{task}-{n}]", spec, sp, tp, h, 3, acts, seed=7,
+                           threads=16)
+    assert_north_star_rtol(cols)
 
 
 @pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128)])
