@@ -211,12 +211,11 @@ __device__ __forceinline__ void h_reset_goal(const mg_task_params& tp, float g0,
   for (int k = 7; k < 13; k++) groot[k] = 0.0f;
 }
 
-// compute_hand_reward for one env with the action penalty's sum(actions ** 2) given (the fused step reduces it over
-// the team's lanes); the global running mean is reduced by the caller
-__device__ __forceinline__ void h_reward_pen(const mg_task_params& tp, const float* opos, const float* orot,
-                                             const float* tpos, const float* trot, float pen, int64_t reset_in,
-                                             int64_t goal_in, int64_t* progress, float* successes, float* rew,
-                                             int64_t* reset_out, int64_t* goal_out) {
+// compute_hand_reward for one env (the global running mean is reduced by the caller)
+__device__ __forceinline__ void h_reward(const mg_task_params& tp, const float* opos, const float* orot,
+                                         const float* tpos, const float* trot, const float* act, int64_t reset_in,
+                                         int64_t goal_in, int64_t* progress, float* successes, float* rew,
+                                         int64_t* reset_out, int64_t* goal_out) {
   const float max_episode_length = (float)tp.max_episode_length;
   const float d0 = opos[0] - tpos[0], d1 = opos[1] - tpos[1], d2 = opos[2] - tpos[2];
   const float goal_dist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
@@ -230,6 +229,8 @@ __device__ __forceinline__ void h_reward_pen(const mg_task_params& tp, const flo
   const float rot_dist = 2.0f * asinf(qn);
   const float dist_rew = goal_dist * tp.dist_reward_scale;
   const float rot_rew = 1.0f / (fabsf(rot_dist) + tp.rot_eps) * tp.rot_reward_scale;
+  float pen = 0.0f;
+  for (int i = 0; i < tp.num_actions; i++) pen += act[i] * act[i];
   float reward = dist_rew + rot_rew + pen * tp.action_penalty_scale;
   const int64_t goal_resets = fabsf(rot_dist) <= tol ? 1 : goal_in;
   const float succ = *successes + (float)goal_resets;
@@ -249,15 +250,6 @@ __device__ __forceinline__ void h_reward_pen(const mg_task_params& tp, const flo
   *goal_out = goal_resets;
   *progress = prog;
   *successes = succ;
-}
-// compute_hand_reward for one env, the action penalty summed serially (one thread per env: k_hand_post)
-__device__ __forceinline__ void h_reward(const mg_task_params& tp, const float* opos, const float* orot,
-                                         const float* tpos, const float* trot, const float* act, int64_t reset_in,
-                                         int64_t goal_in, int64_t* progress, float* successes, float* rew,
-                                         int64_t* reset_out, int64_t* goal_out) {
-  float pen = 0.0f;
-  for (int i = 0; i < tp.num_actions; i++) pen += act[i] * act[i];
-  h_reward_pen(tp, opos, orot, tpos, trot, pen, reset_in, goal_in, progress, successes, rew, reset_out, goal_out);
 }
 
 // action -> PD target of DOF d (shadow_hand.py:677-693); returns the new target

@@ -571,45 +571,29 @@ __device__ __forceinline__ void hand_step_item(
     float qdiff[4];
     const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
     mg::t_quat_mul(L.oroot + 3, gc, qdiff);
-    // segment by segment (the layout is the same for every env, so each segment's branch is wave-uniform); the
-    // team's lanes take the segment's entries (a per-column switch over obs_map ran ~7 divergent
-    // passes for the 211 full_state columns)
-    int base = 0;
-    for (int si = 0; si < 12; si++) {
-      const int seg = mg::kHandLayout[tp.obs_type & 3][si];
-      if (seg == mg::HS_END) break;
-      const int len = mg::h_seg_size(seg, nd, tp.num_fingertips, na);
-      for (int i = t.tl; i < len; i += T) {
-        float x;
-        if (seg == mg::HS_ACTIONS) {  // self.actions (clamped)
-          x = mg::clampf(tb.actions[(size_t)na * ec + i], tp.clip_actions);
-        } else if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {  // fingertip state from the post-step FK
-          int b, c;
-          mg::h_ft_ref(tp, seg, i, &b, &c);
-          x = bst[13 * b + c];
-        } else {
-          x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
-        }
-        if (base + i < no) L.obs[base + i] = x;
+    for (int k = t.tl; k < no; k += T) {
+      const int mk = tp.obs_map[k], seg = mk >> 8, i = mk & 255;   // column -> (segment, index)
+      float x;
+      if (seg == mg::HS_ACTIONS) {  // self.actions (clamped)
+        x = mg::clampf(tb.actions[(size_t)na * ec + i], tp.clip_actions);
+      } else if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {  // fingertip state from the post-step FK
+        int b, c;
+        mg::h_ft_ref(tp, seg, i, &b, &c);
+        x = bst[13 * b + c];
+      } else {
+        x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
       }
-      base += len;
+      L.obs[k] = x;
     }
   }
   mg::wsync();
   int64_t ro = 0;
   float fin = 0.0f;
-  // the action penalty's sum(actions ** 2) over the team's lanes (one action per lane), then the leader finishes
-  // compute_hand_reward
-  float pen;
-  {
-    const float a = t.tl < na ? L.obs[no - na + t.tl] : 0.0f;
-    pen = mg::team_sum<T>(a * a, 0);
-  }
   if (t.tl == 0) {
     const float* gs = L.goal + 13;
     float succ = env_reset ? 0.0f : tb.successes[ec], rew;
     int64_t prog = progress_in + 1, go;
-    mg::h_reward_pen(tp, L.oroot, L.oroot + 3, gs, gs + 3, pen, 0, 0, &prog, &succ, &rew, &ro, &go);
+    mg::h_reward(tp, L.oroot, L.oroot + 3, gs, gs + 3, L.obs + (no - na), 0, 0, &prog, &succ, &rew, &ro, &go);
     if (bad) {
       ro = 1;
       rew = 0.0f;
@@ -678,24 +662,18 @@ __device__ __forceinline__ void hand_step_item(
       float qdiff[4];
       const float gc[4] = {-gs[3], -gs[4], -gs[5], gs[6]};
       mg::t_quat_mul(L.oroot + 3, gc, qdiff);
-      int base = 0;   // the full_state layout, segment by segment as the observations above
-      for (int si = 0; si < 12; si++) {
-        const int seg = mg::kHandLayout[0][si];
-        if (seg == mg::HS_END) break;
-        const int len = mg::h_seg_size(seg, nd, tp.num_fingertips, na);
-        for (int i = t.tl; i < len; i += T) {
-          float x;
-          if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
-            int b, c;
-            mg::h_ft_ref(tp, seg, i, &b, &c);
-            x = bst[13 * b + c];
-          } else {
-            x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
-                                L.obs + (no - na));
-          }
-          if (base + i < tp.num_states) tb.states[(size_t)tp.num_states * e + base + i] = bad ? 0.0f : x;   // NaN guard
+      for (int k = t.tl; k < tp.num_states; k += T) {
+        const int mk = tp.state_map[k], seg = mk >> 8, i = mk & 255;
+        float x;
+        if (seg == mg::HS_FT_STATE || seg == mg::HS_FT_POS) {
+          int b, c;
+          mg::h_ft_ref(tp, seg, i, &b, &c);
+          x = bst[13 * b + c];
+        } else {
+          x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
+                              L.obs + (no - na));
         }
-        base += len;
+        tb.states[(size_t)tp.num_states * e + k] = bad ? 0.0f : x;   // NaN guard, as for obs
       }
     }
   }

@@ -247,10 +247,11 @@ def hand_physics_input(h, mnp, tp, seed, step):
     return g
 
 
-def assert_steps_explained(test, bad, flags, sens=None, reach_cap=REACH_CAP, sens_cap=SENS_CAP):
+def assert_steps_explained(test, bad, flags, sens=None, reach_cap=REACH_CAP, sens_cap=SENS_CAP, allow_unexplained=0.0):
     """bad, flags: (steps, envs).  Every disagreeing env-step must be flagged by orc_step_flips at that step (or,
     through `sens(t, i)`, sit where the oracle itself is sensitive); the flags' reach (the fraction of ALL env-steps
-    they would exempt) and the sensitivity fallback's use are recorded and capped"""
+    they would exempt) and the sensitivity fallback's use are recorded and capped.  allow_unexplained: a stated
+    fraction of env-steps that may disagree with neither (the fast-spin stress states; recorded)"""
     bad = np.asarray(bad, bool)
     flagged = np.asarray(flags) != 0
     why = flagged.copy()
@@ -264,10 +265,13 @@ def assert_steps_explained(test, bad, flags, sens=None, reach_cap=REACH_CAP, sen
     rec = {"env_steps": int(total), "disagreeing": int(bad.sum()), "flagged_reach": float(flagged.mean()),
            "explained_by_flags": int((bad & flagged).sum()), "explained_by_sensitivity": nsens,
            "bits": {str(b): float(((np.asarray(flags) & b) != 0).mean()) for b in (1, 2, 4, 8, 16, 32, 64)}}
-    _REPORT.setdefault(test, {})["exemptions"] = rec
     unexplained = np.argwhere(bad & ~why)
-    assert unexplained.size == 0, (f"{test}: {len(unexplained)} of {int(bad.sum())} disagreeing env-steps are not at a "
-                                   f"discontinuity (step, env): {unexplained[:10].tolist()}")
+    rec["unexplained"] = int(len(unexplained))
+    rec["allowed_unexplained"] = float(allow_unexplained)
+    _REPORT.setdefault(test, {})["exemptions"] = rec
+    assert len(unexplained) <= allow_unexplained * total, (
+        f"{test}: {len(unexplained)} of {int(bad.sum())} disagreeing env-steps are not at a discontinuity "
+        f"(allowed {allow_unexplained} x {total}) (step, env): {unexplained[:10].tolist()}")
     assert flagged.mean() <= reach_cap, f"{test}: the predicates exempt {flagged.mean():.3f} of the env-steps (cap {reach_cap})"
     assert nsens <= sens_cap * total, f"{test}: {nsens} env-steps excused by oracle sensitivity (cap {sens_cap} x {total})"
     return rec
