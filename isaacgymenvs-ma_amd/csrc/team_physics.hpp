@@ -192,6 +192,9 @@ constexpr int kJYRegs = MG_KJY;
 // 32-lane teams -5 % / -34 %); hand teams and Cartpole keep 6
 constexpr int kRBLoco = 12;
 
+#ifndef MG_PART_B_LDS
+#define MG_PART_B_LDS 0  // part-B PGS rows in the dead tree tiles (TeamLDS::PBL); an A/B variant
+#endif
 template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
@@ -201,10 +204,27 @@ struct TeamLDS {
   // (not for the egg instance: 17.16 vs 17.73 M env-steps/s and 450 vs 409 MB per launch, measured on its fp32 build)
   static constexpr int KR0 = OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : ((T >= 32 && !OBJ) ? MG_KJY_LOCO32 : kJYRegs);
   static constexpr int KR = (KR0 < MR ? KR0 : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
+  // part-B rows whose (J, Y) columns live in the LDS left dead by the tree phases (R[1..MN-1], x, V: written by
+  // fk(), read by collide(), not again until the next fk()) instead of scratch, one float per lane and row for J
+  // and for Y; locomotion instances only (the hand kernels keep their tree tiles live longer: egg_stage /
+  // reload_tree, the object rows).  Off by default (MG_PART_B_LDS=1 builds it): same box, it cut Humanoid 32,768's
+  // HBM-side traffic 156 -> 119 MB per launch and Ant 65,536's 70.5 -> 61.6 MB, but cost 1.2 % (Humanoid) to 3 %
+  // (Ant 16,384, MA-Ant) of throughput (profiles/r05/ab_part_b_lds.txt)
+  static constexpr int PBL0 = (OBJ || !MG_PART_B_LDS) ? 0 : (int)(((MN - 1) * 9 + MN * 9) / (2 * T));
+  static constexpr int PBL = KR + PBL0 <= MR ? PBL0 : (MR - KR > 0 ? MR - KR : 0);
+#if MG_PART_B_LDS
+  // S first: the link axes outlive the solve (clamp_ang_vel reads them after the PGS), as does R[0]; the storage
+  // from R[1] through V is dead from the end of collide() to the next fk(), and holds part-B PGS rows (PBL)
+  float S[MN][6];
+  float R[MN][9];
+  float x[MN][3];
+  float V[MN][6];
+#else
   float R[MN][9];
   float x[MN][3];
   float V[MN][6];
   float S[MN][6];
+#endif
   float U[MN][6];
   float Dinv[MN];
   unsigned long long anc[MN];
@@ -2262,6 +2282,32 @@ struct Team {
     // (J_r[j], Y_r[j]) of the first KR rows live in registers (the index is wave-uniform, so the compiler
     // promotes the arrays to VGPRs and addresses them with relative moves); the remaining rows are
     // private arrays in scratch.  Wave-uniform branches pick the side.
+#if MG_PART_B_LDS
+    constexpr int KR = L::KR, PBL = L::PBL;
+    float Jr[KR > 0 ? KR : 1], Yr[KR > 0 ? KR : 1];
+    float Js[MR - KR - PBL > 0 ? MR - KR - PBL : 1], Ys[MR - KR - PBL > 0 ? MR - KR - PBL : 1];
+    // part B: rows KR .. KR + PBL - 1 in the dead tree tiles (J rows, then Y rows, lane-contiguous), the rest scratch
+    float* const pbj = &s->R[1][0] + tl;
+    float* const pby = pbj + PBL * T;
+#define MG_JSET(r, j, y)                                   \
+  do {                                                     \
+    if ((r) < KR) {                                        \
+      Jr[r] = (j); Yr[r] = (y);                            \
+    } else if ((r) < KR + PBL) {                           \
+      pbj[((r) - KR) * T] = (j); pby[((r) - KR) * T] = (y); \
+    } else {                                               \
+      Js[(r) - KR - PBL] = (j); Ys[(r) - KR - PBL] = (y);   \
+    }                                                      \
+  } while (0)
+#define MG_JGET(r, jo, yo)                                     \
+  do {                                                         \
+    if ((r) < KR + PBL) {                                      \
+      jo = pbj[((r) - KR) * T]; yo = pby[((r) - KR) * T];      \
+    } else {                                                   \
+      jo = Js[(r) - KR - PBL]; yo = Ys[(r) - KR - PBL];        \
+    }                                                          \
+  } while (0)
+#else
     constexpr int KR = L::KR;
     float Jr[KR > 0 ? KR : 1], Yr[KR > 0 ? KR : 1];
     float Js[MR - KR > 0 ? MR - KR : 1], Ys[MR - KR > 0 ? MR - KR : 1];
@@ -2273,6 +2319,11 @@ struct Team {
       Js[(r) - KR] = (j); Ys[(r) - KR] = (y); \
     }                                    \
   } while (0)
+#define MG_JGET(r, jo, yo)               \
+  do {                                   \
+    jo = Js[(r) - KR]; yo = Ys[(r) - KR]; \
+  } while (0)
+#endif
     for (int r0 = 0; r0 < wave_rows; r0 += L::RB) {
       float jb[L::RB], yb[L::RB];
 #pragma unroll
@@ -2358,8 +2409,7 @@ struct Team {
     if (prow > KR) {
 #pragma unroll
       for (int k = 0; k < PF; k++) {
-        pJ[k] = Js[k];
-        pY[k] = Ys[k];
+        MG_JGET(KR + k, pJ[k], pY[k]);
         pR[k] = s->u.sv.rows[KR + k];
       }
     }
@@ -2394,10 +2444,7 @@ struct Team {
         // compiler barrier keeps the scheduler from sinking them behind the first visits
         float nJ[PF], nY[PF];
 #pragma unroll
-        for (int k = 0; k < PF; k++) {
-          nJ[k] = Js[rn - KR + k];
-          nY[k] = Ys[rn - KR + k];
-        }
+        for (int k = 0; k < PF; k++) MG_JGET(rn + k, nJ[k], nY[k]);
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int k = 0; k < PF; k++) {
@@ -2410,6 +2457,7 @@ struct Team {
     }
     wsync();
 #undef MG_JSET
+#undef MG_JGET
     ph_mark(6);
     clamp_ang_vel();
     integrate();
