@@ -182,7 +182,7 @@ def pmc_traffic(task, n, kern_ms, object_type="block"):
     None when no pass was recorded for this workload."""
     path = None
     tag = task if (task != "ShadowHand" or object_type == "block") else f"{task}-{object_type}"   # per kernel instance
-    for rnd in ("r04", "r03", "r02", "r01"):   # the newest round's passes of this workload
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):   # the newest round's passes of this workload
         cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_{n}.json")
         if os.path.exists(cand):
             path = cand

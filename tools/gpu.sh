@@ -14,7 +14,8 @@
 #   tools/gpu.sh traffic OUT "VAR..." SPEC      FETCH_SIZE / WRITE_SIZE passes (and a bench line) per variant
 #   tools/gpu.sh phase OUT SPEC...              per-phase cycle profile (the --timing build)
 #   tools/gpu.sh multirank N                    torchrun x N ranks sharing the one GPU (gloo), both gather modes
-#   tools/gpu.sh round R                        a round's evidence: kernel stats, PMC per instance, bench lines
+#   tools/gpu.sh profile R                      a round's kernel stats and PMC passes per kernel instance
+#   tools/gpu.sh lines R                        a round's bench lines of every config
 #
 # Every GPU step runs under its own timeout and the first failure ends the job (no retries).
 set -u
@@ -132,18 +133,21 @@ case $mode in
       rc=$?; echo "rc=$rc"; tail -n 2 gpurun_out/multirank/x${N}_$gm.log
       [ $rc -eq 0 ] || exit $rc
     done ;;
-  round)
+  profile)   # a round's kernel stats + PMC passes per kernel instance (copy the pmc_*.json into profiles/R after)
     R=${1:?round}; OUT=gpurun_out/$R; mkdir -p "$OUT"
     "$0" stats "$R/stats" --steps 50 --warmup 5 --no-cpu-baseline --no-strong || exit 1
     for spec in "Ant 65536 block" "Humanoid 32768 block" "ShadowHand 16384 block" "ShadowHand 16384 egg" \
-                "ShadowHand 16384 pen"; do
+                "ShadowHand 16384 pen" "MAAnt 8192 block" "ShadowHand 4096 block"; do
       set -- $spec
       "$0" pmc "$R/pmc_$1_$2_$3" "$1" "$2" "$3" > "$OUT/pmc_$1_$2_$3.log" 2>&1 || { tail -5 "$OUT/pmc_$1_$2_$3.log"; exit 1; }
       tag=$1; [ "$3" != block ] && tag=$1-$3
       mkdir -p "profiles/$R"; cp "$OUT/pmc_$1_$2_$3/pmc_${tag}_$2.json" "profiles/$R/"   # bench lines cite this build
-    done
-    BENCH_ARGS="--cpu-seconds 10" "$0" bench "$R/bench" Ant:65536 Ant:32768 Ant:16384 Ant:8192 Humanoid:32768 \
-      MAAnt:8192 MAAnt:65536 ShadowHand:16384 ShadowHand:4096 ShadowHand:32768 Cartpole:256::1000 \
+      echo "pmc $spec done"
+    done ;;
+  lines)     # the round's bench lines of every config (cpu baselines included)
+    R=${1:?round}
+    BENCH_ARGS="--cpu-seconds 10 --no-strong" "$0" bench "$R/bench" Ant:65536 Ant:32768 Ant:16384 Ant:8192 \
+      Humanoid:32768 MAAnt:8192 MAAnt:65536 ShadowHand:16384 ShadowHand:4096 ShadowHand:32768 Cartpole:256::1000 \
       ShadowHand:16384:egg ShadowHand:16384:pen ;;
   *) echo "unknown mode $mode"; exit 2 ;;
 esac
