@@ -64,7 +64,7 @@ def usable_cores():
     return max(1, n), ", ".join(how)
 
 
-def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
+def cpu_baseline(task, seconds=10.0, n=65536, object_type="block", solver="pgs"):
     """The oracle's fp32 restatement of the same step (oracle/build/liboracle_f32.so: fp32 physics, fp32 task
     layer, OpenMP over envs), timed on this box's host cores at the workload's own env count on a bounded
     sample of steps: once with every core this process may use (``usable_cores``: affinity, cgroup quota,
@@ -81,6 +81,7 @@ def cpu_baseline(task, seconds=10.0, n=65536, object_type="block"):
     A = int(cfg["env"].get("numAgents", 1)) if task == "MAAnt" else 1
     if task == "ShadowHand":
         cfg["env"]["objectType"] = object_type
+    cfg["sim"]["physx"]["solver"] = solver
     spec = taskdefs.hand_spec(object_type) if task == "ShadowHand" else M.load_builtin(taskdefs.TASK_INFO[base][1])
     sp = taskdefs.sim_params(cfg, taskdefs.TASK_INFO[base][5], A)
     tp = taskdefs.task_params(task, cfg, spec)
@@ -227,10 +228,12 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
     import torch.distributed as dist
     import migym
     mk = {}
-    if task == "ShadowHand" and object_type != "block":
+    if (task == "ShadowHand" and object_type != "block") or args.solver != "pgs":
         from migym import configs
-        tcfg = configs.task_config("ShadowHand", n, sim_device=dev)
-        tcfg["env"]["objectType"] = object_type
+        tcfg = configs.task_config(task, n, sim_device=dev)
+        if task == "ShadowHand":
+            tcfg["env"]["objectType"] = object_type
+        tcfg["sim"]["physx"]["solver"] = args.solver
         mk["cfg"] = {"task": tcfg}
     env = migym.make(seed=seed, task=task, num_envs=n, sim_device=dev, rl_device=dev, headless=True,
                      multi_gpu=world > 1, **mk)
@@ -291,7 +294,10 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, event_ms = float(t[0]), float(t[1]), float(t[2])
-    info = {"substeps": env.sim_params.substeps, "pos_iters": env.sim_params.pos_iters, "agents": env.num_agents}
+    info = {"substeps": env.sim_params.substeps, "pos_iters": env.sim_params.pos_iters, "agents": env.num_agents,
+            "solver": "TGS" if env.sim_params.solver_type == 1 else "PGS",
+            "vel_sweeps": max(env.sim_params.pos_iters, env.sim_params.vel_iters) if env.sim_params.solver_type == 1
+            else 0}
     env.close()
     del env, pool, gather
     value = n * world * args.steps / elapsed
@@ -329,6 +335,8 @@ def main():
                     help="skip the strong-scaling lines (BASELINE configs[3]/[4] and Ant 65,536 as fixed totals "
                          "split over the ranks)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--solver", default="pgs", choices=["pgs", "tgs"],
+                    help="sim.physx.solver: north_star's PGS (default) or the build-defined TGS (DESIGN.md §4)")
     ap.add_argument("--object-type", default="block", choices=["block", "egg", "pen"],
                     help="ShadowHand objectType (shadow_hand.py:86-100)")
     args = ap.parse_args()
@@ -375,7 +383,8 @@ def main():
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (U(-1,1) actions, device-resident)",
             "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, {env['substeps']} substeps, "
-                                   f"PGS x{env['pos_iters']}",
+                                   + (f"PGS x{env['pos_iters']}" if env["solver"] == "PGS" else
+                                      f"TGS x{env['pos_iters']} sub-steps + {env['vel_sweeps']} velocity sweeps"),
                        "task": args.task, "num_envs_per_gpu": n, "num_envs_total": n * world,
                        "agents_per_env": env["agents"], "agent_steps_per_s": value * env["agents"],
                        "obs_gather": (f"{gather_mode}: kernel-packed [obs|rew|reset] rows, double-buffered, "
@@ -397,7 +406,7 @@ def main():
             out["strong_scaling"] = [{k: v for k, v in r.items() if k != "env_info"} for r in strong]
         if not args.no_cpu_baseline and world == 1:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n, args.object_type)
+                out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_seconds, n, args.object_type, args.solver)
             except Exception as ex:  # noqa: BLE001
                 out["cpu_baseline"] = {"error": repr(ex)}
         if not args.no_cpu_baseline and world == 1:

@@ -167,7 +167,14 @@ typedef struct mg_sim_params {
   float limit_margin;       /* joint-limit rows are built when within this distance */
   int32_t max_contacts;     /* per-actor contact capacity (<= MG_MAX_CONTACTS) */
   int32_t agents;           /* articulations per env (MA layouts; 1 otherwise) */
+  int16_t solver_type;      /* MG_SOLVER_PGS (0, north_star) or MG_SOLVER_TGS (1, the reference's default,
+                             * config.yaml:31): build-defined TGS, DESIGN.md §4 */
+  int16_t vel_iters;        /* physx.num_velocity_iterations: TGS runs max(pos_iters, vel_iters) bias-free velocity
+                             * sweeps after its sub-steps; unused by PGS.  (Two int16 keep the struct at 60 bytes:
+                             * the kernels' argument layout, and so their code, stays as it was) */
 } mg_sim_params;
+#define MG_SOLVER_PGS 0
+#define MG_SOLVER_TGS 1
 
 /* Gym-visible state buffers the sim reads/writes (zero-copy, caller owned). */
 typedef struct mg_state_views {

@@ -533,6 +533,8 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
       return fail(MG_EINVAL, "mg_sim_create: nodes must be topologically ordered (parent < child)");
   if (params->substeps < 1 || params->dt <= 0.0f || params->max_contacts < 0)
     return fail(MG_EINVAL, "mg_sim_create: bad sim params");
+  if ((params->solver_type != MG_SOLVER_PGS && params->solver_type != MG_SOLVER_TGS) || params->vel_iters < 0)
+    return fail(MG_EINVAL, "mg_sim_create: solver_type must be MG_SOLVER_PGS or MG_SOLVER_TGS, vel_iters >= 0");
   // the exact hull-object candidates are computed before the tree phases (team_physics.hpp hull_stage), from
   // the fixed root's pose: a convex-mesh geom colliding with a block / pen object must sit on that root
   if (model->obj_type == MG_GT_BOX || model->obj_type == MG_GT_CAPSULE)
@@ -630,6 +632,8 @@ int mg_sim_set_params(mg_sim* sim, const mg_sim_params* params) {
     return fail(MG_EINVAL, "mg_sim_set_params: bad arguments");
   if (params->max_contacts != sim->params.max_contacts || params->agents != sim->params.agents)
     return fail(MG_EINVAL, "mg_sim_set_params: max_contacts / agents are fixed at mg_sim_create");
+  if ((params->solver_type != MG_SOLVER_PGS && params->solver_type != MG_SOLVER_TGS) || params->vel_iters < 0)
+    return fail(MG_EINVAL, "mg_sim_set_params: solver_type must be MG_SOLVER_PGS or MG_SOLVER_TGS, vel_iters >= 0");
   sim->params = *params;  // taken by value by every later launch
   return MG_OK;
 }

@@ -117,7 +117,7 @@ __device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
-template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
+template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR, bool TGS = false>
 __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_simulate(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_state_views v, int n) {
   using SH = Shape<T, MN, MC, MG, MP, OBJ, DR>;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors;
-  mg::Team<T, MN, MC, MG, MP, OBJ> t;
+  mg::Team<T, MN, MC, MG, MP, OBJ, TGS> t;
   t.init(&lds[team].v, &tile, m, &p);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
@@ -195,7 +195,7 @@ __device__ __forceinline__ int ordered_actor(const MgOrder& ord, int slot, int n
 }
 
 // one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
-template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
+template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void env_step_item(
     const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
@@ -209,7 +209,7 @@ __device__ __forceinline__ void env_step_item(
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
   mg::TeamLDS<T, MN, MC>& L = lds[team].v;
-  mg::Team<T, MN, MC, MG, MP> t;
+  mg::Team<T, MN, MC, MG, MP, 0, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
@@ -395,7 +395,7 @@ __device__ __forceinline__ void env_step_item(
   MG_PHASE_FLUSH(t, item)
 }
 
-template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP>
+template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
 __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_env_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
@@ -409,14 +409,14 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {
     // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
-    if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
+    if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   } else {
     // multi-wave blocks: the work queue (wq_next), the grid being the resident capacity
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
       const int z = opaque_zero();
-      env_step_item<T, MN, MC, MG, MP, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
+      env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
                                                (&rp)[z], item, (&ord)[z]);
     }
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -437,7 +437,7 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // the running mean) -> timeout, obs clamp, state write-back.  One team of T lanes per env.
 // RP: physics-bypass replay instance (mg_env_step_replay), as k_env_step's.
 // one work item of k_hand_step: the E1 teams of one wave (item = the wave's global index)
-template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
+template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void hand_step_item(
     const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
@@ -451,7 +451,7 @@ __device__ __forceinline__ void hand_step_item(
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
   mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
-  mg::Team<T, MN, MC, MG, MP, OT> t;
+  mg::Team<T, MN, MC, MG, MP, OT, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ec, m, t.tl);
@@ -682,7 +682,7 @@ __device__ __forceinline__ void hand_step_item(
   MG_PHASE_FLUSH(t, item)
 }
 
-template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP>
+template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP, bool TGS = false>
 __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_hand_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
@@ -695,13 +695,13 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {  // as k_env_step
-    if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
+    if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   } else {
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
       const int z = opaque_zero();
-      hand_step_item<T, MN, MC, MG, MP, OT, DR, RP>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z],
+      hand_step_item<T, MN, MC, MG, MP, OT, DR, RP, TGS>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z],
                                                     (&tb)[z], n, (&rp)[z], item, (&ord)[z]);
     }
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -770,13 +770,22 @@ int BuildTile<T, MN, MC, MG, MP, OBJ>::run(mg_sim* sim) {
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int RunSimulate<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim) {
   if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_sim_simulate: no model tile (model exceeds every kernel instance)");
-  // the domain-randomized instance reads each actor's env_props row (mg_dr_apply)
-  if (sim->views.env_props)
-    launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_simulate<T, MN, MC, MG, MP, OBJ, true>, s, sim->n, sim->d_model,
-                                                 (const void*)sim->d_tile, sim->params, sim->views, sim->n);
-  else
+  // the domain-randomized instance reads each actor's env_props row (mg_dr_apply); TGS runs its own instances
+  const bool tgs = sim->params.solver_type == MG_SOLVER_TGS;
+  if (sim->views.env_props) {
+    if (tgs)
+      launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_simulate<T, MN, MC, MG, MP, OBJ, true, true>, s, sim->n, sim->d_model,
+                                                   (const void*)sim->d_tile, sim->params, sim->views, sim->n);
+    else
+      launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_simulate<T, MN, MC, MG, MP, OBJ, true>, s, sim->n, sim->d_model,
+                                                   (const void*)sim->d_tile, sim->params, sim->views, sim->n);
+  } else if (tgs) {
+    launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_simulate<T, MN, MC, MG, MP, OBJ, false, true>, s, sim->n, sim->d_model,
+                                                  (const void*)sim->d_tile, sim->params, sim->views, sim->n);
+  } else {
     launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_simulate<T, MN, MC, MG, MP, OBJ, false>, s, sim->n, sim->d_model,
                                                   (const void*)sim->d_tile, sim->params, sim->views, sim->n);
+  }
   return MG_OK;
 }
 
@@ -800,15 +809,22 @@ int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, co
     return fail(MG_EINVAL, "mg_env_step_replay: no replay instance with domain randomization");
   const mg_replay r = rp ? *rp : mg_replay{};
   const void* ti = sim->d_tile;
+  const bool tgs = sim->params.solver_type == MG_SOLVER_TGS;  // TGS runs its own instances (not the replay's: no physics)
   if constexpr (OBJ != 0) {
     mg_task_params tpm = *tp;  // observation column maps (hand_task.hpp h_fill_maps)
     mg::h_fill_maps(&tpm);
     if (rp)
       return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, true>, s, sim, false,
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
+    else if (sim->views.env_props && tgs)
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false, true>, s, sim,
+                                                   true, sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
       return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_hand_step<T, MN, MC, MG, MP, OBJ, true, false>, s, sim, true,
                                                    sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
+    else if (tgs)
+      return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false, true>, s, sim,
+                                                    true, sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
     else
       return launch_wq<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_hand_step<T, MN, MC, MG, MP, OBJ, false, false>, s, sim, true,
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
@@ -816,9 +832,15 @@ int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, co
     if (rp)
       return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim, false, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
+    else if (sim->views.env_props && tgs)
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false, true>, s, sim, true,
+                                                 sim->d_model, ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
       return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim, true, sim->d_model,
                                                  ti, sim->params, *tp, sim->views, *tb, sim->n, r);
+    else if (tgs)
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false, true>, s, sim, true,
+                                                  sim->d_model, ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else
       return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim, true, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);

@@ -679,7 +679,9 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
 // Per-lane context of one team.  Every member function is force-inlined: one that the inliner leaves as a
 // call (it declined fk() once the egg kernel grew) takes `this`, which puts the whole Team object in scratch
 // memory, and every phase then runs from scratch (egg: 7.4 -> 4.7 M env-steps/s until this was found).
-template <int T, int MN, int MC, int MG, int MP, int OBJ = 0>  // OBJ: the free object's type (0: none)
+// OBJ: the free object's type (0: none); TGS: the build's TGS solver (mg_sim_params.solver_type) -- its
+// own kernel instances, so the PGS instances are the code they were
+template <int T, int MN, int MC, int MG, int MP, int OBJ = 0, bool TGS = false>
 struct Team {
   using L = TeamLDS<T, MN, MC, OBJ>;
   using MT = ModelTile<MN, MG, MP, tile_hull_verts(OBJ)>;
@@ -2192,7 +2194,7 @@ struct Team {
       s->ct2[c][0] = t2.x; s->ct2[c][1] = t2.y; s->ct2[c][2] = t2.z;
       float deff = s->cd[c] - p->rest_offset;
       float bn = deff >= 0.0f ? -deff * ih : fminf(-p->baumgarte * deff * ih, p->max_depen_vel);
-      s->u.sv.rows[3 * c].b = bn;
+      s->u.sv.rows[3 * c].b = TGS ? deff : bn;   // TGS: the gap; its target is set per sweep (substep())
       s->u.sv.rows[3 * c + 1].b = 0.0f;
       s->u.sv.rows[3 * c + 2].b = 0.0f;
       if constexpr (L::OROWS > 1) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
@@ -2226,7 +2228,7 @@ struct Team {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
       float d = side == 0 ? dl : du;
-      s->u.sv.rows[3 * ncon + li].b = d >= 0.0f ? -d * ih : fminf(-p->baumgarte * d * ih, p->max_depen_vel);
+      s->u.sv.rows[3 * ncon + li].b = TGS ? d : (d >= 0.0f ? -d * ih : fminf(-p->baumgarte * d * ih, p->max_depen_vel));
       s->lmeta[li] = (2 + side) | (node << 4);
       li++;
     }
@@ -2390,6 +2392,13 @@ struct Team {
     // row records are loaded one block ahead); the rows from KR on run part B, whose scratch columns and
     // row records rotate through PF registers loaded a block ahead and wrap into the next sweep's part B.
     float lamn = 0.0f;
+    // TGS: the sub-steps' accumulated displacement of this lane's column, 1 / (h / N), and the sweeps: N position
+    // sub-steps, then max(N, vel_iters) velocity sweeps with the bias off (a separated row's speculative target on h)
+    float dqs = 0.0f;
+    const float hs = TGS ? h / (float)(p->pos_iters > 0 ? p->pos_iters : 1) : 0.0f;
+    const float ihs = TGS ? prcp(hs) : 0.0f;
+    float tisp = ihs, tbz = TGS ? p->baumgarte : 0.0f;
+    const int n_sweeps = TGS ? p->pos_iters + max(p->pos_iters, p->vel_iters) : p->pos_iters;
     auto visit = [&](float J, float Y, const typename L::Row& R, int r) {
       const float v = team_sum<T>(J * nu, tb);
       const float lam = R.lam, m = R.mu;
@@ -2398,7 +2407,13 @@ struct Team {
       const bool fric = m >= 0.0f;
       const float t = fric ? m * lamn : 0.0f;
       const float hi = fric ? t : __builtin_inff();
-      const float lnew = __builtin_amdgcn_fmed3f(lam + (R.b - v) * R.iw, -t, hi);
+      float tgt = R.b;
+      if constexpr (TGS) {  // target from the gap moved by the sub-steps so far: e = e0 + J . dq, on h / N
+        const float e = R.b + team_sum<T>(J * dqs, tb);
+        const float te = e >= 0.0f ? -e * tisp : fminf(-tbz * e * ihs, p->max_depen_vel);
+        tgt = fric ? 0.0f : te;
+      }
+      const float lnew = __builtin_amdgcn_fmed3f(lam + (tgt - v) * R.iw, -t, hi);
       lamn = m == -1.0f ? lnew : lamn;
       s->u.sv.rows[r].lam = lnew;
       nu += Y * (lnew - lam);
@@ -2413,7 +2428,13 @@ struct Team {
         pR[k] = s->u.sv.rows[KR + k];
       }
     }
-    for (int it = 0; it < p->pos_iters; it++) {
+    for (int it = 0; it < n_sweeps; it++) {
+      if constexpr (TGS) {
+        if (it == p->pos_iters) {  // the velocity sweeps: bias off
+          tisp = prcp(h);
+          tbz = 0.0f;
+        }
+      }
       if constexpr (KR > 0) {
         typename L::Row cR[PF];
         if (pa > 0) {
@@ -2454,13 +2475,20 @@ struct Team {
           pR[k] = s->u.sv.rows[rn + k];
         }
       }
+      if constexpr (TGS) {  // the sub-step's displacement
+        if (it < p->pos_iters) dqs += hs * nu;
+      }
     }
     wsync();
 #undef MG_JSET
 #undef MG_JGET
     ph_mark(6);
     clamp_ang_vel();
-    integrate();
+    if constexpr (TGS) {
+      integrate_tgs(dqs);
+    } else {
+      integrate();
+    }
     ph_mark(7);
   }
 
@@ -2585,6 +2613,50 @@ struct Team {
       const float l = prsq(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
       for (int k = 0; k < 4; k++) oq[k] = qn[k] * l;
       op = op + vc * h;
+    }
+  }
+
+  // TGS: positions by the sub-steps' accumulated displacement dq (this lane's column) instead of h nu -- the root's
+  // rotation vector dq[0..2] by the exponential map, its origin by dq[3..5], the final twist re-expressed at the new
+  // origin; joints q += dq; the free object likewise; velocities are the final nu, after the velocity sweeps and the
+  // cap (oracle tgs_integrate).
+  __device__ __forceinline__ static void rotvec_quat(V3 th, float* q) {
+    const float tn = sqrtf(dot(th, th));
+    float d[4];
+    if (tn > 1e-12f) {
+      const float ha = 0.5f * tn, sn = sinf(ha) * prcp(tn);
+      d[0] = th.x * sn; d[1] = th.y * sn; d[2] = th.z * sn; d[3] = cosf(ha);
+    } else {
+      d[0] = 0.5f * th.x; d[1] = 0.5f * th.y; d[2] = 0.5f * th.z; d[3] = 1.0f;
+    }
+    const float* a = d;
+    const float b[4] = {q[0], q[1], q[2], q[3]};
+    float qn[4] = {a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1],
+                   a[3] * b[1] - a[0] * b[2] + a[1] * b[3] + a[2] * b[0],
+                   a[3] * b[2] + a[0] * b[1] - a[1] * b[0] + a[2] * b[3],
+                   a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2]};
+    const float l = prsq(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+    for (int k = 0; k < 4; k++) q[k] = qn[k] * l;
+  }
+  __device__ __forceinline__ void integrate_tgs(float dq) {
+    if (freeb) {
+      const V3 th = v3(__shfl(dq, tb + 0), __shfl(dq, tb + 1), __shfl(dq, tb + 2));
+      const V3 dp = v3(__shfl(dq, tb + 3), __shfl(dq, tb + 4), __shfl(dq, tb + 5));
+      const V3 om = v3(__shfl(nu, tb + 0), __shfl(nu, tb + 1), __shfl(nu, tb + 2));
+      const V3 vo = v3(__shfl(nu, tb + 3), __shfl(nu, tb + 4), __shfl(nu, tb + 5));
+      rotvec_quat(th, q0);
+      p0 = p0 + dp;
+      const V3 vn = vo + cross(om, dp);
+      if (tl == 3) nu = vn.x;
+      if (tl == 4) nu = vn.y;
+      if (tl == 5) nu = vn.z;
+    }
+    if (node > 0) qj += dq;
+    if (OBJ) {
+      const V3 th = v3(__shfl(dq, tb + ob0), __shfl(dq, tb + ob0 + 1), __shfl(dq, tb + ob0 + 2));
+      const V3 dp = v3(__shfl(dq, tb + ob0 + 3), __shfl(dq, tb + ob0 + 4), __shfl(dq, tb + ob0 + 5));
+      rotvec_quat(th, oq);
+      op = op + dp;
     }
   }
 

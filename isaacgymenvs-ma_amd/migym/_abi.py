@@ -29,7 +29,11 @@ class SimParams(C.Structure):
     _fields_ = [("dt", C.c_float), ("substeps", C.c_int32), ("gravity", C.c_float * 3),
                 ("pos_iters", C.c_int32), ("contact_offset", C.c_float), ("rest_offset", C.c_float),
                 ("max_depen_vel", C.c_float), ("friction", C.c_float), ("baumgarte", C.c_float),
-                ("limit_margin", C.c_float), ("max_contacts", C.c_int32), ("agents", C.c_int32)]
+                ("limit_margin", C.c_float), ("max_contacts", C.c_int32), ("agents", C.c_int32),
+                ("solver_type", C.c_int16), ("vel_iters", C.c_int16)]
+
+
+MG_SOLVER_PGS, MG_SOLVER_TGS = 0, 1
 
 
 class StateViews(C.Structure):

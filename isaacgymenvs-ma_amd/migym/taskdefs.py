@@ -46,6 +46,13 @@ def sim_params(cfg: dict, max_contacts: int, agents: int = 1) -> _abi.SimParams:
     p.limit_margin = LIMIT_MARGIN
     p.max_contacts = int(max_contacts)
     p.agents = int(agents)
+    # the solver: north_star fixes PGS for this build, so the reference's `physx.solver_type` (config.yaml:31, 1 = TGS
+    # by default) does not select it; `physx.solver: tgs` opts in to the build's TGS
+    solver = str(px.get("solver", "pgs")).lower()
+    if solver not in ("pgs", "tgs"):
+        raise ValueError(f"sim.physx.solver must be 'pgs' or 'tgs', got {solver!r}")
+    p.solver_type = _abi.MG_SOLVER_TGS if solver == "tgs" else _abi.MG_SOLVER_PGS
+    p.vel_iters = int(px.get("num_velocity_iterations", 0))
     return p
 
 

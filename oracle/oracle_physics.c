@@ -2450,6 +2450,44 @@ typedef struct {
   int row_ref[MAXR];  /* contact index or node */
 } substep_out;
 
+/* TGS integration: positions by the accumulated sub-step displacement dq instead of h nu (root: rotation vector
+ * dq[0..2] by the exponential map, origin by dq[3..5], the final twist re-expressed at the new origin; joints
+ * q += dq; the free object likewise); velocities are the final nu (after the velocity sweeps and the cap) */
+static void tgs_rot(const real* th, const real* q, real* out) {
+  real tn = sqrt(dot3(th, th)), d[4];
+  if (tn > 1e-12) {
+    real sn = sin(0.5 * tn) / tn;
+    d[0] = th[0] * sn; d[1] = th[1] * sn; d[2] = th[2] * sn; d[3] = cos(0.5 * tn);
+  } else {
+    d[0] = 0.5 * th[0]; d[1] = 0.5 * th[1]; d[2] = 0.5 * th[2]; d[3] = 1.0;
+  }
+  real qn[4];
+  quat_mul_d(d, q, qn);
+  real l = sqrt(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+  for (int a = 0; a < 4; a++) out[a] = qn[a] / l;
+}
+static void tgs_integrate(const mg_model* m, astate* s, const real* nu, const real* dq) {
+  const int nv = nv_of(m), nn = m->num_nodes;
+  if (!m->fixed_base) {
+    tgs_rot(dq, s->q, s->q);
+    real dp[3] = {dq[3], dq[4], dq[5]}, w[3] = {nu[0], nu[1], nu[2]}, wxdp[3];
+    cross3(w, dp, wxdp);
+    for (int a = 0; a < 3; a++) { s->p[a] += dp[a]; s->nu0[a] = w[a]; s->nu0[3 + a] = nu[3 + a] + wxdp[a]; }
+  }
+  for (int i = 1; i < nn; i++) {
+    s->qd[i] = nu[dof_col(m, i)];
+    s->qj[i] += dq[dof_col(m, i)];
+  }
+  if (m->obj_type) {
+    tgs_rot(dq + nv, s->oq, s->oq);
+    for (int a = 0; a < 3; a++) {
+      s->ow[a] = nu[nv + a];
+      s->ov[a] = nu[nv + 3 + a];
+      s->op[a] += dq[nv + 3 + a];
+    }
+  }
+}
+
 static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const real* tau_act, substep_out* so) {
   int nv = nv_of(m), nvt = nvt_of(m), nn = m->num_nodes;
   real h = p->dt / p->substeps;
@@ -2515,8 +2553,17 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
   int cap = p->max_contacts < MAXC ? p->max_contacts : MAXC;
   so->ncon = collide(m, p, &k, so->con, cap);
   static __thread real J[MAXR][MAXV], Y[MAXR][MAXV];
-  real b[MAXR], W[MAXR];
+  real b[MAXR], W[MAXR], e0[MAXR];
   int nr = 0;
+  /* TGS (p->solver_type == 1): the position iterations are sub-steps of h / N; a normal / limit row's target is
+   * recomputed each sweep from its gap moved by the accumulated displacement, e = e0 + J . dq (e0 = the row's gap
+   * at the substep start), with the PGS rule on h / N, and each sub-step moves the positions by (h / N) nu.  Then
+   * max(N, vel_iters) velocity sweeps with the bias off (a penetrating row targets 0, a separated one -e / h) take
+   * the depenetration velocity back out of nu: the position error is corrected through dq, not carried on as
+   * momentum.  Friction rows target 0 throughout, as in PGS */
+  const int tgs = p->solver_type == MG_SOLVER_TGS;
+  const real hs = h / (p->pos_iters > 0 ? p->pos_iters : 1);
+  const int n_sweeps = p->pos_iters + (tgs ? (p->vel_iters > p->pos_iters ? p->vel_iters : p->pos_iters) : 0);
   for (int c = 0; c < so->ncon; c++) {
     contact* ct = &so->con[c];
     real t1[3], t2[3];
@@ -2527,6 +2574,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     for (int r = 0; r < 3; r++) {
       jac_row(m, &k, ct->nodeA, ct->nodeB, ct->p, dirs[r], J[nr]);
       b[nr] = r == 0 ? bn : 0.0;
+      e0[nr] = r == 0 ? deff : 0.0;
       so->row_kind[nr] = r == 0 ? 0 : 1;
       so->row_ref[nr] = c;
       nr++;
@@ -2541,6 +2589,7 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       memset(J[nr], 0, sizeof(real) * nvt);
       J[nr][dof_col(m, i)] = side == 0 ? 1.0 : -1.0;
       b[nr] = d >= 0 ? -d / h : fmin(-p->baumgarte * d / h, p->max_depen_vel);
+      e0[nr] = d;
       so->row_kind[nr] = 2 + side;
       so->row_ref[nr] = i;
       nr++;
@@ -2556,12 +2605,25 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     so->lam[r] = 0;
     so->lmax[r] = 0;
   }
-  for (int it = 0; it < p->pos_iters; it++) {
+  real dq[MAXV];   /* TGS: the accumulated displacement of the sub-steps (generalized coordinates) */
+  for (int c = 0; c < nvt; c++) dq[c] = 0.0;
+  for (int it = 0; it < n_sweeps; it++) {
+    const int vel_sweep = it >= p->pos_iters;
     for (int r = 0; r < nr; r++) {
       if (W[r] <= 1e-12) continue;
       real v = 0;
       for (int c = 0; c < nvt; c++) v += J[r][c] * nu[c];
-      real lnew = so->lam[r] + (b[r] - v) / W[r];
+      real tr = b[r];
+      if (tgs && so->row_kind[r] != 1) {
+        real ed = 0;
+        for (int c = 0; c < nvt; c++) ed += J[r][c] * dq[c];
+        const real e = e0[r] + ed;
+        if (vel_sweep)
+          tr = e >= 0 ? -e / h : 0.0;
+        else
+          tr = e >= 0 ? -e / hs : fmin(-p->baumgarte * e / hs, p->max_depen_vel);
+      }
+      real lnew = so->lam[r] + (tr - v) / W[r];
       if (so->row_kind[r] == 1) {
         real mu = p->friction;
         if (s->gmu) { /* DR: mean of the two shapes' friction (ground plane: sim friction) */
@@ -2583,8 +2645,15 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
       if (fabs(lnew) > so->lmax[r]) so->lmax[r] = fabs(lnew);
       for (int c = 0; c < nvt; c++) nu[c] += Y[r][c] * dl;
     }
+    /* TGS: the sub-step's displacement */
+    if (tgs && !vel_sweep)
+      for (int c = 0; c < nvt; c++) dq[c] += hs * nu[c];
   }
   clamp_ang_vel(m, &k, nu);
+  if (tgs) {
+    tgs_integrate(m, s, nu, dq);
+    return;
+  }
   /* integrate */
   if (!m->fixed_base) {
     real w[3] = {nu[0], nu[1], nu[2]}, vo[3] = {nu[3], nu[4], nu[5]};

@@ -352,7 +352,8 @@ def test_hand_physics_hull_exact_matches_oracle(lib, kind):
     assert touching >= n // 2, touching
 
 
-def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra=None, obs_tol=2e-3):
+def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra=None, obs_tol=2e-3,
+                         reach_cap=PS.REACH_CAP):
     """mg_env_step vs orc_hand_env_step step by step, both sides started each step from the oracle's state (all
     buffers reloaded: DOF / root / rigid-body state, targets, goal, resets, successes, running mean, forces), so a
     step's fp32-vs-fp64 difference cannot grow chaotically over the next ones.  Per step: progress, targets and goals
@@ -396,7 +397,7 @@ def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra
         lib.mg_sim_destroy(sim)
     sens = lambda t, i: PS.oracle_sensitive_step(mnp, sp, tp, pres[t], actions[t], i, outs[t][0][i], outs[t][1][i],
                                                  seed=seed, step=t, hand=True)
-    PS.assert_steps_explained(test, bad, flags, sens)
+    PS.assert_steps_explained(test, bad, flags, sens, reach_cap=reach_cap)
     return ncon
 
 

@@ -354,3 +354,95 @@ def test_link_angular_velocity_cap(task, DOF, rate):
         outs.append((r, d))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+# ------------------------------------------------------------------ the build-defined TGS solver
+def test_tgs_selected_by_config():
+    """sim.physx.solver picks the solver ('pgs', north_star's, by default; 'tgs' opts in); num_velocity_iterations
+    goes to vel_iters; anything else is refused"""
+    cfg = configs.task_config("Ant", 4)
+    assert taskdefs.sim_params(cfg, 16).solver_type == 0
+    cfg["sim"]["physx"]["solver"] = "TGS"
+    cfg["sim"]["physx"]["num_velocity_iterations"] = 6
+    sp = taskdefs.sim_params(cfg, 16)
+    assert (sp.solver_type, sp.vel_iters) == (1, 6)
+    cfg["sim"]["physx"]["solver"] = "sor"
+    with pytest.raises(ValueError):
+        taskdefs.sim_params(cfg, 16)
+
+
+def test_tgs_without_rows_is_pgs():
+    """no contact or limit rows (in the air, limits off): the sub-steps move the positions by sum (h / N) nu = h nu,
+    so TGS is the PGS step up to the rounding of that sum"""
+    out = []
+    for st in (0, 1):
+        spec, mnp, sp, tp = setup("Ant", gravity=(0.0, 0.0, -9.81), max_contacts=0)
+        sp.limit_margin = -1.0
+        sp.solver_type = st
+        rng = np.random.default_rng(4)
+        root, dof = rand_state(spec, tp, rng, z=5.0)
+        dof[:, 0] = 0.5 * (np.array(tp.dof_lower[:8]) + np.array(tp.dof_upper[:8]))   # mid-range
+        dof[:, 1] *= 0.2
+        root, dof = root[None].copy(), dof[None].copy()
+        act = (rng.uniform(-1, 1, (1, 8)) * 2).astype(np.float32)
+        for _ in range(5):
+            O.simulate(mnp, sp, root, dof, act)
+            # the joints stay inside their limits (a limit row would make the solvers differ)
+            assert np.all((dof[0, :, 0] > tp.dof_lower[:8]) & (dof[0, :, 0] < tp.dof_upper[:8]))
+        out.append((root, dof))
+    np.testing.assert_allclose(out[1][0], out[0][0], atol=2e-6, rtol=1e-6)
+    np.testing.assert_allclose(out[1][1], out[0][1], atol=2e-6, rtol=1e-6)
+
+
+def _settled_ant(solver, steps=300):
+    spec, mnp, sp, tp = setup("Ant")
+    sp.solver_type = solver
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = 0.44
+    root[0, 6] = 1.0
+    dof = np.zeros((1, 8, 2), np.float32)
+    dof[0, :, 0] = np.array(tp.initial_dof_pos[:8])
+    for _ in range(steps):
+        O.simulate(mnp, sp, root, dof)
+    return mnp, sp, root, dof
+
+
+def test_tgs_corrects_penetration_without_momentum():
+    """A settled Ant pushed 2 cm into the plane: TGS moves the torso out through the sub-steps' displacement and its
+    velocity sweeps take the depenetration velocity back out -- it is nearly out after one step and never rises above
+    its rest height -- while PGS (Baumgarte, 0.2 per substep) needs ~10 steps"""
+    tr = {}
+    for st in (0, 1):
+        mnp, sp, root, dof = _settled_ant(st)
+        z0 = float(root[0, 2])
+        assert np.abs(root[0, 7:13]).max() < 0.05
+        root[0, 2] -= 0.02
+        root[0, 7:13] = 0
+        dof[0, :, 1] = 0
+        tr[st] = []
+        for _ in range(20):
+            O.simulate(mnp, sp, root, dof)
+            tr[st].append(float(root[0, 2]) - z0)
+    pgs, tgs = np.array(tr[0]), np.array(tr[1])
+    assert tgs[0] > -0.01 and abs(tgs[2]) < 1e-3, tgs       # measured: -6.6 mm after 1 step, -0.3 mm after 3
+    assert abs(pgs[2]) > 4e-3                                # PGS: -5.2 mm after 3
+    assert tgs.max() < 1e-3, tgs                             # no pop above the rest height (no injected momentum)
+    assert abs(tgs[-1]) < 1e-4 and abs(pgs[-1]) < 1e-4
+
+
+def test_tgs_dropped_ant_rests_and_holds_limits():
+    """TGS keeps the contact / limit behaviour: a dropped Ant rests on its feet, and saturating torque does not
+    push a joint through its limit"""
+    mnp, sp, root, dof = _settled_ant(1)
+    assert 0.3 < root[0, 2] < 0.44 and np.abs(root[0, 7:13]).max() < 0.05
+    spec, mnp, sp, tp = setup("Ant", gravity=(0.0, 0.0, 0.0))
+    sp.solver_type = 1
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = 3.0
+    root[0, 6] = 1.0
+    dof = np.zeros((1, 8, 2), np.float32)
+    dof[0, :, 0] = np.array(tp.initial_dof_pos[:8]) + 0.3
+    act = np.full((1, 8), 15.0, np.float32)
+    for _ in range(60):
+        O.simulate(mnp, sp, root, dof, act)
+    assert np.all(dof[0, :, 0] <= np.array(tp.dof_upper[:8]) + 0.02)
