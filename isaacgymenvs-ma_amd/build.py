@@ -56,7 +56,7 @@ def _run_parallel(cmds, verbose):
 
 def build(force=False, verbose=False, timing=False, variant=None, defines=(), extra=()):
     """variant: build an A/B variant with extra -D defines into migym/_lib/var/<variant>.so (selected at
-    run time through MIGYM_LIB, tools/gpu_variants.sh)."""
+    run time through MIGYM_LIB, tools/gpu.sh ab / traffic / pmc)."""
     out = OUT_TIMING if timing else OUT
     if variant:
         out = os.path.join(HERE, "migym", "_lib", "var", variant + ".so")
