@@ -137,8 +137,11 @@ def _dr_explained(test, mnp, sp, pre, checks, hand):
                               sens=lambda t, i: _physics_sensitive(mnp, sp, pre, i, checks, hand))
 
 
-def test_dr_physics_matches_oracle_ant(lib):
+@pytest.mark.parametrize("solver", ["pgs", "tgs"])
+def test_dr_physics_matches_oracle_ant(lib, solver):
+    """env_props rows on the GPU vs the oracle (solver tgs: the DR instance of the TGS kernels)"""
     cfg = configs.task_config("Ant", 16)
+    cfg["sim"]["physx"]["solver"] = solver
     spec = M.load_builtin("ant")
     sp = taskdefs.sim_params(cfg, 16)
     n = 384
@@ -176,7 +179,7 @@ def test_dr_physics_matches_oracle_ant(lib):
     lib.mg_sim_destroy(sim)
     rg, dg = tr.cpu().numpy(), td.cpu().numpy()
     assert np.isfinite(rg).all() and np.isfinite(dg).all()
-    _dr_explained("test_dr_physics_matches_oracle_ant", mnp, sp, pre,
+    _dr_explained(f"test_dr_physics_matches_oracle_ant[{solver}]", mnp, sp, pre,
                   [("root pose", rg[:, 0:7], h.root[:, 0:7], 2e-4, 0, lambda g: g.root[0, 0:7]),
                    ("root twist", rg[:, 7:13], h.root[:, 7:13], 2e-3, 2e-3, lambda g: g.root[0, 7:13]),
                    ("dof pos", dg[..., 0], h.dof[..., 0], 2e-4, 0, lambda g: g.dof[0, :, 0]),
@@ -188,12 +191,13 @@ def test_dr_physics_matches_oracle_ant(lib):
     assert agreement(h2.dof[..., 1], h.dof[..., 1], 2e-3, 2e-3) < 0.5
 
 
-@pytest.mark.parametrize("kind", ["block", "egg", "pen"])
-def test_dr_physics_matches_oracle_hand(lib, kind):
+@pytest.mark.parametrize("kind,solver", [("block", "pgs"), ("egg", "pgs"), ("pen", "pgs"), ("block", "tgs")])
+def test_dr_physics_matches_oracle_hand(lib, kind, solver):
     """env_props rows (masses, drives, friction, object mass / friction / scale) on the GPU vs the oracle;
     the object's scale reaches every shape's size (box half extents, egg semi-axes, pen radius + length)."""
     from test_gpu_hand import DevHandEnv, PALM_DZ, hand_states, setup
     spec, sp, tp = setup(kind=kind)
+    sp.solver_type = _abi.MG_SOLVER_TGS if solver == "tgs" else _abi.MG_SOLVER_PGS
     n = 192
     rng = np.random.default_rng(23)
     h = hand_states(spec, tp, n, rng, PALM_DZ[kind], pen=kind == "pen")
@@ -214,7 +218,7 @@ def test_dr_physics_matches_oracle_hand(lib, kind):
     lib.mg_sim_destroy(sim)
     rg, dg = e.root.cpu().numpy(), e.dof.cpu().numpy()
     assert np.isfinite(rg).all() and np.isfinite(dg).all()
-    _dr_explained(f"test_dr_physics_matches_oracle_hand[{kind}]", mnp, sp, pre,
+    _dr_explained(f"test_dr_physics_matches_oracle_hand[{kind}{'-tgs' if solver == 'tgs' else ''}]", mnp, sp, pre,
                   [("object pose", rg[:, 1, 0:7], h.root[:, 1, 0:7], 2e-4, 0, lambda g: g.root[0, 1, 0:7]),
                    ("object twist", rg[:, 1, 7:13], h.root[:, 1, 7:13], 2e-3, 2e-3, lambda g: g.root[0, 1, 7:13]),
                    ("dof pos", dg[..., 0], h.dof[..., 0], 2e-4, 0, lambda g: g.dof[0, :, 0]),
