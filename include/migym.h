@@ -151,7 +151,13 @@ typedef struct mg_model {
   float link_max_ang_vel;
   float obj_max_ang_vel;
   int32_t pad_model;
+  /* Dry joint friction per DOF node: the MJCF joint `frictionloss` (the hand's default class, shared.xml:13:
+   * 0.001), MuJoCo's constant friction torque bound, as the smooth law tau = -f tanh(qd / MG_FRICTIONLOSS_VS)
+   * treated linearly implicitly like the damping (diagonal += h f / v_s sech^2); 0 = none */
+  float frictionloss[MG_MAX_NODES];
 } mg_model;
+/* the regularization speed of the joint friction law (rad/s for hinges, m/s for slides) */
+#define MG_FRICTIONLOSS_VS 0.01f
 
 /* Simulation parameters (cfg['sim'] of the task YAML: Ant.yaml:42-61). */
 typedef struct mg_sim_params {
@@ -331,7 +337,8 @@ typedef struct mg_sim mg_sim;
  * floats, bound through mg_state_views.env_props), which mg_dr_apply rewrites for the actors being
  * randomized and the physics kernels read instead of the model's constants.  Row layout (offsets
  * from mg_env_props_layout):
- *   MG_EP_NODE    num_nodes x 8: [mass, armature, damping, stiffness, lower, upper, drive kp, effort]
+ *   MG_EP_NODE    num_nodes x MG_EP_NODE_WIDTH (9): [mass, armature, damping, stiffness, lower, upper, drive kp,
+ *                 effort, frictionloss]
  *                 (mass of the node's body; its inertia scales with mass / model mass:
  *                 set_actor_rigid_body_properties(..., recomputeInertia=True))
  *   MG_EP_GEOM    num_geoms: friction of each collision shape (a contact's friction is the mean of
@@ -340,6 +347,7 @@ typedef struct mg_sim mg_sim;
  *   MG_EP_OBJECT  4: [mass, friction, scale, 0] of the free object (scale: half extents x s,
  *                 mass x s^3, inertia x s^5) */
 enum { MG_EP_NODE = 0, MG_EP_GEOM = 1, MG_EP_TENDON = 2, MG_EP_OBJECT = 3 };
+#define MG_EP_NODE_WIDTH 9
 enum { MG_DR_UNIFORM = 0, MG_DR_GAUSSIAN = 1, MG_DR_LOGUNIFORM = 2 };
 enum { MG_DR_ADDITIVE = 0, MG_DR_SCALING = 1 };
 enum { MG_DR_SCHED_NONE = 0, MG_DR_SCHED_LINEAR = 1, MG_DR_SCHED_CONSTANT = 2 };

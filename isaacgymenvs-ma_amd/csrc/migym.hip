@@ -640,7 +640,7 @@ int mg_sim_set_params(mg_sim* sim, const mg_sim_params* params) {
 
 int mg_env_props_layout(const mg_model* m, int32_t offsets[4]) {
   if (!m) return fail(MG_EINVAL, "mg_env_props_layout: bad model");
-  const int o0 = 0, o1 = 8 * m->num_nodes, o2 = o1 + m->num_geoms, o3 = o2 + 2 * m->num_tendons;
+  const int o0 = 0, o1 = MG_EP_NODE_WIDTH * m->num_nodes, o2 = o1 + m->num_geoms, o3 = o2 + 2 * m->num_tendons;
   if (offsets) { offsets[0] = o0; offsets[1] = o1; offsets[2] = o2; offsets[3] = o3; }
   return (o3 + 4 + 3) & ~3;
 }
@@ -651,9 +651,10 @@ int mg_env_props_defaults(const mg_model* m, float* row) {
   const int stride = mg_env_props_layout(m, off);
   for (int k = 0; k < stride; k++) row[k] = 0.0f;
   for (int i = 0; i < m->num_nodes; i++) {
-    float* r = row + off[MG_EP_NODE] + 8 * i;
+    float* r = row + off[MG_EP_NODE] + MG_EP_NODE_WIDTH * i;
     r[0] = m->mass[i]; r[1] = m->armature[i]; r[2] = m->damping[i]; r[3] = m->stiffness[i];
     r[4] = m->lower[i]; r[5] = m->upper[i]; r[6] = m->drive_kp[i]; r[7] = m->effort_limit[i];
+    r[8] = m->frictionloss[i];
   }
   for (int g = 0; g < m->num_geoms; g++) row[off[MG_EP_GEOM] + g] = 1.0f;  // shape friction (build-defined default)
   for (int q = 0; q < m->num_tendons; q++) {

@@ -57,7 +57,7 @@ struct alignas(16) ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
   float nf[MN][33];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
-                      // 27 stiff, 28 lower, 29 upper, 30 drive kp, 31 effort limit
+                      // 27 stiff, 28 lower, 29 upper, 30 drive kp, 31 effort limit, 32 frictionloss
   int gtype[MG], gnode[MG], gbody[MG], gfil[MG];
   int tdof[MG_MAX_TENDONS][2];
   float tf[MG_MAX_TENDONS][6];   // coef0, coef1, lo, hi, limit stiffness, damping
@@ -96,6 +96,7 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, HV>* t, const mg_model
     f[24] = m->mass[i]; f[25] = m->armature[i]; f[26] = m->damping[i]; f[27] = m->stiffness[i];
     f[28] = m->lower[i]; f[29] = m->upper[i];
     f[30] = m->drive_kp[i]; f[31] = m->effort_limit[i];
+    f[32] = m->frictionloss[i];
   }
   const int nten = m->num_tendons < MG_MAX_TENDONS ? m->num_tendons : MG_MAX_TENDONS;
   for (int q = tid; q < nten; q += nt) {
@@ -312,8 +313,8 @@ struct alignas(16) BankSlot<L, T, 0> {
 };
 
 // Per-actor properties under domain randomization (mg_state_views.env_props), one copy per team in
-// LDS: nodes [mass, armature, damping, stiffness, lower, upper, drive kp, effort] (rows of 9 floats:
-// a node's lane reads its own row, odd stride), geom friction, tendons [limit stiffness, damping],
+// LDS: nodes [mass, armature, damping, stiffness, lower, upper, drive kp, effort, frictionloss] (rows of 9
+// floats, MG_EP_NODE_WIDTH: a node's lane reads its own row, odd stride), geom friction, tendons [limit stiffness, damping],
 // object [mass, friction, scale].  The layout of the global row is mg_env_props_layout's.
 template <int MN, int MG>
 struct DrTile {
@@ -326,8 +327,9 @@ struct DrTile {
 template <int T, int MN, int MG>
 __device__ __forceinline__ void load_dr(DrTile<MN, MG>* d, const float* row, const mg_model* m, int tl) {
   const int nn = m->num_nodes, ng = m->num_geoms, nt = m->num_tendons;
-  for (int k = tl; k < 8 * nn; k += T) d->node[k >> 3][k & 7] = row[k];
-  const float* g = row + 8 * nn;
+  static_assert(MG_EP_NODE_WIDTH == 9, "DrTile node rows are the global rows");
+  for (int k = tl; k < MG_EP_NODE_WIDTH * nn; k += T) (&d->node[0][0])[k] = row[k];
+  const float* g = row + MG_EP_NODE_WIDTH * nn;
   for (int k = tl; k < ng; k += T) d->geom[k] = g[k];
   const float* tr = g + ng;
   for (int k = tl; k < 2 * nt; k += T) d->ten[k >> 1][k & 1] = tr[k];
@@ -740,7 +742,8 @@ struct Team {
   const float* drt;    // tendons (stride 2)
   const float* dro;    // object [mass, friction, scale]
   // node property row [mass, armature, damping, stiffness, lower, upper, drive kp, effort]
-  __device__ __forceinline__ const float* nprop(int i) const { return drn ? drn + 9 * i : &mt->nf[i][24]; }
+  // [mass, arm, damp, stiff, lower, upper, kp, effort, frictionloss]: the DR row or the tile's nf[24..32]
+  __device__ __forceinline__ const float* nprop(int i) const { return drn ? drn + MG_EP_NODE_WIDTH * i : &mt->nf[i][24]; }
   __device__ __forceinline__ float omass() const { return dro ? dro[0] : m->obj_mass; }
   __device__ __forceinline__ float oscale() const { return dro ? dro[2] : 1.0f; }
   __device__ __forceinline__ V3 osize() const { return ld3(m->obj_size) * oscale(); }
@@ -908,7 +911,7 @@ struct Team {
       const float* nf = mt->nf[node];
       V3 cc = x + mul(R, ld3(nf + 15)) - o;
       const float* in = nf + 18;
-      const float isc = (drn && nf[24] > 0.0f) ? drn[9 * node] / nf[24] : 1.0f;  // DR: inertia scales with the body mass
+      const float isc = (drn && nf[24] > 0.0f) ? drn[MG_EP_NODE_WIDTH * node] / nf[24] : 1.0f;  // DR: inertia scales with the body mass
       float Il[3][3] = {{in[0] * isc, in[3] * isc, in[4] * isc}, {in[3] * isc, in[1] * isc, in[5] * isc},
                         {in[4] * isc, in[5] * isc, in[2] * isc}};
       float Tm[3][3], Iw[6];
@@ -919,7 +922,7 @@ struct Team {
         int a = idx[k][0], b = idx[k][1];
         Iw[k] = Tm[a][0] * R.m[b][0] + Tm[a][1] * R.m[b][1] + Tm[a][2] * R.m[b][2];
       }
-      const float mass = drn ? drn[9 * node] : nf[24];
+      const float mass = drn ? drn[MG_EP_NODE_WIDTH * node] : nf[24];
       IA = body_inertia(mass, cc, Iw);
       SV IV = mul(IA, V);
       V3 mg = ld3(p->gravity) * (mass * gscale());
@@ -954,6 +957,17 @@ struct Team {
       }
       Dj = np[1] + h * bb + h * h * kk;
       tj = tau + tadd + ttend - bb * nu - kk * (qj - ref + h * nu);
+      // dry joint friction (MJCF frictionloss; not domain-randomized): -f tanh(qd / v_s), linearly implicit
+#ifndef MG_NO_FRICTIONLOSS  // (A/B builds only)
+      const float fl = np[8];  // nf[32] or the DR row's
+#else
+      const float fl = 0.0f;
+#endif
+      if (fl > 0.0f) {
+        const float th = ptanh(nu * (1.0f / MG_FRICTIONLOSS_VS));
+        tj -= fl * th;
+        Dj += h * fl * (1.0f / MG_FRICTIONLOSS_VS) * (1.0f - th * th);
+      }
     }
     ph_mark(16);
     for (int lev = maxdepth; lev >= 1; lev--) {
@@ -2763,6 +2777,12 @@ struct Team {
       } else {
         t += -np[2] * nu - np[3] * qj;
       }
+#ifndef MG_NO_FRICTIONLOSS
+      const float fl = np[8];
+#else
+      const float fl = 0.0f;
+#endif
+      if (fl > 0.0f) t -= fl * ptanh(nu * (1.0f / MG_FRICTIONLOSS_VS));  // the joint friction at the post-step state
       // the node's own limit rows of the last substep (lower, then upper: consecutive from the index build_rows
       // kept in sat), instead of a scan over every limit row
       const int lr = 3 * s->ncon + (sat >> 3);

@@ -45,6 +45,7 @@ class StateViews(C.Structure):
 
 # ---- domain randomization (include/migym.h; vec_task.py:612-842, dr_utils.py)
 MG_EP_NODE, MG_EP_GEOM, MG_EP_TENDON, MG_EP_OBJECT = 0, 1, 2, 3
+MG_EP_NODE_WIDTH = 9   # [mass, armature, damping, stiffness, lower, upper, drive kp, effort, frictionloss]
 MG_DR_UNIFORM, MG_DR_GAUSSIAN, MG_DR_LOGUNIFORM = 0, 1, 2
 MG_DR_ADDITIVE, MG_DR_SCALING = 0, 1
 MG_DR_SCHED_NONE, MG_DR_SCHED_LINEAR, MG_DR_SCHED_CONSTANT = 0, 1, 2

@@ -16,7 +16,7 @@ the host to know which envs reset (``reset_buf.nonzero()``).  Here:
 
 Supported actor properties (everything the shipped task configs randomize):
   dof_properties       damping, stiffness (the PD drive's kp on position-driven DOFs), lower, upper,
-                       armature, effort
+                       armature, effort, friction (the joint's dry friction bound, mg_model.frictionloss)
   rigid_body_properties  mass (inertia rescaled with it, recomputeInertia=True)
   rigid_shape_properties friction (a contact's friction is the mean of its two shapes'), restitution
                        (accepted; the build's contacts are inelastic, so it has no effect)
@@ -56,7 +56,8 @@ _DIST = {"uniform": _abi.MG_DR_UNIFORM, "gaussian": _abi.MG_DR_GAUSSIAN, "loguni
 _OPS = {"additive": _abi.MG_DR_ADDITIVE, "scaling": _abi.MG_DR_SCALING}
 _SCHED = {None: _abi.MG_DR_SCHED_NONE, "linear": _abi.MG_DR_SCHED_LINEAR, "constant": _abi.MG_DR_SCHED_CONSTANT}
 # dof_properties attribute -> column of a node row [mass, armature, damping, stiffness, lower, upper, kp, effort]
-_DOF_COL = {"armature": 1, "damping": 2, "stiffness": 3, "lower": 4, "upper": 5, "effort": 7}
+_DOF_COL = {"armature": 1, "damping": 2, "stiffness": 3, "lower": 4, "upper": 5, "effort": 7, "friction": 8}
+_W = _abi.MG_EP_NODE_WIDTH
 _NOOP_ATTRS = {("rigid_shape_properties", "restitution"), ("tendon_properties", "stiffness")}
 _LIST_PROPS = ("rigid_body_properties", "rigid_shape_properties", "tendon_properties")
 
@@ -158,16 +159,16 @@ def build_actor_attrs(actor_params: Dict[str, Any], actors: Dict[str, str], spec
                         n = spec.nodes[d + 1]
                         col = _DOF_COL[a]
                         og = {1: n.armature, 2: n.damping, 3: n.stiffness, 4: n.lower, 5: n.upper,
-                              7: n.effort_limit}[col]
+                              7: n.effort_limit, 8: n.frictionloss}[col]
                         if a == "stiffness" and n.drive_kp > 0:   # DOF_MODE_POS: stiffness is the drive's kp
                             col, og = 6, n.drive_kp
-                        attrs.append((o_node + 8 * (d + 1) + col, base + j, float(og)))
+                        attrs.append((o_node + _W * (d + 1) + col, base + j, float(og)))
                         names.append((actor, prop, d, a))
                 continue
             if prop not in _LIST_PROPS:
                 raise NotImplementedError(f"domain randomization of {prop}")
             if prop == "rigid_body_properties":
-                elems = [(o_node + 8 * b.node, {"mass": float(spec.nodes[b.node].mass)}) for b in spec.bodies]
+                elems = [(o_node + _W * b.node, {"mass": float(spec.nodes[b.node].mass)}) for b in spec.bodies]
             elif prop == "rigid_shape_properties":
                 elems = [(o_geom + g, {"friction": 1.0}) for g in range(len(spec.geoms))]
             else:

@@ -158,6 +158,7 @@ class Node:
     limited: int = 0
     drive_kp: float = 0.0          # MJCF <position kp>: PD position drive (DOF_MODE_POS)
     effort_limit: float = 0.0      # actuator forcerange (|force| clamp of the drive)
+    frictionloss: float = 0.0      # MJCF joint frictionloss: dry friction torque bound (mg_model.frictionloss)
 
 
 @dataclass
@@ -520,7 +521,7 @@ def load_mjcf(path, name=None, self_collision=False, merge_world_bodies=True, co
                                   axis=[float(v) for v in axis], body=body_idx,
                                   armature=float(a.get("armature", "0")), damping=float(a.get("damping", "0")),
                                   stiffness=float(a.get("stiffness", "0")), lower=lo, upper=hi,
-                                  limited=int(limited)))
+                                  limited=int(limited), frictionloss=float(a.get("frictionloss", "0"))))
                 dof_names.append(nodes[-1].name)
                 node_idx = len(nodes) - 1
                 prev_anchor = p
@@ -820,6 +821,7 @@ def _model_dtype():
         ("hull_num_verts", i4), ("hull_num_planes", i4),
         ("hull_vert", f4, (MAX_HULL_VERTS, 3)), ("hull_plane", f4, (MAX_HULL_PLANES, 4)),
         ("link_ang_damping", f4), ("link_max_ang_vel", f4), ("obj_max_ang_vel", f4), ("pad_model", i4),
+        ("frictionloss", f4, N),
     ])
 
 
@@ -860,6 +862,7 @@ def pack_model(spec: ModelSpec) -> np.ndarray:
         m["upper"][i] = n.upper
         m["drive_kp"][i] = n.drive_kp
         m["effort_limit"][i] = n.effort_limit
+        m["frictionloss"][i] = n.frictionloss
     for i, b in enumerate(spec.bodies):
         m["body_node"][i] = b.node
         m["body_parent"][i] = b.parent_body

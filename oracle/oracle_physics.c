@@ -37,6 +37,7 @@ typedef float real;
 #define fmin fminf
 #define sin sinf
 #define cos cosf
+#define tanh tanhf
 #else
 typedef double real;
 #endif
@@ -2503,6 +2504,14 @@ static void substep(const mg_model* m, const mg_sim_params* p, astate* s, const 
     dofterm t = dof_term(m, s, i);
     kk[i] = t.k; bb[i] = t.b; ref[i] = t.ref; tadd[i] = t.tadd; s->sat[i] = t.sat;
     diag[i] = m->armature[i] + h * t.b + h * h * t.k;
+    /* dry joint friction (MJCF frictionloss, mg_model.frictionloss): tau = -f tanh(qd / v_s), linearly implicit:
+     * tau(qd + h qdd) ~ tau(qd) - (f / v_s) sech^2(qd / v_s) h qdd */
+    const real fl = m->frictionloss[i];
+    if (fl > 0.0) {
+      const real th = tanh(s->qd[i] / (real)MG_FRICTIONLOSS_VS);
+      tadd[i] -= fl * th;
+      diag[i] += h * fl / (real)MG_FRICTIONLOSS_VS * (1.0 - th * th);
+    }
   }
   mass_matrix(m, &k, h, M, diag, nvt, h * m->link_ang_damping);
   bias_forces(m, &k, s, g, C, m->link_ang_damping);
@@ -2748,6 +2757,7 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
       } else {
         t += -m->damping[i] * s->qd[i] - m->stiffness[i] * s->qj[i];
       }
+      if (m->frictionloss[i] > 0.0f) t -= m->frictionloss[i] * tanh(s->qd[i] / (real)MG_FRICTIONLOSS_VS);
       for (int r = 0; r < so->nrows; r++) {
         if (so->row_ref[r] != i) continue;
         if (so->row_kind[r] == 2) t += so->lam[r] / so->h;
@@ -2809,14 +2819,15 @@ static void apply_env_props(const mg_model* m, const float* row, mg_model* mm, r
   *mm = *m;
   const int nn = m->num_nodes, ng = m->num_geoms, nt = m->num_tendons;
   for (int i = 0; i < nn; i++) {
-    const float* r = row + 8 * i;
+    const float* r = row + MG_EP_NODE_WIDTH * i;
     const real sc = m->mass[i] > 0.0f ? (real)r[0] / (real)m->mass[i] : 1.0;
     mm->mass[i] = r[0];
     for (int k = 0; k < 6; k++) mm->inertia[i][k] = (float)((real)m->inertia[i][k] * sc);
     mm->armature[i] = r[1]; mm->damping[i] = r[2]; mm->stiffness[i] = r[3];
     mm->lower[i] = r[4]; mm->upper[i] = r[5]; mm->drive_kp[i] = r[6]; mm->effort_limit[i] = r[7];
+    mm->frictionloss[i] = r[8];
   }
-  const float* g = row + 8 * nn;
+  const float* g = row + MG_EP_NODE_WIDTH * nn;
   for (int k = 0; k < ng; k++) gmu[k] = g[k];
   const float* t = g + ng;
   for (int q = 0; q < nt; q++) { mm->tendon_limit_stiffness[q] = t[2 * q]; mm->tendon_damping[q] = t[2 * q + 1]; }

@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-from migym import dr as DR
+from migym import _abi, dr as DR
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -53,7 +53,8 @@ def trace_params():
 def layout(spec):
     """Python statement of mg_env_props_layout (include/migym.h)."""
     nn, ng, nt = len(spec.nodes), len(spec.geoms), len(spec.tendons)
-    offs = (0, 8 * nn, 8 * nn + ng, 8 * nn + ng + 2 * nt)
+    W = _abi.MG_EP_NODE_WIDTH
+    offs = (0, W * nn, W * nn + ng, W * nn + ng + 2 * nt)
     return (offs[3] + 4 + 3) & ~3, offs
 
 
@@ -62,8 +63,9 @@ def defaults(spec):
     stride, offs = layout(spec)
     row = np.zeros(stride, np.float32)
     for i, n in enumerate(spec.nodes):
-        row[8 * i:8 * i + 8] = [n.mass, n.armature, n.damping, n.stiffness, n.lower, n.upper, n.drive_kp,
-                                n.effort_limit]
+        W = _abi.MG_EP_NODE_WIDTH
+        row[W * i:W * i + W] = [n.mass, n.armature, n.damping, n.stiffness, n.lower, n.upper, n.drive_kp,
+                                n.effort_limit, n.frictionloss]
     row[offs[1]:offs[1] + len(spec.geoms)] = 1.0
     for q, t in enumerate(spec.tendons):
         row[offs[2] + 2 * q:offs[2] + 2 * q + 2] = [t["limit_stiffness"], t["damping"]]
@@ -115,10 +117,11 @@ def dr_tensor_props(env_props, spec, d_t):
     """(masses per body, frictions per geom, dof [damping, stiffness, lower, upper]) from env_props rows,
     in the layout of the reference's recorded setter values."""
     stride, offs = layout(spec)
-    mass = np.stack([env_props[:, 8 * b.node] for b in spec.bodies], 1)
+    W = _abi.MG_EP_NODE_WIDTH
+    mass = np.stack([env_props[:, W * b.node] for b in spec.bodies], 1)
     fric = env_props[:, offs[1]:offs[1] + len(spec.geoms)]
     nd = spec.num_dofs
     cols = {"damping": 2, "stiffness": 3, "lower": 4, "upper": 5}
-    dof = np.stack([np.stack([env_props[:, 8 * (j + 1) + cols[k]] for j in range(nd)], 1)
+    dof = np.stack([np.stack([env_props[:, W * (j + 1) + cols[k]] for j in range(nd)], 1)
                     for k in ("damping", "stiffness", "lower", "upper")])
     return mass, fric, dof

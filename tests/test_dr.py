@@ -104,6 +104,22 @@ def test_unsupported_attributes_raise():
                              layout(spec)[1])
 
 
+def test_dof_friction_randomizes_the_frictionloss_column():
+    """dof_properties.friction (vec_task.py:780-800) targets the node rows' frictionloss column (MG_EP_NODE_WIDTH 9,
+    column 8) with the model's frictionloss as the original value (the hand's 0.001, shared.xml:13)"""
+    from migym import taskdefs
+    spec = taskdefs.hand_spec("block")
+    _, attrs, names = DR.build_actor_attrs({"hand": {"dof_properties": {"friction": {
+        "range": [0.5, 2.0], "operation": "scaling", "distribution": "uniform"}}}}, {"hand": "articulation"}, spec,
+        layout(spec)[1])
+    slots = [a[0] for a in attrs]
+    assert [a[2] for a in attrs] == [np.float32(0.001)] * spec.num_dofs   # the original values
+    W = _abi.MG_EP_NODE_WIDTH
+    assert sorted(slots) == [W * (d + 1) + 8 for d in range(spec.num_dofs)]
+    row = defaults(spec)
+    assert all(row[s] == np.float32(0.001) for s in slots)
+
+
 class OracleBackend:
     """orc_dr_apply / orc_dr_noise on host buffers"""
 

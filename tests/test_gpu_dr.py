@@ -72,7 +72,7 @@ def random_props(spec, n, rng):
     props = np.tile(defaults(spec), (n, 1))
     nn = len(spec.nodes)
     for i in range(nn):
-        r = props[:, 8 * i:8 * i + 8]
+        r = props[:, _abi.MG_EP_NODE_WIDTH * i:_abi.MG_EP_NODE_WIDTH * (i + 1)]
         r[:, 0] *= rng.uniform(0.5, 1.5, n)          # mass
         r[:, 1] *= rng.uniform(0.5, 1.5, n)          # armature
         r[:, 2] *= rng.uniform(0.3, 3.0, n)          # damping
@@ -80,6 +80,7 @@ def random_props(spec, n, rng):
         r[:, 4] += rng.normal(0, 0.02, n)            # lower
         r[:, 5] += rng.normal(0, 0.02, n)            # upper
         r[:, 6] *= rng.uniform(0.75, 1.5, n)         # drive kp
+        r[:, 8] *= rng.uniform(0.3, 3.0, n)          # frictionloss (the hand's 0.001; 0 elsewhere)
     props[:, offs[1]:offs[1] + len(spec.geoms)] *= rng.uniform(0.3, 1.3, (n, len(spec.geoms)))
     nt = len(spec.tendons)
     props[:, offs[2]:offs[2] + 2 * nt] *= rng.uniform(0.3, 3.0, (n, 2 * nt))
@@ -236,8 +237,9 @@ def test_make_with_randomize(task, n):
     spec = env.model_spec
     props = env.env_props.cpu().numpy()
     base = defaults(spec)
-    mass = np.stack([props[:, 8 * b.node] for b in spec.bodies], 1)
-    m0 = np.array([base[8 * b.node] for b in spec.bodies])
+    W = _abi.MG_EP_NODE_WIDTH
+    mass = np.stack([props[:, W * b.node] for b in spec.bodies], 1)
+    m0 = np.array([base[W * b.node] for b in spec.bodies])
     r = mass / np.where(m0 > 0, m0, 1)
     assert r[:, m0 > 0].min() >= 0.5 - 1e-6 and r[:, m0 > 0].max() <= 1.5 + 1e-6
     if task == "Humanoid":   # mass is setup_only with a linear schedule: scale 0 at setup, never randomized
@@ -288,7 +290,7 @@ def test_actor_params_generator_ant():
     spec = env.model_spec
     base = defaults(spec)
     stride, offs = layout(spec)
-    assert params[i_d] == pytest.approx(float(env.env_props[5, offs[0] + 8 * 4 + 2]), rel=0, abs=0)
+    assert params[i_d] == pytest.approx(float(env.env_props[5, offs[0] + _abi.MG_EP_NODE_WIDTH * 4 + 2]), rel=0, abs=0)
     before = env.env_props.clone()
     gen = _Gen(len(names))
     env.actor_params_generator = gen
@@ -306,13 +308,14 @@ def test_actor_params_generator_ant():
     for e in (2, 9, 40):
         ext = env.extern_actor_params[e]
         for d in range(nd):
-            col = offs[0] + 8 * (d + 1)
+            col = offs[0] + _abi.MG_EP_NODE_WIDTH * (d + 1)
             j = names.index(f"dof_properties_0_damping_{d}")
             assert props[e, col + 2] == pytest.approx(base[col + 2] * ext[j], rel=1e-6, abs=1e-7)
             j = names.index(f"dof_properties_0_lower_{d}")
             assert props[e, col + 4] == pytest.approx(base[col + 4] + ext[j], rel=1e-6, abs=1e-6)
         # mass is setup_only: unchanged by the generator
-        assert np.array_equal(props[e, offs[0]::8][:len(spec.nodes)], before.cpu().numpy()[e, offs[0]::8][:len(spec.nodes)])
+        W = _abi.MG_EP_NODE_WIDTH
+        assert np.array_equal(props[e, offs[0]::W][:len(spec.nodes)], before.cpu().numpy()[e, offs[0]::W][:len(spec.nodes)])
     env.actor_params_generator = _Gen(len(names) + 1)
     env.randomize_buf_actors[:] = 10 ** 6      # the call above restarted the randomized envs' counters
     with pytest.raises(Exception, match="extern_sample size"):

@@ -346,6 +346,44 @@ def test_free_link_damping_and_cap_on_device(lib):
     np.testing.assert_allclose(rg, r_h, atol=1e-6, rtol=1e-6)
 
 
+def test_frictionloss_on_device(lib):
+    """the dry joint friction law (MJCF frictionloss, -f tanh(qd / v_s) linearly implicit) in k_simulate: one hinge
+    link spun at rates across v_s (0 .. 2 rad/s, both signs) under torques below and above f, 20 steps on the
+    device against the oracle (tests/test_oracle_physics.py pins the law itself)"""
+    from test_oracle_physics import hinge_link_spec
+    f = 0.01
+    mnp = M.pack_model(hinge_link_spec(f))
+    sp = taskdefs.sim_params(configs.task_config("Ant", 1), 1)
+    for i in range(3):
+        sp.gravity[i] = 0.0
+    sp.limit_margin = -1.0
+    n = 64
+    rng = np.random.default_rng(3)
+    root = np.zeros((n, 13), np.float32)
+    root[:, 6] = 1.0
+    dof = np.zeros((n, 1, 2), np.float32)
+    dof[:, 0, 1] = np.concatenate([rng.uniform(-0.03, 0.03, n // 2), rng.uniform(-2.0, 2.0, n // 2)])
+    act = (rng.uniform(-2.0, 2.0, (n, 1)) * f).astype(np.float32)
+    r_d, d_d, a_d = T(root), T(dof), T(act)
+    h = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(h)), lib)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state, v.dof_actuation = P(r_d), P(d_d), P(a_d)
+    _abi.check(lib.mg_sim_bind(h, C.byref(v)), lib)
+    r_h, d_h = root.copy(), dof.copy()
+    for _ in range(20):
+        _abi.check(lib.mg_sim_simulate(h, stream()), lib)
+        O.simulate(mnp, sp, r_h, d_h, act)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(h)
+    dg = d_d.cpu().numpy()
+    np.testing.assert_allclose(dg[..., 1], d_h[..., 1], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(dg[..., 0], d_h[..., 0], rtol=1e-4, atol=1e-6)
+    # the friction acted: the rates moved from where a frictionless hinge would take them
+    free = dof[:, 0, 1] + act[:, 0] / 0.02 * 20 * sp.dt
+    assert np.abs(d_h[:, 0, 1] - free).max() > 0.05
+
+
 def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=None, threads=8):
     """mg_env_step vs orc_env_step step by step, each step started on both sides from the oracle's state (the GPU
     buffers are reloaded from it), so one step's fp32-vs-fp64 difference cannot grow into a chaotic divergence

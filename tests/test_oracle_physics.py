@@ -446,3 +446,50 @@ def test_tgs_dropped_ant_rests_and_holds_limits():
     for _ in range(60):
         O.simulate(mnp, sp, root, dof, act)
     assert np.all(dof[0, :, 0] <= np.array(tp.dof_upper[:8]) + 0.02)
+
+
+# ------------------------------------------------------------------ dry joint friction (MJCF frictionloss)
+def hinge_link_spec(f, I=0.02):
+    """a fixed base and one hinge link (COM on the axis, inertia I about it), MJCF frictionloss f"""
+    root = M.Node(name="base", parent=-1, jtype=M.JT_FIXED, t=[0, 0, 0], r0=[0, 0, 0, 1], axis=[0, 0, 1], body=0)
+    link = M.Node(name="hinge", parent=0, jtype=M.JT_HINGE, t=[0, 0, 0], r0=[0, 0, 0, 1], axis=[0, 0, 1], body=1,
+                  mass=1.0, inertia=[I, I, I, 0.0, 0.0, 0.0], limited=0, frictionloss=f)
+    bodies = [M.Body(name="base", node=0, pos=[0, 0, 0], quat=[0, 0, 0, 1], parent_body=-1, mass=0.0),
+              M.Body(name="link", node=1, pos=[0, 0, 0], quat=[0, 0, 0, 1], parent_body=0, mass=1.0)]
+    return M.ModelSpec(name="hinge", fixed_base=1, nodes=[root, link], bodies=bodies, geoms=[], pairs=[],
+                       actuators=[], dof_names=["hinge"], angular_damping=0.0, max_angular_velocity=0.0)
+
+
+def test_frictionloss_is_read_from_the_mjcf():
+    """shared.xml:13's default joint class gives every hand joint frictionloss 0.001; the locomotion MJCFs none"""
+    hand = M.pack_model(taskdefs.hand_spec("block"))
+    assert np.all(hand["frictionloss"][1:25] == np.float32(0.001)) and hand["frictionloss"][0] == 0
+    for name in ("ant", "humanoid", "cartpole"):
+        assert not M.pack_model(M.load_builtin(name))["frictionloss"].any(), name
+
+
+def test_frictionloss_decelerates_then_creeps():
+    """-f tanh(qd / v_s) (v_s = MG_FRICTIONLOSS_VS 0.01): a hinge spun at 2 rad/s with no other force slows at
+    f / I (Coulomb) and comes to rest; a constant torque 0.5 f then drives the creep rate v_s atanh(0.5)"""
+    f, I = 0.01, 0.02
+    mnp = M.pack_model(hinge_link_spec(f, I))
+    sp = taskdefs.sim_params(configs.task_config("Ant", 1), 0)
+    for i in range(3):
+        sp.gravity[i] = 0.0
+    sp.limit_margin = -1.0
+    root = np.zeros((1, 13), np.float32)
+    root[0, 6] = 1.0
+    dof = np.zeros((1, 1, 2), np.float32)
+    dof[0, 0, 1] = 2.0
+    steps = 60                                  # 0.996 s: 2 - 0.5 t stays well above v_s
+    for _ in range(steps):
+        O.simulate(mnp, sp, root, dof)
+    t = steps * sp.dt
+    assert abs(dof[0, 0, 1] - (2.0 - f / I * t)) < 1e-3, dof[0, 0, 1]
+    for _ in range(300):                         # ~4 s more: stopped (the law is smooth: |qd| << v_s at rest)
+        O.simulate(mnp, sp, root, dof)
+    assert abs(dof[0, 0, 1]) < 1e-4
+    act = np.full((1, 1), 0.5 * f, np.float32)
+    for _ in range(200):
+        O.simulate(mnp, sp, root, dof, act)
+    np.testing.assert_allclose(dof[0, 0, 1], 0.01 * np.arctanh(0.5), rtol=1e-3)
