@@ -69,7 +69,16 @@ OBS_GROUPS = {
     108: {"height": [0], "vel_loc": [1, 2, 3], "angvel_loc": [4, 5, 6], "yaw/roll/angle_to_target": [7, 8, 9],
           "up/heading proj": [10, 11], "dof pos (scaled)": list(range(12, 33)), "dof vel": list(range(33, 54)),
           "dof force": list(range(54, 75)), "foot force-torques": list(range(75, 87)), "actions": list(range(87, 108))},
+    # ShadowHand full_state (shadow_hand.py:528-575)
+    211: {"dof pos (unscaled)": list(range(0, 24)), "dof vel": list(range(24, 48)), "dof force": list(range(48, 72)),
+          "object pose": list(range(72, 79)), "object linvel": list(range(79, 82)), "object angvel": list(range(82, 85)),
+          "goal pose": list(range(85, 92)), "object-goal rot": list(range(92, 96)),
+          "fingertip states": list(range(96, 161)), "fingertip force-torques": list(range(161, 191)),
+          "actions": list(range(191, 211))},
 }
+# MA-Ant: the Ant layout plus the other agents' torso positions relative to self (3 (A - 1), taskdefs.task_params)
+for _A in (2, 4, 8):
+    OBS_GROUPS[60 + 3 * (_A - 1)] = dict(OBS_GROUPS[60], **{"other agents": list(range(60, 60 + 3 * (_A - 1)))})
 NORTH_STAR_RTOL = 1e-4   # BASELINE.json north_star: "obs/reward parity to CPU reference within 1e-4 rel"
 
 

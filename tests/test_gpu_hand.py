@@ -353,7 +353,7 @@ def test_hand_physics_hull_exact_matches_oracle(lib, kind):
 
 
 def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra=None, obs_tol=2e-3,
-                         reach_cap=PS.REACH_CAP):
+                         reach_cap=PS.REACH_CAP, north_star=False, threads=8):
     """mg_env_step vs orc_hand_env_step step by step, both sides started each step from the oracle's state (all
     buffers reloaded: DOF / root / rigid-body state, targets, goal, resets, successes, running mean, forces), so a
     step's fp32-vs-fp64 difference cannot grow chaotically over the next ones.  Per step: progress, targets and goals
@@ -367,7 +367,7 @@ def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra
     _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
     bad = np.zeros((steps, n), bool)
     flags = np.zeros((steps, n), np.int32)
-    pres, outs = [], []
+    pres, outs, rews = [], [], []
     ncon = 0
     try:
         for t in range(steps):
@@ -376,7 +376,7 @@ def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra
             _abi.check(lib.mg_sim_bind(sim, C.byref(e.views())), lib)
             flags[t] = PS.step_flags(mnp, sp, PS.hand_physics_input(h, mnp, tp, seed, t))
             pres.append(copy.deepcopy(h))
-            h.env_step(mnp, sp, tp, seed=seed, step=t, threads=8)
+            h.env_step(mnp, sp, tp, seed=seed, step=t, threads=threads)
             _abi.check(lib.mg_env_step(sim, C.byref(tp), C.byref(e.buffers(seed=seed, step=t)), stream()), lib)
             torch.cuda.synchronize()
             np.testing.assert_array_equal(np_(e.progress), h.progress)
@@ -390,6 +390,7 @@ def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra
                 b |= extra(e, h)
             bad[t] = b
             outs.append((og, h.obs.copy()))
+            rews.append((np_(e.rew), h.rew.copy()))
             PS.record(test, f"obs step {t}", og, h.obs, envs_outside=int(b.sum()))
             ncon = sum(len(O.contacts(mnp, sp, h.root[i].ravel(), h.dof[i], 64)) > 0 for i in range(n))
             np.testing.assert_allclose(np_(e.cons), h.cons, atol=2e-2)
@@ -398,7 +399,27 @@ def _hand_teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, extra
     sens = lambda t, i: PS.oracle_sensitive_step(mnp, sp, tp, pres[t], actions[t], i, outs[t][0][i], outs[t][1][i],
                                                  seed=seed, step=t, hand=True)
     PS.assert_steps_explained(test, bad, flags, sens, reach_cap=reach_cap)
-    return ncon
+    if not north_star:
+        return ncon
+    # per column group against north_star's 1e-4 relative over the unflagged env-steps that agree within the step's
+    # tolerances (a disagreeing one is explained above: a discontinuity, or the oracle's own sensitivity), with the
+    # oracle's fp32 twin from the same states (test_gpu_parity._teacher_forced)
+    keep = ((flags == 0) & ~bad).ravel()
+    groups = PS.OBS_GROUPS[tp.num_obs]
+    og, oh = np.concatenate([o[0] for o in outs]), np.concatenate([o[1] for o in outs])
+    rg, rh = np.concatenate([r[0] for r in rews])[:, None], np.concatenate([r[1] for r in rews])[:, None]
+    cols = PS.column_stats(test, "columns vs 1e-4 rel (agreeing unflagged env-steps)", og, oh, keep, groups)
+    cols.update(PS.column_stats(test, "reward vs 1e-4 rel (agreeing unflagged env-steps)", rg, rh, keep, {"reward": [0]}))
+    o32, r32 = [], []
+    for t in range(steps):
+        g = copy.deepcopy(pres[t])
+        g.env_step(mnp, sp, tp, seed=seed, step=t, threads=threads, fp32=True)
+        o32.append(g.obs.copy())
+        r32.append(g.rew.copy())
+    twin = PS.column_stats(test, "fp32 twin: columns vs 1e-4 rel", np.concatenate(o32), oh, keep, groups)
+    twin.update(PS.column_stats(test, "fp32 twin: reward vs 1e-4 rel", np.concatenate(r32)[:, None], rh, keep,
+                                {"reward": [0]}))
+    return ncon, (cols, twin, 0.0)
 
 
 @pytest.mark.parametrize("kind", ["block", "egg", "pen"])
@@ -413,6 +434,28 @@ def test_hand_fused_env_step_matches_oracle(lib, kind):
     acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(12)]
     ncon = _hand_teacher_forced(lib, f"test_hand_fused_env_step_matches_oracle[{kind}]", spec, sp, tp, h, 12, acts, 5)
     assert ncon >= n // 2   # the objects are on the hand by now
+
+
+def test_hand_fused_parity_at_baseline_shard(lib):
+    """BASELINE.json configs[4] (ShadowHand, 32,768 envs over 8 GPUs) at its per-GPU shard, 4,096 envs: the oracle
+    rolls every env 12 steps on from the all-reset start (random actions: objects dropped, caught, some reset), then 3
+    fused steps are teacher-forced as in test_hand_fused_env_step_matches_oracle, and every obs column group and the
+    reward are held to north_star's 1e-4 relative (test_gpu_parity.assert_north_star_rtol: 1e-4 of the group's scale,
+    or 4x what the oracle's own fp32 build needs from the same states)"""
+    from test_gpu_parity import assert_north_star_rtol
+    spec, sp, tp = setup(n=4096, kind="block")
+    n = 4096
+    h = O.HandHostEnv(tp, spec, n)
+    mnp = M.pack_model(spec)
+    rng = np.random.default_rng(37)
+    for t in range(12):
+        h.actions[:] = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+        h.env_step(mnp, sp, tp, seed=11, step=200 + t, threads=16)
+    acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(3)]
+    ncon, res = _hand_teacher_forced(lib, "test_hand_fused_parity_at_baseline_shard[block-4096]", spec, sp, tp, h, 3,
+                                     acts, 11, north_star=True, threads=16)
+    assert ncon >= n // 4
+    assert_north_star_rtol(res)
 
 
 def test_hand_fused_forces_and_states_match_oracle(lib):

@@ -603,6 +603,24 @@ def test_multi_agent_env_step_matches_oracle(lib, A):
     _teacher_forced(lib, f"test_multi_agent_env_step_matches_oracle[{A}]", spec, sp, tp, h, 4, acts, seed=9, mutate=mutate)
 
 
+def test_multi_agent_parity_at_baseline_shard(lib):
+    """BASELINE.json configs[3] (MA-Ant, 65,536 envs x 4 agents over 8 GPUs) at its per-GPU shard, 8,192 envs x 4
+    agents: a 12-step oracle pre-roll, then 3 teacher-forced fused steps; every obs column group (the other agents'
+    relative torso positions included) and the reward against north_star's 1e-4 relative"""
+    spec, sp, tp = ma_setup(4)
+    n = 4 * 8192
+    h = O.HostEnv(tp, spec, n)
+    mnp = M.pack_model(spec)
+    rng = np.random.default_rng(41)
+    for t in range(12):
+        h.actions[:] = rng.uniform(-1, 1, (n, tp.num_actions)).astype(np.float32)
+        h.env_step(mnp, sp, tp, seed=13, step=300 + t, threads=16)
+    acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(3)]
+    res = _teacher_forced(lib, "test_multi_agent_parity_at_baseline_shard[8192x4]", spec, sp, tp, h, 3, acts, seed=13,
+                          threads=16)
+    assert_north_star_rtol(res)
+
+
 def test_multi_agent_rejects_agents_spanning_waves(lib):
     """Ant teams are 16 lanes (4 actors per wave): 8 agents per env cannot share one wave."""
     spec, sp, tp = ma_setup(8)
