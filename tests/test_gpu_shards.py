@@ -61,6 +61,34 @@ def test_rank_shards_equal_slices_of_the_node_rollout(task, world, per_rank, ran
         sh.close()
 
 
+@pytest.mark.parametrize("task,n,per_rank", [("Ant", 1 << 20, 8192), ("ShadowHand", 1 << 17, 4096)])
+def test_largest_batch_equals_its_last_shard(task, n, per_rank):
+    """the large end of the size range: Ant at 1,048,576 envs (16x the headline, ~0.5 GB of state) and ShadowHand at
+    131,072 envs (4x BASELINE configs[4]'s node total, one GPU), 4 steps; its last shard, stepped alone with
+    env_offset = n - per_rank, must equal the batch's tail bit for bit (every index past 2^19 / 2^16 envs -- grid,
+    work queue, counter RNG keys, row offsets -- as in the small runs)"""
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    steps = 4
+    full = _make(task, n, 0)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    acts = [torch.rand((full.num_actors, full.num_actions), device=DEV, generator=g) * 2.4 - 1.2 for _ in range(steps)]
+    lo = n - per_rank
+    ref = []
+    for a in acts:
+        obs, rew, reset, _ = full.step(a)
+        assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all()
+        ref.append((obs["obs"][lo:].clone(), rew[lo:].clone(), reset[lo:].clone()))
+    full.close()
+    del full
+    torch.cuda.empty_cache()
+    sh = _make(task, per_rank, lo)
+    for k, a in enumerate(acts):
+        obs, rew, reset, _ = sh.step(a[lo:].contiguous())
+        o, w, d = ref[k]
+        assert torch.equal(obs["obs"], o) and torch.equal(rew, w) and torch.equal(reset, d), f"{task} step {k}"
+    sh.close()
+
+
 @pytest.mark.parametrize("task,obj", [("Humanoid", "block"), ("ShadowHand", "egg"), ("ShadowHand", "pen")])
 def test_work_queue_items_equal_the_static_grid(task, obj):
     """Multi-wave-block instances (Humanoid: 4 waves per block, hand block / pen 2, egg 8) run a work queue
