@@ -187,11 +187,17 @@ constexpr int kPgsPrefetch = 4;
 #ifndef MG_KJY_EGG
 #define MG_KJY_EGG 0
 #endif
+#ifndef MG_KJY_HAND
+#define MG_KJY_HAND 12  // block / pen
+#endif
 constexpr int kJYRegs = MG_KJY;
 // test-solve columns per batch (a multiple of 3): 12 for the 16- and 32-lane locomotion teams (12 walkers
 // instead of 6 halve the batches per substep: Ant +0.7 %, MA-Ant +1.0 %; 15 columns -3.5 %, 9 or 18 for
 // 32-lane teams -5 % / -34 %); Cartpole keeps 6
 constexpr int kRBLoco = 12;
+#ifndef MG_RB_LOCO32
+#define MG_RB_LOCO32 12  // the 32- and 64-lane locomotion teams (Humanoid)
+#endif
 // and for the hand instances (round 5, same box, profiles/r05/ab_hand_test_solve_width.txt): 12 for the block and
 // the pen (ShadowHand 16,384 / 4,096 +1.6 / +2.0 %, pen +1.8 %; 9: +0.4 %, 15: -1 %, 18: -3 to -5 %), 6 for the egg
 // (its LDS object rows leave no room: 9 or 12 cost it 18-21 %)
@@ -209,10 +215,10 @@ template <int T, int MN, int MC, int OBJ = 0>
 struct TeamLDS {
   // row capacity, rounded up to a multiple of the PGS prefetch depth (the sweep pads to it)
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + kPgsPrefetch - 1) / kPgsPrefetch * kPgsPrefetch;
-  static constexpr int RB = OBJ ? (OBJ == MG_GT_ELLIPSOID ? MG_RB_EGG : MG_RB_HAND) : (kRBLoco <= T ? kRBLoco : 6);
+  static constexpr int RB = OBJ ? (OBJ == MG_GT_ELLIPSOID ? MG_RB_EGG : MG_RB_HAND) : (T >= 32 ? MG_RB_LOCO32 : (kRBLoco <= T ? kRBLoco : 6));
   // rows whose (J, Y) columns stay in registers during the PGS (a multiple of the prefetch depth)
   // (not for the egg instance: 17.16 vs 17.73 M env-steps/s and 450 vs 409 MB per launch, measured on its fp32 build)
-  static constexpr int KR0 = OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : ((T >= 32 && !OBJ) ? MG_KJY_LOCO32 : kJYRegs);
+  static constexpr int KR0 = OBJ == MG_GT_ELLIPSOID ? MG_KJY_EGG : (OBJ ? MG_KJY_HAND : (T >= 32 ? MG_KJY_LOCO32 : kJYRegs));
   static constexpr int KR = (KR0 < MR ? KR0 : MR) / kPgsPrefetch * kPgsPrefetch;  // right-hand sides per test solve (rows of 2-4 contacts)
   // part-B rows whose (J, Y) columns live in the LDS left dead by the tree phases (R[1..MN-1], x, V: written by
   // fk(), read by collide(), not again until the next fk()) instead of scratch, one float per lane and row for J
