@@ -756,8 +756,8 @@ struct Team {
   const float* drg;    // geom friction
   const float* drt;    // tendons (stride 2)
   const float* dro;    // object [mass, friction, scale]
-  // node property row [mass, armature, damping, stiffness, lower, upper, drive kp, effort]
-  // [mass, arm, damp, stiff, lower, upper, kp, effort, frictionloss]: the DR row or the tile's nf[24..32]
+  // node property row [mass, armature, damping, stiffness, lower, upper, drive kp, effort, frictionloss]: the DR row
+  // or the tile's nf[24..32]
   __device__ __forceinline__ const float* nprop(int i) const { return drn ? drn + MG_EP_NODE_WIDTH * i : &mt->nf[i][24]; }
   __device__ __forceinline__ float omass() const { return dro ? dro[0] : m->obj_mass; }
   __device__ __forceinline__ float oscale() const { return dro ? dro[2] : 1.0f; }
