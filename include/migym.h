@@ -516,6 +516,10 @@ int mg_env_step_replay(mg_sim* sim, const mg_task_params* tp, const mg_task_buff
  * synchronises the device and returns the recorded spans in milliseconds, in launch order. */
 int mg_kernel_span_begin(mg_sim* sim, int32_t cap);
 int mg_kernel_span_read(mg_sim* sim, double* ms, int32_t cap, int32_t* n_out);
+/* mg_kernel_span_waves(sim, launch, out, cap, &n): the raw per-wave (start, end) GPU wall-clock ticks of recorded
+ * launch `launch` (out: 2 * cap uint64; n = the launch's waves, at most cap; ticks at hipDeviceAttributeWallClockRate
+ * kHz) -- the launch's tail and dispatch ramp for tools/span_diag.py --waves */
+int mg_kernel_span_waves(mg_sim* sim, int32_t launch, uint64_t* out, int32_t cap, int32_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -744,6 +744,19 @@ int mg_kernel_span_read(mg_sim* sim, double* ms, int32_t cap, int32_t* n_out) {
   return MG_OK;
 }
 
+int mg_kernel_span_waves(mg_sim* sim, int32_t launch, uint64_t* out, int32_t cap, int32_t* n_out) {
+  if (!sim || !out || !n_out || cap < 0 || launch < 0) return fail(MG_EINVAL, "mg_kernel_span_waves: bad arguments");
+  *n_out = 0;
+  if (!sim->d_span || launch >= sim->span_next) return MG_OK;
+  const int w = sim->span_waves[launch] < cap ? sim->span_waves[launch] : cap;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_kernel_span_waves: sync failed");
+  if (w > 0 && hipMemcpy(out, sim->d_span + 2 * (size_t)sim->span_stride * launch, 2 * (size_t)w * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(MG_EDEVICE, "mg_kernel_span_waves: copy failed");
+  *n_out = w;
+  return MG_OK;
+}
+
 int mg_set_indexed(mg_sim* sim, int32_t which, const float* src, const int32_t* idx, int32_t n, void* stream) {
   if (!sim || !sim->bound || !src || (n > 0 && !idx)) return fail(MG_EINVAL, "mg_set_indexed: bad arguments");
   if (n == 0) return MG_OK;
