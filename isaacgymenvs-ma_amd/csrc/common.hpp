@@ -17,26 +17,36 @@ struct mg_sim {
   int32_t device;
   mg_state_views views;
   bool bound;
-  // work ordering of the fused step (32-lane instances: K = 1 from 16,384 envs, 8 below; else off;
-  // MIGYM_ORDER_EVERY = K overrides at mg_sim_create): every K-th mg_env_step
-  // first sorts the envs by their last step's constraint-row count, descending (k_order), and the step kernels
-  // take their envs in that order -- teams of similar cost share a wave (the wave runs its slowest team's rows)
-  // and the heavy envs start first.  Envs are independent, so every result is the same bit for bit.
-  int order_every;
-  long long order_steps;
-  bool order_valid;
-  int* d_order;        // (n / A) env slots -> env
-  unsigned char* d_cost; // (n) the last step's row count per actor (saturated at 255)
+  // work ordering of the fused step (step_kernels.hpp MgOrder; on for the 16- and 32-lane instances,
+  // MIGYM_ORDER_EVERY = 0 turns it off at mg_sim_create): every mg_env_step takes its envs in descending order of
+  // their constraint-row counts of the previous step -- teams of similar cost share a wave (the wave runs its slowest
+  // team's rows) and the heavy envs start first.  The previous launch built the order itself: each env appended its
+  // index to the bucket of its row count (two sets of kOrderBuckets lists, alternating launch by launch), and that
+  // launch's last wave cleared the set it had read.  Envs are independent, so every result is the same bit for bit.
+  int order_every;     // > 0: on
+  long long order_steps;  // ordered launches so far (the parity of the set they write)
+  bool order_valid;    // a set holds the previous ordered launch's lists
+  unsigned* d_bq;      // [2][kOrderBuckets] bucket counts, then the launch's finished-wave counter
+  int* d_blist;        // [2][kOrderBuckets][bq_cap] env indices per bucket
+  int bq_cap;          // env units (n / A)
   // kernel spans (mg_kernel_span_begin): per recorded launch, span_stride (start, end) pairs, one per wave
   unsigned long long* d_span;
   int span_cap, span_next, span_stride;
   int span_waves[1024];  // waves of each recorded launch
 };
 
-// the step kernels' ordering arguments (nullptr order: slot = env)
+// the step kernels' ordering arguments: the bucket lists this launch reads (rcnt nullptr: slot = env) and writes
+// (wcnt nullptr: no ordering), the read set's counts the last wave clears, the finished-wave counter
+constexpr int kOrderBuckets = 32;  // row-count classes of width kOrderWidth, descending (bucket 0: 62 rows and more)
+constexpr int kOrderWidth = 2;
 struct MgOrder {
-  const int* order;
-  unsigned char* cost;
+  const unsigned* rcnt;
+  const int* rlist;
+  unsigned* wcnt;
+  int* wlist;
+  unsigned* rclear;  // the read set's counts (cleared by the last wave)
+  unsigned* done;
+  int cap;
   unsigned long long* clk;  // nullptr, or this launch's span slot (mg_kernel_span_begin)
 };
 

@@ -569,25 +569,27 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   // the LDS model tile of the instance that will run this model, prebuilt once on the host; a model no
   // instance fits is still created (its launches report MG_ECAPACITY)
   s->d_tile = nullptr;
-  // work ordering (MIGYM_ORDER_EVERY = K: every K-th env step sorts the envs by their last row count, k_order)
+  // work ordering (MgOrder, step_kernels.hpp: the envs in descending order of their last row counts)
   s->order_every = 0;
   s->order_steps = 0;
   s->order_valid = false;
-  s->d_order = nullptr;
-  s->d_cost = nullptr;
+  s->d_bq = nullptr;
+  s->d_blist = nullptr;
+  s->bq_cap = 0;
   s->d_span = nullptr;
   s->span_cap = s->span_next = s->span_stride = 0;
-  // default: on for the 32-lane instances (ShadowHand, Humanoid: two teams per wave), off for the narrower ones
-  // (Ant's four 16-lane teams: no gain); every step from 16,384 envs up (the last step's row counts are the best
-  // guess of this one's: Humanoid 32,768 K = 8 35.4 -> K = 1 36.5 M, ShadowHand 16,384 18.9 -> 19.4 M), every 8th
-  // below (ShadowHand 4,096: the sort's own launch outweighs the fresher order, 12.4 vs 12.2 M); MIGYM_ORDER_EVERY
-  // overrides (0: off)
-  s->order_every = mgi::team_size(s->host_model, s->params.max_contacts) >= 32 ? (num_envs >= 16384 ? 1 : 8) : 0;
+  // default: on for the 32-lane instances (Humanoid, ShadowHand) from 16,384 envs, off otherwise: Ant's 16-lane
+  // teams and the one-round small shards pay more for the lists' atomics and gathers than the order saves (same box:
+  // Ant 65,536 119.7 vs 153.1 M, MA-Ant 8,192 -4 %, ShadowHand 4,096 -2 %; Humanoid 32,768 +9.3 %, ShadowHand 16,384
+  // +6.3 %); MIGYM_ORDER_EVERY = 0 turns it off, > 0 on
+  s->order_every = (mgi::team_size(s->host_model, s->params.max_contacts) >= 32 && num_envs >= 16384) ? 1 : 0;
   if (const char* e = getenv("MIGYM_ORDER_EVERY")) s->order_every = atoi(e);
   if (s->order_every > 0) {
     const int A = params->agents > 1 ? params->agents : 1;
-    if (hipMalloc(&s->d_order, sizeof(int) * (size_t)((num_envs + A - 1) / A)) != hipSuccess ||
-        hipMalloc(&s->d_cost, (size_t)num_envs) != hipSuccess || hipMemset(s->d_cost, 0, (size_t)num_envs) != hipSuccess) {
+    s->bq_cap = (num_envs + A - 1) / A;
+    if (hipMalloc(&s->d_bq, sizeof(unsigned) * (2 * kOrderBuckets + 1)) != hipSuccess ||
+        hipMemset(s->d_bq, 0, sizeof(unsigned) * (2 * kOrderBuckets + 1)) != hipSuccess ||
+        hipMalloc(&s->d_blist, sizeof(int) * 2 * (size_t)kOrderBuckets * (size_t)s->bq_cap) != hipSuccess) {
       mg_sim_destroy(s);
       return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(work order) failed");
     }
@@ -689,8 +691,8 @@ int mg_sim_destroy(mg_sim* sim) {
   if (sim->d_model) (void)hipFree(sim->d_model);
   if (sim->d_tile) (void)hipFree(sim->d_tile);
   if (sim->d_wq) (void)hipFree(sim->d_wq);
-  if (sim->d_order) (void)hipFree(sim->d_order);
-  if (sim->d_cost) (void)hipFree(sim->d_cost);
+  if (sim->d_bq) (void)hipFree(sim->d_bq);
+  if (sim->d_blist) (void)hipFree(sim->d_blist);
   if (sim->d_span) (void)hipFree(sim->d_span);
   delete sim;
   return MG_OK;
@@ -881,33 +883,6 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
   return check_launch("mg_post_physics");
 }
 
-// Work ordering (sim->order_every): a counting sort of the envs by their last step's row count, descending
-// (the largest first), one workgroup.  An env of A agents takes its agents' largest count.  Ties land in
-// atomic order: which env a team runs never changes its results, only which envs share a wave.
-__global__ __launch_bounds__(1024) void k_order(const unsigned char* __restrict__ cost, int* __restrict__ order, int nenv,
-                                                int A) {
-  __shared__ int cnt[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) cnt[i] = 0;
-  __syncthreads();
-  auto key = [&](int e) {
-    int k = 0;
-    for (int j = 0; j < A; j++) k = max(k, (int)cost[(size_t)e * A + j]);
-    return 255 - k;  // descending
-  };
-  for (int e = threadIdx.x; e < nenv; e += blockDim.x) atomicAdd(&cnt[key(e)], 1);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int i = 0; i < 256; i++) {
-      const int c = cnt[i];
-      cnt[i] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < nenv; e += blockDim.x) order[atomicAdd(&cnt[key(e)], 1)] = e;
-}
-
 static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
                     void* stream) {
   if (!sim || !sim->bound || !tp || !tb || !tb->actions || !tb->obs || !tb->rew || !tb->reset || !tb->progress ||
@@ -940,16 +915,16 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   if (tp->num_actions > 64 || tp->num_obs > 256 || tp->num_states > 256)
     return fail(MG_EINVAL, "mg_env_step: num_actions > 64, num_obs > 256 or num_states > 256");
   if (sim->order_every > 0 && !rp) {
-    if (sim->order_steps > 0 && sim->order_steps % sim->order_every == 0) {
-      const int A = tp->num_agents > 1 ? tp->num_agents : 1;
-      hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, (hipStream_t)stream, sim->d_cost, sim->d_order, sim->n / A, A);
-      sim->order_valid = true;
-    }
-    sim->order_steps++;
+    const int A = tp->num_agents > 1 ? tp->num_agents : 1;
+    if (sim->bq_cap != (sim->n + A - 1) / A) return fail(MG_EINVAL, "mg_env_step: num_agents differs from mg_sim_params.agents");
   }
   int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
                                           (const mg_sim*)sim, tp, tb, rp);
   if (rc) return rc;
+  if (sim->order_every > 0 && !rp) {  // the launch wrote the other set's lists: the next one reads them
+    sim->order_steps++;
+    sim->order_valid = true;
+  }
   if (hand && !tb->defer_finalize)  // consecutive_successes running mean from the step's partial sums
     hipLaunchKernelGGL(k_hand_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, *tp, *tb);
   return check_launch(rp ? "mg_env_step_replay" : "mg_env_step");

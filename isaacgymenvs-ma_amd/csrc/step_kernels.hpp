@@ -184,14 +184,50 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
 // are latency-bound; occupancy is the lever — DESIGN.md §3)
 // RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
 // post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
-// the actor a team slot works on: the slot itself, or under a work ordering (MgOrder, sim->order_every) the
-// slot's env in k_order's permutation (envs of A agents stay whole and aligned: the AND filter and the "others"
-// block exchange within the env's A consecutive teams of one wave)
+// the actor a team slot works on: the slot itself, or under a work ordering (MgOrder, sim->order_every) the env at
+// the slot's position in the previous launch's bucket lists, heaviest bucket first (envs of A agents stay whole and
+// aligned: the AND filter and the "others" block exchange within the env's A consecutive teams of one wave).  The
+// wave's lanes 0..kOrderBuckets-1 load the counts and scan them; each lane finds its position's bucket through the
+// wave-uniform prefixes.
 __device__ __forceinline__ int ordered_actor(const MgOrder& ord, int slot, int n, int A) {
-  if (slot >= n) return n - 1;
-  if (!ord.order) return slot;
+  if (!ord.rcnt) return slot < n ? slot : n - 1;
   const int a1 = A > 1 ? A : 1;
-  return ord.order[slot / a1] * a1 + slot % a1;
+  const int lane = (int)(threadIdx.x & 63);
+  unsigned inc = lane < kOrderBuckets ? ord.rcnt[lane] : 0u;
+#pragma unroll
+  for (int d = 1; d < kOrderBuckets; d <<= 1) {
+    const unsigned y = __shfl_up(inc, d);
+    inc += lane >= d ? y : 0u;
+  }
+  const unsigned p = (unsigned)((slot < n ? slot : n - 1) / a1);
+  unsigned b = 0u, base = 0u;
+#pragma unroll
+  for (int j = 0; j < kOrderBuckets; j++) {
+    const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)inc, j);
+    b += v <= p ? 1u : 0u;
+    base = v <= p ? v : base;
+  }
+  b = b < (unsigned)kOrderBuckets ? b : (unsigned)kOrderBuckets - 1u;
+  return ord.rlist[(size_t)b * ord.cap + (p - base)] * a1 + (slot < n ? slot : n - 1) % a1;
+}
+// the bucket of an env whose step used `rows` constraint rows (descending: the heaviest first)
+__device__ __forceinline__ int order_bucket(int rows) {
+  const int c = rows / kOrderWidth;
+  return kOrderBuckets - 1 - (c < kOrderBuckets - 1 ? c : kOrderBuckets - 1);
+}
+// the next launch's lists: env unit u (of this launch's step) appended to the bucket of its row count
+__device__ __forceinline__ void order_append(const MgOrder& ord, int rows, int u) {
+  const int b = order_bucket(rows);
+  const unsigned k = atomicAdd(&ord.wcnt[b], 1u);
+  ord.wlist[(size_t)b * ord.cap + k] = u;
+}
+// every wave of an ordered launch checks out; the last one clears the counts the launch read (every wave has read
+// them: it started before the last one finished) and the counter, for the launch after next
+__device__ __forceinline__ void order_done(const MgOrder& ord, int grid_waves) {
+  if (ord.wcnt && (threadIdx.x & 63) == 0 && atomicAdd(ord.done, 1u) == (unsigned)grid_waves - 1u) {
+    for (int b = 0; b < kOrderBuckets; b++) atomicExch(&ord.rclear[b], 0u);
+    atomicExch(ord.done, 0u);
+  }
 }
 
 // one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
@@ -390,7 +426,15 @@ __device__ __forceinline__ void env_step_item(
     if (v.dof_force)
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
-  if (valid && ord.cost && t.tl == 0) ord.cost[a] = (unsigned char)(L.nrows < 255 ? L.nrows : 255);
+  if (ord.wcnt) {  // the next launch's order: the env's largest agent row count
+    int rows = L.nrows;
+    const int A = tp.num_agents > 1 ? tp.num_agents : 1;
+    if (A > 1) {
+      const int k0 = wt - wt % A;  // the env's first team in the wave
+      for (int k = 0; k < A; k++) rows = max(rows, __shfl(rows, (k0 + k) * T));
+    }
+    if (valid && t.tl == 0 && a % A == 0) order_append(ord, rows, a / A);
+  }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
 }
@@ -411,6 +455,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
     // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
     if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
+    order_done(ord, (int)gridDim.x);
   } else {
     // multi-wave blocks: the work queue (wq_next), the grid being the resident capacity
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
@@ -420,6 +465,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
                                                (&rp)[z], item, (&ord)[z]);
     }
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
+    order_done(ord, gwv);
     wq_done(wq, gwv);
   }
 }
@@ -677,7 +723,7 @@ __device__ __forceinline__ void hand_step_item(
       }
     }
   }
-  if (valid && ord.cost && t.tl == 0) ord.cost[e] = (unsigned char)(L.nrows < 255 ? L.nrows : 255);
+  if (ord.wcnt && valid && t.tl == 0) order_append(ord, L.nrows, e);  // the next launch's order
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
 }
@@ -697,6 +743,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   if constexpr (W == 1) {  // as k_env_step
     if ((int)blockIdx.x * SH::E1 < n) hand_step_item<T, MN, MC, MG, MP, OT, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
+    order_done(ord, (int)gridDim.x);
   } else {
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
@@ -705,6 +752,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
                                                     (&tb)[z], n, (&rp)[z], item, (&ord)[z]);
     }
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
+    order_done(ord, gwv);
     wq_done(wq, gwv);
   }
 }
@@ -744,7 +792,16 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     clk = ms->d_span + 2 * (size_t)ms->span_stride * ms->span_next;
     ms->span_waves[ms->span_next++] = blocks * SH::W;
   }
-  const MgOrder ord{(ordered && sim->order_valid) ? sim->d_order : nullptr, ordered ? sim->d_cost : nullptr, clk};
+  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk};
+  if (ordered && sim->order_every > 0 && sim->d_bq) {
+    const int rs = (int)(sim->order_steps & 1), ws = 1 - rs;   // this launch reads set rs, writes set ws
+    ord.rcnt = sim->order_valid ? sim->d_bq + rs * kOrderBuckets : nullptr;
+    ord.rlist = sim->d_blist + (size_t)rs * kOrderBuckets * sim->bq_cap;
+    ord.wcnt = sim->d_bq + ws * kOrderBuckets;
+    ord.wlist = sim->d_blist + (size_t)ws * kOrderBuckets * sim->bq_cap;
+    ord.rclear = sim->d_bq + rs * kOrderBuckets;
+    ord.done = sim->d_bq + 2 * kOrderBuckets;
+  }
   // one-wave blocks: the static grid, one block per item; multi-wave blocks: the resident capacity (work queue)
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), MG_LDS_PAD, s, args..., sim->d_wq, ord);
   return MG_OK;
