@@ -17,18 +17,24 @@ struct mg_sim {
   int32_t device;
   mg_state_views views;
   bool bound;
-  // work ordering of the fused step (step_kernels.hpp MgOrder; on for the 16- and 32-lane instances,
-  // MIGYM_ORDER_EVERY = 0 turns it off at mg_sim_create): every mg_env_step takes its envs in descending order of
+  // work ordering of the fused step (step_kernels.hpp MgOrder; mg_sim_create picks the mode per instance and env
+  // count, MIGYM_ORDER = off | lists | sort overrides): every mg_env_step takes its envs in descending order of
   // their constraint-row counts of the previous step -- teams of similar cost share a wave (the wave runs its slowest
-  // team's rows) and the heavy envs start first.  The previous launch built the order itself: each env appended its
-  // index to the bucket of its row count (two sets of kOrderBuckets lists, alternating launch by launch), and that
-  // launch's last wave cleared the set it had read.  Envs are independent, so every result is the same bit for bit.
-  int order_every;     // > 0: on
-  long long order_steps;  // ordered launches so far (the parity of the set they write)
-  bool order_valid;    // a set holds the previous ordered launch's lists
-  unsigned* d_bq;      // [2][kOrderBuckets] bucket counts, then the launch's finished-wave counter
-  int* d_blist;        // [2][kOrderBuckets][bq_cap] env indices per bucket
+  // team's rows) and the heavy envs start first.  Envs are independent, so every result is the same bit for bit.
+  //   lists (kOrderLists): the previous launch built the order itself: each env appended its index to the bucket of
+  //     its row count (two sets of kOrderBuckets lists, alternating launch by launch), and that launch's last wave
+  //     cleared the set it had read;
+  //   sort (kOrderSort): the previous launch wrote each env's row count, and a two-pass counting sort
+  //     (k_ohist, k_oscatter) before the launch turns them into the permutation it reads.
+  int order_mode;      // kOrderOff / kOrderLists / kOrderSort
+  long long order_steps;  // ordered launches so far (the parity of the set they write / of the sort's totals)
+  bool order_valid;    // the previous ordered launch left an order for this one
+  unsigned* d_bq;      // lists: [2][kOrderBuckets] bucket counts, then the launch's finished-wave counter
+  int* d_blist;        // lists: [2][kOrderBuckets][bq_cap] env indices per bucket
   int bq_cap;          // env units (n / A)
+  int* d_order;        // sort: (bq_cap) slot -> env unit
+  unsigned char* d_cost;  // sort: (bq_cap) the last launch's row count per env unit (its agents' largest, <= 255)
+  unsigned* d_osort;   // sort: [2][256] bin totals (alternating), [blocks][256] the blocks' bases, then ushort ranks
   // kernel spans (mg_kernel_span_begin): per recorded launch, span_stride (start, end) pairs, one per wave
   unsigned long long* d_span;
   int span_cap, span_next, span_stride;
@@ -39,7 +45,10 @@ struct mg_sim {
 // (wcnt nullptr: no ordering), the read set's counts the last wave clears, the finished-wave counter
 constexpr int kOrderBuckets = 32;  // row-count classes of width kOrderWidth, descending (bucket 0: 62 rows and more)
 constexpr int kOrderWidth = 2;
+constexpr int kOrderOff = 0, kOrderLists = 1, kOrderSort = 2;
 struct MgOrder {
+  const int* order;     // sort: this launch's permutation (nullptr: none yet)
+  unsigned char* cost;  // sort: the row counts this launch writes
   const unsigned* rcnt;
   const int* rlist;
   unsigned* wcnt;

@@ -570,26 +570,54 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   // instance fits is still created (its launches report MG_ECAPACITY)
   s->d_tile = nullptr;
   // work ordering (MgOrder, step_kernels.hpp: the envs in descending order of their last row counts)
-  s->order_every = 0;
+  s->order_mode = kOrderOff;
   s->order_steps = 0;
   s->order_valid = false;
   s->d_bq = nullptr;
   s->d_blist = nullptr;
   s->bq_cap = 0;
+  s->d_order = nullptr;
+  s->d_cost = nullptr;
+  s->d_osort = nullptr;
   s->d_span = nullptr;
   s->span_cap = s->span_next = s->span_stride = 0;
-  // default: on for the 32-lane instances (Humanoid, ShadowHand) from 16,384 envs, off otherwise: Ant's 16-lane
-  // teams and the one-round small shards pay more for the lists' atomics and gathers than the order saves (same box:
-  // Ant 65,536 119.7 vs 153.1 M, MA-Ant 8,192 -4 %, ShadowHand 4,096 -2 %; Humanoid 32,768 +9.3 %, ShadowHand 16,384
-  // +6.3 %); MIGYM_ORDER_EVERY = 0 turns it off, > 0 on
-  s->order_every = (mgi::team_size(s->host_model, s->params.max_contacts) >= 32 && num_envs >= 16384) ? 1 : 0;
-  if (const char* e = getenv("MIGYM_ORDER_EVERY")) s->order_every = atoi(e);
-  if (s->order_every > 0) {
+  // default (same box, M env-steps/s unordered -> ordered):
+  //   ShadowHand from 16,384 envs: the lists (16,384 19.1 -> 20.3; the sort 20.15: its two launches cost more than
+  //     the in-kernel lists);
+  //   Humanoid from 16,384 and Ant from 32,768 one-agent envs: the sort (Humanoid 32,768 33.8 -> 37.3, lists 37.0;
+  //     Ant 65,536 153.0 -> 156.0, 32,768 143.0 -> 145.9; the lists' hot-bucket atomics cost Ant 65,536 22 %);
+  //   off: MA-Ant (8,192 -1.1 %, 65,536 -1.0 % sorted), Cartpole and the smaller batches (Ant 16,384 -1.1 %,
+  //     ShadowHand 4,096 -2 %: the sort's launches or the lists' atomics outweigh the tail they save).
+  // MIGYM_ORDER = off | lists | sort overrides.
+  {
+    const int T = mgi::team_size(s->host_model, s->params.max_contacts);
+    const int A = params->agents > 1 ? params->agents : 1;
+    if (s->host_model.obj_type) s->order_mode = num_envs >= 16384 ? kOrderLists : kOrderOff;
+    else if (T >= 32) s->order_mode = num_envs >= 16384 ? kOrderSort : kOrderOff;
+    else if (T == 16 && A == 1) s->order_mode = num_envs >= 32768 ? kOrderSort : kOrderOff;
+  }
+  if (const char* e = getenv("MIGYM_ORDER")) {
+    if (!strcmp(e, "off")) s->order_mode = kOrderOff;
+    else if (!strcmp(e, "lists")) s->order_mode = kOrderLists;
+    else if (!strcmp(e, "sort")) s->order_mode = kOrderSort;
+    else {
+      mg_sim_destroy(s);
+      return fail(MG_EINVAL, "mg_sim_create: MIGYM_ORDER must be off, lists or sort");
+    }
+  }
+  if (s->order_mode != kOrderOff) {
     const int A = params->agents > 1 ? params->agents : 1;
     s->bq_cap = (num_envs + A - 1) / A;
-    if (hipMalloc(&s->d_bq, sizeof(unsigned) * (2 * kOrderBuckets + 1)) != hipSuccess ||
-        hipMemset(s->d_bq, 0, sizeof(unsigned) * (2 * kOrderBuckets + 1)) != hipSuccess ||
-        hipMalloc(&s->d_blist, sizeof(int) * 2 * (size_t)kOrderBuckets * (size_t)s->bq_cap) != hipSuccess) {
+    const size_t nu = (size_t)s->bq_cap, nb = (nu + 255) / 256;
+    const bool ok = s->order_mode == kOrderLists
+        ? hipMalloc(&s->d_bq, sizeof(unsigned) * (2 * kOrderBuckets + 1)) == hipSuccess &&
+              hipMemset(s->d_bq, 0, sizeof(unsigned) * (2 * kOrderBuckets + 1)) == hipSuccess &&
+              hipMalloc(&s->d_blist, sizeof(int) * 2 * (size_t)kOrderBuckets * nu) == hipSuccess
+        : hipMalloc(&s->d_osort, sizeof(unsigned) * (512 + 256 * nb) + sizeof(unsigned short) * (nu + 2)) == hipSuccess &&
+              hipMemset(s->d_osort, 0, sizeof(unsigned) * 512) == hipSuccess &&
+              hipMalloc(&s->d_order, sizeof(int) * nu) == hipSuccess &&
+              hipMalloc(&s->d_cost, nu) == hipSuccess && hipMemset(s->d_cost, 0, nu) == hipSuccess;
+    if (!ok) {
       mg_sim_destroy(s);
       return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(work order) failed");
     }
@@ -693,6 +721,9 @@ int mg_sim_destroy(mg_sim* sim) {
   if (sim->d_wq) (void)hipFree(sim->d_wq);
   if (sim->d_bq) (void)hipFree(sim->d_bq);
   if (sim->d_blist) (void)hipFree(sim->d_blist);
+  if (sim->d_order) (void)hipFree(sim->d_order);
+  if (sim->d_cost) (void)hipFree(sim->d_cost);
+  if (sim->d_osort) (void)hipFree(sim->d_osort);
   if (sim->d_span) (void)hipFree(sim->d_span);
   delete sim;
   return MG_OK;
@@ -883,6 +914,66 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
   return check_launch("mg_post_physics");
 }
 
+// Work ordering, sort mode (kOrderSort): a counting sort of the env units by the last launch's row counts,
+// descending (the largest first), in two grid-wide passes of 256-unit blocks.  Pass 1 (k_ohist): each block's
+// histogram in LDS -- the lanes of one key aggregated into one LDS add per key and wave, since a few hot bins would
+// otherwise serialise every add -- then one global atomic per block and used bin reserves the block's range inside
+// the bin, and each unit keeps its rank inside its block's range.  Pass 2 (k_oscatter): the bins' starts (a block
+// scan of the 256 totals) and each unit's slot.  Where a unit lands inside its bin never changes a result, only
+// which units share a wave.  The totals alternate between two buffers; pass 1 clears the one the next sort fills.
+// (Fusing the histogram into the step kernel -- a global add per env -- and placing by per-bin cursors measured far
+// slower: one hot bin's atomics serialise, Ant 65,536 156.0 -> 108.5 M)
+__global__ __launch_bounds__(256) void k_ohist(const unsigned char* __restrict__ cost, int nu,
+                                               unsigned* __restrict__ tot, unsigned* __restrict__ tot_clear,
+                                               unsigned* __restrict__ bbase, unsigned short* __restrict__ rank) {
+  __shared__ unsigned h[256];
+  h[threadIdx.x] = 0u;
+  if (blockIdx.x == 0) tot_clear[threadIdx.x] = 0u;
+  __syncthreads();
+  const int u = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int lane = (int)(threadIdx.x & 63);
+  const int key = u < nu ? 255 - (int)cost[u] : -1;
+  unsigned r = 0u;
+  unsigned long long rem = __ballot(key >= 0);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const int k = __shfl(key, leader);
+    const unsigned long long same = __ballot(key == k) & rem;
+    unsigned base = 0u;
+    if (lane == leader) base = atomicAdd(&h[k], (unsigned)__popcll(same));
+    base = (unsigned)__shfl((int)base, leader);
+    if ((same >> lane) & 1ull) r = base + (unsigned)__popcll(same & ((1ull << lane) - 1ull));
+    rem &= ~same;
+  }
+  __syncthreads();
+  const unsigned c = h[threadIdx.x];
+  bbase[(size_t)blockIdx.x * 256 + threadIdx.x] = c ? atomicAdd(&tot[threadIdx.x], c) : 0u;
+  if (u < nu) rank[u] = (unsigned short)r;
+}
+__global__ __launch_bounds__(256) void k_oscatter(const unsigned char* __restrict__ cost, int nu,
+                                                  const unsigned* __restrict__ tot, const unsigned* __restrict__ bbase,
+                                                  const unsigned short* __restrict__ rank, int* __restrict__ order) {
+  __shared__ unsigned wsum[4], start[256];
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  const unsigned v = tot[threadIdx.x];
+  unsigned inc = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned y = (unsigned)__shfl_up((int)inc, d);
+    inc += lane >= d ? y : 0u;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  unsigned off = 0u;
+  for (int w = 0; w < wv; w++) off += wsum[w];
+  start[threadIdx.x] = off + inc - v;
+  __syncthreads();
+  const int u = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (u < nu) {
+    const int key = 255 - (int)cost[u];
+    order[start[key] + bbase[(size_t)blockIdx.x * 256 + key] + rank[u]] = u;
+  }
+}
+
 static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers* tb, const mg_replay* rp,
                     void* stream) {
   if (!sim || !sim->bound || !tp || !tb || !tb->actions || !tb->obs || !tb->rew || !tb->reset || !tb->progress ||
@@ -914,14 +1005,23 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   }
   if (tp->num_actions > 64 || tp->num_obs > 256 || tp->num_states > 256)
     return fail(MG_EINVAL, "mg_env_step: num_actions > 64, num_obs > 256 or num_states > 256");
-  if (sim->order_every > 0 && !rp) {
+  if (sim->order_mode != kOrderOff && !rp) {
     const int A = tp->num_agents > 1 ? tp->num_agents : 1;
     if (sim->bq_cap != (sim->n + A - 1) / A) return fail(MG_EINVAL, "mg_env_step: num_agents differs from mg_sim_params.agents");
+    if (sim->order_mode == kOrderSort && sim->order_valid) {  // the last launch's row counts -> this one's order
+      const int nu = sim->bq_cap, nb = (nu + 255) / 256, b = (int)(sim->order_steps & 1);
+      unsigned* bbase = sim->d_osort + 512;
+      unsigned short* rank = reinterpret_cast<unsigned short*>(sim->d_osort + 512 + 256 * (size_t)nb);
+      hipLaunchKernelGGL(k_ohist, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu,
+                         sim->d_osort + 256 * b, sim->d_osort + 256 * (b ^ 1), bbase, rank);
+      hipLaunchKernelGGL(k_oscatter, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu,
+                         sim->d_osort + 256 * b, bbase, rank, sim->d_order);
+    }
   }
   int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
                                           (const mg_sim*)sim, tp, tb, rp);
   if (rc) return rc;
-  if (sim->order_every > 0 && !rp) {  // the launch wrote the other set's lists: the next one reads them
+  if (sim->order_mode != kOrderOff && !rp) {  // the launch wrote the next one's lists / row counts
     sim->order_steps++;
     sim->order_valid = true;
   }

@@ -184,14 +184,18 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
 // are latency-bound; occupancy is the lever — DESIGN.md §3)
 // RP: physics-bypass replay instance (mg_env_step_replay): the task layer below runs unchanged on the
 // post-simulate state `rp` supplies instead of the substeps (tests only; never the bench path).
-// the actor a team slot works on: the slot itself, or under a work ordering (MgOrder, sim->order_every) the env at
-// the slot's position in the previous launch's bucket lists, heaviest bucket first (envs of A agents stay whole and
+// the actor a team slot works on: the slot itself, or under a work ordering (MgOrder, sim->order_mode) the env at
+// the slot's position in the sort's permutation, or in the previous launch's bucket lists, heaviest bucket first (envs of A agents stay whole and
 // aligned: the AND filter and the "others" block exchange within the env's A consecutive teams of one wave).  The
 // wave's lanes 0..kOrderBuckets-1 load the counts and scan them; each lane finds its position's bucket through the
 // wave-uniform prefixes.
 __device__ __forceinline__ int ordered_actor(const MgOrder& ord, int slot, int n, int A) {
-  if (!ord.rcnt) return slot < n ? slot : n - 1;
   const int a1 = A > 1 ? A : 1;
+  if (ord.order) {  // sort: the permutation k_oscatter wrote
+    const int s = slot < n ? slot : n - 1;
+    return ord.order[s / a1] * a1 + s % a1;
+  }
+  if (!ord.rcnt) return slot < n ? slot : n - 1;
   const int lane = (int)(threadIdx.x & 63);
   unsigned inc = lane < kOrderBuckets ? ord.rcnt[lane] : 0u;
 #pragma unroll
@@ -426,14 +430,17 @@ __device__ __forceinline__ void env_step_item(
     if (v.dof_force)
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
   }
-  if (ord.wcnt) {  // the next launch's order: the env's largest agent row count
+  if (ord.wcnt || ord.cost) {  // the next launch's order: the env's largest agent row count
     int rows = L.nrows;
     const int A = tp.num_agents > 1 ? tp.num_agents : 1;
     if (A > 1) {
       const int k0 = wt - wt % A;  // the env's first team in the wave
       for (int k = 0; k < A; k++) rows = max(rows, __shfl(rows, (k0 + k) * T));
     }
-    if (valid && t.tl == 0 && a % A == 0) order_append(ord, rows, a / A);
+    if (valid && t.tl == 0 && a % A == 0) {
+      if (ord.wcnt) order_append(ord, rows, a / A);
+      else ord.cost[a / A] = (unsigned char)(rows < 255 ? rows : 255);
+    }
   }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
@@ -723,7 +730,10 @@ __device__ __forceinline__ void hand_step_item(
       }
     }
   }
-  if (ord.wcnt && valid && t.tl == 0) order_append(ord, L.nrows, e);  // the next launch's order
+  if (valid && t.tl == 0) {  // the next launch's order
+    if (ord.wcnt) order_append(ord, L.nrows, e);
+    else if (ord.cost) ord.cost[e] = (unsigned char)(L.nrows < 255 ? L.nrows : 255);
+  }
   t.ph_mark(9);
   MG_PHASE_FLUSH(t, item)
 }
@@ -792,8 +802,11 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     clk = ms->d_span + 2 * (size_t)ms->span_stride * ms->span_next;
     ms->span_waves[ms->span_next++] = blocks * SH::W;
   }
-  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk};
-  if (ordered && sim->order_every > 0 && sim->d_bq) {
+  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk};
+  if (ordered && sim->order_mode == kOrderSort) {
+    ord.order = sim->order_valid ? sim->d_order : nullptr;
+    ord.cost = sim->d_cost;
+  } else if (ordered && sim->order_mode == kOrderLists) {
     const int rs = (int)(sim->order_steps & 1), ws = 1 - rs;   // this launch reads set rs, writes set ws
     ord.rcnt = sim->order_valid ? sim->d_bq + rs * kOrderBuckets : nullptr;
     ord.rlist = sim->d_blist + (size_t)rs * kOrderBuckets * sim->bq_cap;

@@ -170,11 +170,11 @@ def test_ragged_shards_equal_slices_of_one_rollout(task, obj):
         sh.close()
 
 
-def _rollout_with_order(task, n, env_cfg, order_every, steps):
-    """`steps` fused steps of `task` with MIGYM_ORDER_EVERY = order_every (read at mg_sim_create), a short episode
-    so that timeouts and terminations reset envs inside the run; every step's outputs and state, cloned"""
-    old = os.environ.get("MIGYM_ORDER_EVERY")
-    os.environ["MIGYM_ORDER_EVERY"] = str(order_every)
+def _rollout_with_order(task, n, env_cfg, mode, steps):
+    """`steps` fused steps of `task` with MIGYM_ORDER = mode (read at mg_sim_create), a short episode so that
+    timeouts and terminations reset envs inside the run; every step's outputs and state, cloned"""
+    old = os.environ.get("MIGYM_ORDER")
+    os.environ["MIGYM_ORDER"] = mode
     try:
         cfg = configs.task_config(task, n, sim_device=DEV)
         cfg["env"].update(env_cfg)
@@ -182,9 +182,9 @@ def _rollout_with_order(task, n, env_cfg, order_every, steps):
                          cfg={"task": cfg})
     finally:
         if old is None:
-            del os.environ["MIGYM_ORDER_EVERY"]
+            del os.environ["MIGYM_ORDER"]
         else:
-            os.environ["MIGYM_ORDER_EVERY"] = old
+            os.environ["MIGYM_ORDER"] = old
     g = torch.Generator(device=DEV).manual_seed(23)
     out = []
     for _ in range(steps):
@@ -197,21 +197,26 @@ def _rollout_with_order(task, n, env_cfg, order_every, steps):
     return out, resets
 
 
-@pytest.mark.parametrize("task,n,env_cfg", [("Humanoid", 301, {}),
+@pytest.mark.parametrize("mode", ["lists", "sort"])
+@pytest.mark.parametrize("task,n,env_cfg", [("Ant", 301, {}),
+                                            ("Ant", 4099, {}),
+                                            ("Humanoid", 301, {}),
                                             ("ShadowHand", 301, {"objectType": "block"}),
                                             ("ShadowHand", 301, {"objectType": "egg"}),
                                             ("ShadowHand", 301, {"objectType": "pen"}),
                                             ("MAAnt", 301, {"numAgents": 2})])
-def test_work_order_changes_no_result(task, n, env_cfg):
-    """Work ordering (k_order + the ordered actor permutation) only changes which envs share a wave:
-    sorting every step (MIGYM_ORDER_EVERY=1, the first sort on the second step) and never (0) give the same
-    obs, rew, reset, root and DOF state bit for bit over 12 steps with resets, on a ragged env count (the last
-    wave partly filled).  MAAnt with 2 agents per env has the ordering forced on, so the agent alignment that the
-    AND filter and the 'others' shuffles rely on is exercised under the permutation."""
+def test_work_order_changes_no_result(task, n, env_cfg, mode):
+    """Work ordering (the in-kernel bucket lists, or the two-pass counting sort k_ohist / k_oscatter
+    and its permutation) only changes which envs share a wave: ordering every step (MIGYM_ORDER=lists / sort, the
+    first ordered launch the second step) and never (off) give the same obs, rew, reset, root and DOF state bit for
+    bit over 12 steps with resets, on ragged env counts (the last wave and the sort's last block partly filled; Ant
+    4,099: 17 sort blocks, so the blocks' global bin ranges interleave).  MAAnt with 2 agents per env is ordered by
+    env units, so the agent alignment that the AND filter and the 'others' shuffles rely on is exercised under the
+    permutation."""
     assert torch.cuda.is_available(), "GPU tests need the MI355X"
     env_cfg = dict(env_cfg, episodeLength=7)
-    on, r_on = _rollout_with_order(task, n, env_cfg, 1, 12)
-    off, r_off = _rollout_with_order(task, n, env_cfg, 0, 12)
+    on, r_on = _rollout_with_order(task, n, env_cfg, mode, 12)
+    off, r_off = _rollout_with_order(task, n, env_cfg, "off", 12)
     assert r_on == r_off and r_on > 0
     names = ("obs", "rew", "reset", "root state", "dof state", "progress")
     for k, (a, b) in enumerate(zip(on, off)):

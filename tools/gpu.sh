@@ -24,8 +24,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mode=${1:?mode}; shift
 
-uselib() {  # $1 = default | variant name
-  if [ "$1" = default ]; then unset MIGYM_LIB; else export MIGYM_LIB=$PWD/isaacgymenvs-ma_amd/migym/_lib/var/$1.so
+uselib() {  # $1 = default | variant name, either with an optional %MODE suffix (MIGYM_ORDER=off|lists|sort)
+  local name=${1%%\%*}
+  if [ "$name" != "$1" ]; then export MIGYM_ORDER=${1#*%}; else unset MIGYM_ORDER; fi
+  if [ "$name" = default ]; then unset MIGYM_LIB; else export MIGYM_LIB=$PWD/isaacgymenvs-ma_amd/migym/_lib/var/$name.so
     [ -f "$MIGYM_LIB" ] || { echo "no variant library $MIGYM_LIB (build it on the CPU first)"; exit 2; }; fi
 }
 
