@@ -521,6 +521,13 @@ int mg_kernel_span_read(mg_sim* sim, double* ms, int32_t cap, int32_t* n_out);
  * kHz) -- the launch's tail and dispatch ramp for tools/span_diag.py --waves */
 int mg_kernel_span_waves(mg_sim* sim, int32_t launch, uint64_t* out, int32_t cap, int32_t* n_out);
 
+/* Test aid (no reference counterpart): the work ordering's state.  mg_work_order(sim, order, cost,
+ * cap, &mode, &n): synchronises the device; mode = 0 off, 1 lists, 2 sort; under the sort n = the env units (envs,
+ * an MA env's agents counted once), `order` (n int32, or NULL) = the permutation the last mg_env_step ran in (slot ->
+ * unit; the identity before the first sort) and `cost` (n uint8, or NULL) = the row counts that launch wrote (the
+ * next sort's keys); at most cap entries are copied.  Off and lists report n = 0. */
+int mg_work_order(mg_sim* sim, int32_t* order, uint8_t* cost, int32_t cap, int32_t* mode, int32_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

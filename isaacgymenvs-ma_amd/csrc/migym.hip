@@ -790,6 +790,27 @@ int mg_kernel_span_waves(mg_sim* sim, int32_t launch, uint64_t* out, int32_t cap
   return MG_OK;
 }
 
+int mg_work_order(mg_sim* sim, int32_t* order, uint8_t* cost, int32_t cap, int32_t* mode, int32_t* n_out) {
+  if (!sim || !mode || !n_out || cap < 0) return fail(MG_EINVAL, "mg_work_order: bad arguments");
+  *mode = sim->order_mode;
+  *n_out = 0;
+  if (sim->order_mode != kOrderSort) return MG_OK;
+  const int n = sim->bq_cap < cap ? sim->bq_cap : cap;
+  if (hipDeviceSynchronize() != hipSuccess) return fail(MG_EDEVICE, "mg_work_order: sync failed");
+  if (order) {
+    if (sim->order_valid && sim->order_steps > 1) {
+      if (n > 0 && hipMemcpy(order, sim->d_order, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(MG_EDEVICE, "mg_work_order: copy failed");
+    } else {
+      for (int i = 0; i < n; i++) order[i] = i;  // no sort has run yet: the launches took the slots in order
+    }
+  }
+  if (cost && n > 0 && hipMemcpy(cost, sim->d_cost, (size_t)n, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(MG_EDEVICE, "mg_work_order: copy failed");
+  *n_out = n;
+  return MG_OK;
+}
+
 int mg_set_indexed(mg_sim* sim, int32_t which, const float* src, const int32_t* idx, int32_t n, void* stream) {
   if (!sim || !sim->bound || !src || (n > 0 && !idx)) return fail(MG_EINVAL, "mg_set_indexed: bad arguments");
   if (n == 0) return MG_OK;

@@ -222,3 +222,57 @@ def test_work_order_changes_no_result(task, n, env_cfg, mode):
     for k, (a, b) in enumerate(zip(on, off)):
         for name, x, y in zip(names, a, b):
             assert torch.equal(x, y), f"{task} {env_cfg} step {k}: {name} differ with the work order on"
+
+
+def _work_order(env, cap):
+    """(mode, order, cost) of the env's work ordering through mg_work_order (order: the permutation the last launch
+    ran in; cost: the row counts that launch wrote, the next sort's keys)"""
+    import ctypes as C
+    import numpy as np
+    from migym import _abi
+    order = np.zeros(cap, np.int32)
+    cost = np.zeros(cap, np.uint8)
+    mode, n = C.c_int32(-1), C.c_int32(-1)
+    _abi.check(env._lib.mg_work_order(env.sim, order.ctypes.data, cost.ctypes.data, cap, C.byref(mode), C.byref(n)),
+               env._lib)
+    return mode.value, order[:n.value].copy(), cost[:n.value].copy()
+
+
+@pytest.mark.parametrize("task,n,env_cfg,mode", [("Ant", 65536, {}, None),          # the headline size: sorted by default
+                                                 ("Humanoid", 32768, {}, None),     # configs[2]: sorted by default
+                                                 ("Ant", 4099, {}, "sort"),         # 17 ragged sort blocks
+                                                 ("MAAnt", 8192, {"numAgents": 4}, "sort")])  # env units of 4 agents
+def test_sort_order_is_a_descending_permutation(task, n, env_cfg, mode):
+    """The sort mode's counting sort (k_ohist / k_oscatter) at the BASELINE sizes: every launch runs
+    its env units in a permutation of 0..units-1 (each unit exactly once) sorted by the previous launch's row counts,
+    largest first -- checked exactly on the device's own keys (read before the launch) over 6 launches."""
+    import numpy as np
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    old = os.environ.get("MIGYM_ORDER")
+    if mode:
+        os.environ["MIGYM_ORDER"] = mode
+    try:
+        cfg = configs.task_config(task, n, sim_device=DEV)
+        cfg["env"].update(env_cfg)
+        env = migym.make(seed=5, task=task, num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                         cfg={"task": cfg})
+    finally:
+        if old is None:
+            os.environ.pop("MIGYM_ORDER", None)
+        else:
+            os.environ["MIGYM_ORDER"] = old
+    units = n
+    g = torch.Generator(device=DEV).manual_seed(3)
+    prev_cost = None
+    for k in range(7):
+        a = torch.rand((env.num_actors, env.num_actions), device=DEV, generator=g) * 2 - 1
+        env.step(a)
+        m, order, cost = _work_order(env, units)
+        assert m == 2 and order.size == units and cost.size == units, (m, order.size, units)
+        if prev_cost is not None:
+            assert np.array_equal(np.sort(order), np.arange(units)), f"launch {k}: not a permutation"
+            keys = prev_cost[order].astype(np.int32)
+            assert np.all(keys[:-1] >= keys[1:]), f"launch {k}: not in descending row-count order"
+            assert keys[0] > 0, "no constraint rows at all: the test would check nothing"
+        prev_cost = cost
+    env.close()
