@@ -27,7 +27,9 @@ struct mg_sim {
   //   sort (kOrderSort): the previous launch wrote each env's row count, and a two-pass counting sort
   //     (k_ohist, k_oscatter) before the launch turns them into the permutation it reads.
   int order_mode;      // kOrderOff / kOrderLists / kOrderSort
-  long long order_steps;  // ordered launches so far (the parity of the set they write / of the sort's totals)
+  long long order_steps;  // ordered launches so far (the parity of the set the lists' launches write)
+  int sort_every;      // sort: every K-th ordered launch sorts (the launches between keep the last permutation)
+  long long sorts;     // sort: sorts so far (the parity of the sort's totals)
   bool order_valid;    // the previous ordered launch left an order for this one
   unsigned* d_bq;      // lists: [2][kOrderBuckets] bucket counts, then the launch's finished-wave counter
   int* d_blist;        // lists: [2][kOrderBuckets][bq_cap] env indices per bucket

@@ -572,6 +572,8 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   // work ordering (MgOrder, step_kernels.hpp: the envs in descending order of their last row counts)
   s->order_mode = kOrderOff;
   s->order_steps = 0;
+  s->sort_every = 1;
+  s->sorts = 0;
   s->order_valid = false;
   s->d_bq = nullptr;
   s->d_blist = nullptr;
@@ -588,7 +590,8 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   //     Ant 65,536 153.0 -> 156.0, 32,768 143.0 -> 145.9; the lists' hot-bucket atomics cost Ant 65,536 22 %);
   //   off: MA-Ant (8,192 -1.1 %, 65,536 -1.0 % sorted), Cartpole and the smaller batches (Ant 16,384 -1.1 %,
   //     ShadowHand 4,096 -2 %: the sort's launches or the lists' atomics outweigh the tail they save).
-  // MIGYM_ORDER = off | lists | sort overrides.
+  // MIGYM_ORDER = off | lists | sort | sort:K (sort every K-th launch only; A/B: the order goes stale within two
+  // steps) overrides.
   {
     const int T = mgi::team_size(s->host_model, s->params.max_contacts);
     const int A = params->agents > 1 ? params->agents : 1;
@@ -600,9 +603,12 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
     if (!strcmp(e, "off")) s->order_mode = kOrderOff;
     else if (!strcmp(e, "lists")) s->order_mode = kOrderLists;
     else if (!strcmp(e, "sort")) s->order_mode = kOrderSort;
-    else {
+    else if (!strncmp(e, "sort:", 5) && atoi(e + 5) > 0) {
+      s->order_mode = kOrderSort;
+      s->sort_every = atoi(e + 5);
+    } else {
       mg_sim_destroy(s);
-      return fail(MG_EINVAL, "mg_sim_create: MIGYM_ORDER must be off, lists or sort");
+      return fail(MG_EINVAL, "mg_sim_create: MIGYM_ORDER must be off, lists, sort or sort:K (K > 0)");
     }
   }
   if (s->order_mode != kOrderOff) {
@@ -1029,8 +1035,9 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   if (sim->order_mode != kOrderOff && !rp) {
     const int A = tp->num_agents > 1 ? tp->num_agents : 1;
     if (sim->bq_cap != (sim->n + A - 1) / A) return fail(MG_EINVAL, "mg_env_step: num_agents differs from mg_sim_params.agents");
-    if (sim->order_mode == kOrderSort && sim->order_valid) {  // the last launch's row counts -> this one's order
-      const int nu = sim->bq_cap, nb = (nu + 255) / 256, b = (int)(sim->order_steps & 1);
+    // the last launch's row counts -> this one's order (every sort_every-th ordered launch from the second on)
+    if (sim->order_mode == kOrderSort && sim->order_valid && (sim->order_steps - 1) % sim->sort_every == 0) {
+      const int nu = sim->bq_cap, nb = (nu + 255) / 256, b = (int)(sim->sorts++ & 1);
       unsigned* bbase = sim->d_osort + 512;
       unsigned short* rank = reinterpret_cast<unsigned short*>(sim->d_osort + 512 + 256 * (size_t)nb);
       hipLaunchKernelGGL(k_ohist, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu,
