@@ -48,6 +48,13 @@ struct mg_sim {
 constexpr int kOrderBuckets = 32;  // row-count classes of width kOrderWidth, descending (bucket 0: 62 rows and more)
 constexpr int kOrderWidth = 2;
 constexpr int kOrderOff = 0, kOrderLists = 1, kOrderSort = 2;
+#ifndef MG_SORT_REP
+#define MG_SORT_REP 8
+#endif
+// sort: copies of the bin totals (block b adds into copy b % kSortRep): the hot bins' device-scope atomics spread
+// over 8 words each (k_ohist 6.4 -> 4.8 us at 65,536 envs under the profiler; Ant 65,536 +0.3 %)
+constexpr int kSortRep = MG_SORT_REP;
+constexpr int kSortTot = 2 * kSortRep * 256;  // sort: both alternating sets of totals
 struct MgOrder {
   const int* order;     // sort: this launch's permutation (nullptr: none yet)
   unsigned char* cost;  // sort: the row counts this launch writes

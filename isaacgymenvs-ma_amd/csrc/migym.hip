@@ -619,8 +619,8 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
         ? hipMalloc(&s->d_bq, sizeof(unsigned) * (2 * kOrderBuckets + 1)) == hipSuccess &&
               hipMemset(s->d_bq, 0, sizeof(unsigned) * (2 * kOrderBuckets + 1)) == hipSuccess &&
               hipMalloc(&s->d_blist, sizeof(int) * 2 * (size_t)kOrderBuckets * nu) == hipSuccess
-        : hipMalloc(&s->d_osort, sizeof(unsigned) * (512 + 256 * nb) + sizeof(unsigned short) * (nu + 2)) == hipSuccess &&
-              hipMemset(s->d_osort, 0, sizeof(unsigned) * 512) == hipSuccess &&
+        : hipMalloc(&s->d_osort, sizeof(unsigned) * (kSortTot + 256 * nb) + sizeof(unsigned short) * (nu + 2)) == hipSuccess &&
+              hipMemset(s->d_osort, 0, sizeof(unsigned) * kSortTot) == hipSuccess &&
               hipMalloc(&s->d_order, sizeof(int) * nu) == hipSuccess &&
               hipMalloc(&s->d_cost, nu) == hipSuccess && hipMemset(s->d_cost, 0, nu) == hipSuccess;
     if (!ok) {
@@ -955,7 +955,8 @@ __global__ __launch_bounds__(256) void k_ohist(const unsigned char* __restrict__
                                                unsigned* __restrict__ bbase, unsigned short* __restrict__ rank) {
   __shared__ unsigned h[256];
   h[threadIdx.x] = 0u;
-  if (blockIdx.x == 0) tot_clear[threadIdx.x] = 0u;
+  if (blockIdx.x == 0)
+    for (int k = 0; k < kSortRep; k++) tot_clear[256 * k + threadIdx.x] = 0u;
   __syncthreads();
   const int u = (int)blockIdx.x * 256 + (int)threadIdx.x;
   const int lane = (int)(threadIdx.x & 63);
@@ -974,7 +975,7 @@ __global__ __launch_bounds__(256) void k_ohist(const unsigned char* __restrict__
   }
   __syncthreads();
   const unsigned c = h[threadIdx.x];
-  bbase[(size_t)blockIdx.x * 256 + threadIdx.x] = c ? atomicAdd(&tot[threadIdx.x], c) : 0u;
+  bbase[(size_t)blockIdx.x * 256 + threadIdx.x] = c ? atomicAdd(&tot[256 * (blockIdx.x % kSortRep) + threadIdx.x], c) : 0u;
   if (u < nu) rank[u] = (unsigned short)r;
 }
 __global__ __launch_bounds__(256) void k_oscatter(const unsigned char* __restrict__ cost, int nu,
@@ -982,7 +983,15 @@ __global__ __launch_bounds__(256) void k_oscatter(const unsigned char* __restric
                                                   const unsigned short* __restrict__ rank, int* __restrict__ order) {
   __shared__ unsigned wsum[4], start[256];
   const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
-  const unsigned v = tot[threadIdx.x];
+  // the bin's total over the copies, and this block's copy's offset inside the bin (the copies before it)
+  const int rep = (int)(blockIdx.x % kSortRep);
+  unsigned v = 0u, roff = 0u;
+#pragma unroll
+  for (int k = 0; k < kSortRep; k++) {
+    const unsigned x = tot[256 * k + threadIdx.x];
+    roff += k < rep ? x : 0u;
+    v += x;
+  }
   unsigned inc = v;
   for (int d = 1; d < 64; d <<= 1) {
     const unsigned y = (unsigned)__shfl_up((int)inc, d);
@@ -992,7 +1001,7 @@ __global__ __launch_bounds__(256) void k_oscatter(const unsigned char* __restric
   __syncthreads();
   unsigned off = 0u;
   for (int w = 0; w < wv; w++) off += wsum[w];
-  start[threadIdx.x] = off + inc - v;
+  start[threadIdx.x] = off + inc - v + roff;
   __syncthreads();
   const int u = (int)blockIdx.x * 256 + (int)threadIdx.x;
   if (u < nu) {
@@ -1038,12 +1047,13 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
     // the last launch's row counts -> this one's order (every sort_every-th ordered launch from the second on)
     if (sim->order_mode == kOrderSort && sim->order_valid && (sim->order_steps - 1) % sim->sort_every == 0) {
       const int nu = sim->bq_cap, nb = (nu + 255) / 256, b = (int)(sim->sorts++ & 1);
-      unsigned* bbase = sim->d_osort + 512;
-      unsigned short* rank = reinterpret_cast<unsigned short*>(sim->d_osort + 512 + 256 * (size_t)nb);
-      hipLaunchKernelGGL(k_ohist, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu,
-                         sim->d_osort + 256 * b, sim->d_osort + 256 * (b ^ 1), bbase, rank);
-      hipLaunchKernelGGL(k_oscatter, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu,
-                         sim->d_osort + 256 * b, bbase, rank, sim->d_order);
+      unsigned* bbase = sim->d_osort + kSortTot;
+      unsigned short* rank = reinterpret_cast<unsigned short*>(sim->d_osort + kSortTot + 256 * (size_t)nb);
+      unsigned* tot = sim->d_osort + (kSortTot / 2) * b;
+      hipLaunchKernelGGL(k_ohist, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu, tot,
+                         sim->d_osort + (kSortTot / 2) * (b ^ 1), bbase, rank);
+      hipLaunchKernelGGL(k_oscatter, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu, tot, bbase, rank,
+                         sim->d_order);
     }
   }
   int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
