@@ -583,20 +583,17 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   s->d_osort = nullptr;
   s->d_span = nullptr;
   s->span_cap = s->span_next = s->span_stride = 0;
-  // default (same box, M env-steps/s unordered -> ordered):
-  //   ShadowHand from 16,384 envs: the lists (16,384 19.1 -> 20.3; the sort 20.15: its two launches cost more than
-  //     the in-kernel lists);
-  //   Humanoid from 16,384 and Ant from 32,768 one-agent envs: the sort (Humanoid 32,768 33.8 -> 37.3, lists 37.0;
-  //     Ant 65,536 153.0 -> 156.0, 32,768 143.0 -> 145.9; the lists' hot-bucket atomics cost Ant 65,536 22 %);
-  //   off: MA-Ant (8,192 -1.1 %, 65,536 -1.0 % sorted), Cartpole and the smaller batches (Ant 16,384 -1.1 %,
-  //     ShadowHand 4,096 -2 %: the sort's launches or the lists' atomics outweigh the tail they save).
+  // default (same box, M env-steps/s unordered -> ordered): the sort for ShadowHand and Humanoid from
+  // 16,384 envs and for Ant from 32,768 one-agent envs (ShadowHand 16,384 18.9 -> 20.1, in-kernel lists 20.0;
+  // Humanoid 32,768 33.9 -> 37.3, lists 37.0; Ant 65,536 152.7 -> 157.8, lists 119.4: their hot-bucket atomics);
+  // off for MA-Ant (8,192 -0.8 %, 65,536 -1.0 % sorted), Cartpole and the smaller batches (Ant 16,384 within
+  // noise, ShadowHand 4,096 -2 %: the sort's two launches outweigh the tail they save).
   // MIGYM_ORDER = off | lists | sort | sort:K (sort every K-th launch only; A/B: the order goes stale within two
   // steps) overrides.
   {
     const int T = mgi::team_size(s->host_model, s->params.max_contacts);
     const int A = params->agents > 1 ? params->agents : 1;
-    if (s->host_model.obj_type) s->order_mode = num_envs >= 16384 ? kOrderLists : kOrderOff;
-    else if (T >= 32) s->order_mode = num_envs >= 16384 ? kOrderSort : kOrderOff;
+    if (T >= 32) s->order_mode = num_envs >= 16384 ? kOrderSort : kOrderOff;
     else if (T == 16 && A == 1) s->order_mode = num_envs >= 32768 ? kOrderSort : kOrderOff;
   }
   if (const char* e = getenv("MIGYM_ORDER")) {
@@ -1006,7 +1003,8 @@ __global__ __launch_bounds__(256) void k_oscatter(const unsigned char* __restric
   const int u = (int)blockIdx.x * 256 + (int)threadIdx.x;
   if (u < nu) {
     const int key = 255 - (int)cost[u];
-    order[start[key] + bbase[(size_t)blockIdx.x * 256 + key] + rank[u]] = u;
+    const unsigned pos = start[key] + bbase[(size_t)blockIdx.x * 256 + key] + rank[u];
+    if (pos < (unsigned)nu) order[pos] = u;  // always, unless the totals were not cleared
   }
 }
 

@@ -223,7 +223,7 @@ __device__ __forceinline__ int order_bucket(int rows) {
 __device__ __forceinline__ void order_append(const MgOrder& ord, int rows, int u) {
   const int b = order_bucket(rows);
   const unsigned k = atomicAdd(&ord.wcnt[b], 1u);
-  ord.wlist[(size_t)b * ord.cap + k] = u;
+  if (k < (unsigned)ord.cap) ord.wlist[(size_t)b * ord.cap + k] = u;  // always, unless the counts were not cleared
 }
 // every wave of an ordered launch checks out; the last one clears the counts the launch read (every wave has read
 // them: it started before the last one finished) and the counter, for the launch after next

@@ -240,6 +240,7 @@ def _work_order(env, cap):
 
 @pytest.mark.parametrize("task,n,env_cfg,mode", [("Ant", 65536, {}, None),          # the headline size: sorted by default
                                                  ("Humanoid", 32768, {}, None),     # configs[2]: sorted by default
+                                                 ("ShadowHand", 16384, {"objectType": "block"}, None),  # sorted too
                                                  ("Ant", 4099, {}, "sort"),         # 17 ragged sort blocks
                                                  ("MAAnt", 8192, {"numAgents": 4}, "sort")])  # env units of 4 agents
 def test_sort_order_is_a_descending_permutation(task, n, env_cfg, mode):
