@@ -21,6 +21,10 @@
 #ifndef MG_LDS_PAD
 #define MG_LDS_PAD 0
 #endif
+// the locomotion observation head on four team lanes (mg::obs_head_team) instead of the leader (0: mg::obs_head)
+#ifndef MG_TEAM_OBS_HEAD
+#define MG_TEAM_OBS_HEAD 1
+#endif
 
 namespace mgi {
 #ifdef MG_PHASE_TIMING
@@ -338,7 +342,11 @@ __device__ __forceinline__ void env_step_item(
   if (tp.task_id == MG_TASK_CARTPOLE) {
     if (t.tl < 4) ost[t.tl] = L.u.sv.st.dof[t.tl];
   } else {
+#if MG_TEAM_OBS_HEAD
+    mg::obs_head_team(&tp, off, L.u.sv.st.root, t.tl, t.tb, &pot, &prev, up, hd, ost);  // lanes 0..3, T >= 16
+#else
     if (t.tl == 0) mg::obs_head(&tp, off, L.u.sv.st.root, &pot, &prev, up, hd, ost);
+#endif
     const bool hum = tp.task_id == MG_TASK_HUMANOID;
     for (int q = t.tl; q < nd; q += T) {
       ost[12 + q] = mg::t_unscale(L.u.sv.st.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);

@@ -248,6 +248,75 @@ __device__ __forceinline__ void obs_head(const mg_task_params* tp, const float* 
   o[k++] = f.heading_proj;
 }
 
+// obs_head on a team's first four lanes instead of its leader alone: the same operations on the same operands
+// (FMA contraction is off here, so every value is bit-identical to obs_head's), with the per-env serial chain of
+// four vector rotations, three atan2 and (Humanoid) three angle normalisations issued once per wave instead of
+// one after another.  Lane k of the team: k = 0 rotates e_z (up_vec) and takes the roll, k = 1 rotates e_x
+// (heading_vec) and takes the yaw, k = 2 rotates the velocity into the torso frame and takes the walk-target angle
+// (then angle_to_target = target angle - yaw), k = 3 rotates the angular velocity; the leader gathers the results
+// by shuffles and writes the 12 head entries.  All lanes of the team call it (T >= 4); pot / prev / up / heading
+// are valid on the leader.  (compute_heading_and_up / compute_rot, torch_jit_utils.py:247-276; the head of
+// compute_{ant,humanoid}_observations, ant.py:398-404, humanoid.py:400-409)
+__device__ __forceinline__ void obs_head_team(const mg_task_params* tp, const float* off, const float* root, int tl,
+                                              int tb, float* pot, float* prev_pot, float* up, float* heading, float* o) {
+  const float* pos = root;
+  const float tg0 = tp->target[0] + off[0], tg1 = tp->target[1] + off[1], tg2 = tp->target[2] + off[2];
+  float tt0 = tg0 - pos[0], tt1 = tg1 - pos[1], tt2 = 0.0f;
+  float nrm = sqrtf(tt0 * tt0 + tt1 * tt1 + tt2 * tt2);
+  const float potential = -nrm / tp->dt;
+  float inv[4] = {-tp->start_rot[0], -tp->start_rot[1], -tp->start_rot[2], tp->start_rot[3]};
+  float tq[4];
+  t_quat_mul(root + 3, inv, tq);
+  const int k = tl < 4 ? tl : 3;
+  // the lane's rotation: e_z, e_x (forward), the linear / angular velocity (inverse)
+  float vin[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float e = (k == 0 && i == 2) || (k == 1 && i == 0) ? 1.0f : 0.0f;
+    vin[i] = k < 2 ? e : root[(k == 2 ? 7 : 10) + i];
+  }
+  float r3[3];
+  t_quat_rotate(tq, vin, r3, k >= 2);
+  // the lane's angle: roll, yaw (get_euler_xyz, floor-mod 2 pi), the walk-target angle atan2(dz, dx)
+  const float qx = tq[0], qy = tq[1], qz = tq[2], qw = tq[3];
+  const float sinr = 2.0f * (qw * qx + qy * qz);
+  const float cosr = qw * qw - qx * qx - qy * qy + qz * qz;
+  const float siny = 2.0f * (qw * qz + qx * qy);
+  const float cosy = qw * qw + qx * qx - qy * qy - qz * qz;
+  const float ay = k == 0 ? sinr : (k == 1 ? siny : tg2 - pos[2]);
+  const float ax = k == 0 ? cosr : (k == 1 ? cosy : tg0 - pos[0]);
+  float ang = atan2f(ay, ax);
+  if (k < 2) ang = t_mod2pi(ang);
+  const float yaw = __shfl(ang, tb + 1);
+  if (k == 2) ang = ang - yaw;  // angle_to_target
+  const bool hum = tp->task_id != MG_TASK_ANT;
+  if (hum) ang = t_normalize_angle(ang);
+  const float hv0 = __shfl(r3[0], tb + 1), hv1 = __shfl(r3[1], tb + 1), hv2 = __shfl(r3[2], tb + 1);
+  const float vl0 = __shfl(r3[0], tb + 2), vl1 = __shfl(r3[1], tb + 2), vl2 = __shfl(r3[2], tb + 2);
+  const float av0 = __shfl(r3[0], tb + 3), av1 = __shfl(r3[1], tb + 3), av2 = __shfl(r3[2], tb + 3);
+  const float a1 = __shfl(ang, tb + 1), a2 = __shfl(ang, tb + 2);
+  *prev_pot = *pot;
+  *pot = potential;
+  if (tl != 0) return;
+  float nc = nrm < 1e-9f ? 1e-9f : nrm;
+  float dirs[3] = {tt0 / nc, tt1 / nc, tt2 / nc};
+  for (int i = 0; i < 3; i++) up[i] = r3[i];
+  heading[0] = hv0; heading[1] = hv1; heading[2] = hv2;
+  o[0] = root[2];
+  o[1] = vl0; o[2] = vl1; o[3] = vl2;
+  const float avs = hum ? tp->angular_velocity_scale : 1.0f;
+  if (hum) {
+    o[4] = av0 * avs; o[5] = av1 * avs; o[6] = av2 * avs;
+  } else {
+    o[4] = av0; o[5] = av1; o[6] = av2;
+  }
+  o[7] = a1;   // yaw
+  o[8] = ang;  // roll (the leader's own angle)
+  o[9] = a2;   // angle_to_target
+  o[10] = r3[2];
+  o[11] = hv0 * dirs[0] + hv1 * dirs[1] + hv2 * dirs[2];
+}
+
 // reward given the team sums of the per-action terms (compute_{ant,humanoid}_reward, ant.py:325-371,
 // humanoid.py:323-375); ac = sum a^2, el = energy term, lim = joints-at-limit term
 __device__ __forceinline__ void reward_from_sums(const mg_task_params* tp, const float* o, float ac, float el,
