@@ -187,11 +187,15 @@ __device__ __forceinline__ bool chol6(const Sym6& I, float* L) {
       M[i][j] = t * inv;
     }
   }
+  // packed lower triangle, the diagonal stored as its reciprocal: chol6_solve multiplies by it instead of
+  // recomputing a reciprocal per step on its dependent chain, and the compiler folds rcp(sqrt(x)) into one
+  // v_rsq_f32 (1 ulp, like the pair it replaces; results move by that rounding only).  Same box, with the team
+  // observation head and load()'s shuffle-free root: Ant +0.8 %, Humanoid +1.3 % (profiles/r05/ab_micro_*.txt)
   int k = 0;
 #pragma unroll
   for (int i = 0; i < 6; i++)
 #pragma unroll
-    for (int j = 0; j <= i; j++) L[k++] = M[i][j];
+    for (int j = 0; j <= i; j++) L[k++] = i == j ? prcp(M[i][i]) : M[i][j];
   return ok;
 }
 __device__ __forceinline__ SV chol6_solve(const float* L, const SV& b) {
@@ -202,7 +206,7 @@ __device__ __forceinline__ SV chol6_solve(const float* L, const SV& b) {
     float s = x[i];
 #pragma unroll
     for (int k = 0; k < i; k++) s -= L[i * (i + 1) / 2 + k] * x[k];
-    x[i] = s * prcp(L[i * (i + 1) / 2 + i]);
+    x[i] = s * L[i * (i + 1) / 2 + i];
   }
   // backward: L^T x = y
 #pragma unroll
@@ -210,7 +214,7 @@ __device__ __forceinline__ SV chol6_solve(const float* L, const SV& b) {
     float s = x[i];
 #pragma unroll
     for (int k = i + 1; k < 6; k++) s -= L[k * (k + 1) / 2 + i] * x[k];
-    x[i] = s * prcp(L[i * (i + 1) / 2 + i]);
+    x[i] = s * L[i * (i + 1) / 2 + i];
   }
   return sv(v3(x[0], x[1], x[2]), v3(x[3], x[4], x[5]));
 }

@@ -2810,14 +2810,13 @@ struct Team {
   // ---------------------------------------------------------------- state I/O (gym layouts)
   __device__ __forceinline__ void load(const float* root, const float* dof, const float* act_tau, const float* orow = nullptr,
                        const float* tg = nullptr) {
-    // root pose/twist: every lane reads the 13 floats (one cache line pair per actor)
-    if (tl == 0) {
+    // root pose/twist: every lane reads the 13 floats (one cache line pair per actor) and normalises the
+    // quaternion itself (the same operations on every lane: no shuffles from the leader)
+    {
       p0 = ld3(root);
       float n = sqrtf(root[3] * root[3] + root[4] * root[4] + root[5] * root[5] + root[6] * root[6]);
       for (int k = 0; k < 4; k++) q0[k] = root[3 + k] / n;
     }
-    q0[0] = __shfl(q0[0], tb); q0[1] = __shfl(q0[1], tb); q0[2] = __shfl(q0[2], tb); q0[3] = __shfl(q0[3], tb);
-    p0.x = __shfl(p0.x, tb); p0.y = __shfl(p0.y, tb); p0.z = __shfl(p0.z, tb);
     if (freeb && tl < 6) {
       M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
       V3 cw = mul(Rr, ld3(m->body_com[0]));
