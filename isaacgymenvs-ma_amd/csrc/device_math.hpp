@@ -150,6 +150,23 @@ __device__ __forceinline__ Sym6 body_inertia(float m, V3 c, const float* Ic) {
 __device__ __forceinline__ float prcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float psqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float prsq(float x) { return __builtin_amdgcn_rsqf(x); }
+// sine and cosine of the physics' angles (joint angles in FK, the root's / object's half rotation per substep; five
+// pairs per lane and step).  HW: the hardware v_sin_f32 / v_cos_f32 on the argument in revolutions reduced to
+// [-1/2, 1/2] (a few instructions instead of the library's ~60; absolute error tools/trig_probe.hip), used by the
+// 16-lane instances (Ant, MA-Ant: +2 % same box); otherwise the library's sinf / cosf (the Humanoid's fast-spin parity
+// case rejects the hardware pair).  The task layer keeps the library's everywhere.
+template <bool HW>
+__device__ __forceinline__ void psincos(float x, float* s, float* c) {
+  if constexpr (HW) {
+    float r = x * 0.159154943091895336f;
+    r = r - __builtin_rintf(r);
+    *s = __builtin_amdgcn_sinf(r);
+    *c = __builtin_amdgcn_cosf(r);
+  } else {
+    *s = sinf(x);
+    *c = cosf(x);
+  }
+}
 // tanh of the joint friction law: (1 - e) / (1 + e), e = exp(-2|x|) by the hardware exp2 (~7 instructions instead of
 // the library's ~50; a few ulp, against a friction torque the oracle checks to 1e-6 relative)
 __device__ __forceinline__ float ptanh(float x) {

@@ -703,6 +703,11 @@ struct Team {
   using L = TeamLDS<T, MN, MC, OBJ>;
   using MT = ModelTile<MN, MG, MP, tile_hull_verts(OBJ)>;
   static constexpr int MR = L::MR;
+#ifndef MG_HW_TRIG_T16
+#define MG_HW_TRIG_T16 1
+#endif
+  // the hardware sine / cosine for the 16-lane teams (Ant, MA-Ant), the library's elsewhere (device_math.hpp psincos)
+  static constexpr bool kHwTrig = MG_HW_TRIG_T16 && T == 16 && OBJ == 0;
   L* s;
   const MT* mt;
   const mg_model* m;
@@ -858,8 +863,7 @@ struct Team {
       qv[2 * node] = qj;
       qv[2 * node + 1] = nu;
       if (mt->jtype[node] == MG_JT_HINGE) {
-        sn = sinf(qj);
-        cs = cosf(qj);
+        psincos<kHwTrig>(qj, &sn, &cs);
       }
       sc[2 * node] = sn;
       sc[2 * node + 1] = cs;
@@ -2601,8 +2605,10 @@ struct Team {
       float wn = sqrtf(dot(om, om));
       float dq[4];
       if (wn * h > 1e-12f) {
-        float ha = 0.5f * wn * h, sn = sinf(ha) * prcp(wn);
-        dq[0] = om.x * sn; dq[1] = om.y * sn; dq[2] = om.z * sn; dq[3] = cosf(ha);
+        float sh, ch;
+        psincos<kHwTrig>(0.5f * wn * h, &sh, &ch);
+        const float sn = sh * prcp(wn);
+        dq[0] = om.x * sn; dq[1] = om.y * sn; dq[2] = om.z * sn; dq[3] = ch;
       } else {
         dq[0] = 0.5f * h * om.x; dq[1] = 0.5f * h * om.y; dq[2] = 0.5f * h * om.z; dq[3] = 1.0f;
       }
