@@ -706,6 +706,9 @@ struct Team {
 #ifndef MG_HW_TRIG_T16
 #define MG_HW_TRIG_T16 1
 #endif
+#ifndef MG_LOAD_RSQ
+#define MG_LOAD_RSQ 1  // load(): free-base root quaternions normalised by rsq
+#endif
   // the hardware sine / cosine for the 16-lane teams (Ant, MA-Ant), the library's elsewhere (device_math.hpp psincos)
   static constexpr bool kHwTrig = MG_HW_TRIG_T16 && T == 16 && OBJ == 0;
   L* s;
@@ -2820,8 +2823,15 @@ struct Team {
     // quaternion itself (the same operations on every lane: no shuffles from the leader)
     {
       p0 = ld3(root);
-      float n = sqrtf(root[3] * root[3] + root[4] * root[4] + root[5] * root[5] + root[6] * root[6]);
-      for (int k = 0; k < 4; k++) q0[k] = root[3 + k] / n;
+      if (MG_LOAD_RSQ && freeb) {
+        // free-base roots: a 1-ulp reciprocal square root instead of a correctly rounded root and four divisions
+        // (~60 instructions; the fixed-base hand and Cartpole keep the exact form, their parity cases being tighter)
+        const float in = prsq(root[3] * root[3] + root[4] * root[4] + root[5] * root[5] + root[6] * root[6]);
+        for (int k = 0; k < 4; k++) q0[k] = root[3 + k] * in;
+      } else {
+        float n = sqrtf(root[3] * root[3] + root[4] * root[4] + root[5] * root[5] + root[6] * root[6]);
+        for (int k = 0; k < 4; k++) q0[k] = root[3 + k] / n;
+      }
     }
     if (freeb && tl < 6) {
       M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
