@@ -706,6 +706,9 @@ struct Team {
 #ifndef MG_HW_TRIG_T16
 #define MG_HW_TRIG_T16 1
 #endif
+#ifndef MG_SENSOR_MASKS
+#define MG_SENSOR_MASKS 1  // outputs(): per-sensor contact masks by ballots instead of every sensor scanning every contact
+#endif
 #ifndef MG_LOAD_RSQ
 #define MG_LOAD_RSQ 1  // load(): free-base root quaternions normalised by rsq
 #endif
@@ -2769,7 +2772,29 @@ struct Team {
     const int NS = m->num_sensors;
     if constexpr (T >= 32 && !OBJ) {
       if (sens_out && NS > 0) sensors_by_team_sums(sens_out, NS);
-    } else if (sens_out && tl < NS) {
+    } else if (sens_out && NS > 0) {
+#if MG_SENSOR_MASKS
+      // which sensors' bodies each contact touches, one lane per contact (chunks of T lanes), as per-sensor bit masks
+      // by ballots: sensor lane j then visits only its own contacts (a foot has one or two) instead of scanning all
+      // of them with two dependent LDS lookups each; same contacts, same increasing order, so the same sums bit for bit
+      unsigned long long own = 0ull;
+      const int nc = s->ncon;
+      for (int c0 = 0; c0 < nc; c0 += T) {
+        const int c = c0 + tl;
+        int bA = -1, bB = -1;
+        if (c < nc) {
+          const int gA = cside(c, 2), gB = cside(c, 3);
+          bA = gA >= 0 ? mt->gbody[gA] : -1;
+          bB = gB >= 0 ? mt->gbody[gB] : -1;
+        }
+        for (int j = 0; j < NS; j++) {
+          const int sb = m->sensor_body[j];
+          const unsigned long long bits = (__ballot(bA == sb || bB == sb) >> tb) & team_bits<T>();
+          if (tl == j) own |= bits << c0;
+        }
+      }
+#endif
+      if (tl < NS) {
       const int body = m->sensor_body[tl], nd = m->body_node[body];
       M3 Rn;
       for (int a = 0; a < 3; a++)
@@ -2778,11 +2803,17 @@ struct Team {
                                   m->body_quat[body][3]));
       V3 xb = ld3(s->x[nd]) + mul(Rn, ld3(m->body_pos[body]));
       V3 F = v3(0, 0, 0), Tq = v3(0, 0, 0);
+#if MG_SENSOR_MASKS
+      for (unsigned long long mm = own; mm; mm &= mm - 1ull) {
+        const int c = __builtin_ctzll(mm);
+        const float sg = (cside(c, 2) >= 0 && mt->gbody[cside(c, 2)] == body) ? 1.0f : -1.0f;
+#else
       for (int c = 0; c < s->ncon; c++) {
         float sg = 0.0f;
         if (cside(c, 2) >= 0 && mt->gbody[cside(c, 2)] == body) sg = 1.0f;
         else if (cside(c, 3) >= 0 && mt->gbody[cside(c, 3)] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
+#endif
         const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
         V3 f = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) * (sg * ih);
         F = F + f;
@@ -2791,6 +2822,7 @@ struct Team {
       V3 Fl = mulT(Rb, F), Tl = mulT(Rb, Tq);
       float* o = sens_out + 6 * tl;
       o[0] = Fl.x; o[1] = Fl.y; o[2] = Fl.z; o[3] = Tl.x; o[4] = Tl.y; o[5] = Tl.z;
+      }
     }
     if (dforce_out && node > 0) {
       const float* np = nprop(node);
