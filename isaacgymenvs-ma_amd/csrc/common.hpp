@@ -27,6 +27,7 @@ struct mg_sim {
   //   sort (kOrderSort): the previous launch wrote each env's row count, and a two-pass counting sort
   //     (k_ohist, k_oscatter) before the launch turns them into the permutation it reads.
   int order_mode;      // kOrderOff / kOrderLists / kOrderSort
+  int lds_pad;         // dynamic LDS added to every step-kernel launch (MIGYM_LDS_PAD; occupancy experiments, 0)
   long long order_steps;  // ordered launches so far (the parity of the set the lists' launches write)
   int sort_every;      // sort: every K-th ordered launch sorts (the launches between keep the last permutation)
   long long sorts;     // sort: sorts so far (the parity of the sort's totals)

@@ -8,8 +8,12 @@
 // contacts MC, geoms MG, self pairs MP, OBJ = the free object's type in hand-task envs (0: none; one
 // instance per object shape, so the block's kernel carries no egg / pen code).  The smallest
 // instance that fits the model is launched.
+// (occupancy experiments only: the 16-lane locomotion instance's contact capacity)
+#ifndef MG_ANT_MC
+#define MG_ANT_MC 16
+#endif
 #define MG_INSTANCES(X)                                                                                     \
-  X(8, 4, 8, 4, 0, 0) X(16, 9, 16, 16, 0, 0) X(16, 16, 24, 24, 32, 0) X(32, 24, 32, 24, 160, 0)            \
+  X(8, 4, 8, 4, 0, 0) X(16, 9, MG_ANT_MC, 16, 0, 0) X(16, 16, 24, 24, 32, 0) X(32, 24, 32, 24, 160, 0)            \
   X(32, 32, 48, 48, 192, 0) X(64, 40, 48, 48, 192, 0) X(32, 25, 24, 24, 24, MG_GT_BOX)                      \
   X(32, 25, 24, 24, 24, MG_GT_CAPSULE) X(32, 25, 24, 24, 24, MG_GT_ELLIPSOID)
 #define MG_NUM_INST 9

@@ -533,6 +533,10 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
       return fail(MG_EINVAL, "mg_sim_create: nodes must be topologically ordered (parent < child)");
   if (params->substeps < 1 || params->dt <= 0.0f || params->max_contacts < 0)
     return fail(MG_EINVAL, "mg_sim_create: bad sim params");
+#ifdef MG_EXP_CLAMP_CONTACTS  // occupancy experiments only: the contact capacity clamped (never a shipped build)
+  const_cast<mg_sim_params*>(params)->max_contacts =
+      params->max_contacts < MG_EXP_CLAMP_CONTACTS ? params->max_contacts : MG_EXP_CLAMP_CONTACTS;
+#endif
   if ((params->solver_type != MG_SOLVER_PGS && params->solver_type != MG_SOLVER_TGS) || params->vel_iters < 0)
     return fail(MG_EINVAL, "mg_sim_create: solver_type must be MG_SOLVER_PGS or MG_SOLVER_TGS, vel_iters >= 0");
   // the exact hull-object candidates are computed before the tree phases (team_physics.hpp hull_stage), from
@@ -596,6 +600,8 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
     if (T >= 32) s->order_mode = num_envs >= 16384 ? kOrderSort : kOrderOff;
     else if (T == 16 && A == 1) s->order_mode = num_envs >= 32768 ? kOrderSort : kOrderOff;
   }
+  s->lds_pad = 0;
+  if (const char* e = getenv("MIGYM_LDS_PAD")) s->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
   if (const char* e = getenv("MIGYM_ORDER")) {
     if (!strcmp(e, "off")) s->order_mode = kOrderOff;
     else if (!strcmp(e, "lists")) s->order_mode = kOrderLists;

@@ -17,7 +17,20 @@
 #ifndef MG_WAVES_PER_EU
 #define MG_WAVES_PER_EU 2
 #endif
+// ... and for the instances with the compact team layout (mg::TeamLDSC: Ant, MA-Ant), whose LDS holds 12 waves per CU
+#ifndef MG_WAVES_COMPACT
+#define MG_WAVES_COMPACT 3
+#endif
 // dynamic LDS added to every step-kernel launch (0; an occupancy A/B variant pads it to hold fewer waves per CU)
+// an explicit VGPR budget for k_env_step (0: the waves_per_eu budget); register-pressure experiments only
+#ifndef MG_NUM_VGPR
+#define MG_NUM_VGPR 0
+#endif
+#if MG_NUM_VGPR
+#define MG_VGPR_ATTR __attribute__((amdgpu_num_vgpr(MG_NUM_VGPR)))
+#else
+#define MG_VGPR_ATTR
+#endif
 #ifndef MG_LDS_PAD
 #define MG_LDS_PAD 0
 #endif
@@ -51,17 +64,21 @@ static __device__ unsigned long long* g_phase_buf;
 // Waves per block W.  A block's W waves share one LDS model tile (each team's own LDS is per wave), so a
 // larger W leaves more of the CU's 160 KB LDS for resident waves; a smaller W lets the CU refill sooner
 // when a wave finishes (a block's slots free only when its slowest wave is done).  W is the smallest
-// of 1, 2, 4, 8 that reaches the most resident waves per CU (at most 8: the 256-register budget).
+// of 1, 2, 4, 8 that reaches the most resident waves per CU (at most 4 x the instance's waves per SIMD: 8 at the
+// 256-register budget, 12 at 168).
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
 struct Shape {
+  using TL = mg::TeamLDSOf<T, MN, MC, OBJ>;
   static constexpr int E1 = 64 / T;  // teams (actors) per wave
+  // waves per SIMD of the instance (the register budget: 2 -> 256 VGPRs, 3 -> 168) and per CU
+  static constexpr int kWPE = (TL::kCompact && !DR) ? MG_WAVES_COMPACT : MG_WAVES_PER_EU;
+  static constexpr int kMaxWaves = 4 * kWPE;
   static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OBJ)>);
-  static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T>) +
-                                        (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
+  static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<TL, T>) + (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
   static constexpr int per_cu(int w) {
     const size_t blk = (kTile + w * kWave + 511) / 512 * 512;
     const int b = (int)((160 * 1024) / blk);
-    return b * w < 8 ? b * w : 8;
+    return b * w < kMaxWaves ? b * w : kMaxWaves;
   }
   static constexpr int pick() {
     int best = 1;
@@ -73,6 +90,10 @@ struct Shape {
   static constexpr int kThreads = 64 * W;
   static constexpr int E = E1 * W;  // teams per block
   static_assert(per_cu(W) >= 1, "one block must fit the CU's LDS");
+  // one work item per wave on a static grid (no work queue): the one-wave blocks, and the compact instances'
+  // two-wave blocks (a block's waves hold envs of like cost under the sort, so little of its LDS waits on a slower
+  // partner, and the queue's loop costs registers at the 168-VGPR budget)
+  static constexpr bool kStatic = W == 1 || TL::kCompact;
 };
 
 // ------------------------------------------------------------------------------------------------ work queue
@@ -122,12 +143,12 @@ __device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR, bool TGS = false>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_simulate(
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, OBJ, DR>::kWPE))) void k_simulate(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_state_views v, int n) {
   using SH = Shape<T, MN, MC, MG, MP, OBJ, DR>;
   constexpr int E = SH::E, W = SH::W;
   constexpr int ROWS = OBJ ? 3 : 1;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OBJ>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OBJ>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::copy_tile(&tile, static_cast<const typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT*>(timg));
@@ -155,20 +176,20 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
   t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
          OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(lds[team].v.u.sv.st.sens, lds[team].v.u.sv.st.dforce);
+  t.outputs(lds[team].v.st().sens, lds[team].v.st().dforce);
   t.stage_state();
   mg::wsync();
   if (valid) {
-    mg::TeamLDS<T, MN, MC, OBJ>& L = lds[team].v;
+    auto& L = lds[team].v;
     if (!m->fixed_base)
-      for (int k = t.tl; k < 13; k += T) root[k] = L.u.sv.st.root[k];
+      for (int k = t.tl; k < 13; k += T) root[k] = L.st().root[k];
     if (OBJ)
       for (int k = t.tl; k < 13; k += T) root[13 + k] = L.oroot[k];
-    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.u.sv.st.dof[k];
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * a + k] = L.st().dof[k];
     if (v.sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.u.sv.st.sens[k];
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * a + k] = L.st().sens[k];
     if (v.dof_force)
-      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.u.sv.st.dforce[k];
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * a + k] = L.st().dforce[k];
     if (v.rigid_body_states) {
       const int nb = m->num_bodies, nbe = nb + (OBJ ? 2 : 0);
       float* rb = v.rigid_body_states + (size_t)13 * nbe * a;
@@ -241,7 +262,7 @@ __device__ __forceinline__ void order_done(const MgOrder& ord, int grid_waves) {
 // one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void env_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
@@ -252,7 +273,7 @@ __device__ __forceinline__ void env_step_item(
   const int a = ordered_actor(ord, slot, n, tp.num_agents);
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
-  mg::TeamLDS<T, MN, MC>& L = lds[team].v;
+  mg::TeamLDSOf<T, MN, MC, 0>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, 0, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
@@ -282,18 +303,18 @@ __device__ __forceinline__ void env_step_item(
   t.ph_mark(14);
   if constexpr (RP) {  // gym.simulate replaced by the injected post-simulate state
     const float* rr = rp.root_states ? rp.root_states : v.root_states;
-    for (int q = t.tl; q < 13; q += T) L.u.sv.st.root[q] = rr[(size_t)13 * ac + q];
-    for (int q = t.tl; q < 2 * nd; q += T) L.u.sv.st.dof[q] = rp.dof_state[(size_t)2 * nd * ac + q];
-    for (int q = t.tl; q < 6 * ns; q += T) L.u.sv.st.sens[q] = rp.sensors ? rp.sensors[(size_t)6 * ns * ac + q] : 0.0f;
-    for (int q = t.tl; q < nd; q += T) L.u.sv.st.dforce[q] = rp.dof_force ? rp.dof_force[(size_t)nd * ac + q] : 0.0f;
+    for (int q = t.tl; q < 13; q += T) L.st().root[q] = rr[(size_t)13 * ac + q];
+    for (int q = t.tl; q < 2 * nd; q += T) L.st().dof[q] = rp.dof_state[(size_t)2 * nd * ac + q];
+    for (int q = t.tl; q < 6 * ns; q += T) L.st().sens[q] = rp.sensors ? rp.sensors[(size_t)6 * ns * ac + q] : 0.0f;
+    for (int q = t.tl; q < nd; q += T) L.st().dforce[q] = rp.dof_force ? rp.dof_force[(size_t)nd * ac + q] : 0.0f;
   } else {
     // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
     const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
     for (int st = 0; st < nsub; st++) t.substep();
     // no rigid-body states here: pose-only FK; DOF forces only where something reads them (the bound view, or the
     // Humanoid's observation: the reference's Ant and Cartpole never acquire a DOF-force tensor)
-    t.template outputs<true>(L.u.sv.st.sens,
-                             (v.dof_force || tp.task_id == MG_TASK_HUMANOID) ? L.u.sv.st.dforce : nullptr);
+    t.template outputs<true>(L.st().sens,
+                             (v.dof_force || tp.task_id == MG_TASK_HUMANOID) ? L.st().dforce : nullptr);
     t.stage_state();
   }
   mg::wsync();
@@ -321,8 +342,8 @@ __device__ __forceinline__ void env_step_item(
   if (do_reset) {  // reset_idx: one lane per DOF draws its noise; the leader resets root and potentials
     const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr;
     for (int i = t.tl; i < nd; i += T)
-      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset * A + a), tb.step_counter, L.u.sv.st.dof);
-    if (t.tl == 0) mg::reset_root(&tp, off, L.u.sv.st.root, &pot, &prev);
+      mg::reset_dof(&tp, i, nd, nz, tb.seed, (uint64_t)(tb.env_offset * A + a), tb.step_counter, L.st().dof);
+    if (t.tl == 0) mg::reset_root(&tp, off, L.st().root, &pot, &prev);
     progress = 0;
     reset = 0;
   }
@@ -331,34 +352,34 @@ __device__ __forceinline__ void env_step_item(
   // of its env under MA layouts, so the AND filter resets the env in the next step), reward 0 and a zero
   // observation row: no NaN reaches the policy, and the next step's masked reset_idx restores it
   bool nf = false;
-  for (int q = t.tl; q < (m->fixed_base ? 7 : 13); q += T) nf = nf || !isfinite(L.u.sv.st.root[q]);
-  for (int q = t.tl; q < 2 * nd; q += T) nf = nf || !isfinite(L.u.sv.st.dof[q]);
+  for (int q = t.tl; q < (m->fixed_base ? 7 : 13); q += T) nf = nf || !isfinite(L.st().root[q]);
+  for (int q = t.tl; q < 2 * nd; q += T) nf = nf || !isfinite(L.st().dof[q]);
   const unsigned long long nfm = __ballot(nf);
   bool bad = false;
   for (int j = 0; j < A; j++) bad = bad || ((nfm >> ((wt - k + j) * T)) & mg::team_bits<T>()) != 0ull;
   // observations staged in the row storage (dead after outputs()), then stored coalesced
   const int no = tp.num_obs;
-  float* ost = &L.u.sv.rows[0].b;
+  float* ost = L.obs_stage();
   if (tp.task_id == MG_TASK_CARTPOLE) {
-    if (t.tl < 4) ost[t.tl] = L.u.sv.st.dof[t.tl];
+    if (t.tl < 4) ost[t.tl] = L.st().dof[t.tl];
   } else {
 #if MG_TEAM_OBS_HEAD
-    mg::obs_head_team(&tp, off, L.u.sv.st.root, t.tl, t.tb, &pot, &prev, up, hd, ost);  // lanes 0..3, T >= 16
+    mg::obs_head_team(&tp, off, L.st().root, t.tl, t.tb, &pot, &prev, up, hd, ost);  // lanes 0..3, T >= 16
 #else
-    if (t.tl == 0) mg::obs_head(&tp, off, L.u.sv.st.root, &pot, &prev, up, hd, ost);
+    if (t.tl == 0) mg::obs_head(&tp, off, L.st().root, &pot, &prev, up, hd, ost);
 #endif
     const bool hum = tp.task_id == MG_TASK_HUMANOID;
     for (int q = t.tl; q < nd; q += T) {
-      ost[12 + q] = mg::t_unscale(L.u.sv.st.dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
-      ost[12 + nd + q] = L.u.sv.st.dof[2 * q + 1] * tp.dof_vel_scale;
-      if (hum) ost[12 + 2 * nd + q] = L.u.sv.st.dforce[q] * tp.contact_force_scale;
+      ost[12 + q] = mg::t_unscale(L.st().dof[2 * q], tp.dof_lower[q], tp.dof_upper[q]);
+      ost[12 + nd + q] = L.st().dof[2 * q + 1] * tp.dof_vel_scale;
+      if (hum) ost[12 + 2 * nd + q] = L.st().dforce[q] * tp.contact_force_scale;
     }
     const int bs = 12 + (hum ? 3 : 2) * nd, nss = mg::t_sensors(&tp);
-    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.u.sv.st.sens[q] * tp.contact_force_scale;
+    for (int q = t.tl; q < 6 * nss; q += T) ost[bs + q] = L.st().sens[q] * tp.contact_force_scale;
     if (alane) ost[bs + 6 * nss + t.tl] = act_l;
   }
   if (A > 1) {  // others block, cyclic shift after self (franka_reach_MA.py:604-608)
-    const float px = L.u.sv.st.root[0], py = L.u.sv.st.root[1], pz = L.u.sv.st.root[2];
+    const float px = L.st().root[0], py = L.st().root[1], pz = L.st().root[2];
     const int base = no - 3 * (A - 1);
     {  // lane j - 1 of the team writes agent j's three entries (one shuffle per coordinate, per-lane sources)
       const int j = t.tl + 1 < A ? t.tl + 1 : 0;
@@ -431,12 +452,12 @@ __device__ __forceinline__ void env_step_item(
   mg::wsync();
   if (valid) {  // state write-back (gym layouts), team-cooperative
     if (!m->fixed_base || tp.task_id != MG_TASK_CARTPOLE)
-      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.u.sv.st.root[q];
-    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.u.sv.st.dof[q];
+      for (int q = t.tl; q < 13; q += T) v.root_states[(size_t)13 * a + q] = L.st().root[q];
+    for (int q = t.tl; q < 2 * nd; q += T) v.dof_state[(size_t)2 * nd * a + q] = L.st().dof[q];
     if (v.sensors)
-      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.u.sv.st.sens[q];
+      for (int q = t.tl; q < 6 * ns; q += T) v.sensors[(size_t)6 * ns * a + q] = L.st().sens[q];
     if (v.dof_force)
-      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.u.sv.st.dforce[q];
+      for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.st().dforce[q];
   }
   if (ord.wcnt || ord.cost) {  // the next launch's order: the env's largest agent row count
     int rows = L.nrows;
@@ -455,22 +476,23 @@ __device__ __forceinline__ void env_step_item(
 }
 
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_env_step(
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, 0, DR>::kWPE))) MG_VGPR_ATTR void k_env_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
   constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
-  if constexpr (W == 1) {
-    // one-wave blocks free their slot as soon as their wave is done: the static grid, one item per block
-    if ((int)blockIdx.x * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, blockIdx.x, ord);
-    span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
-    order_done(ord, (int)gridDim.x);
+  if constexpr (SH::kStatic) {
+    // the static grid, one item per wave (one-wave blocks free their slot as soon as their wave is done)
+    const int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64);
+    if (item * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, item, ord);
+    span_end(ord.clk, item);
+    order_done(ord, (int)gridDim.x * W);
   } else {
     // multi-wave blocks: the work queue (wq_next), the grid being the resident capacity
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
@@ -500,7 +522,7 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // one work item of k_hand_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void hand_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
@@ -511,7 +533,7 @@ __device__ __forceinline__ void hand_step_item(
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
-  mg::TeamLDS<T, MN, MC, OT>& L = lds[team].v;
+  mg::TeamLDSOf<T, MN, MC, OT>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, OT, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
@@ -597,14 +619,14 @@ __device__ __forceinline__ void hand_step_item(
     }
     mg::wsync();
     for (int k = t.tl; k < 13; k += T) L.oroot[k] = rp.root_states[(size_t)39 * ec + 13 + k];
-    for (int k = t.tl; k < 2 * nd; k += T) L.u.sv.st.dof[k] = rp.dof_state[(size_t)2 * nd * ec + k];
-    for (int k = t.tl; k < 6 * ns; k += T) L.u.sv.st.sens[k] = rp.sensors ? rp.sensors[(size_t)6 * ns * ec + k] : 0.0f;
-    for (int k = t.tl; k < nd; k += T) L.u.sv.st.dforce[k] = rp.dof_force ? rp.dof_force[(size_t)nd * ec + k] : 0.0f;
+    for (int k = t.tl; k < 2 * nd; k += T) L.st().dof[k] = rp.dof_state[(size_t)2 * nd * ec + k];
+    for (int k = t.tl; k < 6 * ns; k += T) L.st().sens[k] = rp.sensors ? rp.sensors[(size_t)6 * ns * ec + k] : 0.0f;
+    for (int k = t.tl; k < nd; k += T) L.st().dforce[k] = rp.dof_force ? rp.dof_force[(size_t)nd * ec + k] : 0.0f;
   } else {
     // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
     const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
     for (int st = 0; st < nsub; st++) t.substep();
-    t.outputs(L.u.sv.st.sens, L.u.sv.st.dforce);
+    t.outputs(L.st().sens, L.st().dforce);
     t.stage_state();
   }
   mg::wsync();
@@ -613,14 +635,14 @@ __device__ __forceinline__ void hand_step_item(
   // step's pre_physics reset_idx restores the env), reward 0, zero observation row
   bool nf = false;
   for (int k = t.tl; k < 13; k += T) nf = nf || !isfinite(L.oroot[k]);
-  for (int k = t.tl; k < 2 * nd; k += T) nf = nf || !isfinite(L.u.sv.st.dof[k]);
+  for (int k = t.tl; k < 2 * nd; k += T) nf = nf || !isfinite(L.st().dof[k]);
   const bool bad = ((__ballot(nf) >> t.tb) & mg::team_bits<T>()) != 0ull;
   // ---- post_physics_step: full_state obs staged in LDS (team-parallel), reward on the leader
   const int64_t progress_in = env_reset ? 0 : tb.progress[ec];
   float* rbs = v.rigid_body_states + (size_t)13 * nbe * ec;
   // rigid-body states of the hand once (one lane per body) into the dead row storage: the fingertip
   // observations and the rigid_body_states write-back both read them
-  float* bst = &L.u.sv.rows[0].b;
+  float* bst = &L.rows()[0].b;
   if constexpr (RP) {
     for (int k = t.tl; k < 13 * nb; k += T) bst[k] = rp.rigid_body_states[(size_t)13 * nbe * ec + k];
   } else {
@@ -642,7 +664,7 @@ __device__ __forceinline__ void hand_step_item(
         mg::h_ft_ref(tp, seg, i, &b, &c);
         x = bst[13 * b + c];
       } else {
-        x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens, nullptr);
+        x = mg::h_obs_value(tp, seg, i, L.st().dof, L.st().dforce, L.oroot, gs, qdiff, L.st().sens, nullptr);
       }
       L.obs[k] = x;
     }
@@ -705,16 +727,16 @@ __device__ __forceinline__ void hand_step_item(
       root[26 + k] = L.goal[k];
       tb.goal_states[(size_t)13 * e + k] = L.goal[13 + k];
     }
-    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.u.sv.st.dof[k];
+    for (int k = t.tl; k < 2 * nd; k += T) v.dof_state[(size_t)2 * nd * e + k] = L.st().dof[k];
     if (t.node > 0) {
       const int d = t.node - 1;
       const_cast<float*>(v.dof_targets)[(size_t)nd * e + d] = t.tgt;
       tb.prev_targets[(size_t)nd * e + d] = prev;
     }
     if (v.sensors)
-      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.u.sv.st.sens[k];
+      for (int k = t.tl; k < 6 * ns; k += T) v.sensors[(size_t)6 * ns * e + k] = L.st().sens[k];
     if (v.dof_force)
-      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.u.sv.st.dforce[k];
+      for (int k = t.tl; k < nd; k += T) v.dof_force[(size_t)nd * e + k] = L.st().dforce[k];
     for (int k = t.tl; k < 13 * nb; k += T) rbs[k] = bst[k];
     for (int k = t.tl; k < 26; k += T) rbs[13 * nb + k] = k < 13 ? L.oroot[k] : L.goal[k - 13];
     if (v.rb_forces && t.tl < 3) v.rb_forces[((size_t)nbe * e + nb) * 3 + t.tl] = L.oforce[t.tl];
@@ -731,7 +753,7 @@ __device__ __forceinline__ void hand_step_item(
           mg::h_ft_ref(tp, seg, i, &b, &c);
           x = bst[13 * b + c];
         } else {
-          x = mg::h_obs_value(tp, seg, i, L.u.sv.st.dof, L.u.sv.st.dforce, L.oroot, gs, qdiff, L.u.sv.st.sens,
+          x = mg::h_obs_value(tp, seg, i, L.st().dof, L.st().dforce, L.oroot, gs, qdiff, L.st().sens,
                               L.obs + (no - na));
         }
         tb.states[(size_t)tp.num_states * e + k] = bad ? 0.0f : x;   // NaN guard, as for obs
@@ -747,12 +769,12 @@ __device__ __forceinline__ void hand_step_item(
 }
 
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP, bool TGS = false>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(MG_WAVES_PER_EU))) void k_hand_step(
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, OT, DR>::kWPE))) void k_hand_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
   constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDS<T, MN, MC, OT>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -793,17 +815,20 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     if (c.k == kp && c.dev == sim->device) resident = c.blocks;
   if (resident <= 0) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, SH::kThreads, MG_LDS_PAD) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, SH::kThreads, MG_LDS_PAD + sim->lds_pad) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, sim->device) != hipSuccess || per_cu <= 0 ||
         cus <= 0)
       return fail(MG_EDEVICE, "mg_env_step: occupancy query failed");
     resident = per_cu * cus;
+    if (getenv("MIGYM_PRINT_OCC"))  // diagnostics: the resident blocks the runtime reports for this kernel
+      fprintf(stderr, "migym: step kernel W=%d: %d blocks per CU (%d waves), lds pad %d\n", SH::W, per_cu,
+              per_cu * SH::W, MG_LDS_PAD + sim->lds_pad);
     for (Entry& c : cache)
       if (!c.k) { c = Entry{kp, sim->device, resident}; break; }
   }
   const int items = (sim->n + SH::E1 - 1) / SH::E1;
   const int need = (items + SH::W - 1) / SH::W;
-  const int blocks = SH::W == 1 ? need : (need < resident ? need : resident);
+  const int blocks = SH::kStatic ? need : (need < resident ? need : resident);
   unsigned long long* clk = nullptr;  // mg_kernel_span_begin: this launch's slot, one (start, end) pair per wave
   if (sim->d_span && sim->span_next < sim->span_cap && blocks * SH::W <= sim->span_stride) {
     mg_sim* ms = const_cast<mg_sim*>(sim);   // recording bookkeeping only
@@ -824,7 +849,7 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     ord.done = sim->d_bq + 2 * kOrderBuckets;
   }
   // one-wave blocks: the static grid, one block per item; multi-wave blocks: the resident capacity (work queue)
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), MG_LDS_PAD, s, args..., sim->d_wq, ord);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(SH::kThreads), MG_LDS_PAD + sim->lds_pad, s, args..., sim->d_wq, ord);
   return MG_OK;
 }
 
@@ -870,14 +895,14 @@ int RunSimulate<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim) {
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp,
                                              const mg_task_buffers* tb, const mg_replay* rp) {
-  using TL = mg::TeamLDS<T, MN, MC, OBJ>;
+  using TL = mg::TeamLDSOf<T, MN, MC, OBJ>;
   if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_env_step: no model tile (model exceeds every kernel instance)");
   // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
-  if (!OBJ && (size_t)tp->num_obs * sizeof(float) > sizeof(TL::u.sv.rows))
+  if (!OBJ && (size_t)tp->num_obs * sizeof(float) > TL::kObsStageBytes)
     return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the kernel's staging area");
   // hand tasks stage the rigid-body states of the articulation in the same storage, the observation
   // row in the contact storage; the observation / states column maps hold 256 entries
-  if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > sizeof(TL::u.sv.rows))
+  if (OBJ && (size_t)13 * sim->host_model.num_bodies * sizeof(float) > TL::kObsStageBytes)
     return fail(MG_ECAPACITY, "mg_env_step: rigid bodies exceed the kernel's staging area");
   if (OBJ && (tp->num_obs < 0 || (size_t)tp->num_obs > sizeof(TL::obs) / sizeof(float)))
     return fail(MG_ECAPACITY, "mg_env_step: observation row exceeds the hand kernel's staging area");

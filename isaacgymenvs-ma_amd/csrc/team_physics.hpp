@@ -56,6 +56,7 @@ template <int MN, int MG, int MP, int HV = 1>  // HV: hull vertex capacity of th
 struct alignas(16) ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
+  unsigned long long anc[MN];   // ancestor mask of each node (itself and the root included)
   float nf[MN][33];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
                       // 27 stiff, 28 lower, 29 upper, 30 drive kp, 31 effort limit, 32 frictionloss
   int gtype[MG], gnode[MG], gbody[MG], gfil[MG];
@@ -87,6 +88,9 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, HV>* t, const mg_model
     for (int k = 1; k < nn; k++)
       if (m->parent[k] == i) ch |= 1ull << k;
     t->children[i] = ch;
+    unsigned long long an = 1ull;
+    for (int k = i; k > 0; k = m->parent[k]) an |= 1ull << k;
+    t->anc[i] = an;
     float* f = t->nf[i];
     const M3 R0 = quat_to_mat(m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]);
     for (int a = 0; a < 3; a++)
@@ -191,10 +195,15 @@ constexpr int kPgsPrefetch = 4;
 #define MG_KJY_HAND 12  // block / pen
 #endif
 constexpr int kJYRegs = MG_KJY;
-// test-solve columns per batch (a multiple of 3): 12 for the 16- and 32-lane locomotion teams (12 walkers
-// instead of 6 halve the batches per substep: Ant +0.7 %, MA-Ant +1.0 %; 15 columns -3.5 %, 9 or 18 for
-// 32-lane teams -5 % / -34 %); Cartpole keeps 6
-constexpr int kRBLoco = 12;
+// test-solve columns per batch (a multiple of 3).  16-lane teams: 6 (round 6, with the compact layout at three waves
+// per SIMD and 168 VGPRs: the per-batch arrays of 12 columns spilled; same box, two passes, Ant 65,536 177.0 ->
+// 201.1 M env-steps/s, 32,768 161.0 -> 180.2 M, 16,384 124.8 -> 137.9 M, MA-Ant 8,192 39.5 -> 43.4 M; 3 columns 186.4 /
+// 167.1 / 125.4 / 39.7 M, 9 columns 195.0 M at 65,536; profiles/r06/ab_rb.txt.  At two waves per SIMD 12 had
+// beaten 6: +0.7 % Ant).  32-lane locomotion teams: 12 (9 or 18: -5 % / -34 %); Cartpole 6
+#ifndef MG_RB_LOCO16
+#define MG_RB_LOCO16 6
+#endif
+constexpr int kRBLoco = MG_RB_LOCO16;
 #ifndef MG_RB_LOCO32
 #define MG_RB_LOCO32 12  // the 32- and 64-lane locomotion teams (Humanoid)
 #endif
@@ -207,6 +216,15 @@ constexpr int kRBLoco = 12;
 #ifndef MG_RB_EGG
 #define MG_RB_EGG 6
 #endif
+
+// the tangent basis of a contact normal (stored by build_rows, or recomputed where the compact layout keeps none)
+__device__ __forceinline__ void tangent_basis_t(V3 n, V3* t1, V3* t2) {
+  V3 a = fabsf(n.x) < 0.57735f ? v3(1, 0, 0) : v3(0, 1, 0);
+  V3 t = cross(a, n);
+  t = t * prsq(dot(t, t));
+  *t1 = t;
+  *t2 = cross(n, t);
+}
 
 #ifndef MG_PART_B_LDS
 #define MG_PART_B_LDS 0  // part-B PGS rows in the dead tree tiles (TeamLDS::PBL); an A/B variant
@@ -243,7 +261,6 @@ struct TeamLDS {
 #endif
   float U[MN][6];
   float Dinv[MN];
-  unsigned long long anc[MN];
   float L0[21];
   float Iinv[36];
   int ncon, nrows;
@@ -309,7 +326,136 @@ struct TeamLDS {
   static constexpr int HX = (OBJ == MG_GT_BOX || OBJ == MG_GT_CAPSULE) ? 2 : 0;
   float hx[HX > 0 ? HX : 1][7];
   int hxn;
+
+  // ---- accessors: the Team reaches every phase-scoped region through these, so the compact layout below (the
+  // 16-lane locomotion instances) can place the regions differently
+  static constexpr bool kCompact = false;
+  static constexpr size_t kObsStageBytes = sizeof(Row) * MR;   // the locomotion observation staging (the dead rows)
+  static constexpr size_t kGwFloats = (size_t)MN * 27;          // geom frames + pair list + candidate map (collide)
+  static constexpr size_t kUtFloats = (size_t)RB * MN;          // the test solves' ut slab (and their y rows)
+  __device__ __forceinline__ Row* rows() { return u.sv.rows; }
+  __device__ __forceinline__ Stage& st() { return u.sv.st; }
+  __device__ __forceinline__ float* qvsc() { return &u.slot[0][0]; }
+  __device__ __forceinline__ float* slot(int node) { return u.slot[node]; }
+  __device__ __forceinline__ float* acc(int node) { return u.sv.ts.aba.acc[node]; }
+  __device__ __forceinline__ float* aproot() { return u.sv.ts.aba.proot; }
+  __device__ __forceinline__ float* l0() { return L0; }
+  __device__ __forceinline__ float* iinv() { return Iinv; }
+  __device__ __forceinline__ float* ut(int q) { return u.sv.ts.ts.ut[q]; }
+  __device__ __forceinline__ float* tsroot(int q) { return u.sv.ts.ts.proot[q]; }
+  __device__ __forceinline__ float* gw() { return &u.slot[0][0]; }
+  __device__ __forceinline__ float* obs_stage() { return &u.sv.rows[0].b; }
+  __device__ __forceinline__ float gap(int c) const { return cd[c]; }
+  __device__ __forceinline__ void set_gap(int c, float d) { cd[c] = d; }
+  __device__ __forceinline__ int lm(int i) const { return lmeta[i]; }
+  __device__ __forceinline__ void set_lm(int i, int v) { lmeta[i] = v; }
+  __device__ __forceinline__ void tangents(int c, V3* t1, V3* t2) const { *t1 = ld3(ct1[c]); *t2 = ld3(ct2[c]); }
+  __device__ __forceinline__ void set_tangents(int c, V3 t1, V3 t2) {
+    ct1[c][0] = t1.x; ct1[c][1] = t1.y; ct1[c][2] = t1.z;
+    ct2[c][0] = t2.x; ct2[c][1] = t2.y; ct2[c][2] = t2.z;
+  }
 };
+
+// The compact team layout of the 16-lane locomotion instances (Ant, MA-Ant; MG_COMPACT_LDS): 4.2 -> 2.8 KB per team,
+// so that twelve waves fit a CU's 160 KB (three per SIMD) instead of eight.  What it changes against TeamLDS:
+//   * region A holds the poses R, x, V from fk() to collide()'s geom staging, then the contact gaps (row b of the
+//     contact's normal row, from collide()) and the constraint rows (build_rows() to outputs()), then the observation
+//     staging; the rows no longer sit next to the test-solve slab;
+//   * region B holds fk()'s joint sines, the ABA child slots (nodes >= 1 only), the ABA forward pass with the root
+//     factor and inverse (L0, Iinv: dead once the root coupling Wv is taken, right after aba()), collide()'s geom
+//     frames, the test-solve slab, and after the step the stage rows plus the contacts' impulse sums that outputs()
+//     stashes before its fk() overwrites region A;
+//   * no tangent basis is stored (recomputed from the normal by tangent_basis_t, the same bits), no gap array, and the
+//     limit-row metadata is one byte per row.
+// The ancestor masks live in the block's model tile for every instance.
+template <int T, int MN, int MC>
+struct TeamLDSC {
+  static_assert(MN <= 16, "the compact limit-row metadata packs the node in 4 bits");
+  static constexpr int MR = (3 * MC + 2 * (MN - 1) + kPgsPrefetch - 1) / kPgsPrefetch * kPgsPrefetch;
+  static constexpr int RB = T >= 32 ? MG_RB_LOCO32 : (kRBLoco <= T ? kRBLoco : 6);
+  static constexpr int KR0 = T >= 32 ? MG_KJY_LOCO32 : kJYRegs;
+  static constexpr int KR = (KR0 < MR ? KR0 : MR) / kPgsPrefetch * kPgsPrefetch;
+  static constexpr int PBL = 0;
+  static constexpr int OROWS = 1;
+  static constexpr int HX = 0;
+  static constexpr bool kCompact = true;
+  struct alignas(16) Row { float b, iw, lam, mu; };
+  struct Stage {
+    float root[13];
+    float dof[2 * MN];
+    float sens[6 * MG_MAX_SENSORS];
+    float dforce[MN];
+  };
+  float S[MN][6];
+  float U[MN][6];
+  float Dinv[MN];
+  int ncon, nrows;
+  float cp[MC][3], cn[MC][3];
+  int cside[MC];  // packed int8 [node A, node B, geom A, geom B]
+  uint8_t lmeta[(2 * (MN - 1) + 3) / 4 * 4];  // limit rows: kind | node << 4
+  union {  // region A
+    struct {
+      float R[MN][9];
+      float x[MN][3];
+      float V[MN][6];
+    };
+    Row rowsA[MR];
+  };
+  union {  // region B
+    float slots[MN > 1 ? MN - 1 : 1][27];
+    struct {
+      float acc[MN][6];
+      float proot[6];
+      float L0[21];
+      float Iinv[36];
+    } aba;
+    struct {
+      float ut[RB][MN];
+      float proot[RB][6];
+    } ts;
+    struct {
+      Stage st;
+      float fc[MC][3];  // outputs(): each contact's impulse sum n l_n + t1 l_t1 + t2 l_t2
+    } post;
+    struct {  // the free-object fields of TeamLDS (OBJ = 0 here: never written or read at run time)
+      float rwo[1][6];
+      float oroot[1], goal[1], oforce[4];
+      float hx[1][7];
+      int hxn;
+      float obs[1];
+    };
+  };
+  static_assert(sizeof(Stage) >= sizeof(float) * 4 * MN, "the stash must lie past fk()'s joint sines");
+  static constexpr size_t kObsStageBytes = sizeof(Row) * MR > sizeof(float) * 18 * MN ? sizeof(Row) * MR : sizeof(float) * 18 * MN;
+  static constexpr size_t kGwFloats = (size_t)(MN > 1 ? MN - 1 : 1) * 27;
+  static constexpr size_t kUtFloats = (size_t)RB * MN;
+  __device__ __forceinline__ Row* rows() { return rowsA; }
+  __device__ __forceinline__ Stage& st() { return post.st; }
+  __device__ __forceinline__ float* qvsc() { return &slots[0][0]; }
+  __device__ __forceinline__ float* slot(int node) { return slots[node - 1]; }  // nodes >= 1 publish
+  __device__ __forceinline__ float* acc(int node) { return aba.acc[node]; }
+  __device__ __forceinline__ float* aproot() { return aba.proot; }
+  __device__ __forceinline__ float* l0() { return aba.L0; }
+  __device__ __forceinline__ float* iinv() { return aba.Iinv; }
+  __device__ __forceinline__ float* ut(int q) { return ts.ut[q]; }
+  __device__ __forceinline__ float* tsroot(int q) { return ts.proot[q]; }
+  __device__ __forceinline__ float* gw() { return &slots[0][0]; }
+  __device__ __forceinline__ float* obs_stage() { return &rowsA[0].b; }
+  __device__ __forceinline__ float* fc(int c) { return post.fc[c]; }
+  __device__ __forceinline__ float gap(int c) const { return rowsA[3 * c].b; }
+  __device__ __forceinline__ void set_gap(int c, float d) { rowsA[3 * c].b = d; }
+  __device__ __forceinline__ int lm(int i) const { return lmeta[i]; }
+  __device__ __forceinline__ void set_lm(int i, int v) { lmeta[i] = (uint8_t)v; }
+  __device__ __forceinline__ void tangents(int c, V3* t1, V3* t2) const { tangent_basis_t(ld3(cn[c]), t1, t2); }
+  __device__ __forceinline__ void set_tangents(int, V3, V3) {}
+};
+#ifndef MG_COMPACT_LDS
+#define MG_COMPACT_LDS 1
+#endif
+// the team layout of an instance: compact for the 16-lane locomotion teams
+template <int T, int MN, int MC, int OBJ>
+using TeamLDSOf = typename std::conditional<(MG_COMPACT_LDS && T == 16 && OBJ == 0 && MN <= 16), TeamLDSC<T, MN, MC>,
+                                            TeamLDS<T, MN, MC, OBJ>>::type;
 
 // A team's LDS region padded so that consecutive teams start 4*T bytes apart modulo 128 B.  A
 // ds_read/write_b32 is serviced per 32-lane half with bank = dword address mod 32, so teams of
@@ -436,14 +582,6 @@ __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m));
   return v;
-}
-
-__device__ __forceinline__ void tangent_basis_t(V3 n, V3* t1, V3* t2) {
-  V3 a = fabsf(n.x) < 0.57735f ? v3(1, 0, 0) : v3(0, 1, 0);
-  V3 t = cross(a, n);
-  t = t * prsq(dot(t, t));
-  *t1 = t;
-  *t2 = cross(n, t);
 }
 
 constexpr int OBJ_NODE = -2;  // contact side on the free object
@@ -700,7 +838,7 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
 // own kernel instances, so the PGS instances are the code they were
 template <int T, int MN, int MC, int MG, int MP, int OBJ = 0, bool TGS = false>
 struct Team {
-  using L = TeamLDS<T, MN, MC, OBJ>;
+  using L = TeamLDSOf<T, MN, MC, OBJ>;
   using MT = ModelTile<MN, MG, MP, tile_hull_verts(OBJ)>;
   static constexpr int MR = L::MR;
 #ifndef MG_HW_TRIG_T16
@@ -811,16 +949,8 @@ struct Team {
     if (tl >= ncol0 && tl - ncol0 + 1 < nn) node = tl - ncol0 + 1;
     par = node > 0 ? mt->parent[node] : -1;
     depth = 0;
-    unsigned long long anc = 0ull;
-    if (node > 0) {
-      for (int k = node; k > 0; k = mt->parent[k]) {
-        anc |= 1ull << k;
-        depth++;
-      }
-      anc |= 1ull;
-      s->anc[node] = anc;
-    }
-    if (tl == 0) s->anc[0] = 1ull;
+    if (node > 0)
+      for (int k = node; k > 0; k = mt->parent[k]) depth++;
     maxdepth = wave_max<T>(depth);
     h = p->dt / (float)p->substeps;
     nu = 0.0f;
@@ -836,7 +966,7 @@ struct Team {
     oq[3] = 1.0f;
   }
   __device__ __forceinline__ float gscale() const { return m->gravity_off ? 0.0f : 1.0f; }
-  __device__ __forceinline__ bool in_path(int target, int k) const { return target >= 0 && ((s->anc[target] >> k) & 1ull); }
+  __device__ __forceinline__ bool in_path(int target, int k) const { return target >= 0 && ((mt->anc[target] >> k) & 1ull); }
 
   // ---------------------------------------------------------------- FK (level-synchronous)
   // Forward kinematics without a barrier per tree level: every node's lane composes its own path from the
@@ -861,9 +991,9 @@ struct Team {
     if (freeb && tl < 6 && !POSE) s->V[0][tl] = nu;
     // (q, qd) and (sin q, cos q) per node in the union storage (free here: the ABA's child slots are written
     // after): each lane evaluates its own joint's sine and cosine once, its descendants read them
-    float* qv = &s->u.slot[0][0];
+    float* qv = s->qvsc();
     float* sc = qv + 2 * MN;
-    static_assert(sizeof(s->u.slot) >= sizeof(float) * 4 * MN, "joint states must fit the union storage");
+    static_assert(L::kGwFloats >= 4 * MN, "joint states must fit the union storage");
     float sn = 0.0f, cs = 1.0f;
     if (node > 0) {
       qv[2 * node] = qj;
@@ -883,7 +1013,7 @@ struct Team {
     }
     if (node > 0) {
       const V3 x0 = x;
-      for (unsigned long long path = s->anc[node] & ~1ull; path; path &= path - 1) {
+      for (unsigned long long path = mt->anc[node] & ~1ull; path; path &= path - 1) {
         const int k = __builtin_ctzll(path);
         const float* nf = mt->nf[k];
         M3 R0;
@@ -1003,7 +1133,7 @@ struct Team {
         Sym6 Ia = IA;
         rank1_sub(Ia, U, Dinv);
         SV pa = pA + mul(Ia, c) + U * (u * Dinv);
-        float* sl = s->u.slot[node];
+        float* sl = s->slot(node);
         for (int k = 0; k < 6; k++) { sl[k] = Ia.a[k]; sl[15 + k] = Ia.c[k]; }
         for (int k = 0; k < 9; k++) sl[6 + k] = Ia.b[k];
         sl[21] = pa.a.x; sl[22] = pa.a.y; sl[23] = pa.a.z;
@@ -1018,7 +1148,7 @@ struct Team {
         while (ch) {
           const int k = __builtin_ctzll(ch);
           ch &= ch - 1;
-          const float* sl = s->u.slot[k];
+          const float* sl = s->slot(k);
           for (int q = 0; q < 6; q++) { IA.a[q] += sl[q]; IA.c[q] += sl[15 + q]; }
           for (int q = 0; q < 9; q++) IA.b[q] += sl[6 + q];
           pA = pA + sv(v3(sl[21], sl[22], sl[23]), v3(sl[24], sl[25], sl[26]));
@@ -1028,11 +1158,11 @@ struct Team {
     ph_mark(17);
     if (tl == 0) {
       if (freeb) {
-        chol6(IA, s->L0);
-        s->u.sv.ts.aba.proot[0] = pA.a.x; s->u.sv.ts.aba.proot[1] = pA.a.y; s->u.sv.ts.aba.proot[2] = pA.a.z;
-        s->u.sv.ts.aba.proot[3] = pA.l.x; s->u.sv.ts.aba.proot[4] = pA.l.y; s->u.sv.ts.aba.proot[5] = pA.l.z;
+        chol6(IA, s->l0());
+        s->aproot()[0] = pA.a.x; s->aproot()[1] = pA.a.y; s->aproot()[2] = pA.a.z;
+        s->aproot()[3] = pA.l.x; s->aproot()[4] = pA.l.y; s->aproot()[5] = pA.l.z;
       } else {
-        for (int k = 0; k < 6; k++) s->u.sv.ts.aba.acc[0][k] = 0.0f;
+        for (int k = 0; k < 6; k++) s->acc(0)[k] = 0.0f;
       }
     }
     wsync();
@@ -1040,31 +1170,31 @@ struct Team {
       // column tl of IA0^-1 from the Cholesky factor (6 lanes in parallel); a0 = -IA0^-1 pA0
       const SV e = sv(v3(tl == 0 ? 1.f : 0.f, tl == 1 ? 1.f : 0.f, tl == 2 ? 1.f : 0.f),
                       v3(tl == 3 ? 1.f : 0.f, tl == 4 ? 1.f : 0.f, tl == 5 ? 1.f : 0.f));
-      SV col = chol6_solve(s->L0, e);
+      SV col = chol6_solve(s->l0(), e);
       float cv[6] = {col.a.x, col.a.y, col.a.z, col.l.x, col.l.y, col.l.z};
       float a = 0.0f;
       for (int k = 0; k < 6; k++) {
-        s->Iinv[6 * k + tl] = cv[k];
-        a -= cv[k] * s->u.sv.ts.aba.proot[k];
+        s->iinv()[6 * k + tl] = cv[k];
+        a -= cv[k] * s->aproot()[k];
       }
-      s->u.sv.ts.aba.acc[0][tl] = a;
+      s->acc(0)[tl] = a;
     }
     wsync();
     ph_mark(18);
     float qdd = 0.0f;
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
-        SV ap = sv(ld3(s->u.sv.ts.aba.acc[par]), ld3(s->u.sv.ts.aba.acc[par] + 3)) + c;
+        SV ap = sv(ld3(s->acc(par)), ld3(s->acc(par) + 3)) + c;
         qdd = (u - dot(U, ap)) * Dinv;
         SV a = ap + S * qdd;
-        s->u.sv.ts.aba.acc[node][0] = a.a.x; s->u.sv.ts.aba.acc[node][1] = a.a.y; s->u.sv.ts.aba.acc[node][2] = a.a.z;
-        s->u.sv.ts.aba.acc[node][3] = a.l.x; s->u.sv.ts.aba.acc[node][4] = a.l.y; s->u.sv.ts.aba.acc[node][5] = a.l.z;
+        s->acc(node)[0] = a.a.x; s->acc(node)[1] = a.a.y; s->acc(node)[2] = a.a.z;
+        s->acc(node)[3] = a.l.x; s->acc(node)[4] = a.l.y; s->acc(node)[5] = a.l.z;
       }
       wsync();
     }
     // nu* = nu + h * acc
     if (tl < nv) {
-      float a = (freeb && tl < 6) ? s->u.sv.ts.aba.acc[0][tl] : qdd;
+      float a = (freeb && tl < 6) ? s->acc(0)[tl] : qdd;
       nu += h * a;
     }
   }
@@ -1116,7 +1246,9 @@ struct Team {
   __device__ __forceinline__ void obj_jrow(int r, V3* wo, V3* d) const {
     const int c = r / 3, q = r - 3 * c;
     const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
-    const V3 dir = ld3(q == 0 ? s->cn[c] : (q == 1 ? s->ct1[c] : s->ct2[c]));
+    V3 t1, t2;
+    s->tangents(c, &t1, &t2);
+    const V3 dir = q == 0 ? ld3(s->cn[c]) : (q == 1 ? t1 : t2);
     *wo = cross(ld3(s->cp[c]) - op, dir) * so;
     *d = dir * so;
   }
@@ -1144,8 +1276,7 @@ struct Team {
   // level by level, each lane gathers its ancestor's y values with one bpermute per column (no LDS
   // round trip or barrier per level).  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
   __device__ __forceinline__ void test_solve(int r0, int nrows_, const float* Wv, float* y) {
-    auto& ts = s->u.sv.ts.ts;
-    for (int i = tl; i < L::RB * MN; i += T) (&ts.ut[0][0])[i] = 0.0f;
+    for (int i = tl; i < L::RB * MN; i += T) s->ut(0)[i] = 0.0f;
     wsync();
     if (tl < L::RB) {
       const int r = r0 + tl;
@@ -1166,7 +1297,7 @@ struct Team {
           row_w(r, w);
           fw = sv(v3(w[0], w[1], w[2]), v3(w[3], w[4], w[5]));
         }
-        float* ut = ts.ut[tl];
+        float* ut = s->ut(tl);
         // 32-lane locomotion teams (Humanoid: 35 % of the contacts are self contacts with two tree sides): both
         // sides of a contact at once.  Below their lowest common ancestor the two paths are walked in one loop
         // (two independent chains per step), and from there to the root, the map pv -> pv + U D (t - S.pv) being
@@ -1180,7 +1311,7 @@ struct Team {
           if (kind < 2 && nodeA == 0) { proot = proot + pa; ka = -1; }
           if (kind < 2 && nodeB == 0) proot = proot + pb;
           if (kind < 2 && nodeB > 0 && !two) { ka = nodeB; pa = pb; }  // side A off the tree (ground / object)
-          const unsigned long long ma = ka > 0 ? (s->anc[ka] & ~1ull) : 0ull, mb = kb > 0 ? (s->anc[kb] & ~1ull) : 0ull;
+          const unsigned long long ma = ka > 0 ? (mt->anc[ka] & ~1ull) : 0ull, mb = kb > 0 ? (mt->anc[kb] & ~1ull) : 0ull;
           const unsigned long long com = two ? (ma & mb) : 0ull;
           unsigned long long wa = ma & ~com, wb = mb & ~com;
           // below the common ancestor: both chains per step (a lane with one side left idles on the other)
@@ -1229,7 +1360,7 @@ struct Team {
           // the path to the root is the ancestor mask (parents precede children, checked at sim
           // creation), so the next node's S / U / D^-1 are loaded while this one is processed; the
           // ut accumulations are fire-and-forget LDS adds (program order per lane, as the oracle)
-          unsigned long long path = s->anc[k0] & ~1ull;
+          unsigned long long path = mt->anc[k0] & ~1ull;
           int k = 63 - __builtin_clzll(path);
           SV Sk = sv(ld3(s->S[k]), ld3(s->S[k] + 3)), Uk = sv(ld3(s->U[k]), ld3(s->U[k] + 3));
           float Dk = s->Dinv[k];
@@ -1251,7 +1382,7 @@ struct Team {
         }
         }
       }
-      float* pr = ts.proot[tl];
+      float* pr = s->tsroot(tl);
       pr[0] = proot.a.x; pr[1] = proot.a.y; pr[2] = proot.a.z;
       pr[3] = proot.l.x; pr[4] = proot.l.y; pr[5] = proot.l.z;
     }
@@ -1262,19 +1393,19 @@ struct Team {
     float rem[L::RB], yv[L::RB];
 #pragma unroll
     for (int q = 0; q < L::RB; q++) {
-      const float* p0 = ts.proot[q];
-      float b = node > 0 ? ts.ut[q][node] : 0.0f;
+      const float* p0 = s->tsroot(q);
+      float b = node > 0 ? s->ut(q)[node] : 0.0f;
       b += Wv[0] * p0[0] + Wv[1] * p0[1] + Wv[2] * p0[2] + Wv[3] * p0[3] + Wv[4] * p0[4] + Wv[5] * p0[5];
       rem[q] = b;
       yv[q] = 0.0f;
     }
     ph_mark(11);
     // proper ancestors below the root, visited in increasing depth (= increasing index)
-    unsigned long long path = node > 0 ? (s->anc[node] & ~1ull & ~(1ull << node)) : 0ull;
+    unsigned long long path = node > 0 ? (mt->anc[node] & ~1ull & ~(1ull << node)) : 0ull;
     // the level's y values are published in the (now read) ut slab, RB floats per node, and every deeper
     // lane reads its ancestor's row: a few wide LDS accesses per level instead of RB bpermutes
-    float* ybuf = &ts.ut[0][0];
-    static_assert(sizeof(ts.ut) >= sizeof(float) * L::RB * MN, "y rows must fit the ut slab");
+    float* ybuf = s->ut(0);
+    static_assert(L::kUtFloats >= L::RB * MN, "y rows must fit the ut slab");
     wsync();
     for (int lev = 1; lev <= maxdepth; lev++) {
       if (node > 0 && depth == lev) {
@@ -1306,13 +1437,14 @@ struct Team {
   __device__ __forceinline__ int cside(int c, int k) const { return (int)(int8_t)(s->cside[c] >> (8 * k)); }
   // row r -> kind (0 normal, 1 friction, 2 lower limit, 3 upper limit) and ref (contact / node).
   // Rows are [n, t1, t2] per contact, then the joint limits (oracle order).
-  __device__ __forceinline__ int row_kind(int r) const { return r < 3 * ncr ? (r % 3 == 0 ? 0 : 1) : (s->lmeta[r - 3 * ncr] & 3); }
-  __device__ __forceinline__ int row_ref(int r) const { return r < 3 * ncr ? r / 3 : (s->lmeta[r - 3 * ncr] >> 4); }
+  __device__ __forceinline__ int row_kind(int r) const { return r < 3 * ncr ? (r % 3 == 0 ? 0 : 1) : (s->lm(r - 3 * ncr) & 3); }
+  __device__ __forceinline__ int row_ref(int r) const { return r < 3 * ncr ? r / 3 : (s->lm(r - 3 * ncr) >> 4); }
   // spatial direction of contact row r at the team origin: w = [(p - o) x d; d]
   __device__ __forceinline__ void row_w(int r, float* w) const {
     const int c = r / 3, k = r - 3 * c;
-    const float* dp = k == 0 ? s->cn[c] : (k == 1 ? s->ct1[c] : s->ct2[c]);
-    const V3 d = ld3(dp), q = ld3(s->cp[c]) - org, mo = cross(q, d);
+    V3 t1, t2;
+    s->tangents(c, &t1, &t2);
+    const V3 d = k == 0 ? ld3(s->cn[c]) : (k == 1 ? t1 : t2), q = ld3(s->cp[c]) - org, mo = cross(q, d);
     w[0] = mo.x; w[1] = mo.y; w[2] = mo.z; w[3] = d.x; w[4] = d.y; w[5] = d.z;
   }
   // Jacobian code of this lane for row r: 0 none, 1 +, 2 - (contact rows: +-Sl.w; limit rows: +-1
@@ -1379,14 +1511,16 @@ struct Team {
       if (sgn == 0.0f) return;
       const V3 g = cross(v3(Sl[0], Sl[1], Sl[2]), ld3(s->cp[c]) - org) + v3(Sl[3], Sl[4], Sl[5]);
       J[0] = sgn * dot(ld3(s->cn[c]), g);
-      J[1] = sgn * dot(ld3(s->ct1[c]), g);
-      J[2] = sgn * dot(ld3(s->ct2[c]), g);
+      V3 t1, t2;
+      s->tangents(c, &t1, &t2);
+      J[1] = sgn * dot(t1, g);
+      J[2] = sgn * dot(t2, g);
     } else {
 #pragma unroll
       for (int q = 0; q < 3; q++) {
         const int r = r0 + q;
         if (r < nrows_ && node > 0) {
-          const int meta = s->lmeta[r - 3 * ncr];
+          const int meta = s->lm(r - 3 * ncr);
           if ((meta >> 4) == node) J[q] = (meta & 3) == 2 ? 1.0f : -1.0f;
         }
       }
@@ -1409,7 +1543,7 @@ struct Team {
   // world frames of the geoms, staged once per substep by collide() (lane per geom) in the team's
   // union storage (dead between the ABA and build_rows); rows of 13 floats (odd stride): centre, R
   static constexpr int GW = 13;
-  __device__ __forceinline__ float* gw_tile() const { return &s->u.slot[0][0]; }
+  __device__ __forceinline__ float* gw_tile() const { return s->gw(); }
   __device__ __forceinline__ void geom_staged(int g, V3* c, M3* Rg) const {
     const float* w = gw_tile() + GW * g;
     *c = v3(w[0], w[1], w[2]);
@@ -1786,7 +1920,7 @@ struct Team {
   __device__ __forceinline__ void put_contact(int slot, V3 pt, V3 n, float d, int A, int gA, int B, int gB) {
     s->cp[slot][0] = pt.x; s->cp[slot][1] = pt.y; s->cp[slot][2] = pt.z;
     s->cn[slot][0] = n.x; s->cn[slot][1] = n.y; s->cn[slot][2] = n.z;
-    s->cd[slot] = d;
+    s->set_gap(slot, d);
     s->cside[slot] = (A & 0xff) | ((B & 0xff) << 8) | ((gA & 0xff) << 16) | ((gB & 0xff) << 24);
   }
 
@@ -1795,7 +1929,7 @@ struct Team {
     const float off = p->contact_offset;
     int base = 0;
     const int G = mt->ng;
-    static_assert(MN * 27 >= MG * GW, "geom frames must fit the team's union storage");
+    static_assert(L::kGwFloats >= MG * GW, "geom frames must fit the team's union storage");
     for (int g = tl; g < G; g += T) {
       V3 c;
       M3 Rg;
@@ -1932,7 +2066,7 @@ struct Team {
     // of every chunk of pairs.
     const int P = mt->np;
     const float poff = m->pair_mjcf ? 0.0f : off;  // explicit MJCF pairs: in contact from zero distance (margin 0)
-    static_assert(MN * 27 >= MG * GW + MP, "the pair list must fit behind the geom frames");
+    static_assert(L::kGwFloats >= MG * GW + MP, "the pair list must fit behind the geom frames");
     int* plist = reinterpret_cast<int*>(gw_tile() + GW * MG);
     int npc = 0;
     for (int p0 = 0; p0 < P; p0 += T) {
@@ -2145,7 +2279,7 @@ struct Team {
         }
         base += tot;
       } else {
-      static_assert(MN * 27 >= MG * GW + MP + (17 * MG + 1) / 2, "the candidate map must fit behind the pair list");
+      static_assert(L::kGwFloats >= MG * GW + MP + (17 * MG + 1) / 2, "the candidate map must fit behind the pair list");
       uint16_t* cmap = reinterpret_cast<uint16_t*>(plist + MP);
       int NC = 0;
       for (int g0 = 0; g0 < G; g0 += T) {
@@ -2229,13 +2363,12 @@ struct Team {
     for (int c = tl; c < ncon; c += T) {
       V3 n = ld3(s->cn[c]), pt = ld3(s->cp[c]), t1, t2;
       tangent_basis_t(n, &t1, &t2);
-      s->ct1[c][0] = t1.x; s->ct1[c][1] = t1.y; s->ct1[c][2] = t1.z;
-      s->ct2[c][0] = t2.x; s->ct2[c][1] = t2.y; s->ct2[c][2] = t2.z;
-      float deff = s->cd[c] - p->rest_offset;
+      s->set_tangents(c, t1, t2);
+      float deff = s->gap(c) - p->rest_offset;
       float bn = deff >= 0.0f ? -deff * ih : fminf(-p->baumgarte * deff * ih, p->max_depen_vel);
-      s->u.sv.rows[3 * c].b = TGS ? deff : bn;   // TGS: the gap; its target is set per sweep (substep())
-      s->u.sv.rows[3 * c + 1].b = 0.0f;
-      s->u.sv.rows[3 * c + 2].b = 0.0f;
+      s->rows()[3 * c].b = TGS ? deff : bn;   // TGS: the gap; its target is set per sweep (substep())
+      s->rows()[3 * c + 1].b = 0.0f;
+      s->rows()[3 * c + 2].b = 0.0f;
       if constexpr (L::OROWS > 1) {  // the object's columns [w; v_com]: +-[(p - c_obj) x d; d]
         const float so = (cside(c, 0) == OBJ_NODE ? 1.0f : 0.0f) - (cside(c, 1) == OBJ_NODE ? 1.0f : 0.0f);
         V3 dirs[3] = {n, t1, t2};
@@ -2267,12 +2400,27 @@ struct Team {
       bool on = side == 0 ? lo : hi;
       if (!on) continue;
       float d = side == 0 ? dl : du;
-      s->u.sv.rows[3 * ncon + li].b = TGS ? d : (d >= 0.0f ? -d * ih : fminf(-p->baumgarte * d * ih, p->max_depen_vel));
-      s->lmeta[li] = (2 + side) | (node << 4);
+      s->rows()[3 * ncon + li].b = TGS ? d : (d >= 0.0f ? -d * ih : fminf(-p->baumgarte * d * ih, p->max_depen_vel));
+      s->set_lm(li, (2 + side) | (node << 4));
       li++;
     }
     if (tl == 0) s->nrows = 3 * ncon + tot;
     wsync();
+  }
+
+  // the root coupling Wv of the test solves (substep()) from the root inverse aba() left in Iinv
+  __device__ __forceinline__ void root_coupling(float* Wv) const {
+    if (!freeb) return;
+    if (tl < 6) {
+      for (int k = 0; k < 6; k++) Wv[k] = -s->iinv()[6 * tl + k];
+    } else if (node > 0) {
+      const float Uv[6] = {U.a.x, U.a.y, U.a.z, U.l.x, U.l.y, U.l.z};
+      for (int k = 0; k < 6; k++) {
+        float w = 0.0f;
+        for (int c2 = 0; c2 < 6; c2++) w += s->iinv()[6 * c2 + k] * Uv[c2];
+        Wv[k] = w;
+      }
+    }
   }
 
   // ---------------------------------------------------------------- one substep
@@ -2288,11 +2436,17 @@ struct Team {
     ph_mark(0);
     if (OBJ) tendons();
     aba();
+    // root coupling of the test solves: with a0 = -IA0^-1 p0, a joint lane's U.a0 = -(IA0^-1 U).p0
+    // and a root lane's a0[tl] = -(row tl of IA0^-1).p0, so one 6-vector per lane covers both.  The compact
+    // layout takes it now (its Iinv shares region B with collide()'s geom frames), the other after build_rows()
+    float Wv[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (L::kCompact) root_coupling(Wv);
     ph_mark(1);
     obj_free();
     collide();
     ncr = s->ncon;
-    org = ld3(s->x[0]);
+    if constexpr (L::kCompact) org = p0;  // the bits fk() stored in x[0]: region A holds the gaps by now
+    else org = ld3(s->x[0]);
     ph_mark(2);
     build_rows();
     ph_mark(3);
@@ -2305,20 +2459,8 @@ struct Team {
     // row responses Y_r = M~^-1 J_r^T by test-force ABA solves (column distributed over the lanes),
     // W_r = J_r . Y_r.  Lane j keeps (J_r[j], Y_r[j]) of every row in private arrays for the sweeps;
     // rows past this team's count get J = Y = 0 and zero scalars, so the sweeps need no row mask.
-    // root coupling of the test solves: with a0 = -IA0^-1 p0, a joint lane's U.a0 = -(IA0^-1 U).p0
-    // and a root lane's a0[tl] = -(row tl of IA0^-1).p0, so one 6-vector per lane covers both
-    float Wv[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    if (freeb && wave_rows > 0) {
-      if (tl < 6) {
-        for (int k = 0; k < 6; k++) Wv[k] = -s->Iinv[6 * tl + k];
-      } else if (node > 0) {
-        const float Uv[6] = {U.a.x, U.a.y, U.a.z, U.l.x, U.l.y, U.l.z};
-        for (int k = 0; k < 6; k++) {
-          float w = 0.0f;
-          for (int c2 = 0; c2 < 6; c2++) w += s->Iinv[6 * c2 + k] * Uv[c2];
-          Wv[k] = w;
-        }
-      }
+    if constexpr (!L::kCompact) {
+      if (wave_rows > 0) root_coupling(Wv);
     }
     // (J_r[j], Y_r[j]) of the first KR rows live in registers (the index is wave-uniform, so the compiler
     // promotes the arrays to VGPRs and addresses them with relative moves); the remaining rows are
@@ -2375,7 +2517,7 @@ struct Team {
       auto row_record = [&](int r, float Wr) {
         const bool active = r < nrows;
         const bool contact = r < 3 * ncr;
-        typename L::Row& rw = s->u.sv.rows[r];
+        typename L::Row& rw = s->rows()[r];
         rw.iw = (active && Wr > 1e-12f) ? prcp(Wr) : 0.0f;
         rw.lam = 0.0f;
         // DR: a contact's friction is the mean of its two shapes' (vec_task.py rigid_shape_properties)
@@ -2418,7 +2560,7 @@ struct Team {
     static_assert(MR % PF == 0, "row capacity must be a multiple of the PGS prefetch depth");
     const int prow = wave_rows == 0 ? 0 : ((wave_rows + PF - 1) / PF) * PF;
     for (int r = wave_rows; r < prow; r++) MG_JSET(r, 0.0f, 0.0f);
-    if (tl < prow - wave_rows) s->u.sv.rows[wave_rows + tl] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};  // PF - 1 <= T
+    if (tl < prow - wave_rows) s->rows()[wave_rows + tl] = typename L::Row{0.0f, 0.0f, 0.0f, -2.0f};  // PF - 1 <= T
     wsync();
     ph_mark(5);
     // PGS sweeps: per visit one team dot product (DPP), a branch-free clamp (med3), one multiply-add
@@ -2454,7 +2596,7 @@ struct Team {
       }
       const float lnew = __builtin_amdgcn_fmed3f(lam + (tgt - v) * R.iw, -t, hi);
       lamn = m == -1.0f ? lnew : lamn;
-      s->u.sv.rows[r].lam = lnew;
+      s->rows()[r].lam = lnew;
       nu += Y * (lnew - lam);
     };
     const int pa = prow < KR ? prow : KR;  // rows of part A
@@ -2464,7 +2606,7 @@ struct Team {
 #pragma unroll
       for (int k = 0; k < PF; k++) {
         MG_JGET(KR + k, pJ[k], pY[k]);
-        pR[k] = s->u.sv.rows[KR + k];
+        pR[k] = s->rows()[KR + k];
       }
     }
     for (int it = 0; it < n_sweeps; it++) {
@@ -2478,7 +2620,7 @@ struct Team {
         typename L::Row cR[PF];
         if (pa > 0) {
 #pragma unroll
-          for (int k = 0; k < PF; k++) cR[k] = s->u.sv.rows[k];
+          for (int k = 0; k < PF; k++) cR[k] = s->rows()[k];
         }
 #pragma unroll
         for (int r0 = 0; r0 < KR; r0 += PF) {
@@ -2487,7 +2629,7 @@ struct Team {
             const bool more = r0 + PF < pa;
             if (more) {
 #pragma unroll
-              for (int k = 0; k < PF; k++) nR[k] = s->u.sv.rows[r0 + PF + k];
+              for (int k = 0; k < PF; k++) nR[k] = s->rows()[r0 + PF + k];
             }
 #pragma unroll
             for (int k = 0; k < PF; k++) visit(Jr[r0 + k], Yr[r0 + k], cR[k], r0 + k);
@@ -2511,7 +2653,7 @@ struct Team {
           visit(pJ[k], pY[k], pR[k], r0 + k);
           pJ[k] = nJ[k];
           pY[k] = nY[k];
-          pR[k] = s->u.sv.rows[rn + k];
+          pR[k] = s->rows()[rn + k];
         }
       }
       if constexpr (TGS) {  // the sub-step's displacement
@@ -2564,9 +2706,13 @@ struct Team {
           if (tl < 3) {
             nu = tl == 0 ? wr.x : (tl == 1 ? wr.y : wr.z);
           } else if (tl < 6) {
-            M3 Rr;
-            for (int a = 0; a < 3; a++)
-              for (int b = 0; b < 3; b++) Rr.m[a][b] = s->R[0][3 * a + b];
+            M3 Rr;  // fk()'s R[0] (compact: region A holds the rows; quat_to_mat(q0) gives the same bits)
+            if constexpr (L::kCompact) {
+              Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
+            } else {
+              for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) Rr.m[a][b] = s->R[0][3 * a + b];
+            }
             const V3 dv = cross(w0 - wr, mul(Rr, ld3(m->body_com[0])));
             nu += tl == 3 ? dv.x : (tl == 4 ? dv.y : dv.z);
           }
@@ -2724,8 +2870,10 @@ struct Team {
         const int ga = cside(c, 2), gb = cside(c, 3);
         ba[j] = ga >= 0 ? mt->gbody[ga] : -1;
         bb[j] = gb >= 0 ? mt->gbody[gb] : -1;
-        const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
-        f[j] = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) *
+        const V3 n = ld3(s->cn[c]);
+        V3 t1, t2;
+        s->tangents(c, &t1, &t2);  // build_rows' basis
+        f[j] = (n * s->rows()[3 * c].lam + t1 * s->rows()[3 * c + 1].lam + t2 * s->rows()[3 * c + 2].lam) *
                prcp(h);
         pc[j] = ld3(s->cp[c]);
       }
@@ -2767,6 +2915,26 @@ struct Team {
   // rigid-body states from them)
   template <bool POSE = false>
   __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out) {
+    // the compact layout keeps the last substep's rows in region A, which fk() overwrites: each contact's impulse
+    // sum goes to region B (fc) and a node's limit impulses to registers first
+    float llo = 0.0f, lhi = 0.0f;
+    if constexpr (L::kCompact) {
+      const int nc = s->ncon;
+      for (int c = tl; c < nc; c += T) {
+        const V3 n = ld3(s->cn[c]);
+        V3 t1, t2;
+        s->tangents(c, &t1, &t2);  // build_rows' basis
+        const V3 f = n * s->rows()[3 * c].lam + t1 * s->rows()[3 * c + 1].lam + t2 * s->rows()[3 * c + 2].lam;
+        float* o = s->fc(c);
+        o[0] = f.x; o[1] = f.y; o[2] = f.z;
+      }
+      if (node > 0) {
+        const int lr = 3 * nc + (sat >> 3);
+        if (sat & 2) llo = s->rows()[lr].lam;
+        if (sat & 4) lhi = s->rows()[lr + ((sat >> 1) & 1)].lam;
+      }
+      wsync();
+    }
     fk<POSE>();  // post-step pose for the sensor body frames
     const float ih = prcp(h);  // impulses -> forces
     const int NS = m->num_sensors;
@@ -2814,8 +2982,13 @@ struct Team {
         else if (cside(c, 3) >= 0 && mt->gbody[cside(c, 3)] == body) sg = -1.0f;
         if (sg == 0.0f) continue;
 #endif
-        const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
-        V3 f = (n * s->u.sv.rows[3 * c].lam + t1 * s->u.sv.rows[3 * c + 1].lam + t2 * s->u.sv.rows[3 * c + 2].lam) * (sg * ih);
+        V3 f;
+        if constexpr (L::kCompact) {
+          f = ld3(s->fc(c)) * (sg * ih);
+        } else {
+          const V3 n = ld3(s->cn[c]), t1 = ld3(s->ct1[c]), t2 = ld3(s->ct2[c]);  // build_rows' basis
+          f = (n * s->rows()[3 * c].lam + t1 * s->rows()[3 * c + 1].lam + t2 * s->rows()[3 * c + 2].lam) * (sg * ih);
+        }
         F = F + f;
         Tq = Tq + cross(ld3(s->cp[c]) - xb, f);
       }
@@ -2841,9 +3014,14 @@ struct Team {
       if (fl > 0.0f) t -= fl * ptanh(nu * (1.0f / MG_FRICTIONLOSS_VS));  // the joint friction at the post-step state
       // the node's own limit rows of the last substep (lower, then upper: consecutive from the index build_rows
       // kept in sat), instead of a scan over every limit row
-      const int lr = 3 * s->ncon + (sat >> 3);
-      if (sat & 2) t += s->u.sv.rows[lr].lam * ih;
-      if (sat & 4) t -= s->u.sv.rows[lr + ((sat >> 1) & 1)].lam * ih;
+      if constexpr (L::kCompact) {
+        if (sat & 2) t += llo * ih;
+        if (sat & 4) t -= lhi * ih;
+      } else {
+        const int lr = 3 * s->ncon + (sat >> 3);
+        if (sat & 2) t += s->rows()[lr].lam * ih;
+        if (sat & 4) t -= s->rows()[lr + ((sat >> 1) & 1)].lam * ih;
+      }
       dforce_out[node - 1] = t;
     }
   }
@@ -2895,20 +3073,20 @@ struct Team {
     float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
     float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
     if (tl == 0) {
-      s->u.sv.st.root[0] = p0.x; s->u.sv.st.root[1] = p0.y; s->u.sv.st.root[2] = p0.z;
-      for (int k = 0; k < 4; k++) s->u.sv.st.root[3 + k] = q0[k];
+      s->st().root[0] = p0.x; s->st().root[1] = p0.y; s->st().root[2] = p0.z;
+      for (int k = 0; k < 4; k++) s->st().root[3 + k] = q0[k];
       if (freeb) {
         M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
         V3 cw = mul(Rr, ld3(m->body_com[0]));
         V3 om = v3(w0, w1, w2);
         V3 vc = v3(v0, v1, v2) + cross(om, cw);
-        s->u.sv.st.root[7] = vc.x; s->u.sv.st.root[8] = vc.y; s->u.sv.st.root[9] = vc.z;
-        s->u.sv.st.root[10] = om.x; s->u.sv.st.root[11] = om.y; s->u.sv.st.root[12] = om.z;
+        s->st().root[7] = vc.x; s->st().root[8] = vc.y; s->st().root[9] = vc.z;
+        s->st().root[10] = om.x; s->st().root[11] = om.y; s->st().root[12] = om.z;
       }
     }
     if (node > 0) {
-      s->u.sv.st.dof[2 * (node - 1)] = qj;
-      s->u.sv.st.dof[2 * (node - 1) + 1] = nu;
+      s->st().dof[2 * (node - 1)] = qj;
+      s->st().dof[2 * (node - 1) + 1] = nu;
     }
     if (OBJ) {
       const float o0 = __shfl(nu, tb + ob0), o1 = __shfl(nu, tb + ob0 + 1), o2 = __shfl(nu, tb + ob0 + 2);
