@@ -183,7 +183,7 @@ def pmc_traffic(task, n, kern_ms, object_type="block"):
     None when no pass was recorded for this workload."""
     path = None
     tag = task if (task != "ShadowHand" or object_type == "block") else f"{task}-{object_type}"   # per kernel instance
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):   # the newest round's passes of this workload
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):   # the newest round's passes of this workload
         cand = os.path.join(ROOT, "profiles", rnd, f"pmc_{tag}_{n}.json")
         if os.path.exists(cand):
             path = cand
@@ -285,15 +285,32 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
     torch.cuda.synchronize()
     ev = sorted(starts[i].elapsed_time(ends[i]) for i in range(ks))
     event_ms = ev[ks // 2] if ks % 2 else 0.5 * (ev[ks // 2 - 1] + ev[ks // 2])
+    # steady state: a further untimed sample of the same rollout (a short timed run right after the first
+    # reset is not steady state -- early-episode rows make the locomotion steps heavier, the hand's lighter)
+    steady_ms = None
+    if args.steady_steps > 0:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steady_steps):
+            env.step(pool[i % 8])
+        if gather is not None:
+            gather.drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        steady_ms = 1e3 * (time.perf_counter() - t1) / args.steady_steps
     if not span_ok:
         print(f"bench.py: the span hooks recorded {len(spans)} of {nspan} launches; kernel_ms from HIP events",
               file=sys.stderr)
     kern_ms = sum(spans) / len(spans) if span_ok else event_ms
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms, event_ms], dtype=torch.float64,
+        t = torch.tensor([elapsed, kern_ms, event_ms, steady_ms or 0.0], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms, event_ms = float(t[0]), float(t[1]), float(t[2])
+        steady_ms = float(t[3]) if steady_ms is not None else None
     info = {"substeps": env.sim_params.substeps, "pos_iters": env.sim_params.pos_iters, "agents": env.num_agents,
             "solver": "TGS" if env.sim_params.solver_type == 1 else "PGS",
             "vel_sweeps": max(env.sim_params.pos_iters, env.sim_params.vel_iters) if env.sim_params.solver_type == 1
@@ -306,6 +323,12 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
                               f"start to last wave end, GPU wall clock; max over ranks)") if span_ok else
                              f"median of HIP events around {ks} launches (no span hooks in this library)",
          "event_ms": event_ms,
+         "steady_state_ms": steady_ms,
+         "steady_state_value": (n * world / (steady_ms * 1e-3)) if steady_ms else None,
+         "steady_state_sample": (f"{args.steady_steps} further steps of the same rollout after the timed ones and the "
+                                 f"event pass, untimed by the contract (wall clock, barrier + synchronize, max over "
+                                 f"ranks): ms_per_step / steady_state_ms - 1 is the timed run's early-episode bias")
+                                if steady_ms else None,
          "gathered": gather_mode if (gather_mode != "none" and world > 1) else None, "env_info": info}
     if what is not None:
         r.update({"config": what, "task": task, "num_envs_total": total, "num_envs_per_gpu": n, "n_gpus": world,
@@ -334,6 +357,9 @@ def main():
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the strong-scaling lines (BASELINE configs[3]/[4] and Ant 65,536 as fixed totals "
                          "split over the ranks)")
+    ap.add_argument("--steady-steps", type=int, default=200,
+                    help="an untimed further sample of the same rollout after the timed steps, reported as "
+                         "steady_state_ms beside ms_per_step (0: skip)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--solver", default="pgs", choices=["pgs", "tgs"],
                     help="sim.physx.solver: north_star's PGS (default) or the build-defined TGS (DESIGN.md §4)")
@@ -381,6 +407,8 @@ def main():
             "metric": "env-steps/sec (whole node) at num_envs=65536; 1/2/4/8 MI355X scaling",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "steady_state_ms": head["steady_state_ms"], "steady_state_value": head["steady_state_value"],
+            "steady_state_sample": head["steady_state_sample"],
             "dtype": "f32", "data": "synthetic (U(-1,1) actions, device-resident)",
             "config": {"workload": f"{args.task} VecTask.step, {n} envs per GPU, {env['substeps']} substeps, "
                                    + (f"PGS x{env['pos_iters']}" if env["solver"] == "PGS" else
@@ -396,6 +424,10 @@ def main():
                          "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms, args.object_type),
                          "kernel": "k_hand_step" if args.task == "ShadowHand" else "k_env_step",
                          "kernel_ms": kern_ms, "kernel_ms_sample": head["kernel_ms_sample"],
+                         "kernel_ms_scope": ("the fused step kernel only: with work ordering on (DESIGN.md §3) the "
+                                             "sort's two small launches before it (k_ohist, k_oscatter; rocprof "
+                                             "profiles/r06/*kernel_stats.csv) lie outside kernel_ms and inside "
+                                             "event_ms and ms_per_step"),
                          "kernel_ms_le_ms_per_step": kern_ms <= ms_per_step,
                          "event_ms": head["event_ms"],
                          "event_ms_note": "HIP events around each launch of the same pass: kernel + the event "

@@ -30,14 +30,13 @@ struct mg_sim {
   int lds_pad;         // dynamic LDS added to every step-kernel launch (MIGYM_LDS_PAD; occupancy experiments, 0)
   long long order_steps;  // ordered launches so far (the parity of the set the lists' launches write)
   int sort_every;      // sort: every K-th ordered launch sorts (the launches between keep the last permutation)
-  long long sorts;     // sort: sorts so far (the parity of the sort's totals)
   bool order_valid;    // the previous ordered launch left an order for this one
   unsigned* d_bq;      // lists: [2][kOrderBuckets] bucket counts, then the launch's finished-wave counter
   int* d_blist;        // lists: [2][kOrderBuckets][bq_cap] env indices per bucket
   int bq_cap;          // env units (n / A)
   int* d_order;        // sort: (bq_cap) slot -> env unit
   unsigned char* d_cost;  // sort: (bq_cap) the last launch's row count per env unit (its agents' largest, <= 255)
-  unsigned* d_osort;   // sort: [2][256] bin totals (alternating), [blocks][256] the blocks' bases, then ushort ranks
+  unsigned* d_osort;   // sort: [kSortRep][256] bin totals, [blocks][256] the blocks' bases, then ushort ranks
   // kernel spans (mg_kernel_span_begin): per recorded launch, span_stride (start, end) pairs, one per wave
   unsigned long long* d_span;
   int span_cap, span_next, span_stride;
@@ -55,7 +54,8 @@ constexpr int kOrderOff = 0, kOrderLists = 1, kOrderSort = 2;
 // sort: copies of the bin totals (block b adds into copy b % kSortRep): the hot bins' device-scope atomics spread
 // over 8 words each (k_ohist 6.4 -> 4.8 us at 65,536 envs under the profiler; Ant 65,536 +0.3 %)
 constexpr int kSortRep = MG_SORT_REP;
-constexpr int kSortTot = 2 * kSortRep * 256;  // sort: both alternating sets of totals
+constexpr int kSortTot = kSortRep * 256;  // sort: the bin totals (zero before every sort: the step kernel that consumes
+                                         // a sort's permutation clears them, MgOrder::tot_clear)
 struct MgOrder {
   const int* order;     // sort: this launch's permutation (nullptr: none yet)
   unsigned char* cost;  // sort: the row counts this launch writes
@@ -67,6 +67,8 @@ struct MgOrder {
   unsigned* done;
   int cap;
   unsigned long long* clk;  // nullptr, or this launch's span slot (mg_kernel_span_begin)
+  unsigned* tot_clear;      // sort: the bin totals, zeroed by block 0 of the step kernel (k_oscatter, their last reader,
+                            // has finished: stream order), so the next sort starts from zero with no host-side state
 };
 
 namespace mgi {

@@ -577,7 +577,6 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   s->order_mode = kOrderOff;
   s->order_steps = 0;
   s->sort_every = 1;
-  s->sorts = 0;
   s->order_valid = false;
   s->d_bq = nullptr;
   s->d_blist = nullptr;
@@ -950,16 +949,15 @@ int mg_post_physics(mg_sim* sim, const mg_task_params* tp, const mg_state_views*
 // otherwise serialise every add -- then one global atomic per block and used bin reserves the block's range inside
 // the bin, and each unit keeps its rank inside its block's range.  Pass 2 (k_oscatter): the bins' starts (a block
 // scan of the 256 totals) and each unit's slot.  Where a unit lands inside its bin never changes a result, only
-// which units share a wave.  The totals alternate between two buffers; pass 1 clears the one the next sort fills.
+// which units share a wave.  The step kernel that runs this permutation zeroes the totals for the next sort
+// (MgOrder::tot_clear), so the launches carry no host-side state and a captured graph replays them any number of times.
 // (Fusing the histogram into the step kernel -- a global add per env -- and placing by per-bin cursors measured far
 // slower: one hot bin's atomics serialise, Ant 65,536 156.0 -> 108.5 M)
 __global__ __launch_bounds__(256) void k_ohist(const unsigned char* __restrict__ cost, int nu,
-                                               unsigned* __restrict__ tot, unsigned* __restrict__ tot_clear,
-                                               unsigned* __restrict__ bbase, unsigned short* __restrict__ rank) {
+                                               unsigned* __restrict__ tot, unsigned* __restrict__ bbase,
+                                               unsigned short* __restrict__ rank) {
   __shared__ unsigned h[256];
   h[threadIdx.x] = 0u;
-  if (blockIdx.x == 0)
-    for (int k = 0; k < kSortRep; k++) tot_clear[256 * k + threadIdx.x] = 0u;
   __syncthreads();
   const int u = (int)blockIdx.x * 256 + (int)threadIdx.x;
   const int lane = (int)(threadIdx.x & 63);
@@ -1045,17 +1043,22 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   }
   if (tp->num_actions > 64 || tp->num_obs > 256 || tp->num_states > 256)
     return fail(MG_EINVAL, "mg_env_step: num_actions > 64, num_obs > 256 or num_states > 256");
+  if (sim->order_mode == kOrderLists && !rp) {
+    // the in-kernel lists alternate between two sets by the host's launch parity, which a captured graph would freeze
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(MG_EINVAL, "mg_env_step: MIGYM_ORDER=lists cannot be captured into a graph (use sort or off)");
+  }
   if (sim->order_mode != kOrderOff && !rp) {
     const int A = tp->num_agents > 1 ? tp->num_agents : 1;
     if (sim->bq_cap != (sim->n + A - 1) / A) return fail(MG_EINVAL, "mg_env_step: num_agents differs from mg_sim_params.agents");
     // the last launch's row counts -> this one's order (every sort_every-th ordered launch from the second on)
     if (sim->order_mode == kOrderSort && sim->order_valid && (sim->order_steps - 1) % sim->sort_every == 0) {
-      const int nu = sim->bq_cap, nb = (nu + 255) / 256, b = (int)(sim->sorts++ & 1);
+      const int nu = sim->bq_cap, nb = (nu + 255) / 256;
       unsigned* bbase = sim->d_osort + kSortTot;
       unsigned short* rank = reinterpret_cast<unsigned short*>(sim->d_osort + kSortTot + 256 * (size_t)nb);
-      unsigned* tot = sim->d_osort + (kSortTot / 2) * b;
-      hipLaunchKernelGGL(k_ohist, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu, tot,
-                         sim->d_osort + (kSortTot / 2) * (b ^ 1), bbase, rank);
+      unsigned* tot = sim->d_osort;
+      hipLaunchKernelGGL(k_ohist, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu, tot, bbase, rank);
       hipLaunchKernelGGL(k_oscatter, dim3(nb), dim3(256), 0, (hipStream_t)stream, sim->d_cost, nu, tot, bbase, rank,
                          sim->d_order);
     }

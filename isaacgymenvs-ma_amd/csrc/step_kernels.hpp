@@ -132,6 +132,12 @@ __device__ __forceinline__ void span_end(unsigned long long* clk, int wave) {
   if (clk && (threadIdx.x & 63) == 0) clk[2 * (size_t)wave + 1] = (unsigned long long)wall_clock64();
 #endif
 }
+// sort: block 0 zeroes the bin totals this launch's permutation was built from (k_oscatter, their last reader, has
+// finished: stream order), so every sort starts from zero and the launches hold no host-side parity (graph replays)
+__device__ __forceinline__ void sort_totals_clear(const MgOrder& ord) {
+  if (ord.tot_clear && blockIdx.x == 0)
+    for (int i = (int)threadIdx.x; i < kSortTot; i += (int)blockDim.x) ord.tot_clear[i] = 0u;
+}
 __device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
   if ((threadIdx.x & 63) == 0 && atomicAdd(&wq[1], 1u) == (unsigned)grid_waves - 1u) {
     atomicExch(&wq[0], 0u);
@@ -485,6 +491,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
+  sort_totals_clear(ord);
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (SH::kStatic) {
@@ -778,6 +785,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
   __shared__ mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
+  sort_totals_clear(ord);
   mg::copy_tile(&tile, static_cast<const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>*>(timg));
   __syncthreads();  // the only block-wide barrier: every later phase synchronises its own wave
   if constexpr (W == 1) {  // as k_env_step
@@ -835,10 +843,11 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     clk = ms->d_span + 2 * (size_t)ms->span_stride * ms->span_next;
     ms->span_waves[ms->span_next++] = blocks * SH::W;
   }
-  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk};
+  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk, nullptr};
   if (ordered && sim->order_mode == kOrderSort) {
     ord.order = sim->order_valid ? sim->d_order : nullptr;
     ord.cost = sim->d_cost;
+    ord.tot_clear = sim->d_osort;
   } else if (ordered && sim->order_mode == kOrderLists) {
     const int rs = (int)(sim->order_steps & 1), ws = 1 - rs;   // this launch reads set rs, writes set ws
     ord.rcnt = sim->order_valid ? sim->d_bq + rs * kOrderBuckets : nullptr;

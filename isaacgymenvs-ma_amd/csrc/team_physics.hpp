@@ -1112,7 +1112,8 @@ struct Team {
       }
       Dj = np[1] + h * bb + h * h * kk;
       tj = tau + tadd + ttend - bb * nu - kk * (qj - ref + h * nu);
-      // dry joint friction (MJCF frictionloss; not domain-randomized): -f tanh(qd / v_s), linearly implicit
+      // dry joint friction (MJCF frictionloss; domain randomization of dof_properties.friction scales this torque
+      // bound, column 8 of the DR node row -- not a PhysX-style friction coefficient): -f tanh(qd / v_s), linearly implicit
 #ifndef MG_NO_FRICTIONLOSS  // (A/B builds only)
       const float fl = np[8];  // nf[32] or the DR row's
 #else
@@ -2945,6 +2946,7 @@ struct Team {
       // which sensors' bodies each contact touches, one lane per contact (chunks of T lanes), as per-sensor bit masks
       // by ballots: sensor lane j then visits only its own contacts (a foot has one or two) instead of scanning all
       // of them with two dependent LDS lookups each; same contacts, same increasing order, so the same sums bit for bit
+      static_assert(MC <= 64, "the per-sensor contact masks are one 64-bit word");
       unsigned long long own = 0ull;
       const int nc = s->ncon;
       for (int c0 = 0; c0 < nc; c0 += T) {

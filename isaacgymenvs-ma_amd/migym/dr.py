@@ -16,7 +16,9 @@ the host to know which envs reset (``reset_buf.nonzero()``).  Here:
 
 Supported actor properties (everything the shipped task configs randomize):
   dof_properties       damping, stiffness (the PD drive's kp on position-driven DOFs), lower, upper,
-                       armature, effort, friction (the joint's dry friction bound, mg_model.frictionloss)
+                       armature, effort, friction (the joint's dry friction bound, mg_model.frictionloss:
+                       randomizing it scales the MuJoCo-style frictionloss torque bound f, DESIGN.md §4, not a
+                       PhysX-style joint friction coefficient -- parity unpinned)
   rigid_body_properties  mass (inertia rescaled with it, recomputeInertia=True)
   rigid_shape_properties friction (a contact's friction is the mean of its two shapes'), restitution
                        (accepted; the build's contacts are inelastic, so it has no effect)

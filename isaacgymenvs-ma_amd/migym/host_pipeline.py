@@ -86,6 +86,7 @@ class HostPipeline:
         for dev_bytes, hb, snap in self._host.values():
             if not torch.equal(hb, snap):
                 dev_bytes.copy_(hb, non_blocking=True)
+                snap.copy_(hb)   # the device now holds these bytes: the next push leaves them alone
 
     # ------------------------------------------------------------------ attribute surface
     def __getattr__(self, name):

@@ -386,6 +386,12 @@ def test_cpu_pipeline_host_views(task, n, how):
     st = c.get_env_state()
     assert all(v.device.type == "cpu" for v in st.values() if torch.is_tensor(v))
     assert int(st["progress_buf"][0]) == 123 and int(c.unwrapped.progress_buf[0]) == 123
+    # that push refreshed the snapshot: a device-side write made afterwards is not overwritten by the
+    # same host bytes at the next synced call
+    i = int(torch.nonzero(c.unwrapped.reset_buf == 0)[0, 0])
+    c.unwrapped.progress_buf[i] = 7
+    c.step(actions(g, 11).cpu())
+    assert int(c.progress_buf[i]) == 8 and int(c.unwrapped.progress_buf[i]) == 8
     g.close()
     c.close()
 

@@ -277,3 +277,78 @@ def test_sort_order_is_a_descending_permutation(task, n, env_cfg, mode):
             assert keys[0] > 0, "no constraint rows at all: the test would check nothing"
         prev_cost = cost
     env.close()
+
+
+def test_sorted_step_replays_from_a_captured_graph():
+    """The default work ordering holds no host-side state between launches (round 6, ADVICE r5: the totals had
+    alternated between two buffers by the host's launch parity, so a graph with an odd number of captured steps
+    replayed a sort on uncleared totals and could run one env twice): the step kernel that consumes a sort's
+    permutation zeroes the sort's totals.  One sorted Ant step captured in a HIP graph (torch.cuda.graph) and replayed
+    five times runs a valid permutation every replay, and its results equal, bit for bit, an unordered twin stepped
+    eagerly with the same frozen reset counter.  The in-kernel lists mode refuses capture."""
+    import numpy as np
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    n = 4099
+
+    def make(mode):
+        old = os.environ.get("MIGYM_ORDER")
+        os.environ["MIGYM_ORDER"] = mode
+        try:
+            cfg = configs.task_config("Ant", n, sim_device=DEV)
+            cfg["env"]["episodeLength"] = 5
+            return migym.make(seed=11, task="Ant", num_envs=n, sim_device=DEV, rl_device=DEV, headless=True,
+                              cfg={"task": cfg})
+        finally:
+            if old is None:
+                os.environ.pop("MIGYM_ORDER", None)
+            else:
+                os.environ["MIGYM_ORDER"] = old
+
+    env, twin = make("sort"), make("off")
+    g = torch.Generator(device=DEV).manual_seed(4)
+    a = torch.rand((n, env.num_actions), device=DEV, generator=g) * 2 - 1
+    for _ in range(2):   # eager: the second launch is the first sorted one
+        env.step(a)
+        twin.step(a)
+    frozen = env.control_steps
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(device=DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            env.step(a)   # captured, not run
+    torch.cuda.current_stream(DEV).wait_stream(side)
+    torch.cuda.synchronize()
+    for k in range(5):
+        graph.replay()
+        torch.cuda.synchronize()
+        twin.control_steps = frozen   # the graph's frozen reset counter
+        twin.step(a)
+        torch.cuda.synchronize()
+        m, order, _ = _work_order(env, n)
+        assert m == 2 and np.array_equal(np.sort(order), np.arange(n)), f"replay {k}: not a permutation"
+        for name, x, y in (("obs", env.obs_buf, twin.obs_buf), ("rew", env.rew_buf, twin.rew_buf),
+                           ("reset", env.reset_buf, twin.reset_buf), ("root", env.root_states, twin.root_states),
+                           ("dof", env.dof_state, twin.dof_state)):
+            assert torch.equal(x, y), f"replay {k}: {name} differs from the eager unordered twin"
+    lists = make("lists")
+    lists.step(a)
+    lists.step(a)
+    torch.cuda.synchronize()
+    graph2 = torch.cuda.CUDAGraph()
+    err = None
+    try:
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(graph2, stream=side):
+                lists.step(a)
+    except Exception as e:   # the refusal (possibly chained behind the graph's own end-of-capture error)
+        err = e
+    chain, e = "", err
+    while e is not None:
+        chain += str(e) + " | "
+        e = e.__context__
+    assert "cannot be captured" in chain, chain
+    torch.cuda.synchronize()
+    for e in (env, twin, lists):
+        e.close()
