@@ -153,8 +153,46 @@ __device__ __forceinline__ float prsq(float x) { return __builtin_amdgcn_rsqf(x)
 // sine and cosine of the physics' angles (joint angles in FK, the root's / object's half rotation per substep; five
 // pairs per lane and step).  HW: the hardware v_sin_f32 / v_cos_f32 on the argument in revolutions reduced to
 // [-1/2, 1/2] (a few instructions instead of the library's ~60; absolute error tools/trig_probe.hip), used by the
-// 16-lane instances (Ant, MA-Ant: +2 % same box); otherwise the library's sinf / cosf (the Humanoid's fast-spin parity
-// case rejects the hardware pair).  The task layer keeps the library's everywhere.
+// 16-lane instances (Ant, MA-Ant: +2 % same box); otherwise poly_sincos (round 6; before, the library's sinf / cosf:
+// the Humanoid's fast-spin parity case rejects the hardware pair).  The task layer keeps the
+// library's everywhere.
+//
+// poly_sincos: a polynomial pair (one Cody-Waite reduction by pi/2, Cephes' minimax polynomials on [-pi/4, pi/4]),
+// the physics' pair of the instances that are not 16-lane (MG_POLY_TRIG below).  Round 5's first form took the
+// quadrant as (int)rint(x 2/pi) and its first GPU run faulted; its source was not kept.  This
+// form never converts a float to an integer: the quadrant is k - 4 floor(k / 4) in floating point and the result is
+// picked by float compares, so a NaN / infinite / huge x can only give a NaN / wrong value, never an address or a
+// branch target.  MG_POLY_TRIG=2 rebuilds the integer-quadrant form for the disassembly check
+// (tests/test_trig_kat.py: host KAT of both forms over NaN, +-Inf, +-1e30, denormals and Cartpole-range angles).
+__host__ __device__ __forceinline__ void poly_sincos(float x, float* s, float* c, bool int_quadrant = false) {
+  const float k = rintf(x * 0.636619772367581343f);  // nearest multiple of pi / 2
+  const float r = ((x - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.54978995489188216e-8f;
+  const float z = r * r;
+  const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+  const float cp = 1.0f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
+  bool swap, ns, nc;
+  if (int_quadrant) {  // round 5's form (A/B disassembly only)
+    const int q = (int)k & 3;
+    swap = (q & 1) != 0;
+    ns = (q & 2) != 0;
+    nc = q == 1 || q == 2;
+  } else {
+    const float kq = k - 4.0f * floorf(k * 0.25f);  // 0, 1, 2, 3 for a finite k
+    swap = kq == 1.0f || kq == 3.0f;
+    ns = kq >= 2.0f;
+    nc = kq == 1.0f || kq == 2.0f;
+  }
+  const float sv = swap ? cp : sp, cv = swap ? sp : cp;
+  *s = ns ? -sv : sv;
+  *c = nc ? -cv : cv;
+}
+// the physics' pair outside the 16-lane instances (Humanoid, the hand, Cartpole): 1 = poly_sincos (round 6: GPU suite
+// green, 168 passed, the Humanoid fast-spin case included; same box, two passes, Humanoid 32,768 +1.0 %, ShadowHand
+// 4,096 +0.9 %, 16,384 +0.3 %, profiles/r06/ab_poly_trig.txt), 0 = the library's sinf / cosf, 2 = the integer-quadrant
+// form (disassembly check only)
+#ifndef MG_POLY_TRIG
+#define MG_POLY_TRIG 1
+#endif
 template <bool HW>
 __device__ __forceinline__ void psincos(float x, float* s, float* c) {
   if constexpr (HW) {
@@ -162,6 +200,8 @@ __device__ __forceinline__ void psincos(float x, float* s, float* c) {
     r = r - __builtin_rintf(r);
     *s = __builtin_amdgcn_sinf(r);
     *c = __builtin_amdgcn_cosf(r);
+  } else if constexpr (MG_POLY_TRIG != 0) {
+    poly_sincos(x, s, c, MG_POLY_TRIG == 2);
   } else {
     *s = sinf(x);
     *c = cosf(x);
