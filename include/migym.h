@@ -201,6 +201,12 @@ typedef struct mg_state_views {
   /* per-actor physical properties under domain randomization ((N*A, stride), see below); NULL = the
    * model's constants for every actor */
   const float* env_props;
+  /* gym.acquire_net_contact_force_tensor / refresh_net_contact_force_tensor (franka_reach_MA.py:506, 563):
+   * (N*A*nB, 3) in the rigid-body layout (hand tasks: the articulation's bodies, the object, the goal), the
+   * world-frame net contact force on each body over the last substep (contact impulses / h; + on a contact's
+   * side A, - on side B; the ground plane has no row).  Written by mg_sim_simulate and the fused step when bound;
+   * NULL = not computed. */
+  float* net_contact_forces;
 } mg_state_views;
 
 /* Task constants (cfg['env'] of the task YAML). */

@@ -182,7 +182,9 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
   t.load(root, v.dof_state + (size_t)2 * nd * ac, v.dof_actuation ? v.dof_actuation + (size_t)nd * ac : nullptr,
          OBJ ? root + 13 : nullptr, v.dof_targets ? v.dof_targets + (size_t)nd * ac : nullptr);
   for (int st = 0; st < p.substeps; st++) t.substep();
-  t.outputs(lds[team].v.st().sens, lds[team].v.st().dforce);
+  t.outputs(lds[team].v.st().sens, lds[team].v.st().dforce,
+            (valid && v.net_contact_forces) ? v.net_contact_forces + (size_t)3 * (m->num_bodies + (OBJ ? 2 : 0)) * a
+                                            : nullptr);
   t.stage_state();
   mg::wsync();
   if (valid) {
@@ -320,7 +322,8 @@ __device__ __forceinline__ void env_step_item(
     // no rigid-body states here: pose-only FK; DOF forces only where something reads them (the bound view, or the
     // Humanoid's observation: the reference's Ant and Cartpole never acquire a DOF-force tensor)
     t.template outputs<true>(L.st().sens,
-                             (v.dof_force || tp.task_id == MG_TASK_HUMANOID) ? L.st().dforce : nullptr);
+                             (v.dof_force || tp.task_id == MG_TASK_HUMANOID) ? L.st().dforce : nullptr,
+                             (valid && v.net_contact_forces) ? v.net_contact_forces + (size_t)3 * m->num_bodies * a : nullptr);
     t.stage_state();
   }
   mg::wsync();
@@ -633,7 +636,8 @@ __device__ __forceinline__ void hand_step_item(
     // controlFrequencyInv: gym.simulate x cfi between one pre- and one post_physics_step (vec_task.py:381-384)
     const int nsub = p.substeps * (tp.control_freq_inv > 1 ? tp.control_freq_inv : 1);
     for (int st = 0; st < nsub; st++) t.substep();
-    t.outputs(L.st().sens, L.st().dforce);
+    t.outputs(L.st().sens, L.st().dforce,
+              (valid && v.net_contact_forces) ? v.net_contact_forces + (size_t)3 * nbe * e : nullptr);
     t.stage_state();
   }
   mg::wsync();

@@ -2914,8 +2914,9 @@ struct Team {
   }
   // POSE: the caller reads no link velocity / axis afterwards (k_env_step; k_simulate and k_hand_step write the
   // rigid-body states from them)
+  // ncf_out: this actor's rows of the net contact force tensor (mg_state_views.net_contact_forces), or nullptr
   template <bool POSE = false>
-  __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out) {
+  __device__ __forceinline__ void outputs(float* sens_out, float* dforce_out, float* ncf_out = nullptr) {
     // the compact layout keeps the last substep's rows in region A, which fk() overwrites: each contact's impulse
     // sum goes to region B (fc) and a node's limit impulses to registers first
     float llo = 0.0f, lhi = 0.0f;
@@ -2935,6 +2936,34 @@ struct Team {
         if (sat & 4) lhi = s->rows()[lr + ((sat >> 1) & 1)].lam;
       }
       wsync();
+    }
+    // net contact forces (gym acquire_net_contact_force_tensor): lane per body (articulation bodies, then the object
+    // and the goal), the contacts in order as the oracle's net_contact_forces sums them: + on side A, - on side B
+    if (ncf_out) {
+      const int nb = m->num_bodies, nbe = nb + (OBJ ? 2 : 0), nc = s->ncon;
+      const float ihc = prcp(h);
+      for (int b = tl; b < nbe; b += T) {
+        V3 F = v3(0, 0, 0);
+        for (int c = 0; c < nc; c++) {
+          const int gA = cside(c, 2), gB = cside(c, 3);
+          const int bA = gA >= 0 ? mt->gbody[gA] : (gA == -2 ? nb : -1), bB = gB >= 0 ? mt->gbody[gB] : (gB == -2 ? nb : -1);
+          if (bA != b && bB != b) continue;
+          V3 f;
+          if constexpr (L::kCompact) {
+            f = ld3(s->fc(c));
+          } else {
+            const V3 n = ld3(s->cn[c]);
+            V3 t1, t2;
+            s->tangents(c, &t1, &t2);
+            f = n * s->rows()[3 * c].lam + t1 * s->rows()[3 * c + 1].lam + t2 * s->rows()[3 * c + 2].lam;
+          }
+          if (bA == b) F = F + f;
+          if (bB == b) F = F - f;
+        }
+        ncf_out[3 * b] = F.x * ihc;
+        ncf_out[3 * b + 1] = F.y * ihc;
+        ncf_out[3 * b + 2] = F.z * ihc;
+      }
     }
     fk<POSE>();  // post-step pose for the sensor body frames
     const float ih = prcp(h);  // impulses -> forces

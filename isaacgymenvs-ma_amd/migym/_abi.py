@@ -40,7 +40,7 @@ class StateViews(C.Structure):
     _fields_ = [("root_states", C.c_void_p), ("dof_state", C.c_void_p), ("dof_actuation", C.c_void_p),
                 ("sensors", C.c_void_p), ("dof_force", C.c_void_p), ("rigid_body_states", C.c_void_p),
                 ("dof_targets", C.c_void_p), ("rb_forces", C.c_void_p), ("rb_force_space", C.c_int32),
-                ("env_props_stride", C.c_int32), ("env_props", C.c_void_p)]
+                ("env_props_stride", C.c_int32), ("env_props", C.c_void_p), ("net_contact_forces", C.c_void_p)]
 
 
 # ---- domain randomization (include/migym.h; vec_task.py:612-842, dr_utils.py)

@@ -284,6 +284,25 @@ class VecTask(DomainRandomizationMixin, Env):
         elif pending_increment:
             self.randomize_buf_actors += 1
 
+    # ---------------------------------------------------------------------------------- gym tensor API
+    def acquire_net_contact_force_tensor(self) -> torch.Tensor:
+        """gym.acquire_net_contact_force_tensor + gymtorch.wrap_tensor (franka_reach_MA.py:506): the (N*A*nB, 3)
+        world-frame net contact force on each rigid body (hand tasks: the hand's bodies, the object, the goal) over
+        the last substep, in the rigid-body layout.  Binding it (mg_state_views.net_contact_forces) makes the fused
+        step and mg_sim_simulate write it every step; unbound, nothing computes it (the reference's Ant, Humanoid,
+        ShadowHand and Cartpole never acquire it).  Zero-copy, like every gym tensor here."""
+        t = getattr(self, "net_contact_force_tensor", None)
+        if t is None:
+            t = torch.zeros((self.num_actors * self.num_bodies, 3), device=self.device, dtype=torch.float32)
+            self.net_contact_force_tensor = t
+            self._views.net_contact_forces = _abi.ptr(t)
+            _abi.check(self._lib.mg_sim_bind(self.sim, _abi.C.byref(self._views)), self._lib)
+        return t
+
+    def refresh_net_contact_force_tensor(self):
+        """gym.refresh_net_contact_force_tensor (franka_reach_MA.py:563): a no-op -- the bound tensor is written by
+        the step itself"""
+
     def kernel_span_begin(self, n: int):
         """record the device-side duration (first wave start -> last wave end, GPU wall clock) of the next n fused
         step launches (mg_kernel_span_begin; 0 stops recording).  A measurement aid: bench.py's kernel_ms"""

@@ -2768,6 +2768,30 @@ static void sensor_outputs(const mg_model* m, const astate* s, const substep_out
   }
 }
 
+/* gym net contact forces (acquire_net_contact_force_tensor; franka_reach_MA.py:506, 563): per rigid body (the
+ * articulation's bodies, then the object and the goal for hand tasks), the world-frame sum of the last substep's
+ * contact impulses / h acting on it -- + on side A, - on side B of each contact (ground: no body) */
+static void net_contact_forces(const mg_model* m, const substep_out* so, float* ncf) {
+  const int nb = m->num_bodies, nbe = nb + (m->obj_type ? 2 : 0);
+  real F[MG_MAX_BODIES + 2][3];
+  memset(F, 0, sizeof(F));
+  for (int c = 0; c < so->ncon; c++) {
+    const contact* ct = &so->con[c];
+    const int bA = ct->geomA >= 0 ? m->geom_body[ct->geomA] : (ct->geomA == -2 ? nb : -1);
+    const int bB = ct->geomB >= 0 ? m->geom_body[ct->geomB] : (ct->geomB == -2 ? nb : -1);
+    real t1[3], t2[3], f[3];
+    tangent_basis(ct->n, t1, t2);
+    for (int a = 0; a < 3; a++)
+      f[a] = (so->lam[3 * c] * ct->n[a] + so->lam[3 * c + 1] * t1[a] + so->lam[3 * c + 2] * t2[a]) / so->h;
+    for (int a = 0; a < 3; a++) {
+      if (bA >= 0) F[bA][a] += f[a];
+      if (bB >= 0) F[bB][a] -= f[a];
+    }
+  }
+  for (int b = 0; b < nbe; b++)
+    for (int a = 0; a < 3; a++) ncf[3 * b + a] = (float)F[b][a];
+}
+
 static void load_object(astate* s, const float* row) {
   real nq = 0;
   for (int a = 0; a < 3; a++) { s->op[a] = row[a]; s->ov[a] = row[7 + a]; s->ow[a] = row[10 + a]; }
@@ -2845,7 +2869,7 @@ static void apply_env_props(const mg_model* m, const float* row, mg_model* mm, r
 
 static void simulate_env(const mg_model* m0, const mg_sim_params* p, float* root, float* dof, const float* act,
                          const float* tgt, float* sensors, float* dof_force, float* rbs, const float* oforce,
-                         int oforce_local, const float* props) {
+                         int oforce_local, const float* props, float* ncf) {
   astate s;
   memset(&s, 0, sizeof(s));
   mg_model* mdr = NULL;
@@ -2871,6 +2895,7 @@ static void simulate_env(const mg_model* m0, const mg_sim_params* p, float* root
   store_state(m, &s, root, dof);
   if (m->obj_type) store_object(&s, root + 13);
   sensor_outputs(m, &s, so, tau, sensors, dof_force);
+  if (ncf) net_contact_forces(m, so, ncf);
   if (rbs) {
     body_states(m, &s, rbs);
     if (m->obj_type) {
@@ -2898,7 +2923,8 @@ int orc_simulate_views(const mg_model* m, const mg_sim_params* p, int32_t n, con
                  v->rigid_body_states ? v->rigid_body_states + (size_t)13 * nb * e : 0,
                  (m->obj_type && v->rb_forces) ? v->rb_forces + ((size_t)nb * e + m->num_bodies) * 3 : 0,
                  v->rb_force_space == MG_LOCAL_SPACE,
-                 v->env_props ? v->env_props + (size_t)v->env_props_stride * e : 0);
+                 v->env_props ? v->env_props + (size_t)v->env_props_stride * e : 0,
+                 v->net_contact_forces ? v->net_contact_forces + (size_t)3 * nb * e : 0);
   }
   (void)threads;
   return 0;

@@ -248,11 +248,13 @@ class HostEnv:
         self.heading = np.zeros((n, 3), np.float32)
         self.noise = None
         self.env_props = None   # (n, stride) domain-randomized properties, or None
+        self.ncf = None         # (n, num_bodies, 3) net contact forces when bound (acquire_net_contact_force_tensor)
 
     def views(self):
         v = _abi.StateViews()
         v.root_states, v.dof_state, v.dof_actuation = p(self.root), p(self.dof), p(self.act_eff)
         v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), None
+        v.net_contact_forces = p(self.ncf)
         if self.env_props is not None:
             v.env_props, v.env_props_stride = p(self.env_props), self.env_props.shape[1]
         return v
@@ -271,6 +273,12 @@ class HostEnv:
     def post_physics(self, tp, seed=0, step=0, env_offset=0):
         v, b = self.views(), self.buffers(seed, step, env_offset)
         lib().orc_post_physics(C.byref(tp), C.byref(v), C.byref(b), self.n)
+
+    def simulate(self, model_np, sp, threads=0, fp32=False):
+        """gym.simulate alone on these buffers (orc_simulate_views: net contact forces too when self.ncf is set)"""
+        v = self.views()
+        (lib_f32() if fp32 else lib()).orc_simulate_views(model_np.ctypes.data, C.byref(sp), self.n, C.byref(v),
+                                                           threads)
 
     def env_step(self, model_np, sp, tp, seed=0, step=0, threads=0, env_offset=0, fp32=False):
         v, b = self.views(), self.buffers(seed, step, env_offset)
@@ -311,6 +319,7 @@ class HandHostEnv:
         self.sensors = np.zeros((n, len(spec.sensors) * 6), np.float32)
         self.dof_force = np.zeros((n, nd), np.float32)
         self.rbs = np.zeros((n, nb, 13), np.float32)
+        self.ncf = None   # (n, nb, 3) net contact forces when bound (acquire_net_contact_force_tensor)
         self.actions = np.zeros((n, na), np.float32)
         self.actions_out = np.zeros((n, na), np.float32)
         self.obs = np.zeros((n, no), np.float32)
@@ -338,6 +347,7 @@ class HandHostEnv:
         v.sensors, v.dof_force, v.rigid_body_states = p(self.sensors), p(self.dof_force), p(self.rbs)
         v.dof_targets = p(self.targets)
         v.rb_forces, v.rb_force_space = p(self.rb_forces), _abi.MG_LOCAL_SPACE
+        v.net_contact_forces = p(self.ncf)
         if self.env_props is not None:
             v.env_props, v.env_props_stride = p(self.env_props), self.env_props.shape[1]
         return v

@@ -414,3 +414,30 @@ def test_dof_force_tensor_where_the_reference_acquires_one(task, filled):
     if task == "Humanoid":
         ob = obs["obs"]
         torch.testing.assert_close(ob[:, 54:75], f * env.task_params.contact_force_scale, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("task,bodies", [("Ant", 9), ("MAAnt", 9), ("ShadowHand", 27)])
+def test_net_contact_force_tensor_through_the_step(task, bodies):
+    """acquire_net_contact_force_tensor / refresh_net_contact_force_tensor (franka_reach_MA.py:506, 563): the (N*A*nB, 3)
+    tensor is bound into the sim and written by every fused step; before it is acquired nothing computes it.  The
+    Ant's feet carry the weight (the net vertical contact force over all bodies of a resting env is about m g, gravity
+    along -z), the hand's object row (body 25) is pushed up by the palm, the goal row (26) stays zero."""
+    env = make(task, 64)
+    t = env.acquire_net_contact_force_tensor()
+    assert t.shape == (env.num_actors * bodies, 3) and t is env.acquire_net_contact_force_tensor()
+    for k in range(30):
+        env.step(actions(env, k) * 0.0)
+        env.refresh_net_contact_force_tensor()
+    torch.cuda.synchronize()
+    f = t.view(env.num_actors, bodies, 3)
+    assert bool(torch.isfinite(f).all()) and float(f.abs().max()) > 0.0
+    if task == "ShadowHand":
+        assert float(f[:, 26].abs().max()) == 0.0           # the kinematic goal never collides
+        assert float(f[:, 25, 2].max()) > 0.0                # the object rests on the palm in some envs
+    else:
+        fz = f[..., 2].sum(dim=1)                           # every body's vertical contact force, per actor
+        mg = float(env.model_spec.total_mass()) * 9.81 if hasattr(env.model_spec, "total_mass") else None
+        assert float(fz.median()) > 0.0                      # the ground pushes up
+        if mg is not None:
+            assert abs(float(fz.median()) - mg) < 0.5 * mg
+    env.close()

@@ -73,6 +73,7 @@ class DevHandEnv:
         self.rb_forces = T(h.rb_forces)
         self.force_prob = None if h.force_prob is None else T(h.force_prob)
         self.states = None if h.states is None else T(h.states)
+        self.ncf = None if h.ncf is None else T(h.ncf)
 
     def views(self):
         v = _abi.StateViews()
@@ -80,6 +81,7 @@ class DevHandEnv:
         v.sensors, v.dof_force, v.rigid_body_states = P(self.sensors), P(self.dof_force), P(self.rbs)
         v.dof_targets = P(self.targets)
         v.rb_forces, v.rb_force_space = P(self.rb_forces), _abi.MG_LOCAL_SPACE
+        v.net_contact_forces = P(self.ncf)
         return v
 
     def buffers(self, seed=0, step=0):
@@ -174,6 +176,8 @@ def _physics_vs_oracle(lib, spec, sp, h, rng, n, reach_cap=PS.REACH_CAP):
     """one simulate of the states h on the GPU and in the oracle; asserts determinism and per-env agreement"""
     # applied object forces (LOCAL_SPACE) on half of the envs
     h.rb_forces[: n // 2, len(spec.bodies)] = rng.normal(0, 0.3, (n // 2, 3))
+    # the net contact force tensor bound on both sides (acquire_net_contact_force_tensor, franka_reach_MA.py:506)
+    h.ncf = np.zeros((n, len(spec.bodies) + 2, 3), np.float32)
     e = DevHandEnv(h)
     h0 = copy.deepcopy(h)
     mnp = M.pack_model(spec)
@@ -201,7 +205,9 @@ def _physics_vs_oracle(lib, spec, sp, h, rng, n, reach_cap=PS.REACH_CAP):
     # reach go to MIGYM_PARITY_REPORT
     test = os.environ.get("PYTEST_CURRENT_TEST", "hand").split(" ")[0]
     scale = max(1.0, np.abs(h.sensors).max())
-    checks = [("object pose", rg[:, 1, 0:7], h.root[:, 1, 0:7], 2e-4, 0), ("object twist", rg[:, 1, 7:13], h.root[:, 1, 7:13], 2e-3, 2e-3),
+    ncf_scale = max(1.0, np.abs(h.ncf).max())
+    assert np.array_equal(np_(e2.ncf), np_(e.ncf)) and float(np.abs(h.ncf).max()) > 0.0
+    checks = [("net contact forces", np_(e.ncf), h.ncf, 1e-2 * ncf_scale, 0),("object pose", rg[:, 1, 0:7], h.root[:, 1, 0:7], 2e-4, 0), ("object twist", rg[:, 1, 7:13], h.root[:, 1, 7:13], 2e-3, 2e-3),
               ("dof pos", dg[..., 0], h.dof[..., 0], 2e-4, 0), ("dof vel", dg[..., 1], h.dof[..., 1], 2e-3, 2e-3),
               ("dof force", np_(e.dof_force), h.dof_force, 1e-2, 1e-2), ("rigid bodies", np_(e.rbs), h.rbs, 2e-3, 2e-3),
               ("sensors", np_(e.sensors), h.sensors, 1e-2 * scale, 0)]

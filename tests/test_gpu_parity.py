@@ -650,3 +650,40 @@ def test_multi_agent_make_full_size():
     assert obs["obs"].shape == (n * 4, 69) and rew.shape == (n * 4,)
     assert torch.isfinite(obs["obs"]).all()
     env.close()
+
+
+@pytest.mark.parametrize("task,n,z", [("Ant", 512, (0.25, 0.7)), ("Humanoid", 256, (0.6, 1.4))])
+def test_net_contact_forces_match_oracle(lib, task, n, z):
+    """gym's net contact force tensor (acquire / refresh_net_contact_force_tensor, franka_reach_MA.py:506, 563;
+    mg_state_views.net_contact_forces): after one gym.simulate from random states, every body's world-frame net
+    contact force equals the oracle's (orc_simulate_views' net_contact_forces) within 1 % of the batch's largest, like
+    the sensors.  (The hand's rows -- the object and the goal
+    included -- are checked in test_gpu_hand.py's physics tests.)"""
+    spec, sp, tp = setup(task)
+    rng = np.random.default_rng(11)
+    root, dof = random_states(spec, tp, n, rng, z)
+    act = (rng.uniform(-1, 1, (n, spec.num_dofs)) * (15.0 if task == "Ant" else 50.0)).astype(np.float32)
+    nb = len(spec.bodies)
+    mnp = M.pack_model(spec)
+    h = O.HostEnv(tp, spec, n)
+    h.root[:], h.dof[:], h.act_eff[:] = root, dof, act
+    h.ncf = np.zeros((n, nb, 3), np.float32)
+    h.simulate(mnp, sp, threads=8)
+    r_d, d_d, a_d = T(root), T(dof), T(act)
+    s_d = torch.zeros((n, max(len(spec.sensors), 1) * 6), device=DEV)
+    c_d = torch.full((n * nb, 3), float("nan"), device=DEV)   # every row must be written
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    v = _abi.StateViews()
+    v.root_states, v.dof_state, v.dof_actuation, v.sensors = P(r_d), P(d_d), P(a_d), P(s_d)
+    v.net_contact_forces = P(c_d)
+    _abi.check(lib.mg_sim_bind(sim, C.byref(v)), lib)
+    _abi.check(lib.mg_sim_simulate(sim, stream()), lib)
+    torch.cuda.synchronize()
+    lib.mg_sim_destroy(sim)
+    g = c_d.cpu().numpy().reshape(n, nb, 3)
+    assert np.isfinite(g).all()
+    scale = max(1.0, float(np.abs(h.ncf).max()))
+    assert float(np.abs(h.ncf).max()) > 1.0, "no contact force at all: the states would check nothing"
+    PS.record(f"test_net_contact_forces_match_oracle[{task}]", "net contact forces", g, h.ncf, scale=scale)
+    np.testing.assert_allclose(g, h.ncf, atol=1e-2 * scale)
