@@ -7,6 +7,17 @@
 
 #include "../../include/migym.h"
 
+// the compact team layout (team_physics.hpp TeamLDSC): the 16- and 32-lane locomotion instances, whose
+// LDS then holds twelve waves per CU.  Its ABA slots are per tree level (kCompactLevelSlots nodes at one depth at most),
+// which the dispatcher checks against the model (dispatch.hpp MG_FITS)
+#ifndef MG_COMPACT_LDS
+#define MG_COMPACT_LDS 1
+#endif
+constexpr int kCompactLevelSlots = 8;
+constexpr bool mg_compact_layout(int T, int MN, int OBJ) {
+  return MG_COMPACT_LDS && (T == 16 || T == 32) && OBJ == 0 && MN <= 32;
+}
+
 struct mg_sim {
   mg_model host_model;
   mg_model* d_model;

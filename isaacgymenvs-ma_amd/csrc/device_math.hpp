@@ -147,9 +147,19 @@ __device__ __forceinline__ Sym6 body_inertia(float m, V3 c, const float* Ic) {
 }
 // reciprocal / square root / inverse square root of the physics: the 1-ulp hardware instructions instead
 // of the correctly rounded sequences (~10 instructions each); the task layer keeps IEEE division
+// (MG_EXACT_RCP: the correctly rounded forms, a parity A/B only)
+#ifndef MG_EXACT_RCP
+#define MG_EXACT_RCP 0
+#endif
+#if MG_EXACT_RCP
+__device__ __forceinline__ float prcp(float x) { return 1.0f / x; }
+__device__ __forceinline__ float psqrt(float x) { return sqrtf(x); }
+__device__ __forceinline__ float prsq(float x) { return 1.0f / sqrtf(x); }
+#else
 __device__ __forceinline__ float prcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float psqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float prsq(float x) { return __builtin_amdgcn_rsqf(x); }
+#endif
 // sine and cosine of the physics' angles (joint angles in FK, the root's / object's half rotation per substep; five
 // pairs per lane and step).  HW: the hardware v_sin_f32 / v_cos_f32 on the argument in revolutions reduced to
 // [-1/2, 1/2] (a few instructions instead of the library's ~60; absolute error tools/trig_probe.hip), used by the

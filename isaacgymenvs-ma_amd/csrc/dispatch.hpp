@@ -47,13 +47,24 @@ struct RunEnvStep {
 template <int I>
 int phase_buf_publish(unsigned long long* buf);
 
+// the most tree nodes at one depth (the compact layout's ABA slots hold kCompactLevelSlots)
+inline int level_width(const mg_model& m) {
+  int depth[MG_MAX_NODES] = {0}, cnt[MG_MAX_NODES + 1] = {0}, w = 0;
+  for (int i = 1; i < m.num_nodes && i < MG_MAX_NODES; i++) {
+    depth[i] = (m.parent[i] >= 0 && m.parent[i] < i) ? depth[m.parent[i]] + 1 : 1;
+    const int c = ++cnt[depth[i]];
+    w = c > w ? c : w;
+  }
+  return w;
+}
 inline int model_lanes(const mg_model& m) {
   const int nv = (m.fixed_base ? 0 : 6) + m.num_dofs + (m.obj_type ? 6 : 0);
   return nv > m.num_sensors ? nv : m.num_sensors;
 }
 #define MG_FITS(T, MN, MC, MG, MP, OBJ)                                                              \
   (m.num_nodes <= MN && max_contacts <= MC && model_lanes(m) <= T && (m.fixed_base || T >= 6) &&   \
-   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ))
+   m.num_geoms <= MG && m.num_pairs <= MP && m.obj_type == (int)(OBJ) &&                         \
+   (!mg_compact_layout(T, MN, OBJ) || level_width(m) <= kCompactLevelSlots))
 
 // team size the dispatcher picks for a model (0: none fits)
 inline int team_size(const mg_model& m, int max_contacts) {

@@ -21,6 +21,10 @@
 #ifndef MG_WAVES_COMPACT
 #define MG_WAVES_COMPACT 3
 #endif
+// the compact 32-lane instances (Humanoid) on the static grid too (1) or on the work queue (0)
+#ifndef MG_COMPACT_STATIC32
+#define MG_COMPACT_STATIC32 0
+#endif
 // dynamic LDS added to every step-kernel launch (0; an occupancy A/B variant pads it to hold fewer waves per CU)
 // an explicit VGPR budget for k_env_step (0: the waves_per_eu budget); register-pressure experiments only
 #ifndef MG_NUM_VGPR
@@ -68,18 +72,21 @@ static __device__ unsigned long long* g_phase_buf;
 // 256-register budget, 12 at 168).
 template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
 struct Shape {
-  using TL = mg::TeamLDSOf<T, MN, MC, OBJ>;
+  using TL = mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP>;
   static constexpr int E1 = 64 / T;  // teams (actors) per wave
-  // waves per SIMD of the instance (the register budget: 2 -> 256 VGPRs, 3 -> 168) and per CU
-  static constexpr int kWPE = (TL::kCompact && !DR) ? MG_WAVES_COMPACT : MG_WAVES_PER_EU;
-  static constexpr int kMaxWaves = 4 * kWPE;
   static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OBJ)>);
   static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<TL, T>) + (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
-  static constexpr int per_cu(int w) {
+  static constexpr int fit(int w, int cap) {  // resident waves per CU with w-wave blocks, at most cap
     const size_t blk = (kTile + w * kWave + 511) / 512 * 512;
     const int b = (int)((160 * 1024) / blk);
-    return b * w < kMaxWaves ? b * w : kMaxWaves;
+    return b * w < cap ? b * w : cap;
   }
+  // waves per SIMD of the instance (the register budget: 2 -> 256 VGPRs, 3 -> 168): 3 for the compact layouts whose
+  // LDS holds twelve waves per CU with some block width (Ant, MA-Ant, Humanoid), else 2
+  static constexpr bool fits12() { return fit(1, 12) >= 12 || fit(2, 12) >= 12 || fit(4, 12) >= 12 || fit(8, 12) >= 12; }
+  static constexpr int kWPE = (TL::kCompact && !DR && fits12()) ? MG_WAVES_COMPACT : MG_WAVES_PER_EU;
+  static constexpr int kMaxWaves = 4 * kWPE;
+  static constexpr int per_cu(int w) { return fit(w, kMaxWaves); }
   static constexpr int pick() {
     int best = 1;
     for (int w = 2; w <= 8; w *= 2)
@@ -93,7 +100,7 @@ struct Shape {
   // one work item per wave on a static grid (no work queue): the one-wave blocks, and the compact instances'
   // two-wave blocks (a block's waves hold envs of like cost under the sort, so little of its LDS waits on a slower
   // partner, and the queue's loop costs registers at the 168-VGPR budget)
-  static constexpr bool kStatic = W == 1 || TL::kCompact;
+  static constexpr bool kStatic = W == 1 || (TL::kCompact && (T == 16 || MG_COMPACT_STATIC32));
 };
 
 // ------------------------------------------------------------------------------------------------ work queue
@@ -154,7 +161,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
   using SH = Shape<T, MN, MC, MG, MP, OBJ, DR>;
   constexpr int E = SH::E, W = SH::W;
   constexpr int ROWS = OBJ ? 3 : 1;
-  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OBJ>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::copy_tile(&tile, static_cast<const typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT*>(timg));
@@ -270,7 +277,7 @@ __device__ __forceinline__ void order_done(const MgOrder& ord, int grid_waves) {
 // one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void env_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0, MG, MP>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
@@ -281,7 +288,7 @@ __device__ __forceinline__ void env_step_item(
   const int a = ordered_actor(ord, slot, n, tp.num_agents);
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
-  mg::TeamLDSOf<T, MN, MC, 0>& L = lds[team].v;
+  mg::TeamLDSOf<T, MN, MC, 0, MG, MP>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, 0, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
@@ -490,7 +497,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
   constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0, MG, MP>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -532,7 +539,7 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // one work item of k_hand_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void hand_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT, MG, MP>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
@@ -543,7 +550,7 @@ __device__ __forceinline__ void hand_step_item(
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
-  mg::TeamLDSOf<T, MN, MC, OT>& L = lds[team].v;
+  mg::TeamLDSOf<T, MN, MC, OT, MG, MP>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, OT, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
@@ -785,7 +792,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
   constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT, MG, MP>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -908,7 +915,7 @@ int RunSimulate<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim) {
 template <int T, int MN, int MC, int MG, int MP, int OBJ>
 int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp,
                                              const mg_task_buffers* tb, const mg_replay* rp) {
-  using TL = mg::TeamLDSOf<T, MN, MC, OBJ>;
+  using TL = mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP>;
   if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_env_step: no model tile (model exceeds every kernel instance)");
   // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
   if (!OBJ && (size_t)tp->num_obs * sizeof(float) > TL::kObsStageBytes)

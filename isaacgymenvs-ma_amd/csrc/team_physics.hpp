@@ -33,6 +33,7 @@
 #include "convex.hpp"
 #include "device_math.hpp"
 #include "hull.hpp"
+#include "common.hpp"
 
 #include <type_traits>
 
@@ -42,7 +43,57 @@ namespace mg {
 // reference arithmetic in task.hpp / hand_task.hpp keeps contraction off).  The caller's FP state is
 // restored at the end of this header.
 #pragma float_control(push)
+#ifndef MG_PHYS_CONTRACT
+#define MG_PHYS_CONTRACT 1  // 0: no FMA contraction in the physics (a parity A/B only)
+#endif
+#if MG_PHYS_CONTRACT
 #pragma clang fp contract(fast)
+#else
+#pragma clang fp contract(off)
+#endif
+// per-phase contraction switches (parity A/B: which phase's FMA contraction moves the results off the fp64 oracle;
+// MG_NOCONTRACT_MASK bits: 1 PGS visit, 2 ABA, 4 test solves, 8 FK, 16 integrate + velocity cap, 32 row Jacobians)
+#ifndef MG_NOCONTRACT_MASK
+#define MG_NOCONTRACT_MASK 0
+#endif
+#define MG_NC_OFF _Pragma("clang fp contract(off)")
+// PGS visit products kept out of FMAs: 1 the velocity update nu += Y dl (the default, round 6), 2 the impulse update.
+// Fusing the velocity update moved the DOF velocities off the fp64 oracle: the fraction of them within north_star's
+// 1e-4 relative fell 0.8 % below the oracle's own fp32 build (Ant 16,384 / 65,536, MA-Ant), against 0.25 % unfused
+// (the per-phase A/B: only this product matters; profiles/r06/ab_pgs_fusion.txt); it costs Ant 65,536 1.3 %
+#ifndef MG_PGS_UNFUSE
+#define MG_PGS_UNFUSE 1
+#endif
+#if MG_NOCONTRACT_MASK & 1
+#define MG_NC_PGS MG_NC_OFF
+#else
+#define MG_NC_PGS
+#endif
+#if MG_NOCONTRACT_MASK & 2
+#define MG_NC_ABA MG_NC_OFF
+#else
+#define MG_NC_ABA
+#endif
+#if MG_NOCONTRACT_MASK & 4
+#define MG_NC_TS MG_NC_OFF
+#else
+#define MG_NC_TS
+#endif
+#if MG_NOCONTRACT_MASK & 8
+#define MG_NC_FK MG_NC_OFF
+#else
+#define MG_NC_FK
+#endif
+#if MG_NOCONTRACT_MASK & 16
+#define MG_NC_INT MG_NC_OFF
+#else
+#define MG_NC_INT
+#endif
+#if MG_NOCONTRACT_MASK & 32
+#define MG_NC_JAC MG_NC_OFF
+#else
+#define MG_NC_JAC
+#endif
 
 // Block-shared LDS copy of the model tables the hot loops read ("model tile"):
 // every per-node / per-geom constant is an LDS read (~64 cycles) instead of a dependent global load.
@@ -57,6 +108,7 @@ struct alignas(16) ModelTile {
   int parent[MN], jtype[MN], limited[MN];
   unsigned long long children[MN];
   unsigned long long anc[MN];   // ancestor mask of each node (itself and the root included)
+  int lvs[MN];                  // the node's index among the nodes of its depth (compact layout's ABA slot)
   float nf[MN][33];   // 0-8 Rr0, 9-11 t, 12-14 axis, 15-17 com, 18-23 inertia, 24 mass, 25 arm, 26 damp,
                       // 27 stiff, 28 lower, 29 upper, 30 drive kp, 31 effort limit, 32 frictionloss
   int gtype[MG], gnode[MG], gbody[MG], gfil[MG];
@@ -89,8 +141,19 @@ __host__ __device__ void build_tile(ModelTile<MN, MG, MP, HV>* t, const mg_model
       if (m->parent[k] == i) ch |= 1ull << k;
     t->children[i] = ch;
     unsigned long long an = 1ull;
-    for (int k = i; k > 0; k = m->parent[k]) an |= 1ull << k;
+    int di = 0;
+    for (int k = i; k > 0; k = m->parent[k]) {
+      an |= 1ull << k;
+      di++;
+    }
     t->anc[i] = an;
+    int lv = 0;  // nodes of the same depth before this one
+    for (int k = 1; k < i; k++) {
+      int dk = 0;
+      for (int j = k; j > 0; j = m->parent[j]) dk++;
+      lv += dk == di ? 1 : 0;
+    }
+    t->lvs[i] = i > 0 ? lv : 0;
     float* f = t->nf[i];
     const M3 R0 = quat_to_mat(m->r0[i][0], m->r0[i][1], m->r0[i][2], m->r0[i][3]);
     for (int a = 0; a < 3; a++)
@@ -330,13 +393,14 @@ struct TeamLDS {
   // ---- accessors: the Team reaches every phase-scoped region through these, so the compact layout below (the
   // 16-lane locomotion instances) can place the regions differently
   static constexpr bool kCompact = false;
+  static constexpr bool kGwInA = false;
   static constexpr size_t kObsStageBytes = sizeof(Row) * MR;   // the locomotion observation staging (the dead rows)
   static constexpr size_t kGwFloats = (size_t)MN * 27;          // geom frames + pair list + candidate map (collide)
   static constexpr size_t kUtFloats = (size_t)RB * MN;          // the test solves' ut slab (and their y rows)
   __device__ __forceinline__ Row* rows() { return u.sv.rows; }
   __device__ __forceinline__ Stage& st() { return u.sv.st; }
   __device__ __forceinline__ float* qvsc() { return &u.slot[0][0]; }
-  __device__ __forceinline__ float* slot(int node) { return u.slot[node]; }
+  __device__ __forceinline__ float* slot(int node, int) { return u.slot[node]; }
   __device__ __forceinline__ float* acc(int node) { return u.sv.ts.aba.acc[node]; }
   __device__ __forceinline__ float* aproot() { return u.sv.ts.aba.proot; }
   __device__ __forceinline__ float* l0() { return L0; }
@@ -356,29 +420,42 @@ struct TeamLDS {
   }
 };
 
-// The compact team layout of the 16-lane locomotion instances (Ant, MA-Ant; MG_COMPACT_LDS): 4.2 -> 2.8 KB per team,
-// so that twelve waves fit a CU's 160 KB (three per SIMD) instead of eight.  What it changes against TeamLDS:
-//   * region A holds the poses R, x, V from fk() to collide()'s geom staging, then the contact gaps (row b of the
-//     contact's normal row, from collide()) and the constraint rows (build_rows() to outputs()), then the observation
-//     staging; the rows no longer sit next to the test-solve slab;
-//   * region B holds fk()'s joint sines, the ABA child slots (nodes >= 1 only), the ABA forward pass with the root
-//     factor and inverse (L0, Iinv: dead once the root coupling Wv is taken, right after aba()), collide()'s geom
-//     frames, the test-solve slab, and after the step the stage rows plus the contacts' impulse sums that outputs()
-//     stashes before its fk() overwrites region A;
-//   * no tangent basis is stored (recomputed from the normal by tangent_basis_t, the same bits), no gap array, and the
-//     limit-row metadata is one byte per row.
-// The ancestor masks live in the block's model tile for every instance.
-template <int T, int MN, int MC>
+// The compact team layout of the 16- and 32-lane locomotion instances (Ant, MA-Ant, Humanoid; MG_COMPACT_LDS,
+// common.hpp mg_compact_layout): Ant 4.2 -> 2.8 KB per team, Humanoid 9.0 -> 5.6 KB, so that twelve waves fit a CU's
+// 160 KB (three per SIMD) instead of eight.  What it changes against TeamLDS:
+//   * region A holds the poses R, x, V from fk() to collide()'s geom staging, then the constraint rows (build_rows()
+//     to outputs()), then the observation staging.  The 16-lane layout also keeps each contact's gap in its normal
+//     row's b from collide() on; the 32-lane one keeps a gap array and stages collide()'s geom frames in region A
+//     instead (read the poses, wave sync, write the frames);
+//   * region B holds fk()'s joint sines, the ABA child slots (one per node of a tree level: kCompactLevelSlots, the
+//     node's index within its depth from the tile), the ABA forward pass with the root factor and inverse (L0, Iinv:
+//     dead once the root coupling Wv is taken, right after aba()), the 16-lane layout's geom frames, the test-solve
+//     slab, and after the step the stage rows plus the contacts' impulse sums that outputs() stashes before its fk()
+//     overwrites region A;
+//   * no tangent basis is stored (recomputed from the normal by tangent_basis_t, the same bits) and the limit-row
+//     metadata is one byte per row (two for more than 16 nodes).
+// The ancestor masks and the nodes' level slots live in the block's model tile for every instance.
+#ifndef MG_RB_LOCO32C
+#define MG_RB_LOCO32C 6   // test-solve columns per batch of the compact 32-lane teams
+#endif
+#ifndef MG_KJY_LOCO32C
+#define MG_KJY_LOCO32C 8  // register rows of (J, Y) of the compact 32-lane teams
+#endif
+template <int T, int MN, int MC, int MG, int MP>
 struct TeamLDSC {
-  static_assert(MN <= 16, "the compact limit-row metadata packs the node in 4 bits");
+  static_assert(MN <= 32, "the compact limit-row metadata packs the node in 12 bits at most");
+  // geom frames (13 floats per geom) and the pair list in region A (and a gap array) for the 32-lane teams and where
+  // they do not fit region B's slots; else in region B
+  static constexpr bool kGwInA = T >= 32 || MG * 13 + MP > kCompactLevelSlots * 27;
   static constexpr int MR = (3 * MC + 2 * (MN - 1) + kPgsPrefetch - 1) / kPgsPrefetch * kPgsPrefetch;
-  static constexpr int RB = T >= 32 ? MG_RB_LOCO32 : (kRBLoco <= T ? kRBLoco : 6);
-  static constexpr int KR0 = T >= 32 ? MG_KJY_LOCO32 : kJYRegs;
+  static constexpr int RB = T >= 32 ? MG_RB_LOCO32C : (kRBLoco <= T ? kRBLoco : 6);
+  static constexpr int KR0 = T >= 32 ? MG_KJY_LOCO32C : kJYRegs;
   static constexpr int KR = (KR0 < MR ? KR0 : MR) / kPgsPrefetch * kPgsPrefetch;
   static constexpr int PBL = 0;
   static constexpr int OROWS = 1;
   static constexpr int HX = 0;
   static constexpr bool kCompact = true;
+  using LM = typename std::conditional<(MN <= 16), uint8_t, uint16_t>::type;
   struct alignas(16) Row { float b, iw, lam, mu; };
   struct Stage {
     float root[13];
@@ -392,7 +469,8 @@ struct TeamLDSC {
   int ncon, nrows;
   float cp[MC][3], cn[MC][3];
   int cside[MC];  // packed int8 [node A, node B, geom A, geom B]
-  uint8_t lmeta[(2 * (MN - 1) + 3) / 4 * 4];  // limit rows: kind | node << 4
+  float cd[kGwInA ? MC : 1];
+  LM lmeta[(2 * (MN - 1) + 3) / 4 * 4];  // limit rows: kind | node << 4
   union {  // region A
     struct {
       float R[MN][9];
@@ -402,7 +480,7 @@ struct TeamLDSC {
     Row rowsA[MR];
   };
   union {  // region B
-    float slots[MN > 1 ? MN - 1 : 1][27];
+    float slots[kCompactLevelSlots][27];
     struct {
       float acc[MN][6];
       float proot[6];
@@ -426,36 +504,38 @@ struct TeamLDSC {
     };
   };
   static_assert(sizeof(Stage) >= sizeof(float) * 4 * MN, "the stash must lie past fk()'s joint sines");
-  static constexpr size_t kObsStageBytes = sizeof(Row) * MR > sizeof(float) * 18 * MN ? sizeof(Row) * MR : sizeof(float) * 18 * MN;
-  static constexpr size_t kGwFloats = (size_t)(MN > 1 ? MN - 1 : 1) * 27;
+  static_assert(sizeof(slots) >= sizeof(float) * 4 * MN, "fk()'s joint sines must fit region B");
+  static constexpr size_t kRegionA = sizeof(Row) * MR > sizeof(float) * 18 * MN ? sizeof(Row) * MR : sizeof(float) * 18 * MN;
+  static constexpr size_t kObsStageBytes = kRegionA;
+  static constexpr size_t kGwFloats = kGwInA ? kRegionA / sizeof(float) : (size_t)kCompactLevelSlots * 27;
   static constexpr size_t kUtFloats = (size_t)RB * MN;
   __device__ __forceinline__ Row* rows() { return rowsA; }
   __device__ __forceinline__ Stage& st() { return post.st; }
   __device__ __forceinline__ float* qvsc() { return &slots[0][0]; }
-  __device__ __forceinline__ float* slot(int node) { return slots[node - 1]; }  // nodes >= 1 publish
+  __device__ __forceinline__ float* slot(int, int lv) { return slots[lv]; }  // by the node's slot in its level
   __device__ __forceinline__ float* acc(int node) { return aba.acc[node]; }
   __device__ __forceinline__ float* aproot() { return aba.proot; }
   __device__ __forceinline__ float* l0() { return aba.L0; }
   __device__ __forceinline__ float* iinv() { return aba.Iinv; }
   __device__ __forceinline__ float* ut(int q) { return ts.ut[q]; }
   __device__ __forceinline__ float* tsroot(int q) { return ts.proot[q]; }
-  __device__ __forceinline__ float* gw() { return &slots[0][0]; }
+  __device__ __forceinline__ float* gw() { return kGwInA ? &rowsA[0].b : &slots[0][0]; }
   __device__ __forceinline__ float* obs_stage() { return &rowsA[0].b; }
   __device__ __forceinline__ float* fc(int c) { return post.fc[c]; }
-  __device__ __forceinline__ float gap(int c) const { return rowsA[3 * c].b; }
-  __device__ __forceinline__ void set_gap(int c, float d) { rowsA[3 * c].b = d; }
+  __device__ __forceinline__ float gap(int c) const { return kGwInA ? cd[c] : rowsA[3 * c].b; }
+  __device__ __forceinline__ void set_gap(int c, float d) {
+    if constexpr (kGwInA) cd[c] = d;
+    else rowsA[3 * c].b = d;
+  }
   __device__ __forceinline__ int lm(int i) const { return lmeta[i]; }
-  __device__ __forceinline__ void set_lm(int i, int v) { lmeta[i] = (uint8_t)v; }
+  __device__ __forceinline__ void set_lm(int i, int v) { lmeta[i] = (LM)v; }
   __device__ __forceinline__ void tangents(int c, V3* t1, V3* t2) const { tangent_basis_t(ld3(cn[c]), t1, t2); }
   __device__ __forceinline__ void set_tangents(int, V3, V3) {}
 };
-#ifndef MG_COMPACT_LDS
-#define MG_COMPACT_LDS 1
-#endif
-// the team layout of an instance: compact for the 16-lane locomotion teams
-template <int T, int MN, int MC, int OBJ>
-using TeamLDSOf = typename std::conditional<(MG_COMPACT_LDS && T == 16 && OBJ == 0 && MN <= 16), TeamLDSC<T, MN, MC>,
-                                            TeamLDS<T, MN, MC, OBJ>>::type;
+// the team layout of an instance (common.hpp mg_compact_layout)
+template <int T, int MN, int MC, int OBJ, int MG, int MP>
+using TeamLDSOf =
+    typename std::conditional<mg_compact_layout(T, MN, OBJ), TeamLDSC<T, MN, MC, MG, MP>, TeamLDS<T, MN, MC, OBJ>>::type;
 
 // A team's LDS region padded so that consecutive teams start 4*T bytes apart modulo 128 B.  A
 // ds_read/write_b32 is serviced per 32-lane half with bank = dword address mod 32, so teams of
@@ -838,7 +918,7 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
 // own kernel instances, so the PGS instances are the code they were
 template <int T, int MN, int MC, int MG, int MP, int OBJ = 0, bool TGS = false>
 struct Team {
-  using L = TeamLDSOf<T, MN, MC, OBJ>;
+  using L = TeamLDSOf<T, MN, MC, OBJ, MG, MP>;
   using MT = ModelTile<MN, MG, MP, tile_hull_verts(OBJ)>;
   static constexpr int MR = L::MR;
 #ifndef MG_HW_TRIG_T16
@@ -979,6 +1059,7 @@ struct Team {
   // by the same operations either way)
   template <bool POSE = false>
   __device__ __forceinline__ void fk() {
+    MG_NC_FK
     if (OBJ) oR = quat_to_mat(oq[0], oq[1], oq[2], oq[3]);
     const M3 Rr = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
     if (tl == 0) {
@@ -1061,6 +1142,7 @@ struct Team {
 
   // ---------------------------------------------------------------- ABA (unconstrained step)
   __device__ __forceinline__ void aba() {
+    MG_NC_ABA
     if (node >= 0) {
       const V3 o = ld3(s->x[0]);
       const float* nf = mt->nf[node];
@@ -1127,6 +1209,9 @@ struct Team {
     }
     ph_mark(16);
     for (int lev = maxdepth; lev >= 1; lev--) {
+      // compact layout: the slots are per level, so this level's writes reuse the slots the previous level's parents
+      // read just before (a wave's LDS operations complete in order; the sync keeps the compiler from moving them)
+      if constexpr (L::kCompact) wsync();
       if (node > 0 && depth == lev) {
         U = mul(IA, S);
         Dinv = prcp(dot(S, U) + Dj);
@@ -1134,7 +1219,7 @@ struct Team {
         Sym6 Ia = IA;
         rank1_sub(Ia, U, Dinv);
         SV pa = pA + mul(Ia, c) + U * (u * Dinv);
-        float* sl = s->slot(node);
+        float* sl = s->slot(node, mt->lvs[node]);
         for (int k = 0; k < 6; k++) { sl[k] = Ia.a[k]; sl[15 + k] = Ia.c[k]; }
         for (int k = 0; k < 9; k++) sl[6 + k] = Ia.b[k];
         sl[21] = pa.a.x; sl[22] = pa.a.y; sl[23] = pa.a.z;
@@ -1149,7 +1234,7 @@ struct Team {
         while (ch) {
           const int k = __builtin_ctzll(ch);
           ch &= ch - 1;
-          const float* sl = s->slot(k);
+          const float* sl = s->slot(k, mt->lvs[k]);
           for (int q = 0; q < 6; q++) { IA.a[q] += sl[q]; IA.c[q] += sl[15 + q]; }
           for (int q = 0; q < 9; q++) IA.b[q] += sl[6 + q];
           pA = pA + sv(v3(sl[21], sl[22], sl[23]), v3(sl[24], sl[25], sl[26]));
@@ -1277,6 +1362,7 @@ struct Team {
   // level by level, each lane gathers its ancestor's y values with one bpermute per column (no LDS
   // round trip or barrier per level).  y[q] = this lane's entry of Y_{r0+q} (0 off the columns).
   __device__ __forceinline__ void test_solve(int r0, int nrows_, const float* Wv, float* y) {
+    MG_NC_TS
     for (int i = tl; i < L::RB * MN; i += T) s->ut(0)[i] = 0.0f;
     wsync();
     if (tl < L::RB) {
@@ -1484,6 +1570,7 @@ struct Team {
   // g = Sl_ang x (p - o) + Sl_lin, so J_r = sign (d_r . g) (= sign Sl . [(p - o) x d_r; d_r]).
   // Limit rows: +-1 on the DOF's lane.  Object lanes: the stored object part of the contact rows.
   __device__ __forceinline__ void batch_jacobians(int r0, int nrows_, float* J) const {
+    MG_NC_JAC
 #pragma unroll
     for (int q = 0; q < 3; q++) J[q] = 0.0f;
     if (OBJ && objl) {
@@ -1931,14 +2018,37 @@ struct Team {
     int base = 0;
     const int G = mt->ng;
     static_assert(L::kGwFloats >= MG * GW, "geom frames must fit the team's union storage");
-    for (int g = tl; g < G; g += T) {
-      V3 c;
-      M3 Rg;
-      geom_world(g, &c, &Rg);
-      float* w = gw_tile() + GW * g;
-      w[0] = c.x; w[1] = c.y; w[2] = c.z;
-      for (int a = 0; a < 3; a++)
-        for (int b = 0; b < 3; b++) w[3 + 3 * a + b] = Rg.m[a][b];
+    if constexpr (L::kCompact && L::kGwInA) {
+      // the frames go to region A over the poses they are built from: every lane reads its geoms' poses first
+      constexpr int GPL = (MG + T - 1) / T;
+      V3 cs[GPL];
+      M3 Rs[GPL];
+#pragma unroll
+      for (int j = 0; j < GPL; j++) {
+        cs[j] = v3(0, 0, 0);
+        if (tl + j * T < G) geom_world(tl + j * T, &cs[j], &Rs[j]);
+      }
+      wsync();
+#pragma unroll
+      for (int j = 0; j < GPL; j++) {
+        const int g = tl + j * T;
+        if (g < G) {
+          float* w = gw_tile() + GW * g;
+          w[0] = cs[j].x; w[1] = cs[j].y; w[2] = cs[j].z;
+          for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) w[3 + 3 * a + b] = Rs[j].m[a][b];
+        }
+      }
+    } else {
+      for (int g = tl; g < G; g += T) {
+        V3 c;
+        M3 Rg;
+        geom_world(g, &c, &Rg);
+        float* w = gw_tile() + GW * g;
+        w[0] = c.x; w[1] = c.y; w[2] = c.z;
+        for (int a = 0; a < 3; a++)
+          for (int b = 0; b < 3; b++) w[3 + 3 * a + b] = Rg.m[a][b];
+      }
     }
     wsync();
     // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
@@ -2582,6 +2692,7 @@ struct Team {
     float tisp = ihs, tbz = TGS ? p->baumgarte : 0.0f;
     const int n_sweeps = TGS ? p->pos_iters + max(p->pos_iters, p->vel_iters) : p->pos_iters;
     auto visit = [&](float J, float Y, const typename L::Row& R, int r) {
+      MG_NC_PGS
       const float v = team_sum<T>(J * nu, tb);
       const float lam = R.lam, m = R.mu;
       // friction rows (m = mu >= 0): [-mu lambda_n, mu lambda_n]; normal / limit rows (m < 0):
@@ -2595,10 +2706,22 @@ struct Team {
         const float te = e >= 0.0f ? -e * tisp : fminf(-tbz * e * ihs, p->max_depen_vel);
         tgt = fric ? 0.0f : te;
       }
+#if MG_PGS_UNFUSE & 2
+      float dlr = (tgt - v) * R.iw;
+      asm volatile("" : "+v"(dlr));  // (A/B: the impulse update's product rounded, not fused)
+      const float lnew = __builtin_amdgcn_fmed3f(lam + dlr, -t, hi);
+#else
       const float lnew = __builtin_amdgcn_fmed3f(lam + (tgt - v) * R.iw, -t, hi);
+#endif
       lamn = m == -1.0f ? lnew : lamn;
       s->rows()[r].lam = lnew;
+#if MG_PGS_UNFUSE & 1
+      float dv = Y * (lnew - lam);
+      asm volatile("" : "+v"(dv));  // (A/B: the velocity update's product rounded, not fused)
+      nu += dv;
+#else
       nu += Y * (lnew - lam);
+#endif
     };
     const int pa = prow < KR ? prow : KR;  // rows of part A
     float pJ[PF], pY[PF];
@@ -2694,6 +2817,7 @@ struct Team {
   // which holds t = 0 because the parent is clamped already; slides carry the parent's w.  Same rule as the
   // oracle's clamp_ang_vel.  A team bound |w_root| + sum |qd| <= W (no link can reach the cap) skips the pass.
   __device__ __forceinline__ void clamp_ang_vel() {
+    MG_NC_INT
     const float W = m->link_max_ang_vel;
     if (W > 0.0f) {
       const V3 w0 = freeb ? v3(__shfl(nu, tb), __shfl(nu, tb + 1), __shfl(nu, tb + 2)) : v3(0, 0, 0);
@@ -2749,6 +2873,7 @@ struct Team {
   }
 
   __device__ __forceinline__ void integrate() {
+    MG_NC_INT
     // root pose (lane 0 gathers the twist from lanes 0..5)
     float w0 = __shfl(nu, tb + 0), w1 = __shfl(nu, tb + 1), w2 = __shfl(nu, tb + 2);
     float v0 = __shfl(nu, tb + 3), v1 = __shfl(nu, tb + 4), v2 = __shfl(nu, tb + 5);
@@ -2871,11 +2996,15 @@ struct Team {
         const int ga = cside(c, 2), gb = cside(c, 3);
         ba[j] = ga >= 0 ? mt->gbody[ga] : -1;
         bb[j] = gb >= 0 ? mt->gbody[gb] : -1;
-        const V3 n = ld3(s->cn[c]);
-        V3 t1, t2;
-        s->tangents(c, &t1, &t2);  // build_rows' basis
-        f[j] = (n * s->rows()[3 * c].lam + t1 * s->rows()[3 * c + 1].lam + t2 * s->rows()[3 * c + 2].lam) *
-               prcp(h);
+        if constexpr (L::kCompact) {  // the impulse sum outputs() stashed before its fk() overwrote the rows
+          f[j] = ld3(s->fc(c)) * prcp(h);
+        } else {
+          const V3 n = ld3(s->cn[c]);
+          V3 t1, t2;
+          s->tangents(c, &t1, &t2);  // build_rows' basis
+          f[j] = (n * s->rows()[3 * c].lam + t1 * s->rows()[3 * c + 1].lam + t2 * s->rows()[3 * c + 2].lam) *
+                 prcp(h);
+        }
         pc[j] = ld3(s->cp[c]);
       }
     }

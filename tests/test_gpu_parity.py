@@ -282,11 +282,19 @@ def test_physics_step_matches_oracle(lib, task, n, z, fast):
         # and the oracle-sensitivity fallback where the dynamics are stiff (tests/test_step_flags.py)
         # No oracle-sensitivity fallback here (round 4 perturbed each env by the kernel's own first-substep drift, the
         # quantity under test).  These states are a stress case -- every root spins above the 100 rad/s cap, so fp32
-        # rounding of the |w|^2 h Coriolis and cap terms reaches every velocity -- and a stated fraction of their
-        # env-steps may disagree without a flag: 0.1 % (measured round 5: 3 of 4,096 Humanoid env-steps, 0 of 256 Ant;
-        # tests/test_step_flags.py finds the same with the oracle's fp32 build in place of the kernel)
-        PS.assert_steps_explained(test, bad[None], PS.step_flags(mnp, sp, pre)[None], sens=None, reach_cap=0.12,
-                                  allow_unexplained=1e-3)
+        # rounding of the |w|^2 h Coriolis and cap terms reaches every velocity -- and some env-steps may disagree
+        # without a flag.  How many is set by the fp32 twin (the oracle's own fp32 build, an implementation independent
+        # of the kernel) on the same states, not by the kernel's own count: the GPU may leave at most 4 x
+        # the twin's unflagged disagreements unexplained (the factor of the column rule, assert_north_star_rtol).
+        # Measured round 5: twin 1 of 4,096 Humanoid env-steps (tests/test_step_flags.py, same seed), GPU 3; Ant and
+        # the 256-env cases 0 and 0.
+        flags = PS.step_flags(mnp, sp, pre)
+        r32, d32 = root.copy(), dof.copy()
+        O.simulate(mnp, sp, r32, d32, act, np.zeros_like(sens_h), np.zeros_like(dfor_h), threads=8, fp32=True)
+        twin_unexplained = int((PS.spin_bad(r32, d32, r_h, d_h, root, dof, sp.dt) & (flags == 0)).sum())
+        PS.record(test, "fp32 twin: unflagged disagreeing env-steps", np.array([twin_unexplained]), np.array([0]))
+        PS.assert_steps_explained(test, bad[None], flags[None], sens=None, reach_cap=0.12,
+                                  allow_unexplained=4.0 * twin_unexplained / n)
         return
     np.testing.assert_allclose(rg[:, 0:7], r_h[:, 0:7], atol=2e-4)
     np.testing.assert_allclose(dg[..., 0], d_h[..., 0], atol=2e-4)
@@ -452,7 +460,7 @@ def _teacher_forced(lib, test, spec, sp, tp, h, steps, actions, seed, mutate=Non
     return cols, twin, pot_ulp
 
 
-def assert_north_star_rtol(res, twin_factor=4.0):
+def assert_north_star_rtol(res, twin_factor=4.0, frac_margin=0.005):
     """north_star: obs / reward parity within 1e-4 relative.  Per column group g over the unflagged env-steps (the
     teacher-forced fp32 GPU step against the fp64 oracle from the same state): |gpu - oracle| <= 1e-4 |oracle| + a_g,
     a_g = max(1e-4 S_g, 4 x the fp32 twin's need, the reward's potential spacing), S_g the group's magnitude in the
@@ -461,13 +469,20 @@ def assert_north_star_rtol(res, twin_factor=4.0):
     rounding itself needs more -- the oracle's own fp32 build from the same states needs a larger atol (the stiff
     contact / limit impulses behind the Humanoid's foot force-torques and DOF velocities) -- the GPU may need up to
     twin_factor times that (different operation order, FMA contraction, 1-ulp hardware reciprocals).  The reward
-    adds the fp32 spacing of its potentials (DESIGN.md §6 lists the groups where 1e-4 S_g does not hold and why)."""
+    adds the fp32 spacing of its potentials (DESIGN.md §6 lists the groups where 1e-4 S_g does not hold and why).
+    Per element, the fraction of a group's entries within 1e-4 |x| (no floor) must be at least the twin's minus
+    frac_margin (0.5 %)."""
     cols, twin, pot_ulp = res
     bad = {}
     for g, v in cols.items():
         a = max(1e-4 * v["scale"], twin_factor * twin[g]["atol_needed"], pot_ulp if g == "reward" else 0.0)
         if v["atol_needed"] > a:
             bad[g] = dict(v, allowed=a)
+        # and element by element (VERDICT r5): the fraction of the group's entries within 1e-4 |x| alone, with no
+        # floor, at least the fp32 twin's own fraction minus 0.5 % (measured round 6: Ant DOF velocities 88.9 % vs
+        # 89.1 %; the fused PGS velocity update had left them 0.8 % below, team_physics.hpp MG_PGS_UNFUSE)
+        if v["frac_within_rtol"] < twin[g]["frac_within_rtol"] - frac_margin:
+            bad[g + " (fraction within 1e-4 |x|)"] = {"gpu": v["frac_within_rtol"], "twin": twin[g]["frac_within_rtol"]}
     assert not bad, f"column groups outside 1e-4 |x| + a_g: {bad}"
 
 
@@ -482,10 +497,12 @@ def test_fused_env_step_matches_oracle(lib, task, n):
     assert_north_star_rtol(cols)
 
 
-@pytest.mark.parametrize("task,n", [("Ant", 16384), ("Humanoid", 32768)])
+@pytest.mark.parametrize("task,n", [("Ant", 16384), ("Humanoid", 32768), ("Ant", 65536)])
 def test_fused_parity_at_baseline_size(lib, task, n):
-    """BASELINE.json configs[1] (Ant, 16,384 envs) and configs[2] (Humanoid, 32,768 envs: the work-ordered K = 1
-    path) against the oracle at full size: the oracle first rolls every env 12 steps on from the
+    """BASELINE.json configs[1] (Ant, 16,384 envs), configs[2] (Humanoid, 32,768 envs: the work-ordered K = 1
+    path) and the headline configuration (Ant, 65,536 envs: the compact 12-wave kernel on the sorted
+    path, the second and third teacher-forced launches run in the sort's permutation) against the oracle at full
+    size: the oracle first rolls every env 12 steps on from the
     all-reset start (random actions; falls, resets and contacts spread over the batch), then 3 fused steps are
     teacher-forced as in test_fused_env_step_matches_oracle.  The per-column-group errors against north_star's
     1e-4 relative are recorded (MIGYM_PARITY_REPORT)."""
