@@ -315,6 +315,11 @@ def run_workload(task, n, object_type, args, world, rank, dev, gather_mode, seed
             "solver": "TGS" if env.sim_params.solver_type == 1 else "PGS",
             "vel_sweeps": max(env.sim_params.pos_iters, env.sim_params.vel_iters) if env.sim_params.solver_type == 1
             else 0}
+    import ctypes
+    tl, cl = ctypes.c_int32(), ctypes.c_int32()
+    if env._lib.mg_sim_kernel_layout(env.sim, ctypes.byref(tl), ctypes.byref(cl)) == 0:
+        # the step kernel's team layout (MIGYM_LAYOUT): classic 8 / compact 12 waves per CU
+        info["team_layout"] = f"T={tl.value} " + ("compact" if cl.value else "classic")
     env.close()
     del env, pool, gather
     value = n * world * args.steps / elapsed
@@ -418,7 +423,7 @@ def main():
                        "obs_gather": (f"{gather_mode}: kernel-packed [obs|rew|reset] rows, double-buffered, "
                                       f"overlapped with the next step, inside the timed region")
                                      if head["gathered"] else None,
-                       "parallelism": f"env-sharded x{world}",
+                       "parallelism": f"env-sharded x{world}", "team_layout": env.get("team_layout"),
                        **({"object_type": args.object_type} if args.task == "ShadowHand" else {})},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, **pmc_traffic(args.task, n, kern_ms, args.object_type),

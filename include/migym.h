@@ -533,6 +533,10 @@ int mg_kernel_span_waves(mg_sim* sim, int32_t launch, uint64_t* out, int32_t cap
  * unit; the identity before the first sort) and `cost` (n uint8, or NULL) = the row counts that launch wrote (the
  * next sort's keys); at most cap entries are copied.  Off and lists report n = 0. */
 int mg_work_order(mg_sim* sim, int32_t* order, uint8_t* cost, int32_t cap, int32_t* mode, int32_t* n_out);
+/* Diagnostic (no reference counterpart): the step-kernel instance the dispatcher picked for `sim`:
+ * team_lanes = lanes per actor (T), compact = 1 for the 12-waves-per-CU compact team layout, 0 for the classic one
+ * (MIGYM_LAYOUT = auto | compact | classic, read at mg_sim_create). */
+int mg_sim_kernel_layout(mg_sim* sim, int32_t* team_lanes, int32_t* compact);
 
 #ifdef __cplusplus
 }

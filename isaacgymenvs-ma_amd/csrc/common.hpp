@@ -39,6 +39,7 @@ struct mg_sim {
   //     (k_ohist, k_oscatter) before the launch turns them into the permutation it reads.
   int order_mode;      // kOrderOff / kOrderLists / kOrderSort
   int lds_pad;         // dynamic LDS added to every step-kernel launch (MIGYM_LDS_PAD; occupancy experiments, 0)
+  long layout_n;       // the batch the step kernels' LDS layout is picked for (MIGYM_LAYOUT; dispatch.hpp layout_fits)
   long long order_steps;  // ordered launches so far (the parity of the set the lists' launches write)
   int sort_every;      // sort: every K-th ordered launch sorts (the launches between keep the last permutation)
   bool order_valid;    // the previous ordered launch left an order for this one

@@ -9,8 +9,8 @@ static_assert(MG_INST >= 0 && MG_INST < MG_NUM_INST, "MG_INST out of range");
 
 namespace mgi {
 constexpr InstDesc kI = kInst[MG_INST];
-template struct BuildTile<kI.T, kI.MN, kI.MC, kI.MG, kI.MP, kI.OBJ>;
-template struct RunSimulate<kI.T, kI.MN, kI.MC, kI.MG, kI.MP, kI.OBJ>;
-template struct RunEnvStep<kI.T, kI.MN, kI.MC, kI.MG, kI.MP, kI.OBJ>;
+template struct BuildTile<kI.T, kI.MN, kI.MC, kI.MG, kI.MP, kI.OBJ, kI.LAY>;
+template struct RunSimulate<kI.T, kI.MN, kI.MC, kI.MG, kI.MP, kI.OBJ, kI.LAY>;
+template struct RunEnvStep<kI.T, kI.MN, kI.MC, kI.MG, kI.MP, kI.OBJ, kI.LAY>;
 template int phase_buf_publish<MG_INST>(unsigned long long*);
 }  // namespace mgi

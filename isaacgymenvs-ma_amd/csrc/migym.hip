@@ -601,6 +601,19 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   }
   s->lds_pad = 0;
   if (const char* e = getenv("MIGYM_LDS_PAD")) s->lds_pad = atoi(e) > 0 ? atoi(e) : 0;
+  // team LDS layout: by default the classic layout for a batch the classic kernel holds resident
+  // (dispatch.hpp kCompactMinWaves) and the compact 12-wave layout above it.  The two layouts round differently, so
+  // a shard is the bit-identical slice of a bigger rollout only when both pick the same layout:
+  // MIGYM_LAYOUT = compact | classic pins it (auto: the default).
+  s->layout_n = s->n;
+  if (const char* e = getenv("MIGYM_LAYOUT")) {
+    if (!strcmp(e, "classic")) s->layout_n = 0;
+    else if (!strcmp(e, "compact")) s->layout_n = 1L << 40;
+    else if (strcmp(e, "auto")) {
+      mg_sim_destroy(s);
+      return fail(MG_EINVAL, "mg_sim_create: MIGYM_LAYOUT must be auto, compact or classic");
+    }
+  }
   if (const char* e = getenv("MIGYM_ORDER")) {
     if (!strcmp(e, "off")) s->order_mode = kOrderOff;
     else if (!strcmp(e, "lists")) s->order_mode = kOrderLists;
@@ -636,7 +649,7 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
     return fail(MG_ENOMEM, "mg_sim_create: hipMalloc(work queue) failed");
   }
   if (mgi::team_size(s->host_model, s->params.max_contacts) > 0) {
-    const int rc = mgi::dispatch<mgi::BuildTile>(s->host_model, s->params.max_contacts, s);
+    const int rc = mgi::dispatch<mgi::BuildTile>(s->host_model, s->params.max_contacts, s->layout_n, s);
     if (rc) {
       mg_sim_destroy(s);
       return rc;
@@ -659,7 +672,7 @@ int mg_sim_bind(mg_sim* sim, const mg_state_views* views) {
 
 int mg_sim_simulate(mg_sim* sim, void* stream) {
   if (!sim || !sim->bound) return fail(MG_EINVAL, "mg_sim_simulate: sim not bound");
-  int rc = mgi::dispatch<mgi::RunSimulate>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
+  int rc = mgi::dispatch<mgi::RunSimulate>(sim->host_model, sim->params.max_contacts, sim->layout_n, (hipStream_t)stream,
                                  (const mg_sim*)sim);
   if (rc) return rc;
   return check_launch("mg_sim_simulate");
@@ -817,6 +830,14 @@ int mg_work_order(mg_sim* sim, int32_t* order, uint8_t* cost, int32_t cap, int32
     return fail(MG_EDEVICE, "mg_work_order: copy failed");
   *n_out = n;
   return MG_OK;
+}
+
+int mg_sim_kernel_layout(mg_sim* sim, int32_t* team_lanes, int32_t* compact) {
+  if (!sim || !team_lanes || !compact) return fail(MG_EINVAL, "mg_sim_kernel_layout: bad arguments");
+  *team_lanes = 0;
+  *compact = 0;
+  if (mgi::team_size(sim->host_model, sim->params.max_contacts) <= 0) return MG_OK;  // no instance fits: no team kernel
+  return mgi::dispatch<mgi::InstanceOf>(sim->host_model, sim->params.max_contacts, sim->layout_n, team_lanes, compact);
 }
 
 int mg_set_indexed(mg_sim* sim, int32_t which, const float* src, const int32_t* idx, int32_t n, void* stream) {
@@ -1063,7 +1084,7 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
                          sim->d_order);
     }
   }
-  int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, (hipStream_t)stream,
+  int rc = mgi::dispatch<mgi::RunEnvStep>(sim->host_model, sim->params.max_contacts, sim->layout_n, (hipStream_t)stream,
                                           (const mg_sim*)sim, tp, tb, rp);
   if (rc) return rc;
   if (sim->order_mode != kOrderOff && !rp) {  // the launch wrote the next one's lists / row counts

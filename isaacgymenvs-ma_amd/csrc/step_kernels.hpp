@@ -70,9 +70,9 @@ static __device__ unsigned long long* g_phase_buf;
 // when a wave finishes (a block's slots free only when its slowest wave is done).  W is the smallest
 // of 1, 2, 4, 8 that reaches the most resident waves per CU (at most 4 x the instance's waves per SIMD: 8 at the
 // 256-register budget, 12 at 168).
-template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR>
+template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR, int LAY = 0>
 struct Shape {
-  using TL = mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP>;
+  using TL = mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP, LAY>;
   static constexpr int E1 = 64 / T;  // teams (actors) per wave
   static constexpr size_t kTile = sizeof(mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OBJ)>);
   static constexpr size_t kWave = E1 * (sizeof(mg::BankSlot<TL, T>) + (DR ? sizeof(mg::DrTile<MN, MG>) : 0));
@@ -155,13 +155,13 @@ __device__ __forceinline__ void wq_done(unsigned* wq, int grid_waves) {
 // ------------------------------------------------------------------------------------------------ kernels
 // gym.simulate: one team of T lanes per actor (team_physics.hpp).  OBJ: hand-task envs with root
 // rows [articulation, object, goal], PD targets and rigid-body rows [bodies..., object, goal].
-template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR, bool TGS = false>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, OBJ, DR>::kWPE))) void k_simulate(
+template <int T, int MN, int MC, int MG, int MP, int OBJ, bool DR, bool TGS = false, int LAY = 0>
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR, LAY>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, OBJ, DR, LAY>::kWPE))) void k_simulate(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_state_views v, int n) {
-  using SH = Shape<T, MN, MC, MG, MP, OBJ, DR>;
+  using SH = Shape<T, MN, MC, MG, MP, OBJ, DR, LAY>;
   constexpr int E = SH::E, W = SH::W;
   constexpr int ROWS = OBJ ? 3 : 1;
-  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP, LAY>, T> lds[E];
   __shared__ typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   mg::copy_tile(&tile, static_cast<const typename mg::Team<T, MN, MC, MG, MP, OBJ>::MT*>(timg));
@@ -171,7 +171,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR>::kThreads)) __at
   const bool valid = a < n;
   const int ac = valid ? a : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors;
-  mg::Team<T, MN, MC, MG, MP, OBJ, TGS> t;
+  mg::Team<T, MN, MC, MG, MP, OBJ, TGS, LAY> t;
   t.init(&lds[team].v, &tile, m, &p);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
@@ -275,12 +275,12 @@ __device__ __forceinline__ void order_done(const MgOrder& ord, int grid_waves) {
 }
 
 // one work item of k_env_step: the E1 teams of one wave (item = the wave's global index)
-template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
+template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false, int LAY = 0>
 __device__ __forceinline__ void env_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0, MG, MP>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0, MG, MP, LAY>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
-  using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
+  using SH = Shape<T, MN, MC, MG, MP, 0, DR, LAY>;
   const int team = threadIdx.x / T;
   const int wt = (threadIdx.x & 63) / T;  // team index within the wave (ballot / shuffle positions)
   const int slot = item * SH::E1 + wt;
@@ -288,8 +288,8 @@ __device__ __forceinline__ void env_step_item(
   const int a = ordered_actor(ord, slot, n, tp.num_agents);
   const int ac = valid ? a : n - 1;
   const int na = tp.num_actions, nd = m->num_dofs, ns = m->num_sensors;
-  mg::TeamLDSOf<T, MN, MC, 0, MG, MP>& L = lds[team].v;
-  mg::Team<T, MN, MC, MG, MP, 0, TGS> t;
+  mg::TeamLDSOf<T, MN, MC, 0, MG, MP, LAY>& L = lds[team].v;
+  mg::Team<T, MN, MC, MG, MP, 0, TGS, LAY> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
     mg::load_dr<T>(&drt[team], v.env_props + (size_t)v.env_props_stride * ac, m, t.tl);
@@ -491,13 +491,13 @@ __device__ __forceinline__ void env_step_item(
   MG_PHASE_FLUSH(t, item)
 }
 
-template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false>
-__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, 0, DR>::kWPE))) MG_VGPR_ATTR void k_env_step(
+template <int T, int MN, int MC, int MG, int MP, bool DR, bool RP, bool TGS = false, int LAY = 0>
+__global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR, LAY>::kThreads)) __attribute__((amdgpu_waves_per_eu(Shape<T, MN, MC, MG, MP, 0, DR, LAY>::kWPE))) MG_VGPR_ATTR void k_env_step(
     const mg_model* __restrict__ m, const void* __restrict__ timg, mg_sim_params p, mg_task_params tp, mg_state_views v,
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
-  using SH = Shape<T, MN, MC, MG, MP, 0, DR>;
+  using SH = Shape<T, MN, MC, MG, MP, 0, DR, LAY>;
   constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0, MG, MP>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, 0, MG, MP, LAY>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -507,7 +507,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
   if constexpr (SH::kStatic) {
     // the static grid, one item per wave (one-wave blocks free their slot as soon as their wave is done)
     const int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64);
-    if (item * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m, tile, lds, drt, p, tp, v, tb, n, rp, item, ord);
+    if (item * SH::E1 < n) env_step_item<T, MN, MC, MG, MP, DR, RP, TGS, LAY>(m, tile, lds, drt, p, tp, v, tb, n, rp, item, ord);
     span_end(ord.clk, item);
     order_done(ord, (int)gridDim.x * W);
   } else {
@@ -515,7 +515,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, 0, DR>::kThreads)) __attr
     const int nit = (n + SH::E1 - 1) / SH::E1, gwv = (int)gridDim.x * W;
     for (int item = (int)blockIdx.x * W + (int)(threadIdx.x / 64); item < nit; item = wq_next(wq, gwv)) {
       const int z = opaque_zero();
-      env_step_item<T, MN, MC, MG, MP, DR, RP, TGS>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
+      env_step_item<T, MN, MC, MG, MP, DR, RP, TGS, LAY>(m + z, (&tile)[z], lds + z, drt + z, (&p)[z], (&tp)[z], (&v)[z], (&tb)[z], n,
                                                (&rp)[z], item, (&ord)[z]);
     }
     span_end(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -539,7 +539,7 @@ __device__ __forceinline__ int hand_action_of(const mg_task_params& tp, int d) {
 // one work item of k_hand_step: the E1 teams of one wave (item = the wave's global index)
 template <int T, int MN, int MC, int MG, int MP, int OT, bool DR, bool RP, bool TGS = false>
 __device__ __forceinline__ void hand_step_item(
-    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT, MG, MP>, T>* lds,
+    const mg_model* __restrict__ m, const mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)>& tile, mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT, MG, MP, 0>, T>* lds,
     mg::DrTile<DR ? MN : 1, DR ? MG : 1>* drt, const mg_sim_params& p, const mg_task_params& tp, const mg_state_views& v,
     const mg_task_buffers& tb, int n, const mg_replay& rp, int item, const MgOrder& ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
@@ -550,7 +550,7 @@ __device__ __forceinline__ void hand_step_item(
   const int ec = valid ? e : n - 1;
   const int nd = m->num_dofs, ns = m->num_sensors, na = tp.num_actions, no = tp.num_obs;
   const int nb = m->num_bodies, nbe = nb + 2;
-  mg::TeamLDSOf<T, MN, MC, OT, MG, MP>& L = lds[team].v;
+  mg::TeamLDSOf<T, MN, MC, OT, MG, MP, 0>& L = lds[team].v;
   mg::Team<T, MN, MC, MG, MP, OT, TGS> t;
   t.init(&L, &tile, m, &p, SH::W > 1);
   if constexpr (DR) {  // domain randomization: this actor's env_props row into the team's DrTile
@@ -792,7 +792,7 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OT, DR>::kThreads)) __att
     mg_task_buffers tb, int n, mg_replay rp, unsigned* __restrict__ wq, MgOrder ord) {
   using SH = Shape<T, MN, MC, MG, MP, OT, DR>;
   constexpr int E = SH::E, W = SH::W;
-  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT, MG, MP>, T> lds[E];
+  __shared__ mg::BankSlot<mg::TeamLDSOf<T, MN, MC, OT, MG, MP, 0>, T> lds[E];
   __shared__ mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OT)> tile;
   __shared__ mg::DrTile<DR ? MN : 1, DR ? MG : 1> drt[DR ? E : 1];
   span_start(ord.clk, (int)blockIdx.x * W + (int)(threadIdx.x / 64));
@@ -873,8 +873,8 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
   return MG_OK;
 }
 
-template <int T, int MN, int MC, int MG, int MP, int OBJ>
-int BuildTile<T, MN, MC, MG, MP, OBJ>::run(mg_sim* sim) {
+template <int T, int MN, int MC, int MG, int MP, int OBJ, int LAY>
+int BuildTile<T, MN, MC, MG, MP, OBJ, LAY>::run(mg_sim* sim) {
   using MT = mg::ModelTile<MN, MG, MP, mg::tile_hull_verts(OBJ)>;   // the kernels' tile type (Team::MT)
   MT* img = new (std::nothrow) MT();
   if (!img) return fail(MG_ENOMEM, "mg_sim_create: out of host memory (model tile)");
@@ -890,32 +890,32 @@ int BuildTile<T, MN, MC, MG, MP, OBJ>::run(mg_sim* sim) {
   return rc;
 }
 
-template <int T, int MN, int MC, int MG, int MP, int OBJ>
-int RunSimulate<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim) {
+template <int T, int MN, int MC, int MG, int MP, int OBJ, int LAY>
+int RunSimulate<T, MN, MC, MG, MP, OBJ, LAY>::run(hipStream_t s, const mg_sim* sim) {
   if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_sim_simulate: no model tile (model exceeds every kernel instance)");
   // the domain-randomized instance reads each actor's env_props row (mg_dr_apply); TGS runs its own instances
   const bool tgs = sim->params.solver_type == MG_SOLVER_TGS;
   if (sim->views.env_props) {
     if (tgs)
-      launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_simulate<T, MN, MC, MG, MP, OBJ, true, true>, s, sim->n, sim->d_model,
+      launch<Shape<T, MN, MC, MG, MP, OBJ, true, LAY>>(k_simulate<T, MN, MC, MG, MP, OBJ, true, true, LAY>, s, sim->n, sim->d_model,
                                                    (const void*)sim->d_tile, sim->params, sim->views, sim->n);
     else
-      launch<Shape<T, MN, MC, MG, MP, OBJ, true>>(k_simulate<T, MN, MC, MG, MP, OBJ, true>, s, sim->n, sim->d_model,
+      launch<Shape<T, MN, MC, MG, MP, OBJ, true, LAY>>(k_simulate<T, MN, MC, MG, MP, OBJ, true, false, LAY>, s, sim->n, sim->d_model,
                                                    (const void*)sim->d_tile, sim->params, sim->views, sim->n);
   } else if (tgs) {
-    launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_simulate<T, MN, MC, MG, MP, OBJ, false, true>, s, sim->n, sim->d_model,
+    launch<Shape<T, MN, MC, MG, MP, OBJ, false, LAY>>(k_simulate<T, MN, MC, MG, MP, OBJ, false, true, LAY>, s, sim->n, sim->d_model,
                                                   (const void*)sim->d_tile, sim->params, sim->views, sim->n);
   } else {
-    launch<Shape<T, MN, MC, MG, MP, OBJ, false>>(k_simulate<T, MN, MC, MG, MP, OBJ, false>, s, sim->n, sim->d_model,
+    launch<Shape<T, MN, MC, MG, MP, OBJ, false, LAY>>(k_simulate<T, MN, MC, MG, MP, OBJ, false, false, LAY>, s, sim->n, sim->d_model,
                                                   (const void*)sim->d_tile, sim->params, sim->views, sim->n);
   }
   return MG_OK;
 }
 
-template <int T, int MN, int MC, int MG, int MP, int OBJ>
-int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp,
-                                             const mg_task_buffers* tb, const mg_replay* rp) {
-  using TL = mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP>;
+template <int T, int MN, int MC, int MG, int MP, int OBJ, int LAY>
+int RunEnvStep<T, MN, MC, MG, MP, OBJ, LAY>::run(hipStream_t s, const mg_sim* sim, const mg_task_params* tp,
+                                                  const mg_task_buffers* tb, const mg_replay* rp) {
+  using TL = mg::TeamLDSOf<T, MN, MC, OBJ, MG, MP, LAY>;
   if (!sim->d_tile) return fail(MG_ECAPACITY, "mg_env_step: no model tile (model exceeds every kernel instance)");
   // observations are staged in the (dead) row storage of the team's LDS before the coalesced store
   if (!OBJ && (size_t)tp->num_obs * sizeof(float) > TL::kObsStageBytes)
@@ -953,19 +953,19 @@ int RunEnvStep<T, MN, MC, MG, MP, OBJ>::run(hipStream_t s, const mg_sim* sim, co
                                                     sim->d_model, ti, sim->params, tpm, sim->views, *tb, sim->n, r);
   } else {
     if (rp)
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, true>, s, sim, false, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false, LAY>>(k_env_step<T, MN, MC, MG, MP, false, true, false, LAY>, s, sim, false, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props && tgs)
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false, true>, s, sim, true,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true, LAY>>(k_env_step<T, MN, MC, MG, MP, true, false, true, LAY>, s, sim, true,
                                                  sim->d_model, ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (sim->views.env_props)
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true>>(k_env_step<T, MN, MC, MG, MP, true, false>, s, sim, true, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, true, LAY>>(k_env_step<T, MN, MC, MG, MP, true, false, false, LAY>, s, sim, true, sim->d_model,
                                                  ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else if (tgs)
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false, true>, s, sim, true,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false, LAY>>(k_env_step<T, MN, MC, MG, MP, false, false, true, LAY>, s, sim, true,
                                                   sim->d_model, ti, sim->params, *tp, sim->views, *tb, sim->n, r);
     else
-      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false>>(k_env_step<T, MN, MC, MG, MP, false, false>, s, sim, true, sim->d_model,
+      return launch_wq<Shape<T, MN, MC, MG, MP, 0, false, LAY>>(k_env_step<T, MN, MC, MG, MP, false, false, false, LAY>, s, sim, true, sim->d_model,
                                                   ti, sim->params, *tp, sim->views, *tb, sim->n, r);
   }
   return MG_OK;

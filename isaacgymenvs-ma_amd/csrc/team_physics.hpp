@@ -533,9 +533,10 @@ struct TeamLDSC {
   __device__ __forceinline__ void set_tangents(int, V3, V3) {}
 };
 // the team layout of an instance (common.hpp mg_compact_layout)
-template <int T, int MN, int MC, int OBJ, int MG, int MP>
-using TeamLDSOf =
-    typename std::conditional<mg_compact_layout(T, MN, OBJ), TeamLDSC<T, MN, MC, MG, MP>, TeamLDS<T, MN, MC, OBJ>>::type;
+// LAY: the instance's layout (dispatch.hpp MG_INSTANCES; 1 = compact, for the big batches, where twelve waves per CU pay)
+template <int T, int MN, int MC, int OBJ, int MG, int MP, int LAY>
+using TeamLDSOf = typename std::conditional<LAY != 0 && mg_compact_layout(T, MN, OBJ), TeamLDSC<T, MN, MC, MG, MP>,
+                                            TeamLDS<T, MN, MC, OBJ>>::type;
 
 // A team's LDS region padded so that consecutive teams start 4*T bytes apart modulo 128 B.  A
 // ds_read/write_b32 is serviced per 32-lane half with bank = dword address mod 32, so teams of
@@ -916,9 +917,9 @@ __device__ __forceinline__ bool box_box_edge(V3 c, const M3& R, V3 hg, V3 hb, fl
 // memory, and every phase then runs from scratch (egg: 7.4 -> 4.7 M env-steps/s until this was found).
 // OBJ: the free object's type (0: none); TGS: the build's TGS solver (mg_sim_params.solver_type) -- its
 // own kernel instances, so the PGS instances are the code they were
-template <int T, int MN, int MC, int MG, int MP, int OBJ = 0, bool TGS = false>
+template <int T, int MN, int MC, int MG, int MP, int OBJ = 0, bool TGS = false, int LAY = 0>
 struct Team {
-  using L = TeamLDSOf<T, MN, MC, OBJ, MG, MP>;
+  using L = TeamLDSOf<T, MN, MC, OBJ, MG, MP, LAY>;
   using MT = ModelTile<MN, MG, MP, tile_hull_verts(OBJ)>;
   static constexpr int MR = L::MR;
 #ifndef MG_HW_TRIG_T16

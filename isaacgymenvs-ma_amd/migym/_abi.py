@@ -169,6 +169,7 @@ EXPORTS = {
     "mg_kernel_span_waves": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]),
     "mg_work_order": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
                                 C.POINTER(C.c_int32)]),
+    "mg_sim_kernel_layout": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "mg_reset_idx": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.c_void_p, C.c_int32,
                                C.c_void_p]),
     "mg_env_step_replay": (C.c_int, [C.c_void_p, C.POINTER(TaskParams), C.POINTER(TaskBuffers), C.POINTER(Replay),

@@ -497,6 +497,47 @@ def test_fused_env_step_matches_oracle(lib, task, n):
     assert_north_star_rtol(cols)
 
 
+def kernel_layout(lib, spec, sp, n):
+    """(team lanes, compact) of the step-kernel instance mg_sim_create picks for n envs (mg_sim_kernel_layout)"""
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    _abi.check(lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), n, 0, C.byref(sim)), lib)
+    t, lay = C.c_int32(), C.c_int32()
+    try:
+        _abi.check(lib.mg_sim_kernel_layout(sim, C.byref(t), C.byref(lay)), lib)
+    finally:
+        lib.mg_sim_destroy(sim)
+    return t.value, lay.value
+
+
+@pytest.mark.parametrize("layout", ["classic", "compact"])
+@pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128)])
+def test_pinned_layout_matches_oracle(lib, task, n, layout, monkeypatch):
+    """MIGYM_LAYOUT: the locomotion models' two team layouts -- classic (8 waves per CU; the default
+    up to 2,048 waves) and compact (12 waves per CU; the default above) -- each pinned at a small batch and put
+    through test_fused_env_step_matches_oracle's teacher-forced check; mg_sim_kernel_layout shows which ran."""
+    monkeypatch.setenv("MIGYM_LAYOUT", layout)
+    spec, sp, tp = setup(task)
+    assert kernel_layout(lib, spec, sp, n)[1] == (layout == "compact")
+    h = O.HostEnv(tp, spec, n)
+    rng = np.random.default_rng(3)
+    acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(4)]
+    cols = _teacher_forced(lib, f"test_pinned_layout_matches_oracle[{task}-{layout}]", spec, sp, tp, h, 4, acts,
+                           seed=5)
+    assert_north_star_rtol(cols)
+
+
+@pytest.mark.parametrize("task,n,compact", [("Ant", 8192, 0), ("Ant", 8196, 1), ("Humanoid", 4096, 0),
+                                            ("Humanoid", 4098, 1), ("MAAnt", 2048, 0), ("Cartpole", 65536, 0)])
+def test_auto_layout_threshold(lib, task, n, compact, monkeypatch):
+    """the default layout choice: compact once the batch has more than 2,048 waves (dispatch.hpp kCompactMinWaves;
+    Ant / MA-Ant 4 actors per wave, Humanoid 2), never for a model without a compact instance (Cartpole)"""
+    monkeypatch.delenv("MIGYM_LAYOUT", raising=False)
+    spec, sp, tp = ma_setup(4) if task == "MAAnt" else setup(task)
+    assert kernel_layout(lib, spec, sp, n * (4 if task == "MAAnt" else 1)) == ({"Cartpole": 8, "Humanoid": 32}.get(
+        task, 16), compact)
+
+
 @pytest.mark.parametrize("task,n", [("Ant", 16384), ("Humanoid", 32768), ("Ant", 65536)])
 def test_fused_parity_at_baseline_size(lib, task, n):
     """BASELINE.json configs[1] (Ant, 16,384 envs), configs[2] (Humanoid, 32,768 envs: the work-ordered K = 1

@@ -11,7 +11,9 @@ same GPU, with the same actions, and must agree bit for bit on obs, rew and rese
   * Ant, 65,536 envs, shards of 8,192 (rank 5).
 
 (The per-rank consecutive_successes mean is reduced across ranks by the dist layer and is not part of
-obs / rew / reset.)
+obs / rew / reset.)  The tests that compare batches on both sides of the team-layout threshold (the
+classic layout up to 2,048 waves, the compact one above; the two round differently) pin MIGYM_LAYOUT=compact, as a
+deployment replaying a rank's shard alone would; the small-batch tests run the default choice.
 """
 import os
 
@@ -35,8 +37,9 @@ def _make(task, n, offset):
 @pytest.mark.parametrize("task,world,per_rank,ranks", [("MAAnt", 8, 8192, (0, 3, 7)),
                                                         ("ShadowHand", 8, 4096, (0, 7)),
                                                         ("Ant", 8, 8192, (5,))])
-def test_rank_shards_equal_slices_of_the_node_rollout(task, world, per_rank, ranks):
+def test_rank_shards_equal_slices_of_the_node_rollout(task, world, per_rank, ranks, monkeypatch):
     assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    monkeypatch.setenv("MIGYM_LAYOUT", "compact")
     steps = 6
     full = _make(task, world * per_rank, 0)
     A = full.num_agents
@@ -62,12 +65,13 @@ def test_rank_shards_equal_slices_of_the_node_rollout(task, world, per_rank, ran
 
 
 @pytest.mark.parametrize("task,n,per_rank", [("Ant", 1 << 20, 8192), ("ShadowHand", 1 << 17, 4096)])
-def test_largest_batch_equals_its_last_shard(task, n, per_rank):
+def test_largest_batch_equals_its_last_shard(task, n, per_rank, monkeypatch):
     """the large end of the size range: Ant at 1,048,576 envs (16x the headline, ~0.5 GB of state) and ShadowHand at
     131,072 envs (4x BASELINE configs[4]'s node total, one GPU), 4 steps; its last shard, stepped alone with
     env_offset = n - per_rank, must equal the batch's tail bit for bit (every index past 2^19 / 2^16 envs -- grid,
     work queue, counter RNG keys, row offsets -- as in the small runs)"""
     assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    monkeypatch.setenv("MIGYM_LAYOUT", "compact")
     steps = 4
     full = _make(task, n, 0)
     g = torch.Generator(device=DEV).manual_seed(9)
@@ -90,12 +94,13 @@ def test_largest_batch_equals_its_last_shard(task, n, per_rank):
 
 
 @pytest.mark.parametrize("task,obj", [("Humanoid", "block"), ("ShadowHand", "egg"), ("ShadowHand", "pen")])
-def test_work_queue_items_equal_the_static_grid(task, obj):
+def test_work_queue_items_equal_the_static_grid(task, obj, monkeypatch):
     """Multi-wave-block instances (Humanoid: 4 waves per block, hand block / pen 2, egg 8) run a work queue
     (step_kernels.hpp wq_next): at 16,384 envs the waves dequeue most of their items from the device counter;
     a 2,048-env shard fits the resident grid and runs static items only.  Both must give the same envs the same
     bits, over consecutive launches (the counters are re-zeroed by the last wave of every launch)."""
     assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    monkeypatch.setenv("MIGYM_LAYOUT", "compact")
     steps, n, per = 4, 16384, 2048
 
     def make(num, offset):
