@@ -439,8 +439,10 @@ size_t mg_dr_desc_sizeof(void);
 size_t mg_dr_apply_args_sizeof(void);
 size_t mg_dr_noise_args_sizeof(void);
 /* profiling aid (phase-timing build only, see isaacgymenvs-ma_amd/build.py --timing): MG_NUM_PHASES counters */
-#define MG_NUM_PHASES 24
+#define MG_NUM_PHASES 32
 int mg_debug_phase_cycles(uint64_t* out, int32_t reset);
+/* ... and the per-item rows behind it (an item = one wave's teams; cap items of MG_NUM_PHASES counts each) */
+int mg_debug_phase_waves(uint64_t* out, int32_t cap);
 
 int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t num_envs, int32_t device,
                   mg_sim** out);

@@ -31,6 +31,10 @@ namespace mg {
 
 static_assert(offsetof(mg_model, hull_plane) % 16 == 0, "the hull's planes are read as float4");
 
+#ifndef MG_HULL_SUP_UNROLL
+#define MG_HULL_SUP_UNROLL 2  // hull_support: the lane's vertex reads issued together
+#endif
+
 constexpr float HULL_MARGIN = 1e-3f;                      // rounding of the cube's core against the hull (m)
 constexpr float HULL_FEAT_EPS = 1e-6f;                    // a witness lies on a plane within this (m)
 constexpr float HULL_SIN_PARALLEL = 0.0871557427f;        // sin 5 deg
@@ -195,6 +199,9 @@ struct HullQ {
   const float (*hv)[3];
   const float (*pl)[4];
   int nv, np, tl, tb;
+#ifdef MG_PHASE_TIMING
+  mutable unsigned nsup = 0;  // profiling build: support evaluations
+#endif
 };
 
 // the hull's support vertex in direction d (team argmax, ties to the lowest index)
@@ -202,13 +209,21 @@ template <int T>
 __device__ __forceinline__ V3 hull_support(const HullQ& H, V3 d) {
   float best = -3.0e38f;
   int bi = 0x7fffffff;
-  for (int v = H.tl; v < H.nv; v += T) {
-    const float s = H.hv[v][0] * d.x + H.hv[v][1] * d.y + H.hv[v][2] * d.z;
-    if (s > best) { best = s; bi = v; }
+  // the lane's vertices in ascending order (a strict compare keeps the first maximum), their LDS reads issued together
+#pragma unroll MG_HULL_SUP_UNROLL
+  for (int k = 0; k < (MG_MAX_HULL_VERTS + T - 1) / T; k++) {
+    const int v = H.tl + k * T;
+    if (v < H.nv) {
+      const float s = H.hv[v][0] * d.x + H.hv[v][1] * d.y + H.hv[v][2] * d.z;
+      if (s > best) { best = s; bi = v; }
+    }
   }
   // the largest value, then the lowest vertex index holding it (a serial loop's first maximum)
   const float m = team_max_dpp<T>(best);
   bi = team_min_dpp_i<T>(best == m ? bi : 0x7fffffff);
+#ifdef MG_PHASE_TIMING
+  H.nsup++;
+#endif
   return ld3(H.hv[bi]);
 }
 
@@ -381,13 +396,39 @@ __device__ __forceinline__ int hull_face_clip(const HullQ& H, int f, V3 p0, V3 u
 // arguments and gets the same result.
 template <int T>
 __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, V3 ctr, const float (*pl)[4], int np,
-                                                  int tl, int tb, const HullCore& B, float rB, float off, float* out) {
+                                                  int tl, int tb, const HullCore& B, float rB, float off, float* out,
+                                                  unsigned* cyc = nullptr) {
   const HullQ H{hv, pl, nv, np, tl, tb};
+#ifdef MG_PHASE_TIMING
+  // profiling build: shader cycles of GJK, MPR and the feature / clipping rest into cyc[0..2], on every return path
+  struct Report {
+    unsigned* o;
+    unsigned long long t0, t1, t2;
+    int stage;
+    const HullQ& h;
+    unsigned s1;
+    __device__ ~Report() {
+      if (!o) return;
+      const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+      o[4] += stage == 0 ? h.nsup : s1;        // GJK supports
+      o[5] += stage == 2 ? h.nsup - s1 : 0u;   // MPR supports
+      if (stage == 0) { o[0] += (unsigned)(t3 - t0); return; }
+      o[0] += (unsigned)(t1 - t0);
+      if (stage == 2) { o[1] += (unsigned)(t2 - t1); o[2] += (unsigned)(t3 - t2); }
+      else o[2] += (unsigned)(t3 - t1);
+    }
+  } rep{cyc, __builtin_amdgcn_s_memtime(), 0, 0, 0, H, 0u};
+#define MG_HULL_T(k, st) { rep.t##k = __builtin_amdgcn_s_memtime(); rep.stage = st; if (st == 1) rep.s1 = H.nsup; }
+#else
+  (void)cyc;
+#define MG_HULL_T(k, st)
+#endif
   const V3 cb = B.kind == 0 ? (B.p0 + B.p1) * 0.5f : B.c;
   const V3 v0 = ctr - cb;
   V3 pa, pb, x, nrm, pt;
   float dist, d;
   const int gk = hull_gjk<T>(H, v0, B, rB + off, pa, pb, dist);
+  MG_HULL_T(1, 1)
   if (gk == 2) return 0;
   if (gk == 1) {
     if (!(dist > 1e-9f)) return 0;
@@ -395,7 +436,9 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
     pt = (pa + pb + nrm * rB) * 0.5f;
     d = dist - rB;
   } else {
-    if (!hull_mpr<T>(H, v0, B, x, pa)) return 0;
+    const bool ok = hull_mpr<T>(H, v0, B, x, pa);
+    MG_HULL_T(2, 2)
+    if (!ok) return 0;
     const float l = sqrtf(dot(x, x));
     if (!(l > 1e-9f)) return 0;
     nrm = x * (-1.0f / l);
@@ -533,5 +576,6 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
   out[6] = d;
   return 1;
 }
+#undef MG_HULL_T
 
 }  // namespace mg

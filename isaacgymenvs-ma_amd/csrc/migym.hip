@@ -490,10 +490,14 @@ size_t mg_dr_noise_args_sizeof(void) { return sizeof(mg_dr_noise_args); }
 // build only; returns MG_EINVAL otherwise).  Phases: 0 FK, 1 ABA (+tendons), 2 collide (+object
 // free step), 3 rows, 4 row Jacobians / W, 5 test solves, 6 PGS, 7 integrate, 8 outputs, 9 task layer +
 // write-back, 13 constraint rows (count), 14 load + pre-physics, 15 substep entry.
+#ifdef MG_PHASE_TIMING
+static unsigned long long* g_phase_host_buf = nullptr;  // the per-wave rows (kPhaseCap x MG_NUM_PHASES)
+#endif
+
 int mg_debug_phase_cycles(uint64_t* out, int32_t reset) {
 #ifdef MG_PHASE_TIMING
   constexpr int kPhaseCap = 1 << 16;  // blocks tracked (step_kernels.hpp)
-  static unsigned long long* buf = nullptr;
+  unsigned long long*& buf = g_phase_host_buf;
   const size_t bytes = (size_t)kPhaseCap * MG_NUM_PHASES * sizeof(unsigned long long);
   if (!buf) {  // first call: allocate + zero the per-wave rows and publish them to the kernels
     if (hipMalloc(&buf, bytes) != hipSuccess || hipMemset(buf, 0, bytes) != hipSuccess)
@@ -519,6 +523,24 @@ int mg_debug_phase_cycles(uint64_t* out, int32_t reset) {
   (void)out;
   (void)reset;
   return fail(MG_EINVAL, "mg_debug_phase_cycles: library built without MG_PHASE_TIMING");
+#endif
+}
+
+// Profiling aid: the per-item rows behind mg_debug_phase_cycles (an item = one wave's 64 / T teams; rows of
+// MG_NUM_PHASES cycle counts, summed since the last reset), the first `cap` items.  Phase-timing build only.
+int mg_debug_phase_waves(uint64_t* out, int32_t cap) {
+#ifdef MG_PHASE_TIMING
+  constexpr int kPhaseCap = 1 << 16;
+  if (!out || cap < 0 || cap > kPhaseCap) return fail(MG_EINVAL, "mg_debug_phase_waves: bad arguments");
+  if (!g_phase_host_buf) return fail(MG_EINVAL, "mg_debug_phase_waves: call mg_debug_phase_cycles first");
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, g_phase_host_buf, (size_t)cap * MG_NUM_PHASES * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(MG_EDEVICE, "mg_debug_phase_waves: copy failed");
+  return MG_OK;
+#else
+  (void)out;
+  (void)cap;
+  return fail(MG_EINVAL, "mg_debug_phase_waves: library built without MG_PHASE_TIMING");
 #endif
 }
 

@@ -435,6 +435,12 @@ struct TeamLDS {
 //   * no tangent basis is stored (recomputed from the normal by tangent_basis_t, the same bits) and the limit-row
 //     metadata is one byte per row (two for more than 16 nodes).
 // The ancestor masks and the nodes' level slots live in the block's model tile for every instance.
+#ifndef MG_HULL_FACE_GROUP
+#define MG_HULL_FACE_GROUP 4  // collide(): object points per pass of the hull's face argmax
+#endif
+#ifndef MG_HULL_PLANE_UNROLL
+#define MG_HULL_PLANE_UNROLL 5  // collide(): plane loads in flight per pass of the hull's face argmax
+#endif
 #ifndef MG_RB_LOCO32C
 #define MG_RB_LOCO32C 6   // test-solve columns per batch of the compact 32-lane teams
 #endif
@@ -1728,7 +1734,7 @@ struct Team {
   //   egg:   the faces against the ellipsoid's support points.
   // Normal from the object to the geom.  Hull vertex q against the object (block / pen), lane per vertex:
   __device__ __forceinline__ bool hull_vertex_candidate(int q, V3 c, const M3& Rg, V3* pt, V3* nrm, float* dist) const {
-    const V3 w = c + mul(Rg, ld3(m->hull_vert[q]));
+    const V3 w = c + mul(Rg, ld3(mt->hv[q]));  // the tile's copy of m->hull_vert (LDS)
     if constexpr (OBJ == MG_GT_BOX) {
       const V3 pl = mulT(oR, w - op);
       V3 nb, cb;
@@ -1878,6 +1884,11 @@ struct Team {
       float res[14];
       V3 c = v3(0, 0, 0);
       M3 Rg;
+#ifdef MG_PHASE_TIMING
+      // profiling build: the narrowphase's GJK / MPR / rest (hull_core_contacts) and the plane bound, per team
+      unsigned hcyc[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      const unsigned long long th0 = __builtin_amdgcn_s_memtime();
+#endif
       if (g >= 0 && (mt->gfil[g] & MG_COLLIDE_OBJECT)) {
         const M3 R0 = quat_to_mat(q0[0], q0[1], q0[2], q0[3]);
         const float* gf = mt->gf[g];
@@ -1930,11 +1941,26 @@ struct Team {
           // the bound is fp32 on another path than the candidates' own distances (and the oracle has no such
           // cull): a 1 um guard band keeps a candidate just under the offset from being dropped by rounding
           if (lb < off + 1e-6f) {
+#ifdef MG_PHASE_TIMING
+            hcyc[3] += (unsigned)(__builtin_amdgcn_s_memtime() - th0);
+            nx = hull_core_contacts<T>(mt->hv, mt->hnv, ld3(mt->hctr), m->hull_plane, np, tl, tb, B, rB, off, res, hcyc);
+#else
             nx = hull_core_contacts<T>(mt->hv, mt->hnv, ld3(mt->hctr), m->hull_plane, np, tl, tb, B, rB, off, res);
+#endif
             near = true;
           }
         }
       }
+#ifdef MG_PHASE_TIMING
+      for (int k = 0; k < 6; k++) {  // the wave's slowest team (every lane holds its team's value; 0 if not near)
+        unsigned wmax = 0;
+        for (int q = 0; q < 64; q += T) {
+          const unsigned cq = (unsigned)__builtin_amdgcn_readlane((int)hcyc[k], q);
+          wmax = cq > wmax ? cq : wmax;
+        }
+        ph[23 + k] = __builtin_amdgcn_readfirstlane(ph[23 + k] + wmax);
+      }
+#endif
       if (tl == 0) {
         for (int i = 0; i < nx; i++) {
           const V3 pw = mul(Rg, ld3(res + 7 * i)) + c, nw = mul(Rg, ld3(res + 7 * i + 3));
@@ -2326,19 +2352,56 @@ struct Team {
           for (int b = 0; b < 3; b++) Rl.m[a][b] = Rg.m[0][a] * oR.m[0][b] + Rg.m[1][a] * oR.m[1][b] + Rg.m[2][a] * oR.m[2][b];
         float dk = 0.0f;
         int fk = 0;
+        if constexpr (OBJ == MG_GT_ELLIPSOID || MG_HULL_FACE_GROUP == 0) {  // (0: round 5's pass per point)
 #pragma unroll 1
-        for (int k = 0; k < K; k++) {
-          const V3 pk = OBJ == MG_GT_ELLIPSOID ? cl : hull_object_point(k, c, Rg);
-          float best = -3.0e38f;
-          int bf = 0x7fffffff;
-          for (int f = tl; f < np; f += T) {
-            const float* hp = m->hull_plane[f];
-            const V3 x = OBJ == MG_GT_ELLIPSOID ? egg_support_geom(ld3(hp), cl, Rl) : pk;
-            const float sd = hp[0] * x.x + hp[1] * x.y + hp[2] * x.z - hp[3];
-            if (sd > best) { best = sd; bf = f; }
+          for (int k = 0; k < K; k++) {
+            const V3 pk = OBJ == MG_GT_ELLIPSOID ? cl : hull_object_point(k, c, Rg);
+            float best = -3.0e38f;
+            int bf = 0x7fffffff;
+            for (int f = tl; f < np; f += T) {
+              const float* hp = m->hull_plane[f];
+              const V3 x = OBJ == MG_GT_ELLIPSOID ? egg_support_geom(ld3(hp), cl, Rl) : pk;
+              const float sd = hp[0] * x.x + hp[1] * x.y + hp[2] * x.z - hp[3];
+              if (sd > best) { best = sd; bf = f; }
+            }
+            team_argmax<T>(best, bf);
+            if (tl == k) { dk = best; fk = bf; }
           }
-          team_argmax<T>(best, bf);
-          if (tl == k) { dk = best; fk = bf; }
+        } else {
+          // every object point against each plane the lane loads (one pass over the planes in global memory, the
+          // loads of a pass in flight together, instead of one dependent pass per point); per point the same
+          // scan order and strict compare, so the same face
+          constexpr int KG = K < MG_HULL_FACE_GROUP ? K : (MG_HULL_FACE_GROUP > 0 ? MG_HULL_FACE_GROUP : 1);
+#pragma unroll 1
+          for (int k0 = 0; k0 < K; k0 += KG) {
+            V3 pk[KG];
+            float best[KG];
+            int bf[KG];
+#pragma unroll
+            for (int k = 0; k < KG; k++) {
+              pk[k] = hull_object_point(k0 + k, c, Rg);
+              best[k] = -3.0e38f;
+              bf[k] = 0x7fffffff;
+            }
+            constexpr int NPL = (MG_MAX_HULL_PLANES + T - 1) / T;
+#pragma unroll MG_HULL_PLANE_UNROLL
+            for (int j = 0; j < NPL; j++) {
+              const int f = tl + j * T;
+              if (f < np) {
+                const float4 q = *reinterpret_cast<const float4*>(m->hull_plane[f]);
+#pragma unroll
+                for (int k = 0; k < KG; k++) {
+                  const float sd = q.x * pk[k].x + q.y * pk[k].y + q.z * pk[k].z - q.w;
+                  if (sd > best[k]) { best[k] = sd; bf[k] = f; }
+                }
+              }
+            }
+#pragma unroll
+            for (int k = 0; k < KG; k++) {
+              team_argmax<T>(best[k], bf[k]);
+              if (tl == k0 + k) { dk = best[k]; fk = bf[k]; }
+            }
+          }
         }
         int cnt = 0;
         V3 pt = v3(0, 0, 0), nrm = v3(0, 0, 1);
@@ -2539,6 +2602,7 @@ struct Team {
   __device__ __forceinline__ void substep() {
     ph_mark(15);
     hull_stage();
+    ph_mark(22);
     fk();
     if constexpr (OBJ == MG_GT_ELLIPSOID) {
       egg_stage();

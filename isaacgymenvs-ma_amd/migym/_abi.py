@@ -151,6 +151,7 @@ EXPORTS = {
     "mg_sim_params_sizeof": (C.c_size_t, []),
     "mg_state_views_sizeof": (C.c_size_t, []),
     "mg_debug_phase_cycles": (C.c_int, [C.c_void_p, C.c_int32]),
+    "mg_debug_phase_waves": (C.c_int, [C.c_void_p, C.c_int32]),
     "mg_sim_create": (C.c_int, [C.c_void_p, C.POINTER(SimParams), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "mg_sim_bind": (C.c_int, [C.c_void_p, C.POINTER(StateViews)]),
     "mg_sim_simulate": (C.c_int, [C.c_void_p, C.c_void_p]),
