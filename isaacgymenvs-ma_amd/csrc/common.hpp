@@ -45,7 +45,9 @@ struct mg_sim {
   bool order_valid;    // the previous ordered launch left an order for this one
   unsigned* d_bq;      // lists: [2][kOrderBuckets] bucket counts, then the launch's finished-wave counter
   int* d_blist;        // lists: [2][kOrderBuckets][bq_cap] env indices per bucket
-  int bq_cap;          // env units (n / A)
+  int bq_cap;          // env units (n / order_unit)
+  int order_unit;      // actors per unit of the work order: an env's A agents (MG_SORT_WAVE_UNITS: a wave's teams)
+  int order_agents;    // the agents per env the order was sized for
   int* d_order;        // sort: (bq_cap) slot -> env unit
   unsigned char* d_cost;  // sort: (bq_cap) the last launch's row count per env unit (its agents' largest, <= 255)
   unsigned* d_osort;   // sort: [kSortRep][256] bin totals, [blocks][256] the blocks' bases, then ushort ranks
@@ -81,7 +83,14 @@ struct MgOrder {
   unsigned long long* clk;  // nullptr, or this launch's span slot (mg_kernel_span_begin)
   unsigned* tot_clear;      // sort: the bin totals, zeroed by block 0 of the step kernel (k_oscatter, their last reader,
                             // has finished: stream order), so the next sort starts from zero with no host-side state
+  int unit;                 // sort: actors per unit (consecutive actors, one permutation entry; divides a wave's teams)
 };
+// sort units of one wave's consecutive envs (64 / T single-agent envs per unit, keyed by their largest row count):
+// every wave steps 64 / T consecutive envs, so the small per-env arrays keep their lines whole (VERDICT r5 item 3's
+// line-coherent units); 0: one env per unit (an MA env's agents together)
+#ifndef MG_SORT_WAVE_UNITS
+#define MG_SORT_WAVE_UNITS 0
+#endif
 
 namespace mgi {
 constexpr int kBlock = 64;

@@ -603,6 +603,7 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   s->d_bq = nullptr;
   s->d_blist = nullptr;
   s->bq_cap = 0;
+  s->order_unit = s->order_agents = 1;
   s->d_order = nullptr;
   s->d_cost = nullptr;
   s->d_osort = nullptr;
@@ -650,7 +651,13 @@ int mg_sim_create(const mg_model* model, const mg_sim_params* params, int32_t nu
   }
   if (s->order_mode != kOrderOff) {
     const int A = params->agents > 1 ? params->agents : 1;
-    s->bq_cap = (num_envs + A - 1) / A;
+    s->order_agents = A;
+    s->order_unit = A;
+    if (MG_SORT_WAVE_UNITS && s->order_mode == kOrderSort && A == 1 && s->host_model.obj_type == 0) {
+      const int T = mgi::team_size(s->host_model, s->params.max_contacts), U = T > 0 ? 64 / T : 1;
+      if (U > 1 && num_envs % U == 0) s->order_unit = U;  // (a ragged batch keeps one env per unit)
+    }
+    s->bq_cap = (num_envs + s->order_unit - 1) / s->order_unit;
     const size_t nu = (size_t)s->bq_cap, nb = (nu + 255) / 256;
     const bool ok = s->order_mode == kOrderLists
         ? hipMalloc(&s->d_bq, sizeof(unsigned) * (2 * kOrderBuckets + 1)) == hipSuccess &&
@@ -1094,7 +1101,7 @@ static int env_step(mg_sim* sim, const mg_task_params* tp, const mg_task_buffers
   }
   if (sim->order_mode != kOrderOff && !rp) {
     const int A = tp->num_agents > 1 ? tp->num_agents : 1;
-    if (sim->bq_cap != (sim->n + A - 1) / A) return fail(MG_EINVAL, "mg_env_step: num_agents differs from mg_sim_params.agents");
+    if (A != sim->order_agents) return fail(MG_EINVAL, "mg_env_step: num_agents differs from mg_sim_params.agents");
     // the last launch's row counts -> this one's order (every sort_every-th ordered launch from the second on)
     if (sim->order_mode == kOrderSort && sim->order_valid && (sim->order_steps - 1) % sim->sort_every == 0) {
       const int nu = sim->bq_cap, nb = (nu + 255) / 256;

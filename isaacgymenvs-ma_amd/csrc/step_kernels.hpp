@@ -231,9 +231,9 @@ __global__ __launch_bounds__((Shape<T, MN, MC, MG, MP, OBJ, DR, LAY>::kThreads))
 // wave-uniform prefixes.
 __device__ __forceinline__ int ordered_actor(const MgOrder& ord, int slot, int n, int A) {
   const int a1 = A > 1 ? A : 1;
-  if (ord.order) {  // sort: the permutation k_oscatter wrote
+  if (ord.order) {  // sort: the permutation k_oscatter wrote (of units of ord.unit consecutive actors)
     const int s = slot < n ? slot : n - 1;
-    return ord.order[s / a1] * a1 + s % a1;
+    return ord.order[s / ord.unit] * ord.unit + s % ord.unit;
   }
   if (!ord.rcnt) return slot < n ? slot : n - 1;
   const int lane = (int)(threadIdx.x & 63);
@@ -475,16 +475,17 @@ __device__ __forceinline__ void env_step_item(
     if (v.dof_force)
       for (int q = t.tl; q < nd; q += T) v.dof_force[(size_t)nd * a + q] = L.st().dforce[q];
   }
-  if (ord.wcnt || ord.cost) {  // the next launch's order: the env's largest agent row count
+  if (ord.wcnt || ord.cost) {  // the next launch's order: the unit's largest row count (an env's agents, a wave's envs)
     int rows = L.nrows;
     const int A = tp.num_agents > 1 ? tp.num_agents : 1;
-    if (A > 1) {
-      const int k0 = wt - wt % A;  // the env's first team in the wave
-      for (int k = 0; k < A; k++) rows = max(rows, __shfl(rows, (k0 + k) * T));
+    const int U = ord.wcnt ? A : ord.unit;
+    if (U > 1) {
+      const int k0 = wt - wt % U;  // the unit's first team in the wave
+      for (int k = 0; k < U; k++) rows = max(rows, __shfl(rows, (k0 + k) * T));
     }
-    if (valid && t.tl == 0 && a % A == 0) {
+    if (valid && t.tl == 0 && a % U == 0) {
       if (ord.wcnt) order_append(ord, rows, a / A);
-      else ord.cost[a / A] = (unsigned char)(rows < 255 ? rows : 255);
+      else ord.cost[a / U] = (unsigned char)(rows < 255 ? rows : 255);
     }
   }
   t.ph_mark(9);
@@ -854,7 +855,8 @@ static int launch_wq(K kern, hipStream_t s, const mg_sim* sim, bool ordered, A..
     clk = ms->d_span + 2 * (size_t)ms->span_stride * ms->span_next;
     ms->span_waves[ms->span_next++] = blocks * SH::W;
   }
-  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk, nullptr};
+  MgOrder ord{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, sim->bq_cap, clk, nullptr,
+              sim->order_unit};
   if (ordered && sim->order_mode == kOrderSort) {
     ord.order = sim->order_valid ? sim->d_order : nullptr;
     ord.cost = sim->d_cost;
