@@ -201,6 +201,7 @@ struct HullQ {
   int nv, np, tl, tb;
 #ifdef MG_PHASE_TIMING
   mutable unsigned nsup = 0;  // profiling build: support evaluations
+  mutable unsigned tsup = 0, tsimp = 0;  // profiling build: GJK's cycles in the supports and in the simplex solver
 #endif
 };
 
@@ -238,7 +239,13 @@ __device__ __forceinline__ int hull_gjk(const HullQ& H, V3 v0, const HullCore& B
   float vv = dot(v, v);
   float lam[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int it = 0; it < 64; it++) {
+#ifdef MG_PHASE_TIMING
+    const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
     const V3 a = hull_support<T>(H, -v), w = a - hcore_support(B, v);
+#ifdef MG_PHASE_TIMING
+    H.tsup += (unsigned)(__builtin_amdgcn_s_memtime() - ts0);
+#endif
     const float vw = dot(v, w);
     if (vw > 0.0f && vw * vw > vv * cut * cut) {
       dist = vw / sqrtf(vv);
@@ -256,7 +263,14 @@ __device__ __forceinline__ int hull_gjk(const HullQ& H, V3 v0, const HullCore& B
     for (int i = 0; i < 4; i++)
       if (i == n) { W[i] = w; P[i] = a; }
     n++;
+#ifdef MG_PHASE_TIMING
+    const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+    const bool inside = hsimplex(W, P, n, v, lam);
+    H.tsimp += (unsigned)(__builtin_amdgcn_s_memtime() - ts1);
+    if (inside) return 0;
+#else
     if (hsimplex(W, P, n, v, lam)) return 0;
+#endif
     const float vn = dot(v, v);
     if (vn <= 1e-20f) return 0;
     const bool stall = it > 0 && vn >= vv * (1.0f - 1e-7f);
@@ -412,6 +426,8 @@ __device__ __forceinline__ int hull_core_contacts(const float (*hv)[3], int nv, 
       const unsigned long long t3 = __builtin_amdgcn_s_memtime();
       o[4] += stage == 0 ? h.nsup : s1;        // GJK supports
       o[5] += stage == 2 ? h.nsup - s1 : 0u;   // MPR supports
+      o[6] += h.tsup;                           // GJK: cycles in the supports
+      o[7] += h.tsimp;                          // GJK: cycles in the simplex solver
       if (stage == 0) { o[0] += (unsigned)(t3 - t0); return; }
       o[0] += (unsigned)(t1 - t0);
       if (stage == 2) { o[1] += (unsigned)(t2 - t1); o[2] += (unsigned)(t3 - t2); }

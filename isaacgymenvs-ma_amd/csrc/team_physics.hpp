@@ -1886,7 +1886,7 @@ struct Team {
       M3 Rg;
 #ifdef MG_PHASE_TIMING
       // profiling build: the narrowphase's GJK / MPR / rest (hull_core_contacts) and the plane bound, per team
-      unsigned hcyc[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+      unsigned hcyc[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       const unsigned long long th0 = __builtin_amdgcn_s_memtime();
 #endif
       if (g >= 0 && (mt->gfil[g] & MG_COLLIDE_OBJECT)) {
@@ -1952,7 +1952,7 @@ struct Team {
         }
       }
 #ifdef MG_PHASE_TIMING
-      for (int k = 0; k < 6; k++) {  // the wave's slowest team (every lane holds its team's value; 0 if not near)
+      for (int k = 0; k < 8; k++) {  // the wave's slowest team (every lane holds its team's value; 0 if not near)
         unsigned wmax = 0;
         for (int q = 0; q < 64; q += T) {
           const unsigned cq = (unsigned)__builtin_amdgcn_readlane((int)hcyc[k], q);
