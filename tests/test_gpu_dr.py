@@ -138,9 +138,12 @@ def _dr_explained(test, mnp, sp, pre, checks, hand):
                               sens=lambda t, i: _physics_sensitive(mnp, sp, pre, i, checks, hand))
 
 
+@pytest.mark.parametrize("layout", ["auto", "compact"])
 @pytest.mark.parametrize("solver", ["pgs", "tgs"])
-def test_dr_physics_matches_oracle_ant(lib, solver):
-    """env_props rows on the GPU vs the oracle (solver tgs: the DR instance of the TGS kernels)"""
+def test_dr_physics_matches_oracle_ant(lib, solver, layout, monkeypatch):
+    """env_props rows on the GPU vs the oracle (solver tgs: the DR instance of the TGS kernels); at this
+    batch the default picks the classic team layout, `compact` pins the 12-wave one (big batches)"""
+    monkeypatch.setenv("MIGYM_LAYOUT", layout)
     cfg = configs.task_config("Ant", 16)
     cfg["sim"]["physx"]["solver"] = solver
     spec = M.load_builtin("ant")
@@ -180,7 +183,7 @@ def test_dr_physics_matches_oracle_ant(lib, solver):
     lib.mg_sim_destroy(sim)
     rg, dg = tr.cpu().numpy(), td.cpu().numpy()
     assert np.isfinite(rg).all() and np.isfinite(dg).all()
-    _dr_explained(f"test_dr_physics_matches_oracle_ant[{solver}]", mnp, sp, pre,
+    _dr_explained(f"test_dr_physics_matches_oracle_ant[{solver}-{layout}]", mnp, sp, pre,
                   [("root pose", rg[:, 0:7], h.root[:, 0:7], 2e-4, 0, lambda g: g.root[0, 0:7]),
                    ("root twist", rg[:, 7:13], h.root[:, 7:13], 2e-3, 2e-3, lambda g: g.root[0, 7:13]),
                    ("dof pos", dg[..., 0], h.dof[..., 0], 2e-4, 0, lambda g: g.dof[0, :, 0]),

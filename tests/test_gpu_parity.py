@@ -643,10 +643,12 @@ def ma_setup(A=4):
     return spec, taskdefs.sim_params(cfg, 16, A), taskdefs.task_params("MAAnt", cfg, spec)
 
 
+@pytest.mark.parametrize("layout", ["auto", "compact"])
 @pytest.mark.parametrize("A", [2, 4])
-def test_multi_agent_env_step_matches_oracle(lib, A):
+def test_multi_agent_env_step_matches_oracle(lib, A, layout, monkeypatch):
     """MAAnt fused step (AND-filter resets via wave ballot, others-block via shuffles) vs the oracle, teacher-forced
-    step by step (as test_fused_env_step_matches_oracle)."""
+    step by step (as test_fused_env_step_matches_oracle); `compact` pins the 12-wave team layout."""
+    monkeypatch.setenv("MIGYM_LAYOUT", layout)
     spec, sp, tp = ma_setup(A)
     n = A * 96
     h = O.HostEnv(tp, spec, n)
@@ -658,7 +660,8 @@ def test_multi_agent_env_step_matches_oracle(lib, A):
         if t in masks:
             hh.reset[:] = masks[t]
     assert tp.num_obs == 60 + 3 * (A - 1)
-    _teacher_forced(lib, f"test_multi_agent_env_step_matches_oracle[{A}]", spec, sp, tp, h, 4, acts, seed=9, mutate=mutate)
+    _teacher_forced(lib, f"test_multi_agent_env_step_matches_oracle[{A}-{layout}]", spec, sp, tp, h, 4, acts, seed=9,
+                    mutate=mutate)
 
 
 def test_multi_agent_parity_at_baseline_shard(lib):

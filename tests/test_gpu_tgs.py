@@ -76,16 +76,20 @@ def test_tgs_physics_step_matches_oracle(lib, task, n, z):
     PS.assert_steps_explained(test, bad[None], PS.step_flags(mnp, sp, pre)[None], sens=None)
 
 
+@pytest.mark.parametrize("layout", ["auto", "compact"])
 @pytest.mark.parametrize("task,n", [("Ant", 256), ("Humanoid", 128)])
-def test_tgs_fused_env_step_matches_oracle(lib, task, n):
+def test_tgs_fused_env_step_matches_oracle(lib, task, n, layout, monkeypatch):
     """mg_env_step with the TGS instances vs orc_env_step (TGS) over 4 teacher-forced control steps, device-RNG
-    resets; north_star's 1e-4 relative per column group (test_gpu_parity.assert_north_star_rtol)"""
+    resets; north_star's 1e-4 relative per column group (test_gpu_parity.assert_north_star_rtol).  `compact` pins
+    the 12-wave team layout the big batches run (the default picks the classic one at these sizes)"""
+    monkeypatch.setenv("MIGYM_LAYOUT", layout)
     spec, sp, tp = GP.setup(task)
     tgs(sp)
     h = O.HostEnv(tp, spec, n)
     rng = np.random.default_rng(23)
     acts = [rng.uniform(-1.2, 1.2, (n, tp.num_actions)).astype(np.float32) for _ in range(4)]
-    res = GP._teacher_forced(lib, f"test_tgs_fused_env_step_matches_oracle[{task}]", spec, sp, tp, h, 4, acts, seed=5)
+    res = GP._teacher_forced(lib, f"test_tgs_fused_env_step_matches_oracle[{task}-{layout}]", spec, sp, tp, h, 4, acts,
+                             seed=5)
     GP.assert_north_star_rtol(res)
 
 
