@@ -2078,6 +2078,7 @@ struct Team {
       }
     }
     wsync();
+    ph_mark(31);  // (profiling build: the geom frames' staging, apart from the ground candidates)
     // ground contacts: lane per geom, up to 8 candidates each, emitted in geom order.
     // pass 1 counts, a team scan places them, pass 2 recomputes and writes (no private arrays).
     // spheres and capsules only (the locomotion models): at most two candidates per geom, kept in registers,
@@ -2123,8 +2124,16 @@ struct Team {
       int ty = -1;
       if (g < G && (mt->gfil[g] & MG_COLLIDE_GROUND)) {
         geom_staged(g, &c, &Rg);
-        // every candidate's gap is >= c.z - bounding radius: geoms that high cannot touch the plane
+        // every candidate's gap is >= c.z - bounding radius: geoms that high cannot touch the plane; a box's lowest
+        // corner exactly (Cartpole's 8 m rail: its bounding radius reaches the plane from any height), the same test
+        // its corner loop would fail, so the same contacts
         if (c.z - mt->gf[g][15] < off) ty = mt->gtype[g];
+        if (OBJ == 0 && ty == MG_GT_BOX) {  // (the hand instances' box geoms pass the radius test rarely: left as is)
+          const float* hb = mt->gf[g] + 12;
+          const float zlow = c.z - (fabsf(Rg.m[2][0]) * hb[0] + fabsf(Rg.m[2][1]) * hb[1] + fabsf(Rg.m[2][2]) * hb[2]);
+          // (a rounding guard on the scale of the terms: the corner loop rounds its own sums)
+          if (!(zlow < off + 1e-6f * (1.0f + fabsf(c.z) + hb[0] + hb[1] + hb[2]))) ty = -1;
+        }
       }
       const float* gs = g < G ? mt->gf[g] + 12 : mt->gf[0] + 12;
       int cnt = 0;

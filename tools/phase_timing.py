@@ -23,7 +23,8 @@ NAMES = {0: "fk", 1: "aba", 2: "collide", 3: "rows", 4: "row_jacobians", 5: "row
          19: "collide.ground", 20: "collide.pairs", 21: "collide.hull", 22: "hull_stage",
          # inside hull_stage (the wave's slowest team; not added to the total): the narrowphase's parts
          23: "(hull.gjk)", 24: "(hull.mpr)", 25: "(hull.features)", 26: "(hull.bound)",
-         27: "(#gjk supports)", 28: "(#mpr supports)", 29: "(gjk.supports)", 30: "(gjk.simplex)"}
+         27: "(#gjk supports)", 28: "(#mpr supports)", 29: "(gjk.supports)", 30: "(gjk.simplex)",
+         31: "collide.staging"}
 SUB = (13, 23, 24, 25, 26, 27, 28, 29, 30)   # a count and the sub-phases: not part of the total   # slot 2 "collide": the object candidates
 NPHASE = 32
 
