@@ -41,7 +41,7 @@
 // the locomotion observation head on four team lanes (mg::obs_head_team) instead of the leader (0: mg::obs_head)
 // the locomotion task layer's per-env scalars (progress, potentials) loaded at the start of the step (0: after it)
 #ifndef MG_TASK_PREFETCH
-#define MG_TASK_PREFETCH 0
+#define MG_TASK_PREFETCH 1
 #endif
 #ifndef MG_TEAM_OBS_HEAD
 #define MG_TEAM_OBS_HEAD 1
@@ -304,13 +304,17 @@ __device__ __forceinline__ void env_step_item(
   }
   mg::wsync();
   const int64_t reset_in = tb.reset[ac];
-#if MG_TASK_PREFETCH
   // the task layer's per-env scalars, loaded now so that their latency hides under the physics (nothing in the
-  // step writes them before the task layer does)
-  const int64_t progress_in = tb.progress[ac];
-  const float pot_in = tb.potentials ? tb.potentials[ac] : 0.0f;
-  const float prev_in = tb.potentials ? tb.prev_potentials[ac] : 0.0f;
-#endif
+  // step writes them before the task layer does); not for the compact 16-lane kernel, whose 168 registers it costs
+  // (profiles/r06/ab_task_prefetch.txt: Ant 65,536 -0.3 %, MA-Ant -0.4 %; Humanoid +0.6 %, Ant 8,192 +0.9 %)
+  constexpr bool kTaskPf = MG_TASK_PREFETCH && !(SH::TL::kCompact && T == 16);
+  int64_t progress_in = 0;
+  float pot_in = 0.0f, prev_in = 0.0f;
+  if constexpr (kTaskPf) {
+    progress_in = tb.progress[ac];
+    pot_in = tb.potentials ? tb.potentials[ac] : 0.0f;
+    prev_in = tb.potentials ? tb.prev_potentials[ac] : 0.0f;
+  }
   t.ph_start();
   // pre_physics_step: clamp + effort (ant.py:281-285; humanoid.py:281-285; cartpole.py:159-163)
   t.load(v.root_states + (size_t)13 * ac, v.dof_state + (size_t)2 * nd * ac, nullptr);
@@ -359,21 +363,16 @@ __device__ __forceinline__ void env_step_item(
     do_reset = all;
   }
   float pot = 0.0f, prev = 0.0f, up[3] = {0, 0, 0}, hd[3] = {0, 0, 0};
-#if MG_TASK_PREFETCH
-  int64_t progress = progress_in + 1;
-#else
-  int64_t progress = tb.progress[ac] + 1;
-#endif
+  int64_t progress = (kTaskPf ? progress_in : tb.progress[ac]) + 1;
   int64_t reset = reset_in;
   // self.actions: one lane per action column (na <= T, checked by mg_env_step)
   const bool alane = t.tl < na;
   const float act_l = alane ? mg::clampf(tb.actions[(size_t)na * ac + t.tl], tp.clip_actions) : 0.0f;
   if (valid && alane && tb.actions_out) tb.actions_out[(size_t)na * a + t.tl] = act_l;
-#if MG_TASK_PREFETCH
-  if (tb.potentials) { pot = pot_in; prev = prev_in; }
-#else
-  if (tb.potentials) { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
-#endif
+  if (tb.potentials) {
+    if constexpr (kTaskPf) { pot = pot_in; prev = prev_in; }
+    else { pot = tb.potentials[ac]; prev = tb.prev_potentials[ac]; }
+  }
   if (do_reset) {  // reset_idx: one lane per DOF draws its noise; the leader resets root and potentials
     const float* nz = tb.noise ? tb.noise + (size_t)2 * nd * ac : nullptr;
     for (int i = t.tl; i < nd; i += T)
