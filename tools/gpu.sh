@@ -130,7 +130,7 @@ case $mode in
     for gm in all root; do
       echo "== torchrun x$N gather=$gm"
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" --master-addr 127.0.0.1 \
-        --master-port $((29500 + RANDOM % 1000)) bench.py --gpus "$N" --steps 20 --warmup 5 --backend gloo \
+        --master-port $((29500 + RANDOM % 1000)) bench.py --gpus "$N" --steps 20 --warmup 5 --backend gloo --steady-steps 0 \
         --gather $gm > gpurun_out/multirank/x${N}_$gm.log 2>&1
       rc=$?; echo "rc=$rc"; tail -n 2 gpurun_out/multirank/x${N}_$gm.log
       [ $rc -eq 0 ] || exit $rc
