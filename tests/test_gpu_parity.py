@@ -527,6 +527,16 @@ def test_pinned_layout_matches_oracle(lib, task, n, layout, monkeypatch):
     assert_north_star_rtol(cols)
 
 
+def test_layout_env_rejects_unknown_values(lib, monkeypatch):
+    """MIGYM_LAYOUT accepts auto / compact / classic only: anything else fails mg_sim_create with MG_EINVAL"""
+    monkeypatch.setenv("MIGYM_LAYOUT", "fast")
+    spec, sp, tp = setup("Ant")
+    mnp = M.pack_model(spec)
+    sim = C.c_void_p()
+    rc = lib.mg_sim_create(mnp.ctypes.data, C.byref(sp), 64, 0, C.byref(sim))
+    assert rc != 0 and b"MIGYM_LAYOUT" in lib.mg_last_error()
+
+
 @pytest.mark.parametrize("task,n,compact", [("Ant", 8192, 0), ("Ant", 8196, 1), ("Humanoid", 4096, 0),
                                             ("Humanoid", 4098, 1), ("MAAnt", 2048, 0), ("Cartpole", 65536, 0)])
 def test_auto_layout_threshold(lib, task, n, compact, monkeypatch):
